@@ -1,0 +1,471 @@
+"""Generate the golden fixtures under tests/golden/ by running the REFERENCE (rsl_rl 3.1.0) on CPU.
+
+Test infrastructure only: this script runs in the build container (where /root/reference exists) and
+writes small .npz/.json fixtures that the CPU oracle and the HIP path are checked against.  Nothing from
+the reference travels with the repo or to the GPU box; only the captured input/output vectors do.
+
+The reference imports two packages that this image lacks:
+  * ``git`` (GitPython) -- used only by ``store_code_state`` which is never reached with log_dir=None,
+    so an empty module object stands in;
+  * ``tensordict`` -- the reference uses ``TensorDict`` purely as a keyed container with row indexing
+    (``rollout_storage.py:48-52,83,168,188``); it performs no arithmetic on this path.  A container with
+    exactly that behaviour (``_RowDict`` below) is registered under that name.
+All arithmetic that the fixtures pin (GAE, normalisation, randperm, gathers, PPO loss/KL/gradients,
+Adam update) is executed by the reference's own code and by torch 2.10.0 CPU kernels.
+
+Usage:  python tests/golden/make_golden.py [--reference /root/reference]
+"""
+
+from __future__ import annotations
+
+import argparse
+import hashlib
+import json
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+# --------------------------------------------------------------------------------------------------
+# import shims (see module docstring)
+# --------------------------------------------------------------------------------------------------
+class _RowDict:
+    """Keyed container of tensors sharing leading batch dims (the subset of TensorDict rsl_rl uses)."""
+
+    def __init__(self, source, batch_size=None, device=None):
+        self._d = dict(source)
+        if batch_size is None:
+            first = next(iter(self._d.values()))
+            batch_size = [first.shape[0]]
+        self.batch_size = torch.Size(batch_size)
+        self.device = device
+
+    def __getitem__(self, key):
+        if isinstance(key, str):
+            return self._d[key]
+        out = {k: v[key] for k, v in self._d.items()}
+        first = next(iter(out.values()))
+        nb = max(len(self.batch_size) - (1 if isinstance(key, int) else 0), 1)
+        return _RowDict(out, batch_size=list(first.shape[:nb]), device=self.device)
+
+    def __contains__(self, key):
+        return key in self._d
+
+    def keys(self):
+        return self._d.keys()
+
+    def items(self):
+        return self._d.items()
+
+    def values(self):
+        return self._d.values()
+
+    def copy_(self, other):
+        for k, v in self._d.items():
+            v.copy_(other[k])
+        return self
+
+    def flatten(self, a, b):
+        out = {k: v.flatten(a, b) for k, v in self._d.items()}
+        bs = list(self.batch_size)
+        nbs = bs[:a] + [int(np.prod(bs[a : b + 1]))] + bs[b + 1 :]
+        return _RowDict(out, batch_size=nbs, device=self.device)
+
+    def to(self, device):
+        return _RowDict({k: v.to(device) for k, v in self._d.items()}, self.batch_size, device)
+
+    @property
+    def shape(self):
+        return self.batch_size
+
+
+def import_reference(path):
+    sys.dont_write_bytecode = True
+    sys.modules.setdefault("git", types.ModuleType("git"))
+    td = types.ModuleType("tensordict")
+    td.TensorDict = _RowDict
+    sys.modules["tensordict"] = td
+    sys.path.insert(0, path)
+    import rsl_rl  # noqa: F401
+    from rsl_rl.algorithms import PPO
+    from rsl_rl.modules import ActorCritic
+    from rsl_rl.storage import RolloutStorage
+
+    return PPO, ActorCritic, RolloutStorage
+
+
+def f32(x):
+    return np.ascontiguousarray(x.detach().cpu().numpy().astype(np.float32))
+
+
+# --------------------------------------------------------------------------------------------------
+# GAE  (rollout_storage.py:127-149)
+# --------------------------------------------------------------------------------------------------
+GAE_CASES = [
+    # name, T, N, p_done, gamma, lam, seed, done_pattern
+    ("t16_n512", 16, 512, 0.02, 0.99, 0.95, 0, "bernoulli"),
+    ("t24_n4096", 24, 4096, 0.02, 0.99, 0.95, 1, "bernoulli"),
+    ("t1_n70", 1, 70, 0.02, 0.99, 0.95, 2, "bernoulli"),
+    ("t5_n1000_alldone", 5, 1000, 1.0, 0.99, 0.95, 3, "all"),
+    ("t7_n130_nodone", 7, 130, 0.0, 0.99, 0.95, 4, "none"),
+    ("t8_n64_lastdone", 8, 64, 0.0, 0.99, 0.95, 5, "last"),
+    ("t24_n333_g1l1", 24, 333, 0.05, 1.0, 1.0, 6, "bernoulli"),
+    ("t3_n1", 3, 1, 0.5, 0.97, 0.9, 7, "bernoulli"),
+    ("t32_n257_heavy", 32, 257, 0.3, 0.995, 0.98, 8, "bernoulli"),
+]
+
+
+def make_gae(RolloutStorage):
+    out = {}
+    for name, T, N, p, gamma, lam, seed, pat in GAE_CASES:
+        g = torch.Generator().manual_seed(1000 + seed)
+        values = torch.randn(T, N, 1, generator=g)
+        rewards = torch.randn(T, N, 1, generator=g)
+        last_values = torch.randn(N, 1, generator=g)
+        if pat == "bernoulli":
+            dones = (torch.rand(T, N, 1, generator=g) < p).to(torch.uint8)
+        elif pat == "all":
+            dones = torch.ones(T, N, 1, dtype=torch.uint8)
+        elif pat == "none":
+            dones = torch.zeros(T, N, 1, dtype=torch.uint8)
+        else:
+            dones = torch.zeros(T, N, 1, dtype=torch.uint8)
+            dones[T - 1] = 1
+        res = {}
+        for norm in (False, True):
+            st = RolloutStorage("rl", N, T, {"policy": torch.zeros(N, 1)}, [1], "cpu")
+            st.values.copy_(values)
+            st.rewards.copy_(rewards)
+            st.dones.copy_(dones)
+            st.compute_returns(last_values.clone(), gamma, lam, normalize_advantage=norm)
+            res[norm] = (f32(st.returns), f32(st.advantages))
+        assert np.array_equal(res[False][0], res[True][0])
+        out[name] = dict(
+            T=T, N=N, gamma=gamma, lam=lam,
+            values=f32(values).reshape(T, N), rewards=f32(rewards).reshape(T, N),
+            dones=dones.numpy().reshape(T, N).astype(np.uint8), last_values=f32(last_values).reshape(N),
+            returns=res[False][0].reshape(T, N), advantages_raw=res[False][1].reshape(T, N),
+            advantages_norm=res[True][1].reshape(T, N),
+        )
+    arrays = {}
+    meta = {}
+    for name, d in out.items():
+        meta[name] = {k: d[k] for k in ("T", "N", "gamma", "lam")}
+        for k in ("values", "rewards", "dones", "last_values", "returns", "advantages_raw", "advantages_norm"):
+            arrays[f"{name}/{k}"] = d[k]
+    np.savez_compressed(os.path.join(HERE, "gae.npz"), **arrays)
+    return meta
+
+
+# --------------------------------------------------------------------------------------------------
+# randperm  (rollout_storage.py:165 -> torch CPU randperm)
+# --------------------------------------------------------------------------------------------------
+PERM_CASES = [
+    # name, n, seed, pre_draw (consume generator before randperm to exercise a mid-stream state)
+    ("n1", 1, 0, 0),
+    ("n2", 2, 1, 0),
+    ("n3", 3, 2, 0),
+    ("n10", 10, 3, 0),
+    ("n1000", 1000, 4, 0),
+    ("n8192", 8192, 5, 0),
+    ("n98304", 98304, 6, 0),
+    ("n4097_mid", 4097, 7, 1234),
+    ("n777_mid_odd", 777, 8, 623),
+    ("n5000_mid_long", 5000, 9, 5000),
+]
+BIG_PERM = [("n1572864", 1572864, 0), ("n393216", 393216, 11)]
+
+
+def make_perm():
+    arrays, meta = {}, {}
+    for name, n, seed, pre in PERM_CASES:
+        g = torch.Generator().manual_seed(seed)
+        if pre:
+            torch.randint(0, 2**31 - 1, (pre,), generator=g)  # consumes `pre` mt19937 words
+        state = g.get_state().numpy().copy()
+        perm = torch.randperm(n, generator=g).numpy().astype(np.int64)
+        state_after = g.get_state().numpy().copy()
+        arrays[f"{name}/state"] = state
+        arrays[f"{name}/perm"] = perm
+        arrays[f"{name}/state_after"] = state_after
+        meta[name] = {"n": n, "seed": seed, "pre_draw": pre}
+    for name, n, seed in BIG_PERM:
+        g = torch.Generator().manual_seed(seed)
+        perm = torch.randperm(n, generator=g).numpy().astype(np.int64)
+        meta[name] = {
+            "n": n, "seed": seed, "pre_draw": 0,
+            "sha256_int64": hashlib.sha256(perm.tobytes()).hexdigest(),
+            "head": perm[:32].tolist(), "tail": perm[-32:].tolist(),
+        }
+    np.savez_compressed(os.path.join(HERE, "perm.npz"), **arrays)
+    return meta
+
+
+# --------------------------------------------------------------------------------------------------
+# mini-batch generator  (rollout_storage.py:160-203)
+# --------------------------------------------------------------------------------------------------
+def make_minibatch(RolloutStorage):
+    T, N, A, M, E = 4, 6, 2, 3, 2
+    g = torch.Generator().manual_seed(77)
+    obs0 = {"policy": torch.zeros(N, 3), "extra": torch.zeros(N, 2)}
+    st = RolloutStorage("rl", N, T, obs0, [A], "cpu")
+    fields = {}
+    fields["obs_policy"] = torch.randn(T, N, 3, generator=g)
+    fields["obs_extra"] = torch.randn(T, N, 2, generator=g)
+    st.observations["policy"].copy_(fields["obs_policy"])
+    st.observations["extra"].copy_(fields["obs_extra"])
+    for k, shape in (("actions", (T, N, A)), ("values", (T, N, 1)), ("returns", (T, N, 1)),
+                     ("actions_log_prob", (T, N, 1)), ("advantages", (T, N, 1)), ("mu", (T, N, A)),
+                     ("sigma", (T, N, A))):
+        fields[k] = torch.randn(*shape, generator=g)
+        getattr(st, k).copy_(fields[k])
+    torch.manual_seed(4242)
+    state = torch.default_generator.get_state().numpy().copy()
+    batches = list(st.mini_batch_generator(M, E))
+    arrays = {f"in/{k}": f32(v) for k, v in fields.items()}
+    arrays["in/gen_state"] = state
+    names = ["actions", "target_values", "advantages", "returns", "old_logp", "old_mu", "old_sigma"]
+    for j, b in enumerate(batches):
+        arrays[f"mb{j}/obs_policy"] = f32(b[0]["policy"])
+        arrays[f"mb{j}/obs_extra"] = f32(b[0]["extra"])
+        for nm, t in zip(names, b[1:8]):
+            arrays[f"mb{j}/{nm}"] = f32(t)
+        assert b[8] == (None, None) and b[9] is None
+    np.savez_compressed(os.path.join(HERE, "minibatch.npz"), **arrays)
+    return {"T": T, "N": N, "A": A, "M": M, "E": E, "num_batches": len(batches), "torch_seed": 4242}
+
+
+# --------------------------------------------------------------------------------------------------
+# PPO loss / KL / gradients (ppo.py:221-315, 367) and one full update (ppo.py:178-422)
+# --------------------------------------------------------------------------------------------------
+def _fill_storage(st, T, N, A, O, g, policy=None):
+    """Rollout-like storage contents.
+
+    policy=None: obs~N(0,1); mu~N(0,.25); sigma~U(.5,1.5) per action; actions sampled around mu; old
+    log-prob perturbed by N(0,.3^2) (large KL -> exercises the lr-decrease branch).
+    policy given: mu/sigma/values/log-prob are what the policy itself produces for the stored obs, as in
+    a real rollout (ppo.py:129-140), so the first mini-batch's KL is ~0 (lr-increase branch).
+    """
+    obs = torch.randn(T, N, O, generator=g)
+    st.observations["policy"].copy_(obs)
+    st.rewards.copy_(torch.randn(T, N, 1, generator=g))
+    st.dones.copy_((torch.rand(T, N, 1, generator=g) < 0.05).to(torch.uint8))
+    if policy is None:
+        st.values.copy_(torch.randn(T, N, 1, generator=g))
+        mu = torch.randn(T, N, A, generator=g) * 0.5
+        sigma = 0.5 + torch.rand(1, 1, A, generator=g).expand(T, N, A)
+        actions = mu + sigma * torch.randn(T, N, A, generator=g)
+        logp = torch.distributions.Normal(mu, sigma).log_prob(actions).sum(-1, keepdim=True)
+        logp = logp + 0.3 * torch.randn(T, N, 1, generator=g)
+    else:
+        with torch.inference_mode():
+            o = {"policy": obs.reshape(T * N, O)}
+            policy.update_distribution(policy.actor_obs_normalizer(policy.get_actor_obs(o)))
+            mu = policy.action_mean.reshape(T, N, A).clone()
+            sigma = policy.action_std.reshape(T, N, A).clone()
+            actions = mu + sigma * torch.randn(T, N, A, generator=g)
+            logp = policy.distribution.log_prob(actions.reshape(T * N, A)).sum(-1).reshape(T, N, 1).clone()
+            st.values.copy_(policy.evaluate(o).reshape(T, N, 1))
+    st.mu.copy_(mu)
+    st.sigma.copy_(sigma)
+    st.actions.copy_(actions)
+    st.actions_log_prob.copy_(logp)
+    st.step = T
+
+
+def _record_update(PPO, ActorCritic, RolloutStorage, *, T, N, O, A, M, E, hidden, policy_kw, ppo_kw, seed,
+                   normalize_in_storage, consistent=False):
+    """Run ONE reference PPO.update() and capture every per-mini-batch loss input/output.
+
+    Captures via (a) a recording ActorCritic subclass (retain_grad on the distribution loc/scale and on
+    the value head output), (b) the multi-GPU hooks: with multi_gpu_cfg world_size=1 the reference calls
+    torch.distributed.all_reduce(kl_mean) and all_reduce(flat_grads) (ppo.py:273, :453); we intercept
+    those calls (identity over one rank) to read kl_mean and the pre-clip flat gradient exactly as the
+    reference computed them.
+    """
+    torch.manual_seed(seed)
+
+    class RecAC(ActorCritic):
+        def update_distribution(self, obs):
+            super().update_distribution(obs)
+            if torch.is_grad_enabled():
+                self.distribution.loc.retain_grad()
+                self.distribution.scale.retain_grad()
+
+        def evaluate(self, obs, **kw):
+            v = super().evaluate(obs, **kw)
+            if torch.is_grad_enabled() and v.requires_grad:
+                v.retain_grad()
+                self._last_v = v
+            return v
+
+    obs0 = {"policy": torch.zeros(N, O)}
+    groups = {"policy": ["policy"], "critic": ["policy"]}
+    pol = RecAC(obs0, groups, A, actor_hidden_dims=hidden, critic_hidden_dims=hidden, **policy_kw)
+    alg = PPO(pol, num_learning_epochs=E, num_mini_batches=M, device="cpu",
+              multi_gpu_cfg={"global_rank": 0, "local_rank": 0, "world_size": 1}, **ppo_kw)
+    alg.init_storage("rl", N, T, obs0, [A])
+    g = torch.Generator().manual_seed(seed + 1)
+    _fill_storage(alg.storage, T, N, A, O, g, policy=pol if consistent else None)
+    last_obs = torch.randn(N, O, generator=g)
+    with torch.inference_mode():
+        alg.compute_returns({"policy": last_obs})
+
+    init_state = {k: f32(v) for k, v in pol.state_dict().items()}
+    st = alg.storage
+    storage_in = {k: f32(getattr(st, k)) for k in ("rewards", "values", "returns", "advantages",
+                                                   "actions_log_prob", "mu", "sigma", "actions")}
+    storage_in["dones"] = st.dones.numpy().copy()
+    storage_in["obs_policy"] = f32(st.observations["policy"])
+
+    records = []
+    reduce_calls = []
+    orig_ar, orig_bc = torch.distributed.all_reduce, torch.distributed.broadcast
+
+    def fake_all_reduce(t, op=None, **kw):
+        reduce_calls.append(t.detach().clone())
+
+    torch.distributed.all_reduce = fake_all_reduce
+    torch.distributed.broadcast = lambda t, src=0, **kw: None
+
+    orig_gen = st.mini_batch_generator
+
+    def rec_gen(m, e):
+        for b in orig_gen(m, e):
+            records.append({"batch": b})
+            yield b
+
+    st.mini_batch_generator = rec_gen
+    orig_clip = torch.nn.utils.clip_grad_norm_
+
+    def rec_clip(params, max_norm, *a, **kw):
+        rec = records[-1]
+        d = pol.distribution
+        rec["mu"] = f32(d.loc)
+        rec["sigma"] = f32(d.scale)
+        rec["dmu"] = f32(d.loc.grad)
+        rec["dsigma"] = f32(d.scale.grad)
+        rec["V"] = f32(pol._last_v)
+        rec["dV"] = f32(pol._last_v.grad)
+        rec["param_grads"] = {n: f32(p.grad) for n, p in pol.named_parameters()}
+        return orig_clip(params, max_norm, *a, **kw)
+
+    torch.nn.utils.clip_grad_norm_ = rec_clip
+    gen_state = torch.default_generator.get_state().numpy().copy()
+    lr_trace = []
+    orig_step = alg.optimizer.step
+
+    def rec_step(*a, **kw):
+        lr_trace.append(alg.optimizer.param_groups[0]["lr"])
+        return orig_step(*a, **kw)
+
+    alg.optimizer.step = rec_step
+    try:
+        loss_dict = alg.update()
+    finally:
+        torch.distributed.all_reduce, torch.distributed.broadcast = orig_ar, orig_bc
+        torch.nn.utils.clip_grad_norm_ = orig_clip
+    kl_calls = [c for c in reduce_calls if c.dim() == 0]
+    grad_calls = [c for c in reduce_calls if c.dim() == 1]
+    adaptive = ppo_kw.get("schedule", "adaptive") == "adaptive" and ppo_kw.get("desired_kl", 0.01) is not None
+    arrays = {}
+    for j, rec in enumerate(records):
+        b = rec["batch"]
+        names = ["actions", "target_values", "advantages", "returns", "old_logp", "old_mu", "old_sigma"]
+        arrays[f"mb{j}/obs"] = f32(b[0]["policy"])
+        for nm, t in zip(names, b[1:8]):
+            arrays[f"mb{j}/{nm}"] = f32(t)
+        for k in ("mu", "sigma", "dmu", "dsigma", "V", "dV"):
+            arrays[f"mb{j}/{k}"] = rec[k]
+        for n_, gr in rec["param_grads"].items():
+            arrays[f"mb{j}/grad/{n_}"] = gr
+        arrays[f"mb{j}/flat_grad"] = f32(grad_calls[j])
+        if adaptive:
+            arrays[f"mb{j}/kl_mean"] = np.float32(kl_calls[j].item())
+    for k, v in init_state.items():
+        arrays[f"init/{k}"] = v
+    for k, v in storage_in.items():
+        arrays[f"storage/{k}"] = v
+    arrays["storage/last_obs"] = f32(last_obs)
+    arrays["gen_state"] = gen_state
+    for k, v in pol.state_dict().items():
+        arrays[f"final/{k}"] = f32(v)
+    meta = dict(T=T, N=N, O=O, A=A, M=M, E=E, hidden=hidden, policy_kw=policy_kw, ppo_kw=ppo_kw,
+                consistent=consistent, multi_gpu_cfg_world_size=1,
+                normalize_in_storage=normalize_in_storage, loss_dict=loss_dict, lr_trace=lr_trace,
+                final_lr=alg.learning_rate, num_batches=len(records), adaptive=adaptive,
+                param_order=[n for n, _ in pol.named_parameters()])
+    return arrays, meta
+
+
+LOSS_CASES = [
+    # name, T, N, O, A, M, E, hidden, policy_kw, ppo_kw[, consistent]
+    ("default_b111", 3, 37, 5, 3, 1, 1, [8], {}, {}),
+    ("tail_drop_m2", 3, 37, 5, 3, 2, 1, [8], {}, {}),
+    ("consistent_m4e2", 8, 64, 6, 4, 4, 2, [16], {}, {}, True),
+    ("consistent_state_dep", 8, 64, 6, 4, 2, 2, [16], {"state_dependent_std": True}, {}, True),
+    ("default_m2e2", 8, 128, 6, 4, 2, 2, [16], {}, {}),
+    ("noclip_value", 4, 50, 5, 3, 1, 1, [8], {}, {"use_clipped_value_loss": False}),
+    ("log_std", 4, 50, 5, 3, 1, 1, [8], {"noise_std_type": "log"}, {}),
+    ("state_dep_scalar", 4, 50, 5, 3, 1, 1, [8], {"state_dependent_std": True}, {}),
+    ("state_dep_log", 4, 50, 5, 3, 1, 1, [8], {"state_dependent_std": True, "noise_std_type": "log"}, {}),
+    ("mb_adv_norm", 4, 64, 5, 3, 2, 1, [8], {}, {"normalize_advantage_per_mini_batch": True}),
+    ("fixed_schedule", 4, 50, 5, 3, 1, 1, [8], {}, {"schedule": "fixed"}),
+    ("a12_b1536", 6, 256, 48, 12, 1, 1, [32], {}, {}),
+    ("hicoef", 4, 50, 5, 3, 1, 1, [8], {}, {"clip_param": 0.1, "value_loss_coef": 0.5,
+                                          "entropy_coef": 0.05}),
+]
+
+
+def make_loss(PPO, ActorCritic, RolloutStorage):
+    meta = {}
+    for i, case in enumerate(LOSS_CASES):
+        name, T, N, O, A, M, E, hidden, pkw, akw = case[:10]
+        consistent = len(case) > 10 and case[10]
+        arrays, m = _record_update(PPO, ActorCritic, RolloutStorage, T=T, N=N, O=O, A=A, M=M, E=E,
+                                   hidden=hidden, policy_kw=pkw, ppo_kw=akw, seed=100 + i,
+                                   normalize_in_storage=not akw.get("normalize_advantage_per_mini_batch", False),
+                                   consistent=consistent)
+        np.savez_compressed(os.path.join(HERE, f"loss_{name}.npz"), **arrays)
+        meta[name] = m
+    return meta
+
+
+def make_update_c1(PPO, ActorCritic, RolloutStorage):
+    """Config C1 (N512 T16 O16 A4, 2x64 ELU, E5 M4): one full update from a rollout-like storage."""
+    arrays, m = _record_update(PPO, ActorCritic, RolloutStorage, T=16, N=512, O=16, A=4, M=4, E=5,
+                               hidden=[64, 64], policy_kw={}, ppo_kw={}, seed=31337,
+                               normalize_in_storage=True, consistent=True)
+    keep = {k: v for k, v in arrays.items() if not k.startswith("mb") or k.endswith("kl_mean")}
+    np.savez_compressed(os.path.join(HERE, "update_c1.npz"), **keep)
+    return m
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reference", default=os.environ.get("RSL_RL_REFERENCE", "/root/reference"))
+    args = ap.parse_args()
+    torch.set_num_threads(4)
+    PPO, ActorCritic, RolloutStorage = import_reference(args.reference)
+    meta = {
+        "generator": "tests/golden/make_golden.py",
+        "reference": "rsl-rl-lib 3.1.0 (kaixi287/rsl_rl snapshot 2025-10-17)",
+        "torch": torch.__version__,
+        "gae": make_gae(RolloutStorage),
+        "perm": make_perm(),
+        "minibatch": make_minibatch(RolloutStorage),
+        "loss": make_loss(PPO, ActorCritic, RolloutStorage),
+        "update_c1": make_update_c1(PPO, ActorCritic, RolloutStorage),
+    }
+    with open(os.path.join(HERE, "golden.json"), "w") as f:
+        json.dump(meta, f, indent=1, sort_keys=True)
+    print("wrote", sorted(os.listdir(HERE)))
+
+
+if __name__ == "__main__":
+    main()
