@@ -1,0 +1,189 @@
+"""PPO env-steps/sec (rollout + GAE + update) on MI355X -- BASELINE.json's headline metric.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...
+
+Workload (config C3, BASELINE.json configs[2]): per GPU N=65536 synthetic envs, T=24 steps/env, obs 48,
+12 actions, actor/critic MLP 3x256 ELU, fp32, PPO defaults (E=5 epochs x M=4 mini-batches, adaptive
+KL lr).  One "step" = one full OnPolicyRunner iteration: T rollout steps + compute_returns + update.
+With N GPUs every rank owns its own 65536-env shard (weak scaling); gradients are averaged with one
+RCCL all-reduce per mini-batch.  `value` = T * N_envs * world / (max over ranks of the timed seconds).
+
+Extra fields: `roofline` for the dominant hot-path kernel (algorithmic bytes / live HIP-event duration
+on its stream, against 8 TB/s), `hot_path` (per-kernel times per iteration), and `cpu_baseline` (the
+oracle's CPU PPO iteration on the box's host cores, rank 0, N=1 only, bounded sample).
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def train_cfg(args):
+    hidden = [args.hidden] * args.layers
+    return {
+        "num_steps_per_env": args.num_steps_per_env,
+        "save_interval": 10**9,
+        "obs_groups": {"policy": ["policy"], "critic": ["policy"]},
+        "policy": {"class_name": "ActorCritic", "activation": "elu", "actor_hidden_dims": hidden,
+                   "critic_hidden_dims": hidden, "init_noise_std": 1.0, "noise_std_type": "scalar",
+                   "actor_obs_normalization": False, "critic_obs_normalization": False},
+        "algorithm": {"class_name": "PPO", "learning_rate": 1e-3, "num_learning_epochs": 5, "num_mini_batches": 4,
+                      "schedule": "adaptive", "value_loss_coef": 1.0, "clip_param": 0.2,
+                      "use_clipped_value_loss": True, "desired_kl": 0.01, "entropy_coef": 0.01, "gamma": 0.99,
+                      "lam": 0.95, "max_grad_norm": 1.0, "normalize_advantage_per_mini_batch": False},
+    }
+
+
+def cpu_baseline(args):
+    from oracle import cpu_ppo
+
+    threads = min(16, len(os.sched_getaffinity(0)))
+    n = args.cpu_sample_envs
+    rate, secs = cpu_ppo.time_iterations(n, args.num_obs, args.num_actions, T=args.num_steps_per_env, iters=1,
+                                         warmup=1, threads=threads)
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), "")
+    except OSError:
+        pass
+    return {
+        "value": round(rate, 1),
+        "unit": "env-steps/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"1 timed PPO iteration (+1 warmup) of the CPU oracle (oracle/cpu_ppo.py: torch-CPU MLPs + "
+                  f"oracle GAE/randperm/gather/loss) at N={n} envs, T={args.num_steps_per_env}, obs {args.num_obs}, "
+                  f"act {args.num_actions}, 3x256 MLP; {secs:.1f} s timed; {threads} threads; CPU: {model}",
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--num-envs", type=int, default=65536, help="environments per GPU")
+    ap.add_argument("--num-steps-per-env", type=int, default=24)
+    ap.add_argument("--num-obs", type=int, default=48)
+    ap.add_argument("--num-actions", type=int, default=12)
+    ap.add_argument("--hidden", type=int, default=256)
+    ap.add_argument("--layers", type=int, default=3)
+    ap.add_argument("--cpu-sample-envs", type=int, default=8192)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 through torch.distributed.run")
+    torch.cuda.set_device(local_rank)
+    device = f"cuda:{local_rank}"
+
+    from rsl_rl_amd import kernels
+    from rsl_rl_amd.env import SyntheticVecEnv
+    from rsl_rl_amd.runners import OnPolicyRunner
+
+    torch.manual_seed(1)  # policy init; the env stream is seeded per rank
+    env = SyntheticVecEnv(args.num_envs, args.num_obs, args.num_actions, device=device, seed=rank)
+    runner = OnPolicyRunner(env, train_cfg(args), log_dir=None, device=device)  # inits RCCL when world > 1
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    runner.learn(args.warmup)
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    kernels.timer.reset()
+    kernels.timer.enabled = True
+    t0 = time.perf_counter()
+    runner.learn(args.steps)
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kernels.timer.enabled = False
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+
+    T, N, K = args.num_steps_per_env, args.num_envs, args.steps
+    value = T * N * world * K / elapsed
+    prof = kernels.timer.summary()
+    hot = {}
+    for name, s in prof.items():
+        hot[name] = {
+            "launches_per_step": s["launches"] / K,
+            "mean_us": round(s["mean_ms"] * 1e3, 2),
+            "ms_per_step": round(s["total_ms"] / K, 4),
+            "algorithmic_bytes_per_launch": int(s["bytes_per_launch"]),
+            "achieved_GBps": round(s["bytes_per_launch"] / (s["mean_ms"] * 1e-3) / 1e9, 1),
+        }
+    hot_ms = sum(h["ms_per_step"] for h in hot.values())
+    dominant = max(hot, key=lambda k: hot[k]["ms_per_step"]) if hot else None
+    roofline = None
+    if dominant:
+        ach = hot[dominant]["achieved_GBps"]
+        roofline = {"kernel": dominant, "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                    "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": None,
+                    "algorithmic_bytes_per_launch": hot[dominant]["algorithmic_bytes_per_launch"],
+                    "mean_launch_us": hot[dominant]["mean_us"]}
+
+    out = {
+        "metric": "PPO env-steps/sec (rollout+GAE+update) at N=65536 envs, 1->8 MI355X",
+        "value": round(value, 1),
+        "unit": "env-steps/s",
+        "n_gpus": world,
+        "steps": K,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / K * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic (SyntheticVecEnv: obs/reward ~ N(0,1), dones ~ Bernoulli(0.02); random-init weights)",
+        "config": {
+            "workload": f"C3: {N} envs/GPU x T={T}, obs {args.num_obs}, act {args.num_actions}, "
+                        f"actor+critic MLP {args.layers}x{args.hidden} ELU, PPO E=5 M=4 adaptive-KL; "
+                        f"one step = rollout + GAE + update",
+            "num_envs_per_gpu": N,
+            "global_num_envs": N * world,
+            "num_steps_per_env": T,
+            "mini_batch_rows": N * T // 4,
+            "parallelism": f"dp{world} (env shards, RCCL grad all-reduce per mini-batch)",
+        },
+        "roofline": roofline,
+        "hot_path": {"kernels": hot, "ms_per_step": round(hot_ms, 4),
+                     "env_steps_per_s": round(T * N / (hot_ms * 1e-3), 1) if hot_ms else None},
+        "phases_last_iter": {k: round(v, 4) for k, v in runner.last_iteration_stats.items() if k != "loss_dict"},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,148 @@
+/*
+ * rslrl_amd.h -- C ABI of the MI355X (gfx950) PPO hot-path library  librslrl_amd.so
+ *
+ * The reference (kaixi287/rsl_rl, rsl-rl-lib 3.1.0) is pure Python/PyTorch and has no FFI; each
+ * entry point below replaces one group of ATen ops on the PPO hot path, named by the reference
+ * file:line it takes over.  The Python host side (rsl_rl_amd/_lib.py) binds these with ctypes and is
+ * what RolloutStorage / PPO call; INTEGRATION.md shows the binding.
+ *
+ * Conventions
+ *   - Plain pointers and sizes only.  Device pointers are HIP device memory (e.g. torch CUDA/HIP
+ *     tensors' data_ptr()); "host" marks host memory.  `stream` is a hipStream_t (NULL = legacy
+ *     default stream); every device call is stream-ordered, never synchronises the host and
+ *     allocates nothing (capturable into a hipGraph).  Workspaces are caller-owned, sized by the
+ *     matching *_workspace_bytes() query.
+ *   - Return value: 0 = success; < 0 = rslrl argument error (RSLRL_E_*); > 0 = hipError_t of the
+ *     failed launch.  rslrl_status_string() describes a code.  No exceptions cross the ABI.
+ *   - Layouts follow the reference buffers (rollout_storage.py:47-68): [T, N, ...] row-major fp32,
+ *     dones uint8; flat row index = t * N + n (flatten(0, 1), rollout_storage.py:168-177).
+ *   - Determinism: every reduction uses a fixed partition and a fixed combine order, so results are
+ *     bitwise identical run to run for the same inputs and sizes.
+ */
+#ifndef RSLRL_AMD_H_
+#define RSLRL_AMD_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ihipStream_t* rslrl_stream_t; /* == hipStream_t */
+
+#define RSLRL_ABI_VERSION 1
+
+enum {
+    RSLRL_OK = 0,
+    RSLRL_E_INVALID_ARGUMENT = -1,
+    RSLRL_E_WORKSPACE_TOO_SMALL = -2,
+    RSLRL_E_UNSUPPORTED = -3,
+    RSLRL_E_MISALIGNED = -4,
+    RSLRL_E_BAD_GENERATOR_STATE = -5,
+};
+
+int rslrl_abi_version(void);
+const char* rslrl_status_string(int status);
+
+/* ------------------------------------------------------------------------------------------------
+ * RolloutStorage.compute_returns(last_values, gamma, lam, normalize_advantage)
+ *   replaces rsl_rl/storage/rollout_storage.py:127-149 (GAE reverse scan :128-142, advantages
+ *   :145, normalisation :148-149).
+ * values, rewards: [T, N] fp32; dones: [T, N] uint8; last_values: [N] fp32 (device).
+ * returns, advantages: [T, N] fp32 outputs (device).  returns and the un-normalised advantages are
+ * bit-identical to the reference's fp32 evaluation; with normalize_advantage the advantages are
+ * (adv - mean) / (std_unbiased + 1e-8) over all T*N elements (statistics accumulated in fp64).
+ * ----------------------------------------------------------------------------------------------*/
+size_t rslrl_compute_returns_workspace_bytes(int64_t T, int64_t N);
+int rslrl_compute_returns(const float* values, const float* rewards, const uint8_t* dones,
+                          const float* last_values, float gamma, float lam, int64_t T, int64_t N,
+                          int32_t normalize_advantage, float* returns, float* advantages,
+                          void* workspace, size_t workspace_bytes, rslrl_stream_t stream);
+
+/* Advantage statistics + in-place normalisation of an arbitrary fp32 vector (the normalisation half
+ * of rollout_storage.py:148-149; ppo.py:221-223 uses the same expression per mini-batch).          */
+size_t rslrl_normalize_workspace_bytes(int64_t n);
+int rslrl_normalize_advantages(float* advantages, int64_t n, float eps, void* workspace,
+                               size_t workspace_bytes, rslrl_stream_t stream);
+
+/* ------------------------------------------------------------------------------------------------
+ * torch.randperm(n) on a CPU generator -- rollout_storage.py:165.  HOST code.
+ * state: the torch CPU generator state blob (torch.Generator.get_state(), 5056 bytes, host); it is
+ * read and advanced in place exactly as torch's randperm_cpu advances it, so the caller writes it
+ * back with Generator.set_state().  out: host int32 [n].  Requires 0 <= n < 2^31.
+ * ----------------------------------------------------------------------------------------------*/
+int rslrl_randperm_mt19937(uint8_t* state, size_t state_bytes, int64_t n, int32_t* out);
+
+/* ------------------------------------------------------------------------------------------------
+ * Multi-field row gather -- rollout_storage.py:168-197 (`field.flatten(0,1)[batch_idx]` for every
+ * field of the mini-batch in one launch).  dst[r] = src[indices[r]] row by row for each field.
+ * row_bytes must be a multiple of 4; rows with row_bytes % 16 == 0 and 16-byte aligned pointers
+ * move in 16-byte units.  indices: device int32 [num_rows], each in [0, rows of src).
+ * ----------------------------------------------------------------------------------------------*/
+#define RSLRL_MAX_GATHER_FIELDS 16
+typedef struct {
+    const void* src; /* device, [rows, row_bytes] */
+    void* dst;       /* device, [num_rows, row_bytes] */
+    int64_t row_bytes;
+} rslrl_gather_field_t;
+
+int rslrl_gather_rows(const rslrl_gather_field_t* fields /* host array */, int32_t num_fields,
+                      const int32_t* indices, int64_t num_rows, rslrl_stream_t stream);
+
+/* ------------------------------------------------------------------------------------------------
+ * Fused PPO loss forward + backward for one mini-batch -- rsl_rl/algorithms/ppo.py:221-223
+ * (optional per-mini-batch advantage normalisation), :259-269 (KL), :297-302 (clipped surrogate),
+ * :305-313 (clipped value loss), :315 (total), and autograd's backward of :368 down to the policy
+ * outputs (the Normal log_prob / entropy of actor_critic.py:106-171 included).
+ *
+ * Inputs, all device fp32, B rows:
+ *   mu [B, A] (row stride mu_stride elements)   sigma: sigma_mode 0 -> [A] shared by all rows;
+ *   values V [B]                                         sigma_mode 1 -> [B, A] (row stride sigma_stride)
+ *   actions, old_mu, old_sigma [B, A] contiguous; old_logp, advantages, target_values, returns [B]
+ * Outputs:
+ *   grad_mu [B, A] (row stride grad_mu_stride); grad_sigma: mode 0 -> [A] (summed over rows),
+ *   mode 1 -> [B, A] (row stride grad_sigma_stride); grad_values [B]; all are d(loss)/d(input) for
+ *   a unit upstream gradient.
+ *   stats [8] fp32: loss, surrogate_loss, value_loss, entropy_mean, kl_mean, adv_mean, adv_std, 0.
+ * ----------------------------------------------------------------------------------------------*/
+typedef struct {
+    int64_t B;
+    int32_t A;
+    int32_t sigma_mode; /* 0: shared [A]; 1: per-row [B, A] */
+    const float* mu;
+    int64_t mu_stride;
+    const float* sigma;
+    int64_t sigma_stride;
+    const float* values;
+    const float* actions;
+    const float* old_logp;
+    const float* advantages;
+    const float* target_values;
+    const float* returns;
+    const float* old_mu;
+    const float* old_sigma;
+    float clip_param;
+    float value_loss_coef;
+    float entropy_coef;
+    int32_t use_clipped_value_loss;
+    int32_t compute_kl;
+    int32_t normalize_advantage; /* ppo.py:221-223 */
+    float* grad_mu;
+    int64_t grad_mu_stride;
+    float* grad_sigma;
+    int64_t grad_sigma_stride;
+    float* grad_values;
+    float* stats;
+} rslrl_ppo_loss_args_t;
+
+#define RSLRL_PPO_LOSS_MAX_ACTIONS 64
+size_t rslrl_ppo_loss_workspace_bytes(int64_t B, int32_t A);
+int rslrl_ppo_loss_fwd_bwd(const rslrl_ppo_loss_args_t* args /* host struct */, void* workspace,
+                           size_t workspace_bytes, rslrl_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RSLRL_AMD_H_ */

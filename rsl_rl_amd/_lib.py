@@ -1,0 +1,138 @@
+"""ctypes binding of librslrl_amd.so (the C ABI declared in include/rslrl_amd.h).
+
+The library is built in-tree (rsl_rl_amd/csrc/Makefile -> rsl_rl_amd/lib/librslrl_amd.so).  torch is
+imported first so that the HIP runtime torch ships (libamdhip64.so.7) is the one the library binds to:
+the dynamic loader resolves our DT_NEEDED by soname to the already-loaded copy, so torch's streams and
+device pointers are valid in both.
+
+There is no fallback: if the library is missing the hot path raises HipLibraryMissing.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
+
+LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
+LIB_PATH = os.path.join(LIB_DIR, "librslrl_amd.so")
+ABI_VERSION = 1
+
+# symbols declared in include/rslrl_amd.h (tests/test_capi.py checks the header against this list)
+EXPORTED_SYMBOLS = (
+    "rslrl_abi_version",
+    "rslrl_status_string",
+    "rslrl_compute_returns_workspace_bytes",
+    "rslrl_compute_returns",
+    "rslrl_normalize_workspace_bytes",
+    "rslrl_normalize_advantages",
+    "rslrl_randperm_mt19937",
+    "rslrl_gather_rows",
+    "rslrl_ppo_loss_workspace_bytes",
+    "rslrl_ppo_loss_fwd_bwd",
+)
+
+MAX_GATHER_FIELDS = 16
+PPO_LOSS_MAX_ACTIONS = 64
+
+
+class HipLibraryMissing(RuntimeError):
+    pass
+
+
+class RslrlError(RuntimeError):
+    pass
+
+
+class GatherField(ctypes.Structure):
+    _fields_ = [("src", ctypes.c_void_p), ("dst", ctypes.c_void_p), ("row_bytes", ctypes.c_int64)]
+
+
+class PPOLossArgs(ctypes.Structure):
+    _fields_ = [
+        ("B", ctypes.c_int64),
+        ("A", ctypes.c_int32),
+        ("sigma_mode", ctypes.c_int32),
+        ("mu", ctypes.c_void_p),
+        ("mu_stride", ctypes.c_int64),
+        ("sigma", ctypes.c_void_p),
+        ("sigma_stride", ctypes.c_int64),
+        ("values", ctypes.c_void_p),
+        ("actions", ctypes.c_void_p),
+        ("old_logp", ctypes.c_void_p),
+        ("advantages", ctypes.c_void_p),
+        ("target_values", ctypes.c_void_p),
+        ("returns", ctypes.c_void_p),
+        ("old_mu", ctypes.c_void_p),
+        ("old_sigma", ctypes.c_void_p),
+        ("clip_param", ctypes.c_float),
+        ("value_loss_coef", ctypes.c_float),
+        ("entropy_coef", ctypes.c_float),
+        ("use_clipped_value_loss", ctypes.c_int32),
+        ("compute_kl", ctypes.c_int32),
+        ("normalize_advantage", ctypes.c_int32),
+        ("grad_mu", ctypes.c_void_p),
+        ("grad_mu_stride", ctypes.c_int64),
+        ("grad_sigma", ctypes.c_void_p),
+        ("grad_sigma_stride", ctypes.c_int64),
+        ("grad_values", ctypes.c_void_p),
+        ("stats", ctypes.c_void_p),
+    ]
+
+
+_lib = None
+_lock = threading.Lock()
+
+
+def _declare(L):
+    P, I32, I64, F, SZ = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_size_t
+    L.rslrl_abi_version.restype = ctypes.c_int
+    L.rslrl_abi_version.argtypes = []
+    L.rslrl_status_string.restype = ctypes.c_char_p
+    L.rslrl_status_string.argtypes = [ctypes.c_int]
+    L.rslrl_compute_returns_workspace_bytes.restype = SZ
+    L.rslrl_compute_returns_workspace_bytes.argtypes = [I64, I64]
+    L.rslrl_compute_returns.restype = ctypes.c_int
+    L.rslrl_compute_returns.argtypes = [P, P, P, P, F, F, I64, I64, I32, P, P, P, SZ, P]
+    L.rslrl_normalize_workspace_bytes.restype = SZ
+    L.rslrl_normalize_workspace_bytes.argtypes = [I64]
+    L.rslrl_normalize_advantages.restype = ctypes.c_int
+    L.rslrl_normalize_advantages.argtypes = [P, I64, F, P, SZ, P]
+    L.rslrl_randperm_mt19937.restype = ctypes.c_int
+    L.rslrl_randperm_mt19937.argtypes = [P, SZ, I64, P]
+    L.rslrl_gather_rows.restype = ctypes.c_int
+    L.rslrl_gather_rows.argtypes = [ctypes.POINTER(GatherField), I32, P, I64, P]
+    L.rslrl_ppo_loss_workspace_bytes.restype = SZ
+    L.rslrl_ppo_loss_workspace_bytes.argtypes = [I64, I32]
+    L.rslrl_ppo_loss_fwd_bwd.restype = ctypes.c_int
+    L.rslrl_ppo_loss_fwd_bwd.argtypes = [ctypes.POINTER(PPOLossArgs), P, SZ, P]
+
+
+def lib():
+    """Load (once) and return the ctypes handle; raises HipLibraryMissing if the .so is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise HipLibraryMissing(
+                    f"{LIB_PATH} not found: build it with `make -C rsl_rl_amd/csrc` (or "
+                    "`python -c 'import __graft_entry__ as g; g.build()'`). The rsl_rl_amd hot path has "
+                    "no CPU fallback."
+                )
+            L = ctypes.CDLL(LIB_PATH)
+            _declare(L)
+            v = L.rslrl_abi_version()
+            if v != ABI_VERSION:
+                raise HipLibraryMissing(f"{LIB_PATH} has ABI version {v}, expected {ABI_VERSION}; rebuild it")
+            _lib = L
+    return _lib
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = lib().rslrl_status_string(rc)
+        raise RslrlError(f"{what} failed with status {rc}: {msg.decode() if msg else '?'}")

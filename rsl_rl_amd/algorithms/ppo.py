@@ -1,0 +1,335 @@
+"""PPO with the fused HIP loss (rsl_rl/algorithms/ppo.py:19-469).
+
+Constructor, attributes (policy, optimizer, storage, learning_rate, rnd, rnd_optimizer, transition,
+intrinsic_rewards, ...) and methods (init_storage, act, process_env_step, compute_returns, update,
+broadcast_parameters, reduce_parameters) keep the reference's signatures and semantics.  The update
+differs in how each mini-batch is evaluated:
+
+* the actor forward yields (mean, sigma) directly (ActorCritic.action_distribution_params) and the
+  critic yields V; one fused kernel (rsl_rl_amd.kernels.ppo_loss_fwd_bwd) computes the KL, the clipped
+  surrogate, the clipped value loss, the entropy and the exact gradients d(loss)/d(mean, sigma, V);
+  `torch.autograd.backward` then pushes those through the two MLPs (PyTorch-ROCm GEMMs);
+* per-parameter gradients are views of one flat buffer, so the multi-GPU average is a single RCCL
+  all-reduce of that buffer with no cat / copy-back (ppo.py:441-469);
+* the KL is the only value read back per mini-batch (it drives the learning-rate rule, which must run
+  before the optimizer step, as in the reference); the loss statistics stay on the device until the
+  end of update().
+
+Multi-GPU LR rule: the reference all-reduces kl_mean, lets rank 0 decide, broadcasts the lr as an fp32
+tensor and reads it back (ppo.py:272-290).  After the all-reduce every rank holds the same kl_mean, so
+each rank applies the same rule locally and rounds the lr through fp32 exactly like the broadcast did:
+same learning rates on every rank, one collective fewer per mini-batch.
+"""
+
+from __future__ import annotations
+
+from itertools import chain
+
+import torch
+import torch.nn as nn
+import torch.optim as optim
+
+from .. import kernels
+from ..modules import ActorCritic
+from ..modules.rnd import RandomNetworkDistillation
+from ..storage import RolloutStorage
+from ..utils import string_to_callable
+
+
+def adapt_learning_rate(learning_rate: float, kl_mean: float, desired_kl: float) -> float:
+    """The adaptive schedule of ppo.py:280-284."""
+    if kl_mean > desired_kl * 2.0:
+        return max(1e-5, learning_rate / 1.5)
+    if kl_mean < desired_kl / 2.0 and kl_mean > 0.0:
+        return min(1e-2, learning_rate * 1.5)
+    return learning_rate
+
+
+class PPO:
+    """Proximal Policy Optimization algorithm (https://arxiv.org/abs/1707.06347)."""
+
+    policy: ActorCritic
+
+    def __init__(
+        self,
+        policy,
+        num_learning_epochs=5,
+        num_mini_batches=4,
+        clip_param=0.2,
+        gamma=0.99,
+        lam=0.95,
+        value_loss_coef=1.0,
+        entropy_coef=0.01,
+        learning_rate=0.001,
+        max_grad_norm=1.0,
+        use_clipped_value_loss=True,
+        schedule="adaptive",
+        desired_kl=0.01,
+        device="cpu",
+        normalize_advantage_per_mini_batch=False,
+        rnd_cfg: dict | None = None,
+        symmetry_cfg: dict | None = None,
+        multi_gpu_cfg: dict | None = None,
+    ):
+        self.device = device
+        self.is_multi_gpu = multi_gpu_cfg is not None
+        if multi_gpu_cfg is not None:
+            self.gpu_global_rank = multi_gpu_cfg["global_rank"]
+            self.gpu_world_size = multi_gpu_cfg["world_size"]
+        else:
+            self.gpu_global_rank = 0
+            self.gpu_world_size = 1
+
+        if rnd_cfg is not None:
+            rnd_lr = rnd_cfg.pop("learning_rate", 1e-3)
+            self.rnd = RandomNetworkDistillation(device=self.device, **rnd_cfg)
+            self.rnd_optimizer = optim.Adam(self.rnd.predictor.parameters(), lr=rnd_lr)
+        else:
+            self.rnd = None
+            self.rnd_optimizer = None
+        self.intrinsic_rewards = None
+
+        if symmetry_cfg is not None:
+            use_symmetry = symmetry_cfg["use_data_augmentation"] or symmetry_cfg["use_mirror_loss"]
+            if not use_symmetry:
+                print("Symmetry not used for learning. We will use it for logging instead.")
+            if isinstance(symmetry_cfg["data_augmentation_func"], str):
+                symmetry_cfg["data_augmentation_func"] = string_to_callable(symmetry_cfg["data_augmentation_func"])
+            if symmetry_cfg["use_data_augmentation"] and not callable(symmetry_cfg["data_augmentation_func"]):
+                raise ValueError(
+                    "Data augmentation enabled but the function is not callable:"
+                    f" {symmetry_cfg['data_augmentation_func']}"
+                )
+            self.symmetry = symmetry_cfg
+        else:
+            self.symmetry = None
+
+        self.policy = policy
+        self.policy.to(self.device)
+        self.optimizer = optim.Adam(self.policy.parameters(), lr=learning_rate)
+        self.storage: RolloutStorage = None  # type: ignore
+        self.transition = RolloutStorage.Transition()
+
+        self.clip_param = clip_param
+        self.num_learning_epochs = num_learning_epochs
+        self.num_mini_batches = num_mini_batches
+        self.value_loss_coef = value_loss_coef
+        self.entropy_coef = entropy_coef
+        self.gamma = gamma
+        self.lam = lam
+        self.max_grad_norm = max_grad_norm
+        self.use_clipped_value_loss = use_clipped_value_loss
+        self.desired_kl = desired_kl
+        self.schedule = schedule
+        self.learning_rate = learning_rate
+        self.normalize_advantage_per_mini_batch = normalize_advantage_per_mini_batch
+
+        self._flat_grad = None  # one buffer backing every trainable parameter's .grad (see reduce_parameters)
+        self._flat_views = None
+
+    def init_storage(self, training_type, num_envs, num_transitions_per_env, obs, actions_shape):
+        self.storage = RolloutStorage(training_type, num_envs, num_transitions_per_env, obs, actions_shape,
+                                      self.device)
+
+    # ------------------------------------------------------------------ rollout (ppo.py:129-169)
+    def act(self, obs):
+        if self.policy.is_recurrent:
+            self.transition.hidden_states = self.policy.get_hidden_states()
+        self.transition.actions = self.policy.act(obs).detach()
+        self.transition.values = self.policy.evaluate(obs).detach()
+        self.transition.actions_log_prob = self.policy.get_actions_log_prob(self.transition.actions).detach()
+        self.transition.action_mean = self.policy.action_mean.detach()
+        self.transition.action_sigma = self.policy.action_std.detach()
+        self.transition.observations = obs
+        return self.transition.actions
+
+    def process_env_step(self, obs, rewards, dones, extras):
+        self.policy.update_normalization(obs)
+        if self.rnd:
+            self.rnd.update_normalization(obs)
+        self.transition.rewards = rewards.clone()
+        self.transition.dones = dones
+        if self.rnd:
+            self.intrinsic_rewards = self.rnd.get_intrinsic_reward(obs)
+            self.transition.rewards += self.intrinsic_rewards
+        if "time_outs" in extras:  # bootstrap on time-outs (ppo.py:161-164)
+            self.transition.rewards += self.gamma * torch.squeeze(
+                self.transition.values * extras["time_outs"].unsqueeze(1).to(self.device), 1
+            )
+        self.storage.add_transitions(self.transition)
+        self.transition.clear()
+        self.policy.reset(dones)
+
+    def compute_returns(self, obs):
+        last_values = self.policy.evaluate(obs).detach()
+        self.storage.compute_returns(last_values, self.gamma, self.lam,
+                                     normalize_advantage=not self.normalize_advantage_per_mini_batch)
+
+    # ------------------------------------------------------------------ update (ppo.py:178-422)
+    def _trainable_params(self):
+        params = list(self.policy.parameters())
+        if self.rnd:  # only the predictor receives gradients (the target output is detached)
+            params += list(self.rnd.predictor.parameters())
+        return [p for p in params if p.requires_grad]
+
+    def _bind_flat_grads(self):
+        """Make every trainable parameter's .grad a view of one contiguous fp32 buffer, zeroed.
+
+        Order = policy.parameters() then rnd.parameters(), the concatenation order of ppo.py:447-450."""
+        params = self._trainable_params()
+        total = sum(p.numel() for p in params)
+        flat = self._flat_grad
+        if flat is None or flat.numel() != total or flat.device != params[0].device:
+            flat = torch.zeros(total, dtype=torch.float32, device=params[0].device)
+            self._flat_grad = flat
+            self._flat_views = None
+        else:
+            flat.zero_()
+        if self._flat_views is None:
+            views, off = [], 0
+            for p in params:
+                views.append(flat[off:off + p.numel()].view_as(p))
+                off += p.numel()
+            self._flat_views = views
+        for p, v in zip(params, self._flat_views):
+            if p.grad is None or p.grad.data_ptr() != v.data_ptr():
+                p.grad = v
+
+    def _sync_kl_and_lr(self, kl_mean: torch.Tensor):
+        """KL all-reduce + adaptive lr + fp32 lr rounding under multi-GPU (ppo.py:271-294)."""
+        if self.is_multi_gpu:
+            torch.distributed.all_reduce(kl_mean, op=torch.distributed.ReduceOp.SUM)
+            kl_mean /= self.gpu_world_size
+        kl = kl_mean.item()
+        self.learning_rate = adapt_learning_rate(self.learning_rate, kl, self.desired_kl)
+        if self.is_multi_gpu:
+            self.learning_rate = torch.tensor(self.learning_rate, dtype=torch.float32).item()
+        for param_group in self.optimizer.param_groups:
+            param_group["lr"] = self.learning_rate
+        return kl
+
+    def update(self):  # noqa: C901
+        if self.symmetry:
+            raise NotImplementedError(
+                "symmetry augmentation / mirror loss (ppo.py:226-244, :318-348) is outside the MI355X PPO "
+                "hot-path scope (SURVEY.md §2)"
+            )
+        if self.policy.is_recurrent:
+            raise NotImplementedError("recurrent policies are outside the MI355X PPO hot-path scope (SURVEY.md §2)")
+        fused_policy = hasattr(self.policy, "action_distribution_params")
+        adaptive = self.desired_kl is not None and self.schedule == "adaptive"
+        dev = self.storage.values.device
+        sums = torch.zeros(4, dtype=torch.float64, device=dev)  # value, surrogate, entropy, rnd
+        stats_buf = torch.empty(8, dtype=torch.float32, device=dev)
+
+        generator = self.storage.mini_batch_generator(self.num_mini_batches, self.num_learning_epochs)
+        for (
+            obs_batch,
+            actions_batch,
+            target_values_batch,
+            advantages_batch,
+            returns_batch,
+            old_actions_log_prob_batch,
+            old_mu_batch,
+            old_sigma_batch,
+            hid_states_batch,
+            masks_batch,
+        ) in generator:
+            # actor / critic forward (PyTorch-ROCm MLPs)
+            if fused_policy:
+                mean, sigma = self.policy.action_distribution_params(obs_batch)
+            else:
+                self.policy.act(obs_batch, masks=masks_batch, hidden_states=hid_states_batch[0])
+                mean, sigma = self.policy.action_mean, self.policy.action_std
+            value_batch = self.policy.evaluate(obs_batch, masks=masks_batch, hidden_states=hid_states_batch[1])
+
+            # fused loss forward + backward to (mean, sigma, V)  (ppo.py:221-223, :259-315)
+            stats, g_mean, g_sigma, g_value = kernels.ppo_loss_fwd_bwd(
+                mean, sigma, value_batch, actions_batch, old_actions_log_prob_batch, advantages_batch,
+                target_values_batch, returns_batch, old_mu_batch, old_sigma_batch,
+                clip_param=self.clip_param, value_loss_coef=self.value_loss_coef, entropy_coef=self.entropy_coef,
+                use_clipped_value_loss=self.use_clipped_value_loss, compute_kl=adaptive,
+                normalize_advantage=self.normalize_advantage_per_mini_batch, stats=stats_buf,
+            )
+            if adaptive:
+                self._sync_kl_and_lr(stats[kernels.STATS_KL:kernels.STATS_KL + 1].clone())
+
+            # RND loss (ppo.py:352-363)
+            if self.rnd:
+                with torch.no_grad():
+                    rnd_state_batch = self.rnd.get_rnd_state(obs_batch)
+                    rnd_state_batch = self.rnd.state_normalizer(rnd_state_batch)
+                predicted_embedding = self.rnd.predictor(rnd_state_batch)
+                target_embedding = self.rnd.target(rnd_state_batch).detach()
+                rnd_loss = nn.functional.mse_loss(predicted_embedding, target_embedding)
+
+            # backward through the MLPs (ppo.py:367-372) into the flat gradient buffer
+            self._bind_flat_grads()
+            outs, grads = [mean, value_batch], [g_mean, g_value]
+            if sigma.requires_grad:
+                outs.append(sigma)
+                grads.append(g_sigma)
+            torch.autograd.backward(outs, grads)
+            if self.rnd:
+                rnd_loss.backward()
+
+            if self.is_multi_gpu:
+                self.reduce_parameters()
+
+            nn.utils.clip_grad_norm_(self.policy.parameters(), self.max_grad_norm)
+            self.optimizer.step()
+            if self.rnd_optimizer:
+                self.rnd_optimizer.step()
+
+            # loss statistics stay on the device (ppo.py:387-395)
+            sums[0:3] += stats[[kernels.STATS_VALUE, kernels.STATS_SURROGATE, kernels.STATS_ENTROPY]].double()
+            if self.rnd:
+                sums[3] += rnd_loss.detach().double()
+
+        num_updates = self.num_learning_epochs * self.num_mini_batches
+        host = (sums / num_updates).tolist()
+        self.storage.clear()
+        loss_dict = {"value_function": host[0], "surrogate": host[1], "entropy": host[2]}
+        if self.rnd:
+            loss_dict["rnd"] = host[3]
+        return loss_dict
+
+    # ------------------------------------------------------------------ multi-GPU (ppo.py:428-469)
+    def broadcast_parameters(self):
+        """Broadcast model parameters from rank 0 to all ranks."""
+        model_params = [self.policy.state_dict()]
+        if self.rnd:
+            model_params.append(self.rnd.predictor.state_dict())
+        torch.distributed.broadcast_object_list(model_params, src=0)
+        self.policy.load_state_dict(model_params[0])
+        if self.rnd:
+            self.rnd.predictor.load_state_dict(model_params[1])
+
+    def reduce_parameters(self):
+        """Average gradients across ranks: SUM all-reduce then / world_size (ppo.py:441-469).
+
+        When the gradients are views of the flat buffer (always, inside update()) this is one collective
+        on that buffer; otherwise the reference's cat / all-reduce / copy-back is used."""
+        params = self._trainable_params()
+        flat = self._flat_grad
+        if flat is not None and self._flat_views is not None and all(
+            p.grad is not None and p.grad.data_ptr() == v.data_ptr() for p, v in zip(params, self._flat_views)
+        ):
+            torch.distributed.all_reduce(flat, op=torch.distributed.ReduceOp.SUM)
+            flat /= self.gpu_world_size
+            return
+        grads = [p.grad.view(-1) for p in self.policy.parameters() if p.grad is not None]
+        if self.rnd:
+            grads += [p.grad.view(-1) for p in self.rnd.parameters() if p.grad is not None]
+        all_grads = torch.cat(grads)
+        torch.distributed.all_reduce(all_grads, op=torch.distributed.ReduceOp.SUM)
+        all_grads /= self.gpu_world_size
+        all_params = self.policy.parameters()
+        if self.rnd:
+            all_params = chain(all_params, self.rnd.parameters())
+        offset = 0
+        for p in all_params:
+            if p.grad is not None:
+                n = p.numel()
+                p.grad.data.copy_(all_grads[offset:offset + n].view_as(p.grad.data))
+                offset += n

@@ -1,0 +1,236 @@
+// GAE reverse scan + advantage normalisation on gfx950.
+//
+// Replaces rsl_rl/storage/rollout_storage.py:127-149 (RolloutStorage.compute_returns): the reference
+// runs a Python loop over T steps of ~13 ATen kernels each on [N, 1] slabs (~320 launches), then a
+// global mean/std.  Here:
+//   gae_scan_kernel   one lane per environment walks t = T-1 .. 0 (the recurrence is serial in t and
+//                     independent across envs).  All T (value, reward, done) loads of a lane are issued
+//                     before the recurrence (TMAX-unrolled register arrays), so the wave has 3*T
+//                     coalesced loads in flight; writes returns and raw advantages and emits one fp64
+//                     (sum, sum of squares) partial per block for the normalisation.
+//   adv_normalize     every block folds the <= kMaxPartials partials in one fixed order (so all blocks
+//                     agree bitwise), then rescales the advantages with 16-byte accesses.
+// Bytes per element (T*N of them): read 4 (V) + 4 (R) + 1 (done), write 4 (returns) + 4 (adv) = 17 in
+// the scan; read 4 + write 4 = 8 in the normaliser.
+//
+// Bit-exactness: every fp32 operation of the reference expression is issued separately with
+// round-to-nearest intrinsics in the reference's evaluation order (Python left-to-right:
+// (nnt*gamma)*next_v, ((nnt*gamma)*lam)*adv), and advantages = returns - values exactly as :145.
+
+#include "common.h"
+
+namespace rslrl {
+namespace {
+
+constexpr int kMaxPartials = 512;
+
+struct GaeStep {
+    // One reverse step of rollout_storage.py:136-142; returns the new advantage.
+    static __device__ __forceinline__ float step(float v, float r, unsigned d, float next_v, float adv,
+                                                 float gamma, float lam) {
+        const float nnt = __fsub_rn(1.0f, static_cast<float>(d));          // :136
+        const float a = __fmul_rn(nnt, gamma);
+        const float delta = __fsub_rn(__fadd_rn(r, __fmul_rn(a, next_v)), v);  // :138
+        const float g = __fmul_rn(__fmul_rn(nnt, gamma), lam);
+        return __fadd_rn(delta, __fmul_rn(g, adv));                      // :140
+    }
+};
+
+template <int TMAX>
+__global__ __launch_bounds__(kBlock) void gae_scan_kernel(
+    const float* __restrict__ values, const float* __restrict__ rewards, const uint8_t* __restrict__ dones,
+    const float* __restrict__ last_values, float gamma, float lam, int T, int64_t N,
+    float* __restrict__ returns, float* __restrict__ advantages, double2* __restrict__ partials) {
+    __shared__ double scratch[2][kBlock / kWave];
+    double s = 0.0, ss = 0.0;
+    const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
+    for (int64_t n = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; n < N; n += stride) {
+        if constexpr (TMAX > 0) {
+            float v[TMAX], r[TMAX];
+            unsigned d[TMAX];
+#pragma unroll
+            for (int t = 0; t < TMAX; ++t) {
+                if (t < T) {
+                    const int64_t i = static_cast<int64_t>(t) * N + n;
+                    v[t] = values[i];
+                    r[t] = rewards[i];
+                    d[t] = dones[i];
+                }
+            }
+            float next_v = last_values[n];
+            float adv = 0.0f;
+#pragma unroll
+            for (int t = TMAX - 1; t >= 0; --t) {
+                if (t < T) {
+                    const int64_t i = static_cast<int64_t>(t) * N + n;
+                    adv = GaeStep::step(v[t], r[t], d[t], next_v, adv, gamma, lam);
+                    const float ret = __fadd_rn(adv, v[t]);  // :142
+                    const float a = __fsub_rn(ret, v[t]);    // :145
+                    returns[i] = ret;
+                    advantages[i] = a;
+                    s += static_cast<double>(a);
+                    ss += static_cast<double>(a) * static_cast<double>(a);
+                    next_v = v[t];
+                }
+            }
+        } else {  // long rollouts: streaming loop
+            float next_v = last_values[n];
+            float adv = 0.0f;
+            for (int t = T - 1; t >= 0; --t) {
+                const int64_t i = static_cast<int64_t>(t) * N + n;
+                const float v = values[i];
+                adv = GaeStep::step(v, rewards[i], dones[i], next_v, adv, gamma, lam);
+                const float ret = __fadd_rn(adv, v);
+                const float a = __fsub_rn(ret, v);
+                returns[i] = ret;
+                advantages[i] = a;
+                s += static_cast<double>(a);
+                ss += static_cast<double>(a) * static_cast<double>(a);
+                next_v = v;
+            }
+        }
+    }
+    if (partials != nullptr) {
+        s = block_sum(s, scratch[0]);
+        ss = block_sum(ss, scratch[1]);
+        if (threadIdx.x == 0) partials[blockIdx.x] = make_double2(s, ss);
+    }
+}
+
+// (sum, sum of squares) partials of an arbitrary vector (standalone normaliser).
+__global__ __launch_bounds__(kBlock) void moments_kernel(const float* __restrict__ x, int64_t n,
+                                                         double2* __restrict__ partials) {
+    __shared__ double scratch[2][kBlock / kWave];
+    double s = 0.0, ss = 0.0;
+    const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
+    for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < n; i += stride) {
+        const double a = x[i];
+        s += a;
+        ss += a * a;
+    }
+    s = block_sum(s, scratch[0]);
+    ss = block_sum(ss, scratch[1]);
+    if (threadIdx.x == 0) partials[blockIdx.x] = make_double2(s, ss);
+}
+
+// Mean and unbiased std (torch.Tensor.std default, correction = 1) from the partials, in a fixed order.
+__device__ __forceinline__ void fold_moments(const double2* __restrict__ partials, int np, int64_t n,
+                                             float* mean_out, float* std_out) {
+    __shared__ double scratch[2][kBlock / kWave];
+    double s = 0.0, ss = 0.0;
+    for (int i = threadIdx.x; i < np; i += kBlock) {
+        const double2 p = partials[i];
+        s += p.x;
+        ss += p.y;
+    }
+    s = block_sum(s, scratch[0]);
+    ss = block_sum(ss, scratch[1]);
+    const double mean = s / static_cast<double>(n);
+    double var = (ss - s * mean) / static_cast<double>(n - 1);
+    if (var < 0.0) var = 0.0;  // rounding guard for constant inputs (true variance is 0)
+    *mean_out = static_cast<float>(mean);
+    *std_out = static_cast<float>(sqrt(var));
+}
+
+__global__ __launch_bounds__(kBlock) void adv_normalize_kernel(float* __restrict__ adv, int64_t n,
+                                                               const double2* __restrict__ partials, int np,
+                                                               float eps) {
+    float mean, std;
+    fold_moments(partials, np, n, &mean, &std);
+    const float denom = __fadd_rn(std, eps);  // rollout_storage.py:149  (std + 1e-8)
+    const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
+    const int64_t tid = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    const bool vec = (reinterpret_cast<uintptr_t>(adv) & 15) == 0;
+    const int64_t nvec = vec ? n / 4 : 0;
+    float4* adv4 = reinterpret_cast<float4*>(adv);
+    for (int64_t i = tid; i < nvec; i += stride) {
+        float4 a = adv4[i];
+        a.x = __fdiv_rn(__fsub_rn(a.x, mean), denom);
+        a.y = __fdiv_rn(__fsub_rn(a.y, mean), denom);
+        a.z = __fdiv_rn(__fsub_rn(a.z, mean), denom);
+        a.w = __fdiv_rn(__fsub_rn(a.w, mean), denom);
+        adv4[i] = a;
+    }
+    for (int64_t i = nvec * 4 + tid; i < n; i += stride) adv[i] = __fdiv_rn(__fsub_rn(adv[i], mean), denom);
+}
+
+int scan_blocks(int64_t N) { return static_cast<int>(std::min<int64_t>(ceil_div(N, kBlock), kMaxPartials)); }
+
+int elementwise_blocks(int64_t n) {
+    return static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, 4 * kBlock), 2048)));
+}
+
+template <int TMAX>
+void launch_scan(int nb, hipStream_t st, const float* v, const float* r, const uint8_t* d, const float* lv,
+                 float g, float l, int T, int64_t N, float* ret, float* adv, double2* part) {
+    hipLaunchKernelGGL(gae_scan_kernel<TMAX>, dim3(nb), dim3(kBlock), 0, st, v, r, d, lv, g, l, T, N, ret, adv, part);
+}
+
+}  // namespace
+}  // namespace rslrl
+
+using namespace rslrl;
+
+extern "C" size_t rslrl_compute_returns_workspace_bytes(int64_t T, int64_t N) {
+    (void)T;
+    (void)N;
+    return sizeof(double2) * kMaxPartials;
+}
+
+extern "C" size_t rslrl_normalize_workspace_bytes(int64_t n) {
+    (void)n;
+    return sizeof(double2) * kMaxPartials;
+}
+
+extern "C" int rslrl_compute_returns(const float* values, const float* rewards, const uint8_t* dones,
+                                     const float* last_values, float gamma, float lam, int64_t T, int64_t N,
+                                     int32_t normalize_advantage, float* returns, float* advantages,
+                                     void* workspace, size_t workspace_bytes, rslrl_stream_t stream) {
+    if (T < 0 || N < 0 || T > INT32_MAX) return RSLRL_E_INVALID_ARGUMENT;
+    if (T == 0 || N == 0) return RSLRL_OK;
+    if (!values || !rewards || !dones || !last_values || !returns || !advantages) return RSLRL_E_INVALID_ARGUMENT;
+    double2* part = nullptr;
+    if (normalize_advantage) {
+        if (!workspace) return RSLRL_E_INVALID_ARGUMENT;
+        if (workspace_bytes < rslrl_compute_returns_workspace_bytes(T, N)) return RSLRL_E_WORKSPACE_TOO_SMALL;
+        if (reinterpret_cast<uintptr_t>(workspace) & 15) return RSLRL_E_MISALIGNED;
+        part = static_cast<double2*>(workspace);
+    }
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const int nb = scan_blocks(N);
+    const int t = static_cast<int>(T);
+    if (t <= 8)
+        launch_scan<8>(nb, st, values, rewards, dones, last_values, gamma, lam, t, N, returns, advantages, part);
+    else if (t <= 16)
+        launch_scan<16>(nb, st, values, rewards, dones, last_values, gamma, lam, t, N, returns, advantages, part);
+    else if (t <= 24)
+        launch_scan<24>(nb, st, values, rewards, dones, last_values, gamma, lam, t, N, returns, advantages, part);
+    else if (t <= 32)
+        launch_scan<32>(nb, st, values, rewards, dones, last_values, gamma, lam, t, N, returns, advantages, part);
+    else
+        launch_scan<0>(nb, st, values, rewards, dones, last_values, gamma, lam, t, N, returns, advantages, part);
+    int rc = launch_status();
+    if (rc != RSLRL_OK || !normalize_advantage) return rc;
+    const int64_t n = T * N;
+    hipLaunchKernelGGL(adv_normalize_kernel, dim3(elementwise_blocks(n)), dim3(kBlock), 0, st, advantages, n, part,
+                       nb, 1e-8f);
+    return launch_status();
+}
+
+extern "C" int rslrl_normalize_advantages(float* advantages, int64_t n, float eps, void* workspace,
+                                          size_t workspace_bytes, rslrl_stream_t stream) {
+    if (n < 0) return RSLRL_E_INVALID_ARGUMENT;
+    if (n == 0) return RSLRL_OK;
+    if (!advantages || !workspace) return RSLRL_E_INVALID_ARGUMENT;
+    if (workspace_bytes < rslrl_normalize_workspace_bytes(n)) return RSLRL_E_WORKSPACE_TOO_SMALL;
+    if (reinterpret_cast<uintptr_t>(workspace) & 15) return RSLRL_E_MISALIGNED;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    double2* part = static_cast<double2*>(workspace);
+    const int nb = static_cast<int>(std::min<int64_t>(ceil_div(n, kBlock), kMaxPartials));
+    hipLaunchKernelGGL(moments_kernel, dim3(nb), dim3(kBlock), 0, st, advantages, n, part);
+    int rc = launch_status();
+    if (rc != RSLRL_OK) return rc;
+    hipLaunchKernelGGL(adv_normalize_kernel, dim3(elementwise_blocks(n)), dim3(kBlock), 0, st, advantages, n, part,
+                       nb, eps);
+    return launch_status();
+}

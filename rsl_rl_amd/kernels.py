@@ -1,0 +1,308 @@
+"""Tensor-level wrappers over the C ABI (include/rslrl_amd.h) -- the hot path's Python face.
+
+Every device entry point takes torch tensors that live on a ROCm device, launches on the current
+torch stream and never synchronises.  CPU tensors are rejected: there is no CPU fallback.
+"""
+
+from __future__ import annotations
+
+import contextlib
+import ctypes
+from collections import defaultdict
+
+import torch
+
+from . import _lib
+
+__all__ = [
+    "compute_returns",
+    "normalize_advantages_",
+    "randperm_mt19937",
+    "gather_rows",
+    "ppo_loss_fwd_bwd",
+    "PPOLossFunction",
+]
+
+
+def _require_device(*tensors: torch.Tensor):
+    for t in tensors:
+        if t is None:
+            continue
+        if not t.is_cuda:
+            raise RuntimeError(
+                "rsl_rl_amd: the PPO hot path runs only on a ROCm GPU (torch 'cuda' device); got a tensor "
+                f"on {t.device}. There is no CPU fallback."
+            )
+
+
+def _stream(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+class _Workspace:
+    """Per-(device, purpose) scratch buffers from torch's caching allocator, grown on demand.
+
+    Reuse across calls is stream-ordered (all launches go to the current stream of the device).
+    """
+
+    def __init__(self):
+        self._bufs = {}
+
+    def get(self, device: torch.device, key: str, nbytes: int) -> torch.Tensor:
+        k = (device, key)
+        buf = self._bufs.get(k)
+        if buf is None or buf.numel() < nbytes:
+            buf = torch.empty(max(nbytes, 256), dtype=torch.uint8, device=device)
+            self._bufs[k] = buf
+        return buf
+
+
+_ws = _Workspace()
+
+
+class KernelTimer:
+    """Optional HIP-event timing of each C-ABI call, recorded on the stream the kernels launch on.
+
+    bench.py enables it over its timed region to report the dominant kernel's live launch duration
+    (roofline.achieved); disabled it costs one attribute check per call.
+    """
+
+    def __init__(self):
+        self.enabled = False
+        self.spans = defaultdict(list)
+        self.bytes = defaultdict(list)
+
+    def reset(self):
+        self.spans.clear()
+        self.bytes.clear()
+
+    @contextlib.contextmanager
+    def span(self, name: str, device: torch.device, algorithmic_bytes: int):
+        if not self.enabled:
+            yield
+            return
+        stream = torch.cuda.current_stream(device)
+        start = torch.cuda.Event(enable_timing=True)
+        end = torch.cuda.Event(enable_timing=True)
+        start.record(stream)
+        yield
+        end.record(stream)
+        self.spans[name].append((start, end))
+        self.bytes[name].append(algorithmic_bytes)
+
+    def summary(self):
+        """name -> {launches, mean_ms, total_ms, bytes_per_launch}; synchronises the events."""
+        out = {}
+        for name, evs in self.spans.items():
+            ms = [s.elapsed_time(e) for s, e in evs]
+            out[name] = {
+                "launches": len(ms),
+                "mean_ms": sum(ms) / len(ms),
+                "total_ms": sum(ms),
+                "bytes_per_launch": sum(self.bytes[name]) / len(self.bytes[name]),
+            }
+        return out
+
+
+timer = KernelTimer()
+
+
+# ------------------------------------------------------------------------------------------------
+# rollout_storage.py:127-149
+# ------------------------------------------------------------------------------------------------
+def compute_returns(values, rewards, dones, last_values, gamma, lam, normalize_advantage, returns, advantages):
+    """GAE + (optional) normalisation, written into `returns` / `advantages` ([T, N, 1] fp32, in place).
+
+    values/rewards [T, N, 1] fp32, dones [T, N, 1] uint8, last_values [N, 1] fp32, all contiguous.
+    """
+    _require_device(values, rewards, dones, last_values, returns, advantages)
+    T, N = values.shape[0], values.shape[1]
+    for t, dt in ((values, torch.float32), (rewards, torch.float32), (dones, torch.uint8),
+                  (last_values, torch.float32), (returns, torch.float32), (advantages, torch.float32)):
+        if t.dtype != dt or not t.is_contiguous():
+            raise ValueError(f"compute_returns: expected contiguous {dt}, got {t.dtype} (contiguous={t.is_contiguous()})")
+    if values.numel() != T * N or last_values.numel() != N or dones.numel() != T * N or rewards.numel() != T * N:
+        raise ValueError("compute_returns: inconsistent shapes")
+    L = _lib.lib()
+    dev = values.device
+    nbytes = L.rslrl_compute_returns_workspace_bytes(T, N)
+    ws = _ws.get(dev, "gae", nbytes)
+    # with the timer on, scan and normaliser go through two entry points so that each recorded span
+    # covers one pass (bench.py only; the fused entry point launches the same two kernels)
+    split = timer.enabled and normalize_advantage
+    with timer.span("gae_scan", dev, 17 * T * N + 4 * N):
+        rc = L.rslrl_compute_returns(
+            _ptr(values), _ptr(rewards), _ptr(dones), _ptr(last_values), ctypes.c_float(gamma), ctypes.c_float(lam),
+            T, N, 0 if split else int(bool(normalize_advantage)), _ptr(returns), _ptr(advantages), _ptr(ws),
+            ws.numel(), ctypes.c_void_p(_stream(dev)),
+        )
+    _lib.check(rc, "rslrl_compute_returns")
+    if split:
+        normalize_advantages_(advantages.view(-1))
+
+
+def normalize_advantages_(adv: torch.Tensor, eps: float = 1e-8) -> torch.Tensor:
+    """In-place (adv - mean) / (std_unbiased + eps) over all elements (rollout_storage.py:149)."""
+    _require_device(adv)
+    if adv.dtype != torch.float32 or not adv.is_contiguous():
+        raise ValueError("normalize_advantages_: expected a contiguous fp32 tensor")
+    L = _lib.lib()
+    n = adv.numel()
+    ws = _ws.get(adv.device, "norm", L.rslrl_normalize_workspace_bytes(n))
+    with timer.span("adv_normalize", adv.device, 12 * n):
+        rc = L.rslrl_normalize_advantages(_ptr(adv), n, ctypes.c_float(eps), _ptr(ws), ws.numel(),
+                                          ctypes.c_void_p(_stream(adv.device)))
+    _lib.check(rc, "rslrl_normalize_advantages")
+    return adv
+
+
+# ------------------------------------------------------------------------------------------------
+# rollout_storage.py:165 -- torch CPU randperm semantics, host mt19937
+# ------------------------------------------------------------------------------------------------
+def randperm_mt19937(n: int, generator: torch.Generator | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
+    """Exactly torch.randperm(n, generator=generator) for a CPU generator (default: the process default
+    CPU generator), returned as int32 and advancing the generator identically.  Host code."""
+    gen = torch.default_generator if generator is None else generator
+    if gen.device.type != "cpu":
+        raise ValueError("randperm_mt19937 follows torch's CPU generator; pass a CPU torch.Generator")
+    state = gen.get_state()
+    if out is None:
+        out = torch.empty(n, dtype=torch.int32)
+    if out.dtype != torch.int32 or out.device.type != "cpu" or not out.is_contiguous() or out.numel() < n:
+        raise ValueError("randperm_mt19937: `out` must be a contiguous CPU int32 tensor with >= n elements")
+    rc = _lib.lib().rslrl_randperm_mt19937(_ptr(state), state.numel(), n, _ptr(out))
+    _lib.check(rc, "rslrl_randperm_mt19937")
+    gen.set_state(state)
+    return out[:n]
+
+
+# ------------------------------------------------------------------------------------------------
+# rollout_storage.py:168-197 -- all mini-batch fields in one launch
+# ------------------------------------------------------------------------------------------------
+def gather_rows(pairs, indices: torch.Tensor):
+    """pairs: list of (src [rows, ...], dst [count, ...]) contiguous tensors; dst[r] = src[indices[r]]."""
+    if len(pairs) > _lib.MAX_GATHER_FIELDS:
+        for i in range(0, len(pairs), _lib.MAX_GATHER_FIELDS):
+            gather_rows(pairs[i:i + _lib.MAX_GATHER_FIELDS], indices)
+        return
+    _require_device(indices, *[t for p in pairs for t in p])
+    if indices.dtype != torch.int32 or not indices.is_contiguous():
+        raise ValueError("gather_rows: indices must be contiguous int32")
+    count = indices.numel()
+    arr = (_lib.GatherField * max(len(pairs), 1))()
+    moved = 0
+    for i, (src, dst) in enumerate(pairs):
+        if not (src.is_contiguous() and dst.is_contiguous()) or src.dtype != dst.dtype:
+            raise ValueError("gather_rows: fields must be contiguous and of matching dtype")
+        if dst.shape[0] != count or src.shape[1:] != dst.shape[1:]:
+            raise ValueError("gather_rows: shape mismatch")
+        row_bytes = dst[0].numel() * dst.element_size() if dst.dim() > 1 else dst.element_size()
+        arr[i] = _lib.GatherField(src.data_ptr(), dst.data_ptr(), row_bytes)
+        moved += 2 * row_bytes * count
+    dev = indices.device
+    with timer.span("gather_rows", dev, moved + 4 * count):
+        rc = _lib.lib().rslrl_gather_rows(arr, len(pairs), _ptr(indices), count, ctypes.c_void_p(_stream(dev)))
+    _lib.check(rc, "rslrl_gather_rows")
+
+
+# ------------------------------------------------------------------------------------------------
+# ppo.py:221-315 + backward of :368
+# ------------------------------------------------------------------------------------------------
+STATS_LOSS, STATS_SURROGATE, STATS_VALUE, STATS_ENTROPY, STATS_KL, STATS_ADV_MEAN, STATS_ADV_STD = range(7)
+
+
+def _row_stride(t: torch.Tensor, A: int) -> int:
+    if t.dim() != 2 or t.shape[1] != A or t.stride(1) != 1:
+        raise ValueError("ppo_loss: [B, A] operands need unit stride along actions")
+    return t.stride(0)
+
+
+def ppo_loss_fwd_bwd(mu, sigma, values, actions, old_logp, advantages, target_values, returns, old_mu, old_sigma, *,
+                     clip_param=0.2, value_loss_coef=1.0, entropy_coef=0.01, use_clipped_value_loss=True,
+                     compute_kl=True, normalize_advantage=False, grad_mu=None, grad_sigma=None, grad_values=None,
+                     stats=None):
+    """One fused launch sequence: loss scalars + d(loss)/d(mu, sigma, V).
+
+    mu [B, A]; sigma [A] (shared, e.g. ActorCritic.std) or [B, A] (state-dependent std); values [B] or
+    [B, 1]; actions/old_mu/old_sigma [B, A] contiguous; old_logp/advantages/target_values/returns [B]/[B, 1].
+    Returns (stats[8], grad_mu [B, A], grad_sigma (shape of sigma), grad_values (shape of values)).
+    """
+    mu_d, sg_d, v_d = mu.detach(), sigma.detach(), values.detach()
+    _require_device(mu_d, sg_d, v_d, actions, old_logp, advantages, target_values, returns, old_mu, old_sigma)
+    B, A = mu_d.shape
+    if A > _lib.PPO_LOSS_MAX_ACTIONS:
+        raise ValueError(f"ppo_loss: at most {_lib.PPO_LOSS_MAX_ACTIONS} actions supported")
+    sigma_mode = 0 if sg_d.dim() == 1 else 1
+    if sigma_mode == 0 and (sg_d.numel() != A or not sg_d.is_contiguous()):
+        raise ValueError("ppo_loss: shared sigma must be a contiguous [A] tensor")
+    for t in (v_d, old_logp, advantages, target_values, returns):
+        if t.numel() != B or not t.is_contiguous():
+            raise ValueError("ppo_loss: [B] operands must be contiguous with B elements")
+    for t in (actions, old_mu, old_sigma):
+        if tuple(t.shape) != (B, A) or not t.is_contiguous():
+            raise ValueError("ppo_loss: actions/old_mu/old_sigma must be contiguous [B, A]")
+    dev = mu_d.device
+    if grad_mu is None:
+        grad_mu = torch.empty((B, A), dtype=torch.float32, device=dev)
+    if grad_sigma is None:
+        grad_sigma = torch.empty(sg_d.shape, dtype=torch.float32, device=dev)
+    if grad_values is None:
+        grad_values = torch.empty(v_d.shape, dtype=torch.float32, device=dev)
+    if stats is None:
+        stats = torch.empty(8, dtype=torch.float32, device=dev)
+    args = _lib.PPOLossArgs()
+    args.B, args.A, args.sigma_mode = B, A, sigma_mode
+    args.mu, args.mu_stride = mu_d.data_ptr(), _row_stride(mu_d, A)
+    args.sigma = sg_d.data_ptr()
+    args.sigma_stride = _row_stride(sg_d, A) if sigma_mode == 1 else 0
+    args.values = v_d.data_ptr()
+    args.actions, args.old_logp, args.advantages = actions.data_ptr(), old_logp.data_ptr(), advantages.data_ptr()
+    args.target_values, args.returns = target_values.data_ptr(), returns.data_ptr()
+    args.old_mu, args.old_sigma = old_mu.data_ptr(), old_sigma.data_ptr()
+    args.clip_param, args.value_loss_coef, args.entropy_coef = clip_param, value_loss_coef, entropy_coef
+    args.use_clipped_value_loss = 1 if use_clipped_value_loss else 0
+    args.compute_kl = 1 if compute_kl else 0
+    args.normalize_advantage = 1 if normalize_advantage else 0
+    args.grad_mu, args.grad_mu_stride = grad_mu.data_ptr(), _row_stride(grad_mu, A)
+    args.grad_sigma = grad_sigma.data_ptr()
+    args.grad_sigma_stride = _row_stride(grad_sigma, A) if sigma_mode == 1 else 0
+    args.grad_values = grad_values.data_ptr()
+    args.stats = stats.data_ptr()
+    L = _lib.lib()
+    ws = _ws.get(dev, "ppo_loss", L.rslrl_ppo_loss_workspace_bytes(B, A))
+    # algorithmic bytes: read mu, actions, old_mu, old_sigma (+ per-row sigma) and 5 scalars per row;
+    # write d mu, d V (+ per-row d sigma)
+    row_bytes = 4 * (4 * A + 5) + 4 * (A + 1) + (8 * A if sigma_mode == 1 else 0)
+    with timer.span("ppo_loss", dev, row_bytes * B):
+        rc = L.rslrl_ppo_loss_fwd_bwd(ctypes.byref(args), _ptr(ws), ws.numel(), ctypes.c_void_p(_stream(dev)))
+    _lib.check(rc, "rslrl_ppo_loss_fwd_bwd")
+    return stats, grad_mu, grad_sigma, grad_values
+
+
+class PPOLossFunction(torch.autograd.Function):
+    """Autograd wrapper: loss = PPOLossFunction.apply(mu, sigma, values, batch..., hyper) -> scalar.
+
+    Forward runs the fused kernel (it also produces the gradients); backward scales them by the
+    upstream gradient.  The second output is the stats vector (no gradient).
+    """
+
+    @staticmethod
+    def forward(ctx, mu, sigma, values, actions, old_logp, advantages, target_values, returns, old_mu, old_sigma,
+                clip_param, value_loss_coef, entropy_coef, use_clipped_value_loss, compute_kl, normalize_advantage):
+        stats, gmu, gsig, gv = ppo_loss_fwd_bwd(
+            mu, sigma, values, actions, old_logp, advantages, target_values, returns, old_mu, old_sigma,
+            clip_param=clip_param, value_loss_coef=value_loss_coef, entropy_coef=entropy_coef,
+            use_clipped_value_loss=use_clipped_value_loss, compute_kl=compute_kl,
+            normalize_advantage=normalize_advantage)
+        ctx.save_for_backward(gmu, gsig, gv)
+        ctx.mark_non_differentiable(stats)
+        return stats[STATS_LOSS], stats
+
+    @staticmethod
+    def backward(ctx, g_loss, g_stats):
+        gmu, gsig, gv = ctx.saved_tensors
+        return (gmu * g_loss, gsig * g_loss, gv * g_loss) + (None,) * 13

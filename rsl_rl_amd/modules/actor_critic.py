@@ -1,0 +1,162 @@
+"""Gaussian MLP actor + MLP critic (rsl_rl/modules/actor_critic.py:15-195).
+
+Same constructor, attributes, parameter names and behaviour as the reference, so configs and
+checkpoints carry over.  In addition `action_distribution_params()` hands the PPO update the raw
+(mean, sigma) of the policy without materialising a torch Normal's per-row sigma, so the fused HIP
+loss (rsl_rl_amd.kernels.ppo_loss_fwd_bwd) can read a shared [A] sigma and return its gradient
+already reduced over the mini-batch.
+"""
+
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+from torch.distributions import Normal
+
+from ..networks import MLP, EmpiricalNormalization
+
+
+class ActorCritic(nn.Module):
+    is_recurrent = False
+
+    def __init__(
+        self,
+        obs,
+        obs_groups,
+        num_actions,
+        actor_obs_normalization=False,
+        critic_obs_normalization=False,
+        actor_hidden_dims=[256, 256, 256],
+        critic_hidden_dims=[256, 256, 256],
+        activation="elu",
+        init_noise_std=1.0,
+        noise_std_type: str = "scalar",
+        state_dependent_std=False,
+        **kwargs,
+    ):
+        if kwargs:
+            print("ActorCritic.__init__ got unexpected arguments, which will be ignored: " + str(list(kwargs)))
+        super().__init__()
+        self.obs_groups = obs_groups
+        num_actor_obs = self._group_dim(obs, obs_groups["policy"])
+        num_critic_obs = self._group_dim(obs, obs_groups["critic"])
+        self.num_actions = num_actions
+        self.state_dependent_std = state_dependent_std
+        self.noise_std_type = noise_std_type
+        if noise_std_type not in ("scalar", "log"):
+            raise ValueError(f"Unknown standard deviation type: {noise_std_type}. Should be 'scalar' or 'log'")
+
+        out = [2, num_actions] if state_dependent_std else num_actions
+        self.actor = MLP(num_actor_obs, out, actor_hidden_dims, activation)
+        self.actor_obs_normalization = actor_obs_normalization
+        self.actor_obs_normalizer = EmpiricalNormalization(num_actor_obs) if actor_obs_normalization else nn.Identity()
+        print(f"Actor MLP: {self.actor}")
+        self.critic = MLP(num_critic_obs, 1, critic_hidden_dims, activation)
+        self.critic_obs_normalization = critic_obs_normalization
+        self.critic_obs_normalizer = (
+            EmpiricalNormalization(num_critic_obs) if critic_obs_normalization else nn.Identity()
+        )
+        print(f"Critic MLP: {self.critic}")
+
+        if state_dependent_std:
+            # the std half of the last layer starts at weight 0 and bias = init std (actor_critic.py:77-86)
+            last = self.actor[-2]
+            nn.init.zeros_(last.weight[num_actions:])
+            init_bias = init_noise_std if noise_std_type == "scalar" else torch.log(torch.tensor(init_noise_std + 1e-7))
+            nn.init.constant_(last.bias[num_actions:], init_bias)
+        elif noise_std_type == "scalar":
+            self.std = nn.Parameter(init_noise_std * torch.ones(num_actions))
+        else:
+            self.log_std = nn.Parameter(torch.log(init_noise_std * torch.ones(num_actions)))
+
+        self.distribution = None
+        Normal.set_default_validate_args(False)
+
+    @staticmethod
+    def _group_dim(obs, groups):
+        dim = 0
+        for g in groups:
+            assert len(obs[g].shape) == 2, "The ActorCritic module only supports 1D observations."
+            dim += obs[g].shape[-1]
+        return dim
+
+    def reset(self, dones=None):
+        pass
+
+    def forward(self):
+        raise NotImplementedError
+
+    @property
+    def action_mean(self):
+        return self.distribution.mean
+
+    @property
+    def action_std(self):
+        return self.distribution.stddev
+
+    @property
+    def entropy(self):
+        return self.distribution.entropy().sum(dim=-1)
+
+    def _mean_and_std(self, obs):
+        """(mean [B, A], std) with std either the shared [A] parameter-derived vector or per-row [B, A]."""
+        if self.state_dependent_std:
+            mean_and_std = self.actor(obs)
+            mean, std = torch.unbind(mean_and_std, dim=-2)
+            if self.noise_std_type == "log":
+                std = torch.exp(std)
+            return mean, std
+        mean = self.actor(obs)
+        std = self.std if self.noise_std_type == "scalar" else torch.exp(self.log_std)
+        return mean, std
+
+    def update_distribution(self, obs):
+        mean, std = self._mean_and_std(obs)
+        self.distribution = Normal(mean, std.expand_as(mean))
+
+    def action_distribution_params(self, obs):
+        """Actor forward for the fused PPO loss: returns (mean [B, A], sigma) where sigma is [A] (shared
+        std / exp(log_std), gradient flows to the parameter) or [B, A] (state-dependent std).  Also
+        leaves `self.distribution` set, as `act()` would, for logging (on_policy_runner.py:208)."""
+        obs = self.actor_obs_normalizer(self.get_actor_obs(obs))
+        mean, std = self._mean_and_std(obs)
+        self.distribution = Normal(mean.detach(), std.detach().expand_as(mean))
+        return mean, std
+
+    def act(self, obs, **kwargs):
+        obs = self.actor_obs_normalizer(self.get_actor_obs(obs))
+        self.update_distribution(obs)
+        return self.distribution.sample()
+
+    def act_inference(self, obs):
+        obs = self.actor_obs_normalizer(self.get_actor_obs(obs))
+        return self.actor(obs)
+
+    def evaluate(self, obs, **kwargs):
+        obs = self.critic_obs_normalizer(self.get_critic_obs(obs))
+        return self.critic(obs)
+
+    @staticmethod
+    def _concat(obs, groups):
+        # a single group is used as is (the reference's torch.cat of one tensor is a pure copy)
+        return obs[groups[0]] if len(groups) == 1 else torch.cat([obs[g] for g in groups], dim=-1)
+
+    def get_actor_obs(self, obs):
+        return self._concat(obs, self.obs_groups["policy"])
+
+    def get_critic_obs(self, obs):
+        return self._concat(obs, self.obs_groups["critic"])
+
+    def get_actions_log_prob(self, actions):
+        return self.distribution.log_prob(actions).sum(dim=-1)
+
+    def update_normalization(self, obs):
+        if self.actor_obs_normalization:
+            self.actor_obs_normalizer.update(self.get_actor_obs(obs))
+        if self.critic_obs_normalization:
+            self.critic_obs_normalizer.update(self.get_critic_obs(obs))
+
+    def load_state_dict(self, state_dict, strict=True):
+        """Load parameters; returns True (= training resumes), as the reference (actor_critic.py:181-195)."""
+        super().load_state_dict(state_dict, strict=strict)
+        return True

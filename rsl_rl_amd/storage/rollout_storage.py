@@ -1,0 +1,209 @@
+"""Rollout buffer with the PPO hot path on the GPU (rsl_rl/storage/rollout_storage.py:14-260).
+
+Buffers, shapes, dtypes and the public interface are the reference's ([T, N, ...] per field, dones
+uint8, TensorDict observations, Transition, add_transitions, clear, compute_returns,
+mini_batch_generator), so PPO code and external callers see the same object.  What changes is how the
+two hot functions run:
+
+* compute_returns (:127-149) is one HIP reverse-scan kernel (+ one normalisation kernel) over the
+  [T, N] slabs instead of a Python loop of ~320 tiny ATen launches; results are bit-identical to the
+  reference for returns and raw advantages.
+* mini_batch_generator (:160-203) draws its permutation with torch's CPU randperm semantics (host
+  mt19937 Fisher-Yates, bit-exact), uploads it once, and *packs* every field in permuted order with a
+  single multi-field gather launch.  Because the reference reuses one permutation for all epochs, each
+  mini-batch is then a contiguous slice of the packed buffers: the yielded tensors equal the
+  reference's `field.flatten(0, 1)[indices[i*mb:(i+1)*mb]]` exactly, and no epoch re-gathers.
+
+Permutation source: the reference calls `torch.randperm(n, device=self.device)`, i.e. on a GPU it draws
+from the device generator with a device-specific algorithm.  Here the permutation always follows the
+CPU randperm algorithm on `perm_generator` (default: torch's process-wide CPU generator), which makes it
+reproducible under torch.manual_seed and bit-exact with the reference run on CPU.
+"""
+
+from __future__ import annotations
+
+import torch
+
+from .. import kernels
+from ..utils import TensorDict
+
+
+class RolloutStorage:
+    class Transition:
+        def __init__(self):
+            self.observations = None
+            self.actions = None
+            self.privileged_actions = None
+            self.rewards = None
+            self.dones = None
+            self.values = None
+            self.actions_log_prob = None
+            self.action_mean = None
+            self.action_sigma = None
+            self.hidden_states = None
+
+        def clear(self):
+            self.__init__()
+
+    def __init__(self, training_type, num_envs, num_transitions_per_env, obs, actions_shape, device="cpu"):
+        self.training_type = training_type
+        self.device = device
+        self.num_transitions_per_env = num_transitions_per_env
+        self.num_envs = num_envs
+        self.actions_shape = actions_shape
+        T, N = num_transitions_per_env, num_envs
+
+        def zeros(*shape, dtype=torch.float32):
+            return torch.zeros(*shape, dtype=dtype, device=device)
+
+        self.observations = TensorDict({k: zeros(T, *v.shape) for k, v in obs.items()}, batch_size=[T, N], device=device)
+        self.rewards = zeros(T, N, 1)
+        self.actions = zeros(T, N, *actions_shape)
+        self.dones = zeros(T, N, 1, dtype=torch.uint8)
+        if training_type == "distillation":
+            self.privileged_actions = zeros(T, N, *actions_shape)
+        if training_type == "rl":
+            self.values = zeros(T, N, 1)
+            self.actions_log_prob = zeros(T, N, 1)
+            self.mu = zeros(T, N, *actions_shape)
+            self.sigma = zeros(T, N, *actions_shape)
+            self.returns = zeros(T, N, 1)
+            self.advantages = zeros(T, N, 1)
+        self.saved_hidden_states_a = None
+        self.saved_hidden_states_c = None
+        self.step = 0
+
+        # mini-batch machinery (allocated on first use)
+        self.perm_generator: torch.Generator | None = None
+        self.last_indices: torch.Tensor | None = None  # device int32 permutation of the last generator
+        self._packed = None
+        self._packed_key = None
+        self._perm_host = None
+        self._perm_event = None
+
+    # ------------------------------------------------------------------ filling (rollout_storage.py:77-125)
+    def add_transitions(self, transition: Transition):
+        if self.step >= self.num_transitions_per_env:
+            raise OverflowError("Rollout buffer overflow! You should call clear() before adding new transitions.")
+        t = self.step
+        self.observations[t].copy_(transition.observations)
+        self.actions[t].copy_(transition.actions)
+        self.rewards[t].copy_(transition.rewards.view(-1, 1))
+        self.dones[t].copy_(transition.dones.view(-1, 1))
+        if self.training_type == "distillation":
+            self.privileged_actions[t].copy_(transition.privileged_actions)
+        if self.training_type == "rl":
+            self.values[t].copy_(transition.values)
+            self.actions_log_prob[t].copy_(transition.actions_log_prob.view(-1, 1))
+            self.mu[t].copy_(transition.action_mean)
+            self.sigma[t].copy_(transition.action_sigma)
+        self._save_hidden_states(transition.hidden_states)
+        self.step += 1
+
+    def _save_hidden_states(self, hidden_states):
+        if hidden_states is None or hidden_states == (None, None):
+            return
+        hid_a = hidden_states[0] if isinstance(hidden_states[0], tuple) else (hidden_states[0],)
+        hid_c = hidden_states[1] if isinstance(hidden_states[1], tuple) else (hidden_states[1],)
+        if self.saved_hidden_states_a is None:
+            T = self.num_transitions_per_env
+            self.saved_hidden_states_a = [torch.zeros(T, *h.shape, device=self.device) for h in hid_a]
+            self.saved_hidden_states_c = [torch.zeros(T, *h.shape, device=self.device) for h in hid_c]
+        for i in range(len(hid_a)):
+            self.saved_hidden_states_a[i][self.step].copy_(hid_a[i])
+            self.saved_hidden_states_c[i][self.step].copy_(hid_c[i])
+
+    def clear(self):
+        self.step = 0
+
+    # ------------------------------------------------------------------ GAE (rollout_storage.py:127-149)
+    def compute_returns(self, last_values, gamma, lam, normalize_advantage: bool = True):
+        last_values = last_values.detach()
+        if not last_values.is_contiguous():
+            last_values = last_values.contiguous()
+        kernels.compute_returns(self.values, self.rewards, self.dones, last_values, float(gamma), float(lam),
+                                normalize_advantage, self.returns, self.advantages)
+
+    # ------------------------------------------------------------------ distillation (rollout_storage.py:152-157)
+    def generator(self):
+        if self.training_type != "distillation":
+            raise ValueError("This function is only available for distillation training.")
+        for i in range(self.num_transitions_per_env):
+            yield self.observations[i], self.actions[i], self.privileged_actions[i], self.dones[i]
+
+    # ------------------------------------------------------------------ mini-batches (rollout_storage.py:160-203)
+    def _packed_buffers(self, rows: int):
+        key = (rows, tuple(self.observations.keys()))
+        if self._packed_key != key:
+            A = tuple(self.actions_shape)
+            dev = self.device
+            obs = {k: torch.empty(rows, *v.shape[2:], device=dev) for k, v in self.observations.items()}
+            self._packed = {
+                "obs": obs,
+                "actions": torch.empty(rows, *A, device=dev),
+                "values": torch.empty(rows, 1, device=dev),
+                "returns": torch.empty(rows, 1, device=dev),
+                "actions_log_prob": torch.empty(rows, 1, device=dev),
+                "advantages": torch.empty(rows, 1, device=dev),
+                "mu": torch.empty(rows, *A, device=dev),
+                "sigma": torch.empty(rows, *A, device=dev),
+            }
+            self._packed_key = key
+        return self._packed
+
+    def draw_permutation(self, n: int) -> torch.Tensor:
+        """Device int32 permutation of range(n) with torch CPU randperm semantics on perm_generator.
+
+        Host mt19937 Fisher-Yates into a pinned staging buffer, then one async upload on the current
+        stream.  The staging buffer is reused by the next draw only after that upload has completed.
+        """
+        if self._perm_event is not None:
+            self._perm_event.synchronize()
+        if self._perm_host is None or self._perm_host.numel() < n:
+            self._perm_host = torch.empty(n, dtype=torch.int32, pin_memory=True)
+        host = kernels.randperm_mt19937(n, self.perm_generator, out=self._perm_host)
+        dev = torch.empty(n, dtype=torch.int32, device=self.device)
+        dev.copy_(host, non_blocking=True)
+        self._perm_event = torch.cuda.Event()
+        self._perm_event.record(torch.cuda.current_stream(dev.device))
+        return dev
+
+    def mini_batch_generator(self, num_mini_batches, num_epochs=8):
+        if self.training_type != "rl":
+            raise ValueError("This function is only available for reinforcement learning training.")
+        batch_size = self.num_envs * self.num_transitions_per_env
+        mini_batch_size = batch_size // num_mini_batches
+        rows = num_mini_batches * mini_batch_size
+        # permutation (:165) -- drawn lazily at the first next(), like the reference's generator body
+        indices = self.draw_permutation(rows)
+        self.last_indices = indices
+        p = self._packed_buffers(rows)
+        flat = lambda t: t.flatten(0, 1)  # noqa: E731
+        pairs = [(flat(v), p["obs"][k]) for k, v in self.observations.items()]
+        pairs += [(flat(self.actions), p["actions"]), (flat(self.values), p["values"]),
+                  (flat(self.returns), p["returns"]), (flat(self.actions_log_prob), p["actions_log_prob"]),
+                  (flat(self.advantages), p["advantages"]), (flat(self.mu), p["mu"]), (flat(self.sigma), p["sigma"])]
+        kernels.gather_rows(pairs, indices)
+
+        for _epoch in range(num_epochs):
+            for i in range(num_mini_batches):
+                s = slice(i * mini_batch_size, (i + 1) * mini_batch_size)
+                obs_batch = TensorDict({k: v[s] for k, v in p["obs"].items()}, batch_size=[mini_batch_size],
+                                       device=self.device)
+                yield (
+                    obs_batch,
+                    p["actions"][s],
+                    p["values"][s],
+                    p["advantages"][s],
+                    p["returns"][s],
+                    p["actions_log_prob"][s],
+                    p["mu"][s],
+                    p["sigma"][s],
+                    (None, None),
+                    None,
+                )
+
+    def recurrent_mini_batch_generator(self, num_mini_batches, num_epochs=8):
+        raise NotImplementedError(
+            "recurrent policies (rollout_storage.py:206-260) are outside the MI355X PPO hot-path scope (SURVEY.md §2)"
+        )

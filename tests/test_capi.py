@@ -1,0 +1,84 @@
+"""The C ABI library loads, exports every entry point include/rslrl_amd.h declares, and validates its
+arguments before touching the GPU (no compute calls here: this runs without a GPU)."""
+
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import ROOT, golden_path
+from rsl_rl_amd import _lib
+
+HEADER = os.path.join(ROOT, "include", "rslrl_amd.h")
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(rslrl_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_header_matches_binding_list():
+    assert declared_functions() == sorted(_lib.EXPORTED_SYMBOLS)
+
+
+def test_library_exports_every_declared_symbol():
+    L = _lib.lib()
+    for name in declared_functions():
+        assert hasattr(L, name), name
+    assert L.rslrl_abi_version() == _lib.ABI_VERSION
+
+
+def test_status_strings():
+    L = _lib.lib()
+    assert L.rslrl_status_string(0) == b"ok"
+    assert b"invalid" in L.rslrl_status_string(-1)
+    assert b"hipError_t" in L.rslrl_status_string(1)
+
+
+def test_argument_validation_without_gpu():
+    L = _lib.lib()
+    # negative sizes / null pointers are rejected before any launch
+    assert L.rslrl_compute_returns(None, None, None, None, 0.99, 0.95, -1, 4, 1, None, None, None, 0, None) == -1
+    assert L.rslrl_compute_returns(None, None, None, None, 0.99, 0.95, 4, 4, 1, None, None, None, 0, None) == -1
+    assert L.rslrl_compute_returns(None, None, None, None, 0.99, 0.95, 0, 4, 1, None, None, None, 0, None) == 0
+    f = (_lib.GatherField * 1)(_lib.GatherField(8, 8, 6))  # row_bytes not a multiple of 4
+    assert L.rslrl_gather_rows(f, 1, 8, 4, None) == -1
+    assert L.rslrl_gather_rows(f, 17, 8, 4, None) == -1
+    args = _lib.PPOLossArgs()
+    args.B, args.A = 0, 4
+    assert L.rslrl_ppo_loss_fwd_bwd(ctypes.byref(args), None, 0, None) == -1
+    args.B, args.A = 10, 65
+    assert L.rslrl_ppo_loss_fwd_bwd(ctypes.byref(args), None, 0, None) == -1
+    assert L.rslrl_ppo_loss_workspace_bytes(393216, 12) >= 8 * 16 * 1536
+    assert L.rslrl_compute_returns_workspace_bytes(24, 65536) >= 16 * 256
+
+
+def test_randperm_rejects_bad_state():
+    L = _lib.lib()
+    out = np.empty(10, np.int32)
+    bad = np.zeros(100, np.uint8)
+    assert L.rslrl_randperm_mt19937(bad.ctypes.data, bad.nbytes, 10, out.ctypes.data) == -5
+    st = torch.Generator().manual_seed(0).get_state().numpy().copy()
+    st[8:12] = np.frombuffer(np.int32(9999).tobytes(), np.uint8)  # left out of range
+    assert L.rslrl_randperm_mt19937(st.ctypes.data, st.nbytes, 10, out.ctypes.data) == -5
+
+
+def test_hot_path_refuses_cpu_tensors():
+    from rsl_rl_amd import kernels
+
+    t = torch.zeros(4, 3, 1)
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        kernels.compute_returns(t, t, t.to(torch.uint8), torch.zeros(3, 1), 0.99, 0.95, True, t.clone(), t.clone())
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        kernels.normalize_advantages_(torch.zeros(8))
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        kernels.gather_rows([(torch.zeros(4, 2), torch.zeros(2, 2))], torch.zeros(2, dtype=torch.int32))
+
+
+def test_golden_files_present():
+    for f in ("gae.npz", "perm.npz", "minibatch.npz", "update_c1.npz", "golden.json"):
+        assert os.path.exists(golden_path(f)), f

@@ -1,0 +1,85 @@
+"""HIP multi-field gather + RolloutStorage.mini_batch_generator vs the golden mini-batches and the oracle
+(bit-exact: integer indices and gathered fp32 rows)."""
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden_path
+from oracle import ppo_oracle as O
+from rsl_rl_amd import kernels
+from rsl_rl_amd.storage import RolloutStorage
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("row_elems", [1, 3, 4, 12, 48, 50, 257, 1100])
+def test_gather_rows_vs_oracle(row_elems, cuda_device):
+    rng = np.random.default_rng(row_elems)
+    rows, count = 5000, 3001
+    src = rng.standard_normal((rows, row_elems), dtype=np.float32)
+    idx = rng.integers(0, rows, count).astype(np.int32)
+    s = torch.from_numpy(src).to(cuda_device)
+    d = torch.empty(count, row_elems, device=cuda_device)
+    kernels.gather_rows([(s, d)], torch.from_numpy(idx).to(cuda_device))
+    assert np.array_equal(d.cpu().numpy(), O.gather_rows(src, idx.astype(np.int64)))
+
+
+def test_gather_many_fields_and_misaligned(cuda_device):
+    rng = np.random.default_rng(0)
+    rows, count = 777, 600
+    idx = torch.from_numpy(rng.integers(0, rows, count).astype(np.int32)).to(cuda_device)
+    pairs, refs = [], []
+    for k in range(20):  # > RSLRL_MAX_GATHER_FIELDS -> split into several launches
+        w = 1 + (k * 7) % 23
+        base = torch.from_numpy(rng.standard_normal((rows * w + 1,), dtype=np.float32)).to(cuda_device)
+        src = base[1:].view(rows, w) if k % 3 == 0 else base[: rows * w].view(rows, w)  # misaligned start
+        dst = torch.empty(count, w, device=cuda_device)
+        pairs.append((src, dst))
+        refs.append(O.gather_rows(src.cpu().numpy(), idx.cpu().numpy().astype(np.int64)))
+    kernels.gather_rows(pairs, idx)
+    for (_, dst), ref in zip(pairs, refs):
+        assert np.array_equal(dst.cpu().numpy(), ref)
+
+
+def test_golden_minibatches(golden_meta, cuda_device):
+    m = golden_meta["minibatch"]
+    z = np.load(golden_path("minibatch.npz"))
+    T, N, A = m["T"], m["N"], m["A"]
+    obs0 = {"policy": torch.zeros(N, 3), "extra": torch.zeros(N, 2)}
+    st = RolloutStorage("rl", N, T, obs0, [A], cuda_device)
+    st.observations["policy"].copy_(torch.from_numpy(z["in/obs_policy"]))
+    st.observations["extra"].copy_(torch.from_numpy(z["in/obs_extra"]))
+    for k in ("actions", "values", "returns", "actions_log_prob", "advantages", "mu", "sigma"):
+        getattr(st, k).copy_(torch.from_numpy(z[f"in/{k}"]))
+    torch.manual_seed(m["torch_seed"])
+    names = ["actions", "target_values", "advantages", "returns", "old_logp", "old_mu", "old_sigma"]
+    batches = list(st.mini_batch_generator(m["M"], m["E"]))
+    assert len(batches) == m["num_batches"]
+    for j, b in enumerate(batches):
+        assert np.array_equal(b[0]["policy"].cpu().numpy(), z[f"mb{j}/obs_policy"])
+        assert np.array_equal(b[0]["extra"].cpu().numpy(), z[f"mb{j}/obs_extra"])
+        for nm, t in zip(names, b[1:8]):
+            assert np.array_equal(t.cpu().numpy(), z[f"mb{j}/{nm}"]), (j, nm)
+        assert b[8] == (None, None) and b[9] is None
+
+
+def test_permutation_contents_and_tail_drop(cuda_device):
+    """N*T not divisible by M: the tail is dropped and the permutation covers range(M*mb) exactly."""
+    T, N, M = 5, 37, 4
+    st = RolloutStorage("rl", N, T, {"policy": torch.zeros(N, 2)}, [3], cuda_device)
+    st.observations["policy"].copy_(torch.arange(T * N * 2, dtype=torch.float32).view(T, N, 2))
+    g = torch.Generator().manual_seed(9)
+    st.perm_generator = g
+    batches = list(st.mini_batch_generator(M, 2))
+    mb = (T * N) // M
+    idx = st.last_indices.cpu().long()
+    assert idx.numel() == M * mb and torch.equal(idx.sort().values, torch.arange(M * mb))
+    ref = torch.randperm(M * mb, generator=torch.Generator().manual_seed(9))
+    assert torch.equal(idx, ref)
+    flat = st.observations["policy"].flatten(0, 1).cpu()
+    for i, b in enumerate(batches[:M]):
+        assert torch.equal(b[0]["policy"].cpu(), flat[ref[i * mb:(i + 1) * mb]])
+    # epochs reuse the same permutation (rollout_storage.py:165 is outside the epoch loop)
+    for i in range(M):
+        assert torch.equal(batches[i][0]["policy"], batches[M + i][0]["policy"])

@@ -1,0 +1,101 @@
+"""One full PPO.update() on the GPU vs the reference's update captured on CPU (config C1: N512 T16 O16
+A4, 2x64 ELU, E5 M4), and an end-to-end OnPolicyRunner smoke on the synthetic VecEnv.
+
+The fixture ran the reference with multi_gpu_cfg world_size=1 (so its learning rate went through the
+fp32 broadcast, ppo.py:287-290); the test does the same over a one-rank RCCL ("nccl") group, which also
+exercises the flat-gradient all-reduce path.  Same permutation (torch CPU randperm from the captured
+generator state), same storage, same initial weights; the MLP GEMMs run on hipBLASLt instead of CPU
+BLAS, so parameters are compared with a tolerance (atol 2e-5 after 20 Adam steps at lr <= 2.25e-3)
+while the learning-rate trace (the adaptive-KL decisions) must match exactly.
+"""
+
+import os
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden_path
+from rsl_rl_amd.algorithms import PPO
+from rsl_rl_amd.env import SyntheticVecEnv
+from rsl_rl_amd.modules import ActorCritic
+from rsl_rl_amd.runners import OnPolicyRunner
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def one_rank_group(cuda_device):
+    import torch.distributed as dist
+
+    if not dist.is_initialized():
+        fd, path = tempfile.mkstemp()
+        os.close(fd)
+        dist.init_process_group("nccl", init_method=f"file://{path}", rank=0, world_size=1)
+    yield
+    dist.destroy_process_group()
+
+
+def test_update_c1_matches_reference(golden_meta, cuda_device, one_rank_group):
+    m = golden_meta["update_c1"]
+    z = np.load(golden_path("update_c1.npz"))
+    T, N, O, A = m["T"], m["N"], m["O"], m["A"]
+    dev = cuda_device
+    obs0 = {"policy": torch.zeros(N, O)}
+    groups = {"policy": ["policy"], "critic": ["policy"]}
+    pol = ActorCritic(obs0, groups, A, actor_hidden_dims=m["hidden"], critic_hidden_dims=m["hidden"])
+    pol.load_state_dict({k[5:]: torch.from_numpy(z[k]) for k in z.files if k.startswith("init/")})
+    alg = PPO(pol, num_learning_epochs=m["E"], num_mini_batches=m["M"], device=dev,
+              multi_gpu_cfg={"global_rank": 0, "local_rank": 0, "world_size": 1})
+    alg.init_storage("rl", N, T, obs0, [A])
+    st = alg.storage
+    st.observations["policy"].copy_(torch.from_numpy(z["storage/obs_policy"]))
+    for k in ("rewards", "values", "actions_log_prob", "mu", "sigma", "actions"):
+        getattr(st, k).copy_(torch.from_numpy(z[f"storage/{k}"]))
+    st.dones.copy_(torch.from_numpy(z["storage/dones"]))
+    st.step = T
+    with torch.inference_mode():
+        alg.compute_returns({"policy": torch.from_numpy(z["storage/last_obs"]).to(dev)})
+    torch.testing.assert_close(st.returns.cpu(), torch.from_numpy(z["storage/returns"]), rtol=2e-6, atol=2e-6)
+    torch.testing.assert_close(st.advantages.cpu(), torch.from_numpy(z["storage/advantages"]), rtol=1e-5, atol=1e-5)
+
+    lr_trace = []
+    step = alg.optimizer.step
+    alg.optimizer.step = lambda *a, **k: (lr_trace.append(alg.optimizer.param_groups[0]["lr"]), step(*a, **k))[1]
+    torch.default_generator.set_state(torch.from_numpy(z["gen_state"].copy()))
+    loss = alg.update()
+    assert lr_trace == m["lr_trace"]
+    assert alg.learning_rate == m["final_lr"]
+    for k, v in m["loss_dict"].items():
+        assert abs(loss[k] - v) <= 1e-4 * abs(v) + 1e-5, (k, loss[k], v)
+    final = pol.state_dict()
+    for k in z.files:
+        if k.startswith("final/"):
+            ref = torch.from_numpy(z[k])
+            torch.testing.assert_close(final[k[6:]].cpu(), ref, rtol=0, atol=2e-5, msg=k)
+
+
+def test_runner_end_to_end(cuda_device, tmp_path):
+    torch.manual_seed(0)
+    env = SyntheticVecEnv(512, 16, 4, device=cuda_device, seed=0, timeout_prob=0.25)
+    cfg = {
+        "num_steps_per_env": 16, "save_interval": 50, "obs_groups": {"policy": ["policy"]},
+        "policy": {"class_name": "ActorCritic", "actor_hidden_dims": [64, 64], "critic_hidden_dims": [64, 64],
+                   "activation": "elu", "init_noise_std": 1.0},
+        "algorithm": {"class_name": "PPO", "num_learning_epochs": 5, "num_mini_batches": 4},
+    }
+    runner = OnPolicyRunner(env, cfg, log_dir=None, device=str(cuda_device))
+    runner.learn(3)
+    s = runner.last_iteration_stats
+    assert s["total_fps"] > 0 and all(np.isfinite(v) for v in s["loss_dict"].values())
+    path = str(tmp_path / "model.pt")
+    runner.save(path)
+    sd = {k: v.clone() for k, v in runner.alg.policy.state_dict().items()}
+    runner2 = OnPolicyRunner(SyntheticVecEnv(512, 16, 4, device=cuda_device), {
+        **cfg, "policy": dict(cfg["policy"], class_name="ActorCritic"),
+        "algorithm": dict(cfg["algorithm"], class_name="PPO")}, log_dir=None, device=str(cuda_device))
+    runner2.load(path)
+    for k, v in runner2.alg.policy.state_dict().items():
+        assert torch.equal(v, sd[k]), k
+    assert runner2.current_learning_iteration == runner.current_learning_iteration

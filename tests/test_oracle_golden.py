@@ -1,0 +1,105 @@
+"""Pins the CPU oracle (oracle/) to the golden vectors captured from the reference.
+
+Bit-exact: GAE returns and un-normalised advantages, randperm (and the generator state it leaves),
+mini-batch gathers.  Tolerance: normalised advantages (fp64 statistics vs torch's fp32 reduction),
+loss scalars / KL / gradients (rtol 1e-5; the oracle uses numpy's exp/log instead of torch's).
+"""
+
+import hashlib
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden_path
+from oracle import ppo_oracle as O
+
+
+def _gae_cases(meta):
+    return sorted(meta["gae"].items())
+
+
+def test_gae_bit_exact(golden_meta):
+    z = np.load(golden_path("gae.npz"))
+    for name, m in _gae_cases(golden_meta):
+        g = lambda k: z[f"{name}/{k}"]  # noqa: E731
+        ret, adv = O.gae(g("values"), g("rewards"), g("dones"), g("last_values"), m["gamma"], m["lam"])
+        assert np.array_equal(ret, g("returns")), name
+        assert np.array_equal(adv, g("advantages_raw")), name
+
+
+def test_gae_normalized(golden_meta):
+    z = np.load(golden_path("gae.npz"))
+    for name, m in _gae_cases(golden_meta):
+        g = lambda k: z[f"{name}/{k}"]  # noqa: E731
+        _, adv = O.compute_returns(g("values"), g("rewards"), g("dones"), g("last_values"), m["gamma"], m["lam"])
+        ref = g("advantages_norm")
+        if m["T"] * m["N"] == 1:
+            assert np.isnan(adv).all() and np.isnan(ref).all()
+            continue
+        np.testing.assert_allclose(adv, ref, rtol=1e-5, atol=1e-6, err_msg=name)
+
+
+def test_randperm_bit_exact_and_state(golden_meta):
+    z = np.load(golden_path("perm.npz"))
+    for name, m in golden_meta["perm"].items():
+        if f"{name}/state" not in z:
+            continue
+        perm, st = O.randperm(z[f"{name}/state"], m["n"])
+        assert np.array_equal(perm, z[f"{name}/perm"]), name
+        assert np.array_equal(st, z[f"{name}/state_after"]), name
+
+
+@pytest.mark.parametrize("name", ["n393216", "n1572864"])
+def test_randperm_large_hash(golden_meta, name):
+    m = golden_meta["perm"][name]
+    g = torch.Generator().manual_seed(m["seed"])
+    perm, _ = O.randperm(g.get_state().numpy(), m["n"])
+    assert perm[:32].tolist() == m["head"] and perm[-32:].tolist() == m["tail"]
+    assert hashlib.sha256(perm.tobytes()).hexdigest() == m["sha256_int64"]
+
+
+def test_minibatch_generator(golden_meta):
+    m = golden_meta["minibatch"]
+    z = np.load(golden_path("minibatch.npz"))
+    fields = {k[3:]: z[k] for k in z.files if k.startswith("in/") and k != "in/gen_state"}
+    perm, mb, _ = O.minibatch_indices(m["N"], m["T"], m["M"], z["in/gen_state"])
+    order = {"obs_policy": "obs_policy", "obs_extra": "obs_extra", "actions": "actions", "target_values": "values",
+             "advantages": "advantages", "returns": "returns", "old_logp": "actions_log_prob", "old_mu": "mu",
+             "old_sigma": "sigma"}
+    batches = list(O.minibatches(fields, perm, mb, m["M"], m["E"]))
+    assert len(batches) == m["num_batches"]
+    for j, b in enumerate(batches):
+        for out_name, in_name in order.items():
+            assert np.array_equal(b[in_name], z[f"mb{j}/{out_name}"]), (j, out_name)
+
+
+def _loss_kwargs(m):
+    kw = m["ppo_kw"]
+    return dict(clip_param=kw.get("clip_param", 0.2), value_loss_coef=kw.get("value_loss_coef", 1.0),
+                entropy_coef=kw.get("entropy_coef", 0.01), use_clipped_value_loss=kw.get("use_clipped_value_loss", True),
+                compute_kl=m["adaptive"],
+                normalize_advantage_per_mini_batch=kw.get("normalize_advantage_per_mini_batch", False))
+
+
+def _rel_err(a, ref):
+    a = np.asarray(a, np.float64)
+    ref = np.asarray(ref, np.float64)
+    return float(np.max(np.abs(a - ref)) / (np.max(np.abs(ref)) + 1e-30))
+
+
+def test_loss_and_gradients(golden_meta):
+    for name, m in sorted(golden_meta["loss"].items()):
+        z = np.load(golden_path(f"loss_{name}.npz"))
+        for j in range(m["num_batches"]):
+            g = lambda k: z[f"mb{j}/{k}"]  # noqa: E731
+            o = O.ppo_loss(g("mu"), g("sigma"), g("V"), g("actions"), g("old_logp"), g("advantages"),
+                           g("target_values"), g("returns"), g("old_mu"), g("old_sigma"), **_loss_kwargs(m))
+            assert _rel_err(o["dmu"], g("dmu")) < 1e-5, (name, j)
+            assert _rel_err(o["dsigma"], g("dsigma")) < 1e-5, (name, j)
+            assert _rel_err(o["dV"], g("dV").reshape(-1)) < 1e-5, (name, j)
+            if m["adaptive"]:
+                assert abs(o["kl_mean"] - float(g("kl_mean"))) <= 1e-5 * abs(float(g("kl_mean"))) + 1e-9
+            if m["num_batches"] == 1:
+                for k in ("surrogate", "value_function", "entropy"):
+                    assert abs(o[k] - m["loss_dict"][k]) <= 1e-5 * abs(m["loss_dict"][k]) + 1e-7, (name, k)
