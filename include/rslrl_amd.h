@@ -137,6 +137,9 @@ typedef struct {
 } rslrl_ppo_loss_args_t;
 
 #define RSLRL_PPO_LOSS_MAX_ACTIONS 64
+/* The workspace starts with an arrival counter that must be ZERO when the workspace is first used
+ * (e.g. hipMemset once after allocation); every call leaves it zero again.  The partial sums are folded
+ * by the last-arriving workgroup inside the one loss launch (no separate reduction kernel). */
 size_t rslrl_ppo_loss_workspace_bytes(int64_t B, int32_t A);
 int rslrl_ppo_loss_fwd_bwd(const rslrl_ppo_loss_args_t* args /* host struct */, void* workspace,
                            size_t workspace_bytes, rslrl_stream_t stream);

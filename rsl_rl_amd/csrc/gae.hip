@@ -36,11 +36,13 @@ struct GaeStep {
     }
 };
 
-template <int TMAX>
+// EXACT: T == TMAX, the `t < T` guards fold away and all 3*T loads issue back to back.
+template <int TMAX, bool EXACT>
 __global__ __launch_bounds__(kBlock) void gae_scan_kernel(
     const float* __restrict__ values, const float* __restrict__ rewards, const uint8_t* __restrict__ dones,
-    const float* __restrict__ last_values, float gamma, float lam, int T, int64_t N,
+    const float* __restrict__ last_values, float gamma, float lam, int T_, int64_t N,
     float* __restrict__ returns, float* __restrict__ advantages, double2* __restrict__ partials) {
+    const int T = EXACT ? TMAX : T_;
     __shared__ double scratch[2][kBlock / kWave];
     double s = 0.0, ss = 0.0;
     const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
@@ -163,7 +165,12 @@ int elementwise_blocks(int64_t n) {
 template <int TMAX>
 void launch_scan(int nb, hipStream_t st, const float* v, const float* r, const uint8_t* d, const float* lv,
                  float g, float l, int T, int64_t N, float* ret, float* adv, double2* part) {
-    hipLaunchKernelGGL(gae_scan_kernel<TMAX>, dim3(nb), dim3(kBlock), 0, st, v, r, d, lv, g, l, T, N, ret, adv, part);
+    if (T == TMAX)
+        hipLaunchKernelGGL((gae_scan_kernel<TMAX, true>), dim3(nb), dim3(kBlock), 0, st, v, r, d, lv, g, l, T, N, ret,
+                           adv, part);
+    else
+        hipLaunchKernelGGL((gae_scan_kernel<TMAX, false>), dim3(nb), dim3(kBlock), 0, st, v, r, d, lv, g, l, T, N, ret,
+                           adv, part);
 }
 
 }  // namespace

@@ -15,12 +15,14 @@
 // Bytes per sample (sigma shared): read 4A (mu) + 4A (actions) + 8A (old mu, sigma) + 20 (old_logp,
 // adv, target V, returns, V), write 4A (d mu) + 4 (d V) = 20A + 24.
 
+#include <cstdlib>
+
 #include "common.h"
 
 namespace rslrl {
 namespace {
 
-constexpr int kMaxBlocks = 2048;
+constexpr int kMaxBlocks = 512;  // a lane handles ~3 samples at C3; the last block folds <= 512 partials
 constexpr float kLogSqrt2Pi = 0.91893853320467274178f;  // log(sqrt(2*pi)), normal.py log_prob
 constexpr float kEntC = 1.41893853320467274178f;         // 0.5 + 0.5*log(2*pi), normal.py entropy
 
@@ -55,6 +57,7 @@ struct LossParams {
     int64_t grad_sigma_stride;
     float* grad_values;
     const float* adv_stats;  // [2] = (mean, std) when normalize_adv
+    float* stats;
 };
 
 template <int MAXA, bool VEC>
@@ -100,24 +103,58 @@ __device__ __forceinline__ void max_grads(float a, float b, float g, float& ga, 
 // Loss-term columns of the per-block partials; shared-sigma gradient columns follow.
 enum { kColSurr = 0, kColValue, kColEnt, kColKl, kNumScalarCols };
 
-template <int MAXA, bool VEC>
-__global__ __launch_bounds__(kBlock) void ppo_loss_kernel(LossParams p, double* __restrict__ partials) {
+// One lane per sample.  SHARED: sigma is the policy's [A] vector -> its log, reciprocals and the
+// entropy are per-action constants computed once per lane; otherwise sigma is read per row.
+// log-prob and the gradients use those reciprocals (<= 2 ulp from the reference's divisions, inside the
+// 1e-5 tolerance); the KL keeps the reference's exact fp32 operation sequence (true divisions, logf)
+// because near a zero KL its terms cancel to ~1e-5 and any reordering would show up relative to it.
+// EXACT: A == MAXA, so every `a < A` guard folds away at compile time (runtime-A guards split the
+// row loads into branchy basic blocks that serialise on their waits).
+template <int MAXA, bool VEC, bool SHARED, bool EXACT>
+__global__ __launch_bounds__(kBlock) void ppo_loss_kernel(LossParams p, double* __restrict__ partials,
+                                                          unsigned* __restrict__ ticket, float value_loss_coef,
+                                                          float entropy_coef) {
     constexpr int kMaxCols = kNumScalarCols + MAXA;
     __shared__ double wave_part[kBlock / kWave][kMaxCols];
-    const int A = p.A;
-    const bool shared_sigma = p.sigma_mode == 0;
-    const int ncols = kNumScalarCols + (shared_sigma ? A : 0);
+    __shared__ int last_block;
+    const int A = EXACT ? MAXA : p.A;
+    const int ncols = kNumScalarCols + (SHARED ? A : 0);
 
-    float sig_shared[MAXA];
-    if (shared_sigma) load_row<MAXA, false>(p.sigma, A, sig_shared);
+    // per-action constants of a shared sigma: computed once per block by the first A lanes, then
+    // broadcast from LDS into every lane's registers
+    float c_s[MAXA], c_ls[MAXA], c_inv_den[MAXA], c_inv_s[MAXA], c_inv_s3[MAXA];
+    float ent_shared = 0.0f;
+    if constexpr (SHARED) {
+        __shared__ float k_const[5][MAXA];
+        if (threadIdx.x < A) {
+            const float s = p.sigma[threadIdx.x];
+            const float inv_s = 1.0f / s;
+            k_const[0][threadIdx.x] = s;
+            k_const[1][threadIdx.x] = logf(s);
+            k_const[2][threadIdx.x] = 1.0f / __fmul_rn(2.0f, __fmul_rn(s, s));
+            k_const[3][threadIdx.x] = inv_s;
+            k_const[4][threadIdx.x] = inv_s * inv_s * inv_s;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int a = 0; a < MAXA; ++a) {
+            if (a < A) {
+                c_s[a] = k_const[0][a];
+                c_ls[a] = k_const[1][a];
+                c_inv_den[a] = k_const[2][a];
+                c_inv_s[a] = k_const[3][a];
+                c_inv_s3[a] = k_const[4][a];
+                ent_shared = __fadd_rn(ent_shared, __fadd_rn(kEntC, c_ls[a]));
+            }
+        }
+    }
     float adv_mean = 0.0f, adv_den = 1.0f;
     if (p.normalize_adv) {
         adv_mean = p.adv_stats[0];
         adv_den = __fadd_rn(p.adv_stats[1], 1e-8f);  // ppo.py:223  (std + 1e-8)
     }
 
-    // per-lane sums stay fp32 (a lane sees ~B / (grid * 256) <= a few samples); the cross-lane and
-    // cross-block folds are fp64.
+    // per-lane sums stay fp32 (a lane sees a few samples); cross-lane / cross-block folds are fp64
     float acc[kMaxCols];
 #pragma unroll
     for (int c = 0; c < kMaxCols; ++c) acc[c] = 0.0f;
@@ -126,15 +163,12 @@ __global__ __launch_bounds__(kBlock) void ppo_loss_kernel(LossParams p, double* 
     for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < p.B; i += stride) {
         float mu[MAXA], sg[MAXA], x[MAXA], omu[MAXA], osg[MAXA];
         load_row<MAXA, VEC>(p.mu + i * p.mu_stride, A, mu);
-        if (shared_sigma) {
-#pragma unroll
-            for (int a = 0; a < MAXA; ++a) sg[a] = sig_shared[a];
-        } else {
-            load_row<MAXA, VEC>(p.sigma + i * p.sigma_stride, A, sg);
-        }
+        if constexpr (!SHARED) load_row<MAXA, VEC>(p.sigma + i * p.sigma_stride, A, sg);
         load_row<MAXA, VEC>(p.actions + i * A, A, x);
-        load_row<MAXA, VEC>(p.old_mu + i * A, A, omu);
-        load_row<MAXA, VEC>(p.old_sigma + i * A, A, osg);
+        if (p.compute_kl) {
+            load_row<MAXA, VEC>(p.old_mu + i * A, A, omu);
+            load_row<MAXA, VEC>(p.old_sigma + i * A, A, osg);
+        }
         const float old_logp = p.old_logp[i];
         float adv = p.adv[i];
         const float V = p.values[i];
@@ -143,95 +177,104 @@ __global__ __launch_bounds__(kBlock) void ppo_loss_kernel(LossParams p, double* 
         if (p.normalize_adv) adv = __fdiv_rn(__fsub_rn(adv, adv_mean), adv_den);
 
         // Normal(mu, sigma).log_prob(x).sum(-1), entropy().sum(-1), KL (normal.py; ppo.py:262-268)
-        float logp = 0.0f, ent = 0.0f, kl = 0.0f;
+        float logp = 0.0f, ent = SHARED ? ent_shared : 0.0f, kl = 0.0f;
 #pragma unroll
         for (int a = 0; a < MAXA; ++a) {
             if (a < A) {
-                const float s = sg[a];
-                const float var = __fmul_rn(s, s);
-                const float ls = logf(s);
-                const float d = __fsub_rn(x[a], mu[a]);
-                const float num = -__fmul_rn(d, d);
-                const float den = __fmul_rn(2.0f, var);
-                logp = __fadd_rn(logp, __fsub_rn(__fsub_rn(__fdiv_rn(num, den), ls), kLogSqrt2Pi));
-                ent = __fadd_rn(ent, __fadd_rn(kEntC, ls));
+                float s, ls, inv_den;
+                if constexpr (SHARED) {
+                    s = c_s[a];
+                    ls = c_ls[a];
+                    inv_den = c_inv_den[a];
+                } else {
+                    s = sg[a];
+                    ls = logf(s);
+                    inv_den = 1.0f / (2.0f * s * s);
+                    ent += kEntC + ls;
+                }
+                const float d = x[a] - mu[a];
+                logp += (-(d * d) * inv_den - ls) - kLogSqrt2Pi;
                 if (p.compute_kl) {
                     const float os = osg[a];
                     const float dm = __fsub_rn(omu[a], mu[a]);
                     const float t1 = logf(__fadd_rn(__fdiv_rn(s, os), 1.0e-5f));
-                    const float t2 = __fdiv_rn(__fadd_rn(__fmul_rn(os, os), __fmul_rn(dm, dm)), __fmul_rn(2.0f, var));
+                    const float t2 = __fdiv_rn(__fadd_rn(__fmul_rn(os, os), __fmul_rn(dm, dm)),
+                                               __fmul_rn(2.0f, __fmul_rn(s, s)));
                     kl = __fadd_rn(kl, __fsub_rn(__fadd_rn(t1, t2), 0.5f));
                 }
             }
         }
 
         // surrogate (ppo.py:297-302)
-        const float ratio = expf(__fsub_rn(logp, old_logp));
+        const float ratio = expf(logp - old_logp);
         const float nadv = -adv;
-        const float surr = __fmul_rn(nadv, ratio);
+        const float surr = nadv * ratio;
         const float rc = fminf(fmaxf(ratio, p.ratio_lo), p.ratio_hi);
-        const float surr_c = __fmul_rn(nadv, rc);
-        const float surr_max = fmaxf(surr, surr_c);
+        const float surr_c = nadv * rc;
         float g_s, g_sc;
         max_grads(surr, surr_c, p.g_surr, g_s, g_sc);
         const bool in_clip = (ratio >= p.ratio_lo) && (ratio <= p.ratio_hi);
-        float g_ratio = __fmul_rn(g_s, nadv);
-        if (in_clip) g_ratio = __fadd_rn(g_ratio, __fmul_rn(g_sc, nadv));
-        const float g_logp = __fmul_rn(g_ratio, ratio);
+        const float g_ratio = g_s * nadv + (in_clip ? g_sc * nadv : 0.0f);
+        const float g_logp = g_ratio * ratio;
 
         // value loss (ppo.py:305-313)
         float vterm, dV;
         if (p.clipped_value) {
-            const float dv = __fsub_rn(V, tv);
-            const float vc = __fadd_rn(tv, fminf(fmaxf(dv, -p.clip), p.clip));
-            const float e1 = __fsub_rn(V, R);
-            const float e2 = __fsub_rn(vc, R);
-            const float vl = __fmul_rn(e1, e1);
-            const float vlc = __fmul_rn(e2, e2);
+            const float dv = V - tv;
+            const float vc = tv + fminf(fmaxf(dv, -p.clip), p.clip);
+            const float e1 = V - R;
+            const float e2 = vc - R;
+            const float vl = e1 * e1;
+            const float vlc = e2 * e2;
             vterm = fmaxf(vl, vlc);
             float g1, g2;
             max_grads(vl, vlc, p.g_value, g1, g2);
-            dV = __fmul_rn(__fmul_rn(g1, 2.0f), e1);
-            if (dv >= -p.clip && dv <= p.clip) dV = __fadd_rn(dV, __fmul_rn(__fmul_rn(g2, 2.0f), e2));
+            dV = 2.0f * g1 * e1;
+            if (dv >= -p.clip && dv <= p.clip) dV += 2.0f * g2 * e2;
         } else {
-            const float e = __fsub_rn(R, V);
-            vterm = __fmul_rn(e, e);
-            dV = -__fmul_rn(__fmul_rn(p.g_value, 2.0f), e);
+            const float e = R - V;
+            vterm = e * e;
+            dV = -2.0f * p.g_value * e;
         }
         p.grad_values[i] = dV;
 
-        // chain to mu, sigma through log_prob and entropy
+        // d/dmu = g_logp (x - mu) / sigma^2;  d/dsigma = g_logp ((x - mu)^2 / sigma^3 - 1 / sigma) + g_ent / sigma
         float gmu[MAXA], gsg[MAXA];
+        const float g2 = 2.0f * g_logp;
 #pragma unroll
         for (int a = 0; a < MAXA; ++a) {
             if (a < A) {
-                const float s = sg[a];
-                const float var = __fmul_rn(s, s);
-                const float d = __fsub_rn(x[a], mu[a]);
-                const float num = -__fmul_rn(d, d);
-                const float den = __fmul_rn(2.0f, var);
-                const float g_num = __fdiv_rn(g_logp, den);
-                const float g_den = __fdiv_rn(__fmul_rn(-g_logp, num), __fmul_rn(den, den));
-                gmu[a] = __fmul_rn(__fmul_rn(g_num, 2.0f), d);
-                const float g_s2 = __fmul_rn(__fmul_rn(__fmul_rn(2.0f, g_den), 2.0f), s);
-                gsg[a] = __fadd_rn(__fsub_rn(g_s2, __fdiv_rn(g_logp, s)), __fdiv_rn(p.g_ent, s));
+                float inv_den, inv_s, inv_s3;
+                if constexpr (SHARED) {
+                    inv_den = c_inv_den[a];
+                    inv_s = c_inv_s[a];
+                    inv_s3 = c_inv_s3[a];
+                } else {
+                    const float s = sg[a];
+                    inv_s = 1.0f / s;
+                    inv_den = 0.5f * inv_s * inv_s;
+                    inv_s3 = inv_s * inv_s * inv_s;
+                }
+                const float d = x[a] - mu[a];
+                gmu[a] = g2 * d * inv_den;
+                gsg[a] = g_logp * (d * d * inv_s3 - inv_s) + p.g_ent * inv_s;
             }
         }
         store_row<MAXA, VEC>(p.grad_mu + i * p.grad_mu_stride, A, gmu);
-        if (shared_sigma) {
+        if constexpr (SHARED) {
 #pragma unroll
             for (int a = 0; a < MAXA; ++a)
                 if (a < A) acc[kNumScalarCols + a] += gsg[a];
         } else {
             store_row<MAXA, VEC>(p.grad_sigma + i * p.grad_sigma_stride, A, gsg);
         }
-        acc[kColSurr] += surr_max;
+        acc[kColSurr] += fmaxf(surr, surr_c);
         acc[kColValue] += vterm;
         acc[kColEnt] += ent;
         acc[kColKl] += kl;
     }
 
-    // per-block partials: wave butterfly per column, then the 4 waves in order
+    // ---- per-block partials (column-major [ncols][gridDim.x]): wave butterfly per column, then waves in order
     const int lane = threadIdx.x & (kWave - 1);
     const int wid = threadIdx.x / kWave;
 #pragma unroll
@@ -242,43 +285,68 @@ __global__ __launch_bounds__(kBlock) void ppo_loss_kernel(LossParams p, double* 
         }
     }
     __syncthreads();
+    const int nb = gridDim.x;
+    // Partials are stored write-through (sc1: 8-byte agent-scope atomic stores), so no release fence is
+    // needed: a release (buffer_wbl2) would write back every dirty line of the XCD's L2 -- including
+    // all the gradient rows just stored -- once per block, which made the kernel slower the more
+    // blocks it had.  (MI355X_MICROARCH.md, "Valid forms": sc1 payload + drained waves + counter.)
     if (threadIdx.x < ncols) {
         double v = wave_part[0][threadIdx.x];
 #pragma unroll
         for (int w = 1; w < kBlock / kWave; ++w) v += wave_part[w][threadIdx.x];
-        partials[static_cast<int64_t>(blockIdx.x) * ncols + threadIdx.x] = v;
+        __hip_atomic_store(reinterpret_cast<unsigned long long*>(partials + static_cast<int64_t>(threadIdx.x) * nb +
+                                                                 blockIdx.x),
+                           __double_as_longlong(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-}
-
-// Folds the per-block partials (fixed order) into the loss scalars and the shared-sigma gradient.
-__global__ __launch_bounds__(kBlock) void ppo_loss_finalize_kernel(const double* __restrict__ partials, int nb, int ncols,
-                                                                   int64_t B, int normalize_adv, float value_loss_coef,
-                                                                   float entropy_coef, float* __restrict__ stats,
-                                                                   float* __restrict__ grad_sigma) {
-    __shared__ double scratch[kBlock / kWave];
-    for (int c = 0; c < ncols; ++c) {
-        double s = 0.0;
-        for (int r = threadIdx.x; r < nb; r += kBlock) s += partials[static_cast<int64_t>(r) * ncols + c];
-        s = block_sum(s, scratch);
-        if (threadIdx.x == 0) {
-            if (c < kNumScalarCols) {
-                stats[1 + c] = static_cast<float>(s / static_cast<double>(B));
-            } else {
-                grad_sigma[c - kNumScalarCols] = static_cast<float>(s);
-            }
+    // every storing wave drains, barrier, then one lane takes a ticket; the last arriver acquires once
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = (t == static_cast<unsigned>(nb) - 1);
+        if (last) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
+        last_block = last;
+    }
+    __syncthreads();
+    if (!last_block) return;
+    // fixed-order fold: column c is handled by wave c % 4, lanes stride over blocks.  The partials are
+    // read with sc1 buffer loads (L1 bypass) that, unlike atomic loads, the compiler keeps in flight
+    // together instead of serialising one round trip per load.
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        partials, 0, static_cast<int>(sizeof(double) * ncols * nb), 0x00020000);
+    for (int c = wid; c < ncols; c += kBlock / kWave) {
+        double s = 0.0;
+#pragma unroll 8
+        for (int r = lane; r < nb; r += kWave) {
+            const auto bits = __builtin_amdgcn_raw_buffer_load_b64(rsrc, (c * nb + r) * 8, 0, 16 /* sc1 */);
+            s += __builtin_bit_cast(double, bits);
+        }
+        s = wave_sum(s);
+        if (lane == 0) wave_part[0][c] = s;  // row 0 is free again: every wave passed the barrier above
     }
     __syncthreads();
     if (threadIdx.x == 0) {
+        const double Bd = static_cast<double>(p.B);
+        float* stats = p.stats;
+        stats[1] = static_cast<float>(wave_part[0][kColSurr] / Bd);
+        stats[2] = static_cast<float>(wave_part[0][kColValue] / Bd);
+        stats[3] = static_cast<float>(wave_part[0][kColEnt] / Bd);
+        stats[4] = static_cast<float>(wave_part[0][kColKl] / Bd);
         // ppo.py:315 in fp32: surrogate_loss + c_v * value_loss - c_e * entropy.mean()
-        const float l = __fsub_rn(__fadd_rn(stats[1], __fmul_rn(value_loss_coef, stats[2])),
-                                  __fmul_rn(entropy_coef, stats[3]));
-        stats[0] = l;
-        if (!normalize_adv) {  // adv statistics slots are only meaningful with per-mini-batch normalisation
+        stats[0] = __fsub_rn(__fadd_rn(stats[1], __fmul_rn(value_loss_coef, stats[2])),
+                             __fmul_rn(entropy_coef, stats[3]));
+        if (!p.normalize_adv) {
             stats[5] = 0.0f;
             stats[6] = 0.0f;
         }
         stats[7] = 0.0f;
+        __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm (stream-ordered)
+    }
+    if constexpr (SHARED) {
+        if (threadIdx.x < A) p.grad_sigma[threadIdx.x] = static_cast<float>(wave_part[0][kNumScalarCols + threadIdx.x]);
     }
 }
 
@@ -319,15 +387,46 @@ __global__ __launch_bounds__(kBlock) void mb_moments_fold_kernel(const double2* 
 
 constexpr int kMomentBlocks = 256;
 
-int loss_blocks(int64_t B) { return static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(ceil_div(B, kBlock), kMaxBlocks))); }
+// Grid cap; RSLRL_LOSS_MAX_BLOCKS overrides it (tuning knob, read once).
+int max_blocks() {
+    static const int v = [] {
+        const char* e = std::getenv("RSLRL_LOSS_MAX_BLOCKS");
+        const int x = e ? std::atoi(e) : 0;
+        return x > 0 ? std::min(x, 4096) : kMaxBlocks;
+    }();
+    return v;
+}
+
+int loss_blocks(int64_t B) {
+    return static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(ceil_div(B, kBlock), max_blocks())));
+}
+
+template <int MAXA, bool EXACT>
+void launch_loss_exact(const LossParams& p, bool vec, int nb, double* part, unsigned* ticket, float cv, float ce,
+                       hipStream_t st) {
+    const bool shared = p.sigma_mode == 0;
+    const dim3 g(nb), b(kBlock);
+    if (vec && shared)
+        hipLaunchKernelGGL((ppo_loss_kernel<MAXA, true, true, EXACT>), g, b, 0, st, p, part, ticket, cv, ce);
+    else if (vec)
+        hipLaunchKernelGGL((ppo_loss_kernel<MAXA, true, false, EXACT>), g, b, 0, st, p, part, ticket, cv, ce);
+    else if (shared)
+        hipLaunchKernelGGL((ppo_loss_kernel<MAXA, false, true, EXACT>), g, b, 0, st, p, part, ticket, cv, ce);
+    else
+        hipLaunchKernelGGL((ppo_loss_kernel<MAXA, false, false, EXACT>), g, b, 0, st, p, part, ticket, cv, ce);
+}
 
 template <int MAXA>
-void launch_loss(const LossParams& p, bool vec, int nb, double* part, hipStream_t st) {
-    if (vec)
-        hipLaunchKernelGGL((ppo_loss_kernel<MAXA, true>), dim3(nb), dim3(kBlock), 0, st, p, part);
+void launch_loss(const LossParams& p, bool vec, int nb, double* part, unsigned* ticket, float cv, float ce,
+                 hipStream_t st) {
+    if (p.A == MAXA)
+        launch_loss_exact<MAXA, true>(p, vec, nb, part, ticket, cv, ce, st);
     else
-        hipLaunchKernelGGL((ppo_loss_kernel<MAXA, false>), dim3(nb), dim3(kBlock), 0, st, p, part);
+        launch_loss_exact<MAXA, false>(p, vec, nb, part, ticket, cv, ce, st);
 }
+
+// workspace layout: [ticket word | pad to 256 B][fp64 partials [cols][blocks] | pad][mini-batch moments]
+constexpr size_t kTicketBytes = 256;
 
 bool aligned16(const void* ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 15) == 0; }
 
@@ -338,7 +437,7 @@ using namespace rslrl;
 
 extern "C" size_t rslrl_ppo_loss_workspace_bytes(int64_t B, int32_t A) {
     const size_t cols = kNumScalarCols + static_cast<size_t>(A > 0 ? A : 0);
-    return align_up(sizeof(double) * cols * static_cast<size_t>(loss_blocks(B)), 256) +
+    return kTicketBytes + align_up(sizeof(double) * cols * static_cast<size_t>(loss_blocks(B)), 256) +
            sizeof(double2) * kMomentBlocks;
 }
 
@@ -359,9 +458,9 @@ extern "C" int rslrl_ppo_loss_fwd_bwd(const rslrl_ppo_loss_args_t* a, void* work
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     const int A = a->A;
     const int nb = loss_blocks(a->B);
-    const int ncols = kNumScalarCols + (a->sigma_mode == 0 ? A : 0);
-    double* part = static_cast<double*>(workspace);
-    double2* mpart = reinterpret_cast<double2*>(static_cast<char*>(workspace) +
+    unsigned* ticket = static_cast<unsigned*>(workspace);
+    double* part = reinterpret_cast<double*>(static_cast<char*>(workspace) + kTicketBytes);
+    double2* mpart = reinterpret_cast<double2*>(static_cast<char*>(workspace) + kTicketBytes +
                                                 align_up(sizeof(double) * (kNumScalarCols + A) * nb, 256));
 
     LossParams p{};
@@ -396,6 +495,7 @@ extern "C" int rslrl_ppo_loss_fwd_bwd(const rslrl_ppo_loss_args_t* a, void* work
     p.grad_sigma_stride = a->grad_sigma_stride;
     p.grad_values = a->grad_values;
     p.adv_stats = a->stats + 5;
+    p.stats = a->stats;
 
     if (p.normalize_adv) {
         const int mb = static_cast<int>(std::min<int64_t>(ceil_div(a->B, kBlock), kMomentBlocks));
@@ -411,21 +511,18 @@ extern "C" int rslrl_ppo_loss_fwd_bwd(const rslrl_ppo_loss_args_t* a, void* work
     if (a->sigma_mode == 1)
         vec = vec && (a->sigma_stride % 4 == 0) && (a->grad_sigma_stride % 4 == 0) && aligned16(a->sigma) &&
               aligned16(a->grad_sigma);
+    const float cv = a->value_loss_coef, ce = a->entropy_coef;
     if (A <= 4)
-        launch_loss<4>(p, vec, nb, part, st);
+        launch_loss<4>(p, vec, nb, part, ticket, cv, ce, st);
     else if (A <= 8)
-        launch_loss<8>(p, vec, nb, part, st);
+        launch_loss<8>(p, vec, nb, part, ticket, cv, ce, st);
     else if (A <= 12)
-        launch_loss<12>(p, vec, nb, part, st);
+        launch_loss<12>(p, vec, nb, part, ticket, cv, ce, st);
     else if (A <= 16)
-        launch_loss<16>(p, vec, nb, part, st);
+        launch_loss<16>(p, vec, nb, part, ticket, cv, ce, st);
     else if (A <= 32)
-        launch_loss<32>(p, vec, nb, part, st);
+        launch_loss<32>(p, vec, nb, part, ticket, cv, ce, st);
     else
-        launch_loss<64>(p, vec, nb, part, st);
-    int rc = launch_status();
-    if (rc != RSLRL_OK) return rc;
-    hipLaunchKernelGGL(ppo_loss_finalize_kernel, dim3(1), dim3(kBlock), 0, st, part, nb, ncols, a->B, p.normalize_adv,
-                       a->value_loss_coef, a->entropy_coef, a->stats, a->grad_sigma);
+        launch_loss<64>(p, vec, nb, part, ticket, cv, ce, st);
     return launch_status();
 }

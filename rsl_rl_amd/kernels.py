@@ -53,10 +53,12 @@ class _Workspace:
         self._bufs = {}
 
     def get(self, device: torch.device, key: str, nbytes: int) -> torch.Tensor:
+        # zero-filled on allocation: the loss workspace begins with an arrival counter that the library
+        # expects to be zero before its first use and leaves zero after every call
         k = (device, key)
         buf = self._bufs.get(k)
         if buf is None or buf.numel() < nbytes:
-            buf = torch.empty(max(nbytes, 256), dtype=torch.uint8, device=device)
+            buf = torch.zeros(max(nbytes, 256), dtype=torch.uint8, device=device)
             self._bufs[k] = buf
         return buf
 

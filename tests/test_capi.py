@@ -53,7 +53,7 @@ def test_argument_validation_without_gpu():
     assert L.rslrl_ppo_loss_fwd_bwd(ctypes.byref(args), None, 0, None) == -1
     args.B, args.A = 10, 65
     assert L.rslrl_ppo_loss_fwd_bwd(ctypes.byref(args), None, 0, None) == -1
-    assert L.rslrl_ppo_loss_workspace_bytes(393216, 12) >= 8 * 16 * 1536
+    assert L.rslrl_ppo_loss_workspace_bytes(393216, 12) >= 8 * 16 * 512
     assert L.rslrl_compute_returns_workspace_bytes(24, 65536) >= 16 * 256
 
 
