@@ -17,6 +17,7 @@ oracle's CPU PPO iteration on the box's host cores, rank 0, N=1 only, bounded sa
 from __future__ import annotations
 
 import argparse
+import contextlib
 import json
 import os
 import sys
@@ -101,7 +102,8 @@ def main():
 
     torch.manual_seed(1)  # policy init; the env stream is seeded per rank
     env = SyntheticVecEnv(args.num_envs, args.num_obs, args.num_actions, device=device, seed=rank)
-    runner = OnPolicyRunner(env, train_cfg(args), log_dir=None, device=device)  # inits RCCL when world > 1
+    with contextlib.redirect_stdout(sys.stderr):  # stdout carries only the result line
+        runner = OnPolicyRunner(env, train_cfg(args), log_dir=None, device=device)  # inits RCCL when world > 1
 
     def barrier():
         if world > 1:

@@ -2,7 +2,8 @@
 
 An nn.Sequential of Linear + activation blocks whose module indices ("0", "2", ...) match the
 reference, so state_dict keys (actor.0.weight, ...) and checkpoints are interchangeable.  The GEMMs run
-through PyTorch-ROCm (hipBLASLt); fusing them onto MFMA is a later step.
+through PyTorch-ROCm (hipBLASLt) with the weight gradient as a split-K batched GEMM (networks/linear.py);
+fusing the whole MLP onto MFMA is a later step.
 """
 
 from __future__ import annotations
@@ -13,6 +14,7 @@ import torch
 import torch.nn as nn
 
 from ..utils import resolve_nn_activation
+from .linear import linear
 
 
 class MLP(nn.Sequential):
@@ -47,7 +49,7 @@ class MLP(nn.Sequential):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         for layer in self:
-            x = layer(x)
+            x = linear(x, layer.weight, layer.bias) if isinstance(layer, nn.Linear) else layer(x)
         return x
 
     def reset(self, dones=None, hidden_states=None):
