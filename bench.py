@@ -31,6 +31,19 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+# per-launch HBM traffic of the hot-path kernels from rocprofv3 FETCH_SIZE / WRITE_SIZE passes over this same
+# bench command (scripts/pmc_summary.py; raw counters next to it).  PMC passes serialise and slow the
+# run, so they are collected separately and the committed summary is reported here.
+PMC_TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r1_pmc_traffic.json")
+
+
+def pmc_traffic(kernel):
+    try:
+        with open(PMC_TRAFFIC_FILE) as f:
+            k = json.load(f)["kernels"].get(kernel)
+        return (k["traffic_bytes"], os.path.relpath(PMC_TRAFFIC_FILE, ROOT)) if k else (None, None)
+    except (OSError, ValueError, KeyError):
+        return None, None
 
 
 def train_cfg(args):
@@ -144,8 +157,9 @@ def main():
     roofline = None
     if dominant:
         ach = hot[dominant]["achieved_GBps"]
+        traffic, traffic_src = pmc_traffic(dominant)
         roofline = {"kernel": dominant, "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                    "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": None,
+                    "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": traffic, "traffic_source": traffic_src,
                     "algorithmic_bytes_per_launch": hot[dominant]["algorithmic_bytes_per_launch"],
                     "mean_launch_us": hot[dominant]["mean_us"]}
 

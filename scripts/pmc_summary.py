@@ -1,0 +1,76 @@
+"""Summarise rocprofv3 FETCH_SIZE / WRITE_SIZE passes into per-launch HBM traffic per kernel.
+
+    python scripts/pmc_summary.py --fetch DIR --write DIR [--calib-fetch DIR --calib-write DIR] -o profiles/X.json
+
+Correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE / WRITE_SIZE are in KB; on gfx950 FETCH_SIZE
+counts half of the bytes of a wide (16-B/lane) streaming read, WRITE_SIZE counts 16-B stores exactly.
+The calibration pass (scripts/pmc_calibration.py: a 512 MiB copyBuffer) is used to verify both factors
+on the box before they are applied: traffic = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 bytes per launch.
+"""
+
+import argparse
+import csv
+import glob
+import json
+import os
+from collections import defaultdict
+
+SHORT = {
+    "ppo_loss_kernel": "ppo_loss",
+    "gae_scan_kernel": "gae_scan",
+    "adv_normalize_kernel": "adv_normalize",
+    "moments_kernel": "moments",
+    "gather_rows_kernel": "gather_rows",
+    "__amd_rocclr_copyBuffer": "copyBuffer",
+}
+
+
+def load(d, counter):
+    files = glob.glob(os.path.join(d, "*", "*_counter_collection.csv")) + glob.glob(
+        os.path.join(d, "*_counter_collection.csv"))
+    out = defaultdict(list)
+    for f in files:
+        for r in csv.DictReader(open(f)):
+            if r["Counter_Name"] != counter:
+                continue
+            name = next((v for k, v in SHORT.items() if k in r["Kernel_Name"]), None)
+            if name:
+                out[name].append(float(r["Counter_Value"]))
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--fetch", required=True)
+    ap.add_argument("--write", required=True)
+    ap.add_argument("--calib-fetch")
+    ap.add_argument("--calib-write")
+    ap.add_argument("-o", "--out", required=True)
+    args = ap.parse_args()
+    res = {"units": "bytes per launch", "correction": "traffic = (2 * FETCH_SIZE + WRITE_SIZE) * 1024"}
+    if args.calib_fetch and args.calib_write:
+        cf = load(args.calib_fetch, "FETCH_SIZE")["copyBuffer"]
+        cw = load(args.calib_write, "WRITE_SIZE")["copyBuffer"]
+        copy_bytes = 512 * 1024 * 1024
+        res["calibration"] = {
+            "copy_bytes": copy_bytes,
+            "fetch_factor": copy_bytes / (sum(cf) / len(cf) * 1024),
+            "write_factor": copy_bytes / (sum(cw) / len(cw) * 1024),
+        }
+    f = load(args.fetch, "FETCH_SIZE")
+    w = load(args.write, "WRITE_SIZE")
+    kern = {}
+    for name in sorted(set(f) & set(w)):
+        fk = sum(f[name]) / len(f[name])
+        wk = sum(w[name]) / len(w[name])
+        kern[name] = {"launches": len(f[name]), "FETCH_SIZE_KB": round(fk, 1), "WRITE_SIZE_KB": round(wk, 1),
+                      "read_bytes": int(2 * fk * 1024), "write_bytes": int(wk * 1024),
+                      "traffic_bytes": int((2 * fk + wk) * 1024)}
+    res["kernels"] = kern
+    with open(args.out, "w") as fh:
+        json.dump(res, fh, indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
