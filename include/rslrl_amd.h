@@ -144,6 +144,25 @@ size_t rslrl_ppo_loss_workspace_bytes(int64_t B, int32_t A);
 int rslrl_ppo_loss_fwd_bwd(const rslrl_ppo_loss_args_t* args /* host struct */, void* workspace,
                            size_t workspace_bytes, rslrl_stream_t stream);
 
+/* ------------------------------------------------------------------------------------------------
+ * Actor/critic MLP hidden layers on fp32 MFMA -- rsl_rl/networks/mlp.py:59-114
+ * (nn.Linear + ELU(alpha=1) blocks) and their autograd backward.
+ *   rslrl_linear_fwd:       y[M,N] = act(x[M,K] weight[N,K]^T + bias[N]); act 0 = identity, 1 = ELU.
+ *   rslrl_linear_dgrad_elu: dz_prev[M,K] = (dz[M,Nred] weight_t[K,Nred]^T) * ELU'(h[M,K]), where h is the
+ *                           ELU output feeding this layer (ELU'(z) = 1 if h > 0 else h + 1), and the
+ *                           per-128-row-tile column sums of dz_prev into colsum_partials
+ *                           [K, rslrl_linear_tiles(M)] (-> the previous layer's bias gradient);
+ *                           weight_t is the layer weight transposed ([K, Nred] row-major).
+ *   rslrl_column_sum_fold:  out[N] = sum over tiles of partials[N, tiles] (fixed order).
+ * Requirements: N (resp. K) <= 256; K (resp. Nred) % 4 == 0; x/dz and the weights 16-byte aligned.
+ * ----------------------------------------------------------------------------------------------*/
+int64_t rslrl_linear_tiles(int64_t M);
+int rslrl_linear_fwd(const float* x, int64_t M, int32_t K, const float* weight, int32_t N, const float* bias,
+                     int32_t activation, float* y, rslrl_stream_t stream);
+int rslrl_linear_dgrad_elu(const float* dz, int64_t M, int32_t Nred, const float* weight_t, int32_t K,
+                           const float* h, float* dz_prev, float* colsum_partials, rslrl_stream_t stream);
+int rslrl_column_sum_fold(const float* partials, int64_t tiles, int32_t N, float* out, rslrl_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -32,6 +32,10 @@ EXPORTED_SYMBOLS = (
     "rslrl_gather_rows",
     "rslrl_ppo_loss_workspace_bytes",
     "rslrl_ppo_loss_fwd_bwd",
+    "rslrl_linear_tiles",
+    "rslrl_linear_fwd",
+    "rslrl_linear_dgrad_elu",
+    "rslrl_column_sum_fold",
 )
 
 MAX_GATHER_FIELDS = 16
@@ -108,6 +112,14 @@ def _declare(L):
     L.rslrl_ppo_loss_workspace_bytes.argtypes = [I64, I32]
     L.rslrl_ppo_loss_fwd_bwd.restype = ctypes.c_int
     L.rslrl_ppo_loss_fwd_bwd.argtypes = [ctypes.POINTER(PPOLossArgs), P, SZ, P]
+    L.rslrl_linear_tiles.restype = I64
+    L.rslrl_linear_tiles.argtypes = [I64]
+    L.rslrl_linear_fwd.restype = ctypes.c_int
+    L.rslrl_linear_fwd.argtypes = [P, I64, I32, P, I32, P, I32, P, P]
+    L.rslrl_linear_dgrad_elu.restype = ctypes.c_int
+    L.rslrl_linear_dgrad_elu.argtypes = [P, I64, I32, P, I32, P, P, P, P]
+    L.rslrl_column_sum_fold.restype = ctypes.c_int
+    L.rslrl_column_sum_fold.argtypes = [P, I64, I32, P, P]
 
 
 def lib():

@@ -1,9 +1,10 @@
 """MLP network (rsl_rl/networks/mlp.py:15-120).
 
 An nn.Sequential of Linear + activation blocks whose module indices ("0", "2", ...) match the
-reference, so state_dict keys (actor.0.weight, ...) and checkpoints are interchangeable.  The GEMMs run
-through PyTorch-ROCm (hipBLASLt) with the weight gradient as a split-K batched GEMM (networks/linear.py);
-fusing the whole MLP onto MFMA is a later step.
+reference, so state_dict keys (actor.0.weight, ...) and checkpoints are interchangeable.  On a ROCm
+device a Linear+ELU stack runs on the fused fp32 MFMA kernels of networks/fused_mlp.py (bias+ELU in the
+GEMM epilogue, ELU'+bias-gradient in the data-gradient epilogue, split-K weight gradients); any other
+structure runs layer by layer through PyTorch-ROCm with the split-K weight gradient (networks/linear.py).
 """
 
 from __future__ import annotations
@@ -14,6 +15,7 @@ import torch
 import torch.nn as nn
 
 from ..utils import resolve_nn_activation
+from .fused_mlp import fusable_structure, fused_mlp_forward
 from .linear import linear
 
 
@@ -38,6 +40,7 @@ class MLP(nn.Sequential):
             layers.append(resolve_nn_activation(last_activation))
         for i, layer in enumerate(layers):
             self.add_module(str(i), layer)
+        self._fused = fusable_structure(self)
 
     def init_weights(self, scales):
         """Orthogonal weights with per-layer gain (scales indexed by module index) and zero biases."""
@@ -48,6 +51,9 @@ class MLP(nn.Sequential):
                 nn.init.zeros_(module.bias)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        # Linear+ELU stacks on a ROCm device run on the fused MFMA kernels (networks/fused_mlp.py)
+        if self._fused and x.is_cuda and x.dim() == 2 and x.dtype == torch.float32:
+            return fused_mlp_forward(self, x)
         for layer in self:
             x = linear(x, layer.weight, layer.bias) if isinstance(layer, nn.Linear) else layer(x)
         return x

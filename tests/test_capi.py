@@ -57,6 +57,15 @@ def test_argument_validation_without_gpu():
     assert L.rslrl_compute_returns_workspace_bytes(24, 65536) >= 16 * 256
 
 
+def test_linear_abi_rejects_bad_shapes():
+    L = _lib.lib()
+    assert L.rslrl_linear_fwd(8, 10, 6, 8, 16, 8, 1, 8, None) == -1  # K % 4 != 0
+    assert L.rslrl_linear_fwd(8, 10, 8, 8, 300, 8, 1, 8, None) == -1  # N > 256
+    assert L.rslrl_linear_fwd(8, 0, 8, 8, 16, 8, 1, 8, None) == 0  # empty batch
+    assert L.rslrl_linear_dgrad_elu(8, 10, 6, 8, 16, 8, 8, 8, None) == -1  # Nred % 4 != 0
+    assert L.rslrl_linear_tiles(393216) == 3072
+
+
 def test_randperm_rejects_bad_state():
     L = _lib.lib()
     out = np.empty(10, np.int32)
