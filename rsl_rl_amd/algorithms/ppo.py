@@ -45,6 +45,18 @@ def adapt_learning_rate(learning_rate: float, kl_mean: float, desired_kl: float)
     return learning_rate
 
 
+def adapt_learning_rate_device(lr: torch.Tensor, kl_mean: torch.Tensor, desired_kl: float) -> torch.Tensor:
+    """ppo.py:280-284 without leaving the device: lr is an fp64 0-d tensor (the reference's Python float),
+    kl_mean the fp32 KL; the comparisons happen in fp32 against fp32(2 * kl*) / fp32(kl* / 2), exactly as
+    the reference's `tensor > python_float` does."""
+    kl = kl_mean.reshape(())
+    hi = torch.tensor(desired_kl * 2.0, dtype=kl.dtype, device=kl.device)
+    lo = torch.tensor(desired_kl / 2.0, dtype=kl.dtype, device=kl.device)
+    down = torch.clamp(lr / 1.5, min=1e-5)
+    up = torch.clamp(lr * 1.5, max=1e-2)
+    return torch.where(kl > hi, down, torch.where((kl < lo) & (kl > 0.0), up, lr))
+
+
 class PPO:
     """Proximal Policy Optimization algorithm (https://arxiv.org/abs/1707.06347)."""
 
@@ -106,7 +118,9 @@ class PPO:
 
         self.policy = policy
         self.policy.to(self.device)
-        self.optimizer = optim.Adam(self.policy.parameters(), lr=learning_rate)
+        # on a ROCm device Adam runs fused (one kernel per step) and accepts the device-resident lr of update()
+        on_gpu = str(device).startswith("cuda")
+        self.optimizer = optim.Adam(self.policy.parameters(), lr=learning_rate, fused=True if on_gpu else None)
         self.storage: RolloutStorage = None  # type: ignore
         self.transition = RolloutStorage.Transition()
 
@@ -196,7 +210,8 @@ class PPO:
                 p.grad = v
 
     def _sync_kl_and_lr(self, kl_mean: torch.Tensor):
-        """KL all-reduce + adaptive lr + fp32 lr rounding under multi-GPU (ppo.py:271-294)."""
+        """KL all-reduce + adaptive lr + fp32 lr rounding under multi-GPU (ppo.py:271-294), host version
+        (one device read-back); update() uses the device-resident _device_kl_and_lr."""
         if self.is_multi_gpu:
             torch.distributed.all_reduce(kl_mean, op=torch.distributed.ReduceOp.SUM)
             kl_mean /= self.gpu_world_size
@@ -207,6 +222,20 @@ class PPO:
         for param_group in self.optimizer.param_groups:
             param_group["lr"] = self.learning_rate
         return kl
+
+    def _device_kl_and_lr(self, kl_mean: torch.Tensor, lr: torch.Tensor) -> torch.Tensor:
+        """Same rule as _sync_kl_and_lr with the lr kept on the device: no host synchronisation per
+        mini-batch.  Returns the new fp64 lr; the optimizer reads it as a device tensor (fused Adam)."""
+        if self.is_multi_gpu:
+            torch.distributed.all_reduce(kl_mean, op=torch.distributed.ReduceOp.SUM)
+            kl_mean /= self.gpu_world_size
+        lr = adapt_learning_rate_device(lr, kl_mean, self.desired_kl)
+        if self.is_multi_gpu:  # the reference broadcasts the lr as an fp32 tensor (ppo.py:288-290)
+            lr = lr.float().double()
+        lr32 = lr.float()
+        for param_group in self.optimizer.param_groups:
+            param_group["lr"] = lr32
+        return lr
 
     def update(self):  # noqa: C901
         if self.symmetry:
@@ -221,6 +250,9 @@ class PPO:
         dev = self.storage.values.device
         sums = torch.zeros(4, dtype=torch.float64, device=dev)  # value, surrogate, entropy, rnd
         stats_buf = torch.empty(8, dtype=torch.float32, device=dev)
+        # device-resident lr (needs an optimizer that takes a tensor lr: fused / capturable Adam)
+        device_lr = adaptive and dev.type == "cuda" and self._optimizer_takes_tensor_lr()
+        lr_dev = torch.tensor(self.learning_rate, dtype=torch.float64, device=dev) if device_lr else None
 
         generator = self.storage.mini_batch_generator(self.num_mini_batches, self.num_learning_epochs)
         for (
@@ -252,7 +284,11 @@ class PPO:
                 normalize_advantage=self.normalize_advantage_per_mini_batch, stats=stats_buf,
             )
             if adaptive:
-                self._sync_kl_and_lr(stats[kernels.STATS_KL:kernels.STATS_KL + 1].clone())
+                kl_mean = stats[kernels.STATS_KL:kernels.STATS_KL + 1].clone()
+                if device_lr:
+                    lr_dev = self._device_kl_and_lr(kl_mean, lr_dev)
+                else:
+                    self._sync_kl_and_lr(kl_mean)
 
             # RND loss (ppo.py:352-363)
             if self.rnd:
@@ -288,11 +324,19 @@ class PPO:
 
         num_updates = self.num_learning_epochs * self.num_mini_batches
         host = (sums / num_updates).tolist()
+        if device_lr:  # back to a Python float, as the reference keeps it (logging, checkpoints)
+            self.learning_rate = lr_dev.item()
+            for param_group in self.optimizer.param_groups:
+                param_group["lr"] = self.learning_rate
         self.storage.clear()
         loss_dict = {"value_function": host[0], "surrogate": host[1], "entropy": host[2]}
         if self.rnd:
             loss_dict["rnd"] = host[3]
         return loss_dict
+
+    def _optimizer_takes_tensor_lr(self) -> bool:
+        d = self.optimizer.defaults
+        return bool(d.get("fused") or d.get("capturable"))
 
     # ------------------------------------------------------------------ multi-GPU (ppo.py:428-469)
     def broadcast_parameters(self):

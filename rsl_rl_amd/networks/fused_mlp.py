@@ -60,10 +60,6 @@ def linear_dgrad_elu(dz, w, h):
     return out, db
 
 
-def _elu_grad_torch(dh, h):
-    return torch.where(h > 0, dh, dh * (h + 1.0))
-
-
 class FusedMLPFunction(torch.autograd.Function):
     """y = MLP(x) for hidden ELU(alpha=1) layers; args: (x, W1, b1, ..., WL, bL)."""
 
@@ -96,12 +92,14 @@ class FusedMLPFunction(torch.autograd.Function):
             if l == 0:
                 dx = dz.mm(ws[0]) if ctx.needs_input_grad[0] else None
                 break
-            # dZ_{l-1} = (dZ_l W_l) * ELU'(H_{l-1}), db_{l-1} = column sums
-            if dz.shape[1] % 4 == 0:
-                dz, grads_b[l - 1] = linear_dgrad_elu(dz, ws[l], h_in)
-            else:  # e.g. the critic's 1-wide output layer: an outer product, cheaper in torch
-                dz = _elu_grad_torch(dz.mm(ws[l]), h_in)
-                grads_b[l - 1] = dz.sum(0)
+            # dZ_{l-1} = (dZ_l W_l) * ELU'(H_{l-1}), db_{l-1} = column sums; a reduction width that is not a
+            # multiple of 4 (the critic's 1-wide output) is zero-padded to the next multiple
+            w = ws[l]
+            pad = (-dz.shape[1]) % 4
+            if pad:
+                dz = F.pad(dz, (0, pad))
+                w = F.pad(w, (0, 0, 0, pad))
+            dz, grads_b[l - 1] = linear_dgrad_elu(dz, w, h_in)
         out = [dx]
         for gw, gb in zip(grads_w, grads_b):
             out += [gw, gb]
