@@ -31,7 +31,7 @@ extern "C" {
 
 typedef struct ihipStream_t* rslrl_stream_t; /* == hipStream_t */
 
-#define RSLRL_ABI_VERSION 1
+#define RSLRL_ABI_VERSION 2
 
 enum {
     RSLRL_OK = 0,
@@ -154,14 +154,49 @@ int rslrl_ppo_loss_fwd_bwd(const rslrl_ppo_loss_args_t* args /* host struct */, 
  *                           [K, rslrl_linear_tiles(M)] (-> the previous layer's bias gradient);
  *                           weight_t is the layer weight transposed ([K, Nred] row-major).
  *   rslrl_column_sum_fold:  out[N] = sum over tiles of partials[N, tiles] (fixed order).
+ *   bimage (both calls): NULL -> exact f32 arithmetic (v_mfma_f32_32x32x2_f32, a k-ordered f32 fma
+ *                           chain) on weight / weight_t.  Non-NULL -> the "x6" split-bf16 path: the B
+ *                           operand comes from an image built by rslrl_linear_prepare_bimage (weight / weight_t
+ *                           may then be NULL), every fp32 operand is split into three bf16 planes and six bf16
+ *                           MFMA products per k step accumulate in fp32 -- the error of an fp32 GEMM at 2.67x
+ *                           fewer MFMA cycles (tests/test_gpu_fused_mlp.py: error vs fp64 next to torch fp32).
+ *   rslrl_linear_prepare_bimage: image of the B operand B[n][k], n < rows <= 256, k < depth:
+ *                           B[n][k] = transposed ? src[k * rows + n] : src[n * depth + k].  For linear_fwd
+ *                           pass the weight [N, K] (rows N, depth K, transposed 0); for linear_dgrad_elu the
+ *                           weight [Nred, K] itself with rows K, depth Nred, transposed 1.  The image is
+ *                           rslrl_linear_bimage_bytes(depth) bytes, 16-byte aligned; it stays valid until the
+ *                           weight changes.
+ *   rslrl_linear_prepare_bimages: the same for n <= 16 images in one launch (one descriptor each).
  * Requirements: N (resp. K) <= 256; K (resp. Nred) % 4 == 0; x/dz and the weights 16-byte aligned.
  * ----------------------------------------------------------------------------------------------*/
 int64_t rslrl_linear_tiles(int64_t M);
+size_t rslrl_linear_bimage_bytes(int32_t depth);
+int rslrl_linear_prepare_bimage(const float* src, int32_t rows, int32_t depth, int32_t transposed, void* image,
+                                rslrl_stream_t stream);
+typedef struct {
+    const float* src;
+    void* image;
+    int32_t rows;
+    int32_t depth;
+    int32_t transposed;
+    int32_t reserved; /* 0 */
+} rslrl_bimage_desc_t;
+#define RSLRL_MAX_BIMAGES 16
+int rslrl_linear_prepare_bimages(const rslrl_bimage_desc_t* descs, int32_t n, rslrl_stream_t stream);
 int rslrl_linear_fwd(const float* x, int64_t M, int32_t K, const float* weight, int32_t N, const float* bias,
-                     int32_t activation, float* y, rslrl_stream_t stream);
+                     int32_t activation, float* y, const void* bimage, rslrl_stream_t stream);
 int rslrl_linear_dgrad_elu(const float* dz, int64_t M, int32_t Nred, const float* weight_t, int32_t K,
-                           const float* h, float* dz_prev, float* colsum_partials, rslrl_stream_t stream);
+                           const float* h, float* dz_prev, float* colsum_partials, const void* bimage,
+                           rslrl_stream_t stream);
 int rslrl_column_sum_fold(const float* partials, int64_t tiles, int32_t N, float* out, rslrl_stream_t stream);
+
+/* Weight gradient of a linear layer on the x6 path: dw[N,K] = dz[M,N]^T x[M,K] (the autograd backward of
+ * nn.Linear.weight; the reference's cuBLAS GEMM).  N, K <= 256 and % 4 == 0; dz, x 16-byte aligned.  The
+ * rows are split over workgroups whose partial tiles go to the workspace
+ * (rslrl_linear_wgrad_workspace_bytes) and are added in a fixed order in fp64: deterministic. */
+size_t rslrl_linear_wgrad_workspace_bytes(int64_t M, int32_t N, int32_t K);
+int rslrl_linear_wgrad(const float* dz, const float* x, int64_t M, int32_t N, int32_t K, float* dw, void* workspace,
+                       size_t workspace_bytes, rslrl_stream_t stream);
 
 #ifdef __cplusplus
 }

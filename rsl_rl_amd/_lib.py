@@ -18,7 +18,7 @@ import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 LIB_PATH = os.path.join(LIB_DIR, "librslrl_amd.so")
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 # symbols declared in include/rslrl_amd.h (tests/test_capi.py checks the header against this list)
 EXPORTED_SYMBOLS = (
@@ -33,9 +33,14 @@ EXPORTED_SYMBOLS = (
     "rslrl_ppo_loss_workspace_bytes",
     "rslrl_ppo_loss_fwd_bwd",
     "rslrl_linear_tiles",
+    "rslrl_linear_bimage_bytes",
+    "rslrl_linear_prepare_bimage",
+    "rslrl_linear_prepare_bimages",
     "rslrl_linear_fwd",
     "rslrl_linear_dgrad_elu",
     "rslrl_column_sum_fold",
+    "rslrl_linear_wgrad_workspace_bytes",
+    "rslrl_linear_wgrad",
 )
 
 MAX_GATHER_FIELDS = 16
@@ -52,6 +57,14 @@ class RslrlError(RuntimeError):
 
 class GatherField(ctypes.Structure):
     _fields_ = [("src", ctypes.c_void_p), ("dst", ctypes.c_void_p), ("row_bytes", ctypes.c_int64)]
+
+
+class BImageDesc(ctypes.Structure):
+    _fields_ = [("src", ctypes.c_void_p), ("image", ctypes.c_void_p), ("rows", ctypes.c_int32),
+                ("depth", ctypes.c_int32), ("transposed", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+MAX_BIMAGES = 16
 
 
 class PPOLossArgs(ctypes.Structure):
@@ -115,9 +128,19 @@ def _declare(L):
     L.rslrl_linear_tiles.restype = I64
     L.rslrl_linear_tiles.argtypes = [I64]
     L.rslrl_linear_fwd.restype = ctypes.c_int
-    L.rslrl_linear_fwd.argtypes = [P, I64, I32, P, I32, P, I32, P, P]
+    L.rslrl_linear_bimage_bytes.restype = SZ
+    L.rslrl_linear_bimage_bytes.argtypes = [I32]
+    L.rslrl_linear_prepare_bimage.restype = ctypes.c_int
+    L.rslrl_linear_prepare_bimage.argtypes = [P, I32, I32, I32, P, P]
+    L.rslrl_linear_prepare_bimages.restype = ctypes.c_int
+    L.rslrl_linear_prepare_bimages.argtypes = [ctypes.POINTER(BImageDesc), I32, P]
+    L.rslrl_linear_fwd.argtypes = [P, I64, I32, P, I32, P, I32, P, P, P]
     L.rslrl_linear_dgrad_elu.restype = ctypes.c_int
-    L.rslrl_linear_dgrad_elu.argtypes = [P, I64, I32, P, I32, P, P, P, P]
+    L.rslrl_linear_dgrad_elu.argtypes = [P, I64, I32, P, I32, P, P, P, P, P]
+    L.rslrl_linear_wgrad_workspace_bytes.restype = SZ
+    L.rslrl_linear_wgrad_workspace_bytes.argtypes = [I64, I32, I32]
+    L.rslrl_linear_wgrad.restype = ctypes.c_int
+    L.rslrl_linear_wgrad.argtypes = [P, P, I64, I32, I32, P, P, SZ, P]
     L.rslrl_column_sum_fold.restype = ctypes.c_int
     L.rslrl_column_sum_fold.argtypes = [P, I64, I32, P, P]
 

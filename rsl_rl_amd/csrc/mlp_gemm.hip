@@ -18,14 +18,17 @@
 // A[i][4t + 2h .. +1] and B[j][4t + 2h .. +1] with one ds_read_b64 each and feeds two MFMA k-steps
 // (step 2t uses k = 4t + 2h, step 2t+1 uses k = 4t + 2h + 1 -- the same mapping for A and B).
 
+#include <algorithm>
 #include <cstdlib>
+#include <string>
+#include <type_traits>
 
 #include "common.h"
+#include "x6_split.h"
 
 namespace rslrl {
 namespace {
 
-using f32x16 = __attribute__((ext_vector_type(16))) float;
 
 constexpr int kBM = 128;
 constexpr int kBN = 256;
@@ -46,6 +49,7 @@ struct GemmParams {
     int64_t M;
     int K;
     int N;
+    int64_t ctiles;    // dgrad: columns of colsum (= rslrl_linear_tiles(M), 128-row tiles)
 };
 
 // global -> registers for one K chunk: A: 128 x 16 floats = 512 float4 (1 per thread); B: 256 x 16 = 1024
@@ -89,6 +93,128 @@ __device__ __forceinline__ void store_chunk(const Stage& s, float* __restrict__ 
     float2* pb1 = reinterpret_cast<float2*>(b_lds + (r + 128) * kLd + 4 * q);
     pb1[0] = make_float2(s.b1.x, s.b1.y);
     pb1[1] = make_float2(s.b1.z, s.b1.w);
+}
+
+// expm1(v) for v <= 0 (the ELU's negative branch) in ~12 VALU instead of libm expm1f's ~27: degree-9
+// Taylor series (Horner, explicit fma) on [-0.5, 0] (truncation < 3e-10 relative), exp(v) - 1 below
+// (the subtraction is exact there, error = exp's ~1 ulp of a value <= 0.61 -> <= 2 ulp of the result).
+__device__ __forceinline__ float elu_neg(float v) {
+    float t = __fmaf_rn(v, 2.7557319e-6f, 2.4801587e-5f);
+    t = __fmaf_rn(v, t, 1.9841270e-4f);
+    t = __fmaf_rn(v, t, 1.3888889e-3f);
+    t = __fmaf_rn(v, t, 8.3333333e-3f);
+    t = __fmaf_rn(v, t, 4.1666667e-2f);
+    t = __fmaf_rn(v, t, 1.6666667e-1f);
+    t = __fmaf_rn(v, t, 0.5f);
+    t = __fmaf_rn(v, t, 1.0f);
+    const float poly = v * t;
+    const float e = __expf(v) - 1.0f;
+    return v > -0.5f ? poly : e;
+}
+
+// ---- epilogue of one wave's I x J grid of 32x32 tiles at (wrow0, wcol0).  C/D map of a tile:
+// col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5).  Tiles are processed in order b = J i + j;
+// for the ELU' epilogue the 16 h values of tile b + 1 are loaded before tile b is finished, so no h load
+// waits alone.  colpart[j] returns this lane's sum over its rows of column wcol0 + 32 j + (lane & 31).
+template <int EPI, int I, int J, bool FULLT>
+__device__ __forceinline__ void epilogue_tiles_impl(const GemmParams& p, f32x16 (&acc)[I][J], int64_t wrow0,
+                                                    int wcol0, float (&colpart)[J]) {
+    constexpr bool full = FULLT;
+    const int lane = threadIdx.x & 63;
+    const int h = lane >> 5;
+    const int l32 = lane & 31;
+#pragma unroll
+    for (int j = 0; j < J; ++j) colpart[j] = 0.f;
+    float hcur[16], hnext[16];
+    auto load_h = [&](int b, float (&dst)[16]) {
+        const int i = b / J, j = b % J;
+        const int col = wcol0 + j * 32 + l32;
+        const int64_t rbase = wrow0 + i * 32 + 4 * h;
+        const float* hp = p.h + rbase * p.N + col;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int roff = (r & 3) + 8 * (r >> 2);
+            dst[r] = (full || (rbase + roff < p.M && col < p.N)) ? hp[static_cast<int64_t>(roff) * p.N] : 0.f;
+        }
+    };
+    if constexpr (EPI == kEpiEluGrad) load_h(0, hcur);
+#pragma unroll
+    for (int b = 0; b < I * J; ++b) {
+        const int i = b / J, j = b % J;
+        if constexpr (EPI == kEpiEluGrad) {
+            if (b + 1 < I * J) load_h(b + 1, hnext);
+        }
+        const int col = wcol0 + j * 32 + l32;
+        const bool col_ok = col < p.N;
+        float bias = 0.f;
+        if constexpr (EPI != kEpiEluGrad) bias = col_ok ? p.bias[col] : 0.f;
+        const int64_t rbase = wrow0 + i * 32 + 4 * h;
+        float* cp = p.c + rbase * p.N + col;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int roff = (r & 3) + 8 * (r >> 2);
+            if (full || (rbase + roff < p.M && col_ok)) {
+                float v = acc[i][j][r];
+                if constexpr (EPI == kEpiBias) {
+                    v = v + bias;
+                } else if constexpr (EPI == kEpiBiasElu) {
+                    v = v + bias;
+                    v = v > 0.f ? v : elu_neg(v);  // torch ELU, alpha = 1
+                } else {
+                    const float hv = hcur[r];  // ELU'(z) = 1 if z > 0 else hv + 1
+                    v = hv > 0.f ? v : v * (hv + 1.f);
+                    colpart[j] += v;
+                }
+                // streaming store: the outputs are not re-read by this kernel, and keeping them out of L2
+                // keeps the B image and the A stream resident (-7% kernel time measured)
+                __builtin_nontemporal_store(v, cp + static_cast<int64_t>(roff) * p.N);
+            }
+        }
+        if constexpr (EPI == kEpiEluGrad) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) hcur[r] = hnext[r];
+        }
+    }
+}
+
+// full (wave-uniform): every row and column of the tile exists.  The two paths are separate code: a
+// runtime `full ||` test per element puts a branch around every store, and the compiler then waits
+// vmcnt(0) before each store (64 serialised stores per wave: the epilogue ran 3x longer).
+template <int EPI, int I, int J>
+__device__ __forceinline__ void epilogue_tiles(const GemmParams& p, f32x16 (&acc)[I][J], int64_t wrow0, int wcol0,
+                                               bool full, float (&colpart)[J]) {
+    if (full)
+        epilogue_tiles_impl<EPI, I, J, true>(p, acc, wrow0, wcol0, colpart);
+    else
+        epilogue_tiles_impl<EPI, I, J, false>(p, acc, wrow0, wcol0, colpart);
+}
+
+// f32 kernel epilogue: 128-row tile, waves 2 (m) x 4 (n) of 64 x 64; column sums over the tile's 128 rows
+// (lanes l and l+32 hold the two row halves, the two wm waves the two 64-row halves; fixed combine order)
+// -> colsum[col][blockIdx.x].  colred: 2 x kBN floats of LDS the caller no longer reads.
+template <int EPI>
+__device__ __forceinline__ void epilogue(const GemmParams& p, f32x16 (&acc)[2][2], int64_t row0, float* colred) {
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int wm = wave >> 2;
+    const int wn = wave & 3;
+    const int h = lane >> 5;
+    const int l32 = lane & 31;
+    const bool full = (row0 + kBM <= p.M) && (p.N == kBN);  // wave-uniform: no per-element bounds checks
+    float colpart[2];
+    epilogue_tiles<EPI, 2, 2>(p, acc, row0 + wm * 64, wn * 64, full, colpart);
+    if constexpr (EPI == kEpiEluGrad) {
+        __syncthreads();  // the LDS tiles are no longer read
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const float s = colpart[j] + __shfl_xor(colpart[j], 32, 64);
+            if (h == 0) colred[wm * kBN + wn * 64 + j * 32 + l32] = s;
+        }
+        __syncthreads();
+        // column-major partials [N][tiles]: the fold then reads each column contiguously
+        for (int col = threadIdx.x; col < p.N && col < kBN; col += kThreads)
+            p.colsum[static_cast<int64_t>(col) * gridDim.x + blockIdx.x] = colred[col] + colred[kBN + col];
+    }
 }
 
 // MINW = minimum waves per SIMD the register allocation must allow (4: two workgroups per CU, <= 128
@@ -143,74 +269,393 @@ __global__ __launch_bounds__(kThreads, MINW) void mlp_gemm_kernel(GemmParams p) 
         }
         __syncthreads();
     }
+    epilogue<EPI>(p, acc, row0, lds[0]);
+}
 
-    // ---- epilogue: C/D map of the 32x32 tile: col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5).
-    // Sub-tiles (i, j) are processed in order b = 2 i + j; for the ELU' epilogue the 16 h values of
-    // sub-tile b + 1 are loaded before sub-tile b is finished, so no h load waits alone.
-    float colpart[2] = {0.f, 0.f};
-    const bool full = (row0 + kBM <= p.M) && (p.N == kBN);  // wave-uniform: no per-element bounds checks
-    float hcur[16], hnext[16];
-    auto load_h = [&](int b, float (&dst)[16]) {
-        const int i = b >> 1, j = b & 1;
-        const int col = wn * 64 + j * 32 + l32;
-        const int64_t rbase = row0 + wm * 64 + i * 32 + 4 * h;
-        const float* hp = p.h + rbase * p.N + col;
+// ---- split-bf16 main loop ("x6"): fp32-accurate products on the bf16 MFMA (16x the f32 MFMA rate).
+// Every fp32 operand is split into three bf16 planes (x6_split.h); per 16-deep k step and 32x32 tile six
+// bf16 MFMAs accumulate a0b0 + a0b1 + a1b0 + a1b1 + a0b2 + a2b0 in fp32 -- the error of an fp32 GEMM
+// (tests/test_gpu_fused_mlp.py measures both against fp64) at 2.67x fewer MFMA cycles than
+// v_mfma_f32_32x32x2_f32.
+//
+// Tile: 256 rows x 256 columns per 512-thread workgroup (one per CU), 8 waves as 2 (M) x 4 (N), each wave
+// 128 x 64 = 4 x 2 MFMA tiles.  Operands: A (activations, fp32, read once from HBM) is fetched two chunks
+// ahead into registers and split while it is stored into LDS; B (the weights, re-read by every
+// workgroup from L2) is split once per call by bimage_kernel into an image that is byte-for-byte the
+// kernel's LDS image (three 16-B loads + ds_write_b128 per thread and chunk, no VALU).
+//
+// LDS image per buffer: [A plane 0..2][B plane 0..2], each plane [rows][16 bf16] = 32 B per row; the two
+// 16-B halves of a row are swapped on rows with (row >> 3) & 1, which makes both the staging stores
+// (ds_write_b64, 16-lane groups) and the fragment reads (ds_read_b128: lane l reads row l & 31, half l >> 5)
+// bank-conflict free.
+#ifdef RSLRL_STAMPS
+__device__ uint64_t* g_stamps;
+#endif
+constexpr int kX6RowB = 32;
+constexpr int kX6PlaneB = kBN * kX6RowB;  // 8 KiB
+constexpr int kX6ChunkB = 3 * kX6PlaneB;  // 24 KiB: one chunk of the B image
+
+__device__ __forceinline__ int swz(int row, int half) { return row * kX6RowB + 16 * (half ^ ((row >> 3) & 1)); }
+
+// B image: [chunk][plane][256 rows][32 B swizzled]; element (row n, k) = transposed ? src[k * rows + n] :
+// src[n * depth + k], zero for n >= rows or k >= depth.  One thread per (chunk, row, physical half);
+// blockIdx.y selects the image of a batch (one launch builds every image an MLP pass needs).
+constexpr int kMaxImages = 16;
+struct BImageBatch {
+    rslrl_bimage_desc_t d[kMaxImages];
+};
+
+__global__ __launch_bounds__(kBlock) void bimage_kernel(BImageBatch batch) {
+    const rslrl_bimage_desc_t& dsc = batch.d[blockIdx.y];
+    const int rows = dsc.rows, depth = dsc.depth;
+    const float* __restrict__ src = dsc.src;
+    const int nchunks = (depth + kKC - 1) / kKC;
+    const int id = blockIdx.x * kBlock + threadIdx.x;
+    if (id >= nchunks * kBN * 2) return;
+    const int c = id / (kBN * 2);
+    const int n = (id >> 1) % kBN;
+    const int ph = id & 1;
+    const int lh = ph ^ ((n >> 3) & 1);
+    float v[8];
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int roff = (r & 3) + 8 * (r >> 2);
-            dst[r] = (full || (rbase + roff < p.M && col < p.N)) ? hp[static_cast<int64_t>(roff) * p.N] : 0.f;
-        }
-    };
-    if constexpr (EPI == kEpiEluGrad) load_h(0, hcur);
+    for (int j = 0; j < 8; ++j) {
+        const int k = 16 * c + 8 * lh + j;
+        v[j] = (n < rows && k < depth) ? src[dsc.transposed ? static_cast<int64_t>(k) * rows + n
+                                                            : static_cast<int64_t>(n) * depth + k]
+                                       : 0.f;
+    }
+    uint2 lo[3], hi[3];
+    split4(make_float4(v[0], v[1], v[2], v[3]), lo[0], lo[1], lo[2]);
+    split4(make_float4(v[4], v[5], v[6], v[7]), hi[0], hi[1], hi[2]);
+    uint4* base = static_cast<uint4*>(dsc.image) + static_cast<int64_t>(c) * (kX6ChunkB / 16) +
+                  (n * kX6RowB + 16 * ph) / 16;
 #pragma unroll
-    for (int b = 0; b < 4; ++b) {
-        const int i = b >> 1, j = b & 1;
-        if constexpr (EPI == kEpiEluGrad) {
-            if (b + 1 < 4) load_h(b + 1, hnext);
-        }
-        const int col = wn * 64 + j * 32 + l32;
-        const bool col_ok = col < p.N;
-        float bias = 0.f;
-        if constexpr (EPI != kEpiEluGrad) bias = col_ok ? p.bias[col] : 0.f;
-        const int64_t rbase = row0 + wm * 64 + i * 32 + 4 * h;
-        float* cp = p.c + rbase * p.N + col;
+    for (int q = 0; q < 3; ++q) base[q * (kX6PlaneB / 16)] = make_uint4(lo[q].x, lo[q].y, hi[q].x, hi[q].y);
+}
+
+// A chunk: BM rows x 16 k = BM / 128 float4 per thread (unit u = t + 512 i: row u >> 2, k-quad u & 3).
+// FULL: the tile's rows exist and K % 16 == 0 -> no masks.
+template <int BM>
+struct AStage {
+    float4 v[BM / 128];
+};
+
+template <int BM, bool FULL>
+__device__ __forceinline__ AStage<BM> load_a(const GemmParams& p, int64_t row0, int k0) {
+    AStage<BM> s;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int roff = (r & 3) + 8 * (r >> 2);
-            if (full || (rbase + roff < p.M && col_ok)) {
-                float v = acc[i][j][r];
-                if constexpr (EPI == kEpiBias) {
-                    v = v + bias;
-                } else if constexpr (EPI == kEpiBiasElu) {
-                    v = v + bias;
-                    v = v > 0.f ? v : expm1f(v);  // torch ELU, alpha = 1
-                } else {
-                    const float hv = hcur[r];  // ELU'(z) = 1 if z > 0 else hv + 1
-                    v = hv > 0.f ? v : v * (hv + 1.f);
-                    colpart[j] += v;
-                }
-                cp[static_cast<int64_t>(roff) * p.N] = v;
-            }
-        }
-        if constexpr (EPI == kEpiEluGrad) {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) hcur[r] = hnext[r];
+    for (int i = 0; i < BM / 128; ++i) {
+        const int u = threadIdx.x + kThreads * i;
+        const int k = k0 + 4 * (u & 3);
+        const int64_t row = row0 + (u >> 2);
+        if constexpr (FULL) {
+            s.v[i] = *reinterpret_cast<const float4*>(p.a + row * p.K + k);
+        } else {
+            const bool row_ok = row < p.M;
+            s.v[i] = load4_masked(p.a + (row_ok ? row : row0) * p.K, row_ok && k < p.K, k);
         }
     }
-    if constexpr (EPI == kEpiEluGrad) {
-        // column sums over the tile's 128 rows: lanes l and l+32 hold the two row halves, the two wm waves
-        // the two 64-row halves; fixed combine order -> deterministic
-        __shared__ float colred[2][kBN];
-        __syncthreads();  // the LDS tiles are no longer read
+    return s;
+}
+
+template <int BM>
+__device__ __forceinline__ void store_a_split(const AStage<BM>& s, char* __restrict__ a_lds) {
+    constexpr int plane = BM * kX6RowB;
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const float s = colpart[j] + __shfl_xor(colpart[j], 32, 64);
-            if (h == 0) colred[wm][wn * 64 + j * 32 + l32] = s;
+    for (int i = 0; i < BM / 128; ++i) {
+        const int u = threadIdx.x + kThreads * i;
+        const int q = u & 3;
+        const int r = u >> 2;
+        const int off = swz(r, q >> 1) + 8 * (q & 1);
+        uint2 w0, w1, w2;
+        split4(s.v[i], w0, w1, w2);
+        *reinterpret_cast<uint2*>(a_lds + off) = w0;
+        *reinterpret_cast<uint2*>(a_lds + plane + off) = w1;
+        *reinterpret_cast<uint2*>(a_lds + 2 * plane + off) = w2;
+    }
+}
+
+// B chunk c of the image -> LDS: 1536 16-B units, thread t copies units t, t + 512, t + 1024; the LDS
+// destination of a wave's global_load_lds is (wave-uniform base) + 16 * lane.
+__device__ __forceinline__ void load_b_lds(const uint4* __restrict__ img, int c, char* b_lds) {
+    const int t = threadIdx.x;
+    const uint4* src = img + static_cast<int64_t>(c) * (kX6ChunkB / 16);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const int u = t + kThreads * i;
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + u),
+                                         (__attribute__((address_space(3))) void*)(b_lds + 16 * (u & ~63)), 16, 0, 0);
+    }
+}
+
+__device__ __forceinline__ bf16x8 read_frag(const char* __restrict__ plane, int row, int h) {
+    return __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(plane + swz(row, h)));
+}
+
+// BM = 128: waves 2 (M) x 4 (N) of 64 x 64 (2 x 2 MFMA tiles), two workgroups per CU.
+// BM = 256: waves 2 x 4 of 128 x 64 (4 x 2 MFMA tiles), one workgroup per CU.
+template <int EPI, bool FULL, int BM, int MINW = (BM == 128 ? 4 : 2)>
+__global__ __launch_bounds__(kThreads, MINW) void mlp_gemm_x6_kernel(GemmParams p,
+                                                                                 const uint4* __restrict__ bimg) {
+    constexpr int I = BM / 64;
+    constexpr int planeA = BM * kX6RowB;
+    constexpr int bufBytes = 3 * planeA + kX6ChunkB;
+    __shared__ __attribute__((aligned(16))) char lds[2][bufBytes];
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int wm = wave >> 2;  // rows wm * BM / 2
+    const int wn = wave & 3;   // cols wn * 64
+    const int h = lane >> 5;
+    const int l32 = lane & 31;
+    const int64_t row0 = static_cast<int64_t>(blockIdx.x) * BM;
+#ifdef RSLRL_STAMPS  // diagnostic build only (scripts/experiments/gemm_timeline.hip)
+    uint64_t st0 = __builtin_amdgcn_s_memrealtime();
+    uint64_t ct0 = __builtin_amdgcn_s_memtime();
+#endif
+
+    f32x16 acc[I][2];
+#pragma unroll
+    for (int i = 0; i < I; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
+
+    // Pipeline: B of chunk c+1 is copied (global_load_lds) and A of chunk c+1 fetched into registers at
+    // the start of chunk c; A is split into the other LDS buffer at its end.
+    const int nchunks = (p.K + kKC - 1) / kKC;
+    load_b_lds(bimg, 0, lds[0] + 3 * planeA);
+    store_a_split<BM>(load_a<BM, FULL>(p, row0, 0), lds[0]);
+    __syncthreads();
+    for (int c = 0; c < nchunks; ++c) {
+        const int buf = c & 1;
+        const bool more = c + 1 < nchunks;
+        AStage<BM> an;
+        if (more) {  // the other buffer was last read in chunk c-1, and every wave passed the barrier after it
+            load_b_lds(bimg, c + 1, lds[buf ^ 1] + 3 * planeA);
+            an = load_a<BM, FULL>(p, row0, (c + 1) * kKC);
+        }
+        const char* a_lds = lds[buf];
+        const char* b_lds = lds[buf] + 3 * planeA;
+        bf16x8 bf[2][3];
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int q = 0; q < 3; ++q) bf[j][q] = read_frag(b_lds + q * kX6PlaneB, wn * 64 + j * 32 + l32, h);
+#pragma unroll
+        for (int i = 0; i < I; ++i) {
+            bf16x8 af[3];
+#pragma unroll
+            for (int q = 0; q < 3; ++q) af[q] = read_frag(a_lds + q * planeA, wm * (BM / 2) + i * 32 + l32, h);
+#pragma unroll
+            for (int j = 0; j < 2; ++j) acc[i][j] = mfma_x6(af, bf[j], acc[i][j]);
+        }
+        if (more) store_a_split<BM>(an, lds[buf ^ 1]);
+        __syncthreads();  // also retires the global_load_lds of chunk c+1 (vmcnt(0))
+    }
+
+    const bool full = (row0 + BM <= p.M) && (p.N == kBN);
+    float colpart[2];
+#ifdef RSLRL_STAMPS
+    uint64_t st1 = __builtin_amdgcn_s_memrealtime();
+    uint64_t ct1 = __builtin_amdgcn_s_memtime();
+#endif
+    epilogue_tiles<EPI, I, 2>(p, acc, row0 + wm * (BM / 2), wn * 64, full, colpart);
+#ifdef RSLRL_STAMPS
+    {
+        uint64_t st2 = __builtin_amdgcn_s_memrealtime();
+        uint32_t hw;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        uint32_t xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        if (threadIdx.x == 0 || threadIdx.x == 448) {
+            uint64_t* o = g_stamps + (static_cast<int64_t>(blockIdx.x) * 2 + (threadIdx.x ? 1 : 0)) * 6;
+            o[0] = st0; o[1] = st1; o[2] = st2; o[3] = (static_cast<uint64_t>(xcc) << 32) | hw;
+            o[4] = ct0; o[5] = ct1;
+        }
+    }
+#endif
+    if constexpr (EPI == kEpiEluGrad) {
+        // column sums over the tile's rows -> colsum[col][128-row tile].  BM = 256: each wave row (wm) is
+        // one 128-row tile; BM = 128: the two wave rows are combined (fixed order) through LDS.
+        const int64_t tiles = p.ctiles;
+        float s[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) s[j] = colpart[j] + __shfl_xor(colpart[j], 32, 64);
+        if constexpr (BM == 256) {
+            const int64_t t = 2 * static_cast<int64_t>(blockIdx.x) + wm;
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int col = wn * 64 + j * 32 + l32;
+                if (h == 0 && col < p.N && t < tiles) p.colsum[static_cast<int64_t>(col) * tiles + t] = s[j];
+            }
+        } else {
+            float* colred = reinterpret_cast<float*>(lds[0]);
+            __syncthreads();  // the LDS tiles are no longer read
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+                if (h == 0) colred[wm * kBN + wn * 64 + j * 32 + l32] = s[j];
+            __syncthreads();
+            for (int col = threadIdx.x; col < p.N && col < kBN; col += kThreads)
+                p.colsum[static_cast<int64_t>(col) * tiles + blockIdx.x] = colred[col] + colred[kBN + col];
+        }
+    }
+}
+
+// ---- x6 with register-resident A ("x6r").  Each wave owns 32 rows x all 256 columns (8 MFMA tiles):
+// it loads its A fragments straight from HBM into registers (lane (r, h) reads row r, k 8h..8h+7 of the
+// chunk: two 16-B loads), splits them in registers and feeds the MFMAs -- A never touches LDS and needs
+// no barrier.  Only B (the weight image, shared by the 8 waves) goes through LDS, in a ring of kRB
+// chunk slots filled by global_load_lds.  Both streams run kD = kRB - 1 chunks ahead: the A loads are
+// issued as inline asm so the compiler does not drain them at every barrier (it waits vmcnt(0) for
+// ordinary loads whenever an LDS-DMA is in flight); the kernel counts vmcnt itself.  Per chunk and wave
+// the issue order is fixed: 3 global_load_lds (B) then 2 global_load_dwordx4 (A), so "chunk c has
+// landed" is vmcnt(5 * (kD - 1)) once the loads of chunks up to c + kD - 1 are issued.
+constexpr int kD = 2;
+constexpr int kRB = kD + 1;
+constexpr int kBMR = 256;
+
+using f32x4 = __attribute__((ext_vector_type(4))) float;
+
+struct AFrag {
+    f32x4 lo, hi;  // k 8h .. 8h+3, 8h+4 .. 8h+7 of row r
+};
+
+__device__ __forceinline__ f32x4 gload16(const float* ptr) {
+    f32x4 v;
+    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(ptr) : "memory");
+    return v;
+}
+
+// keeps v live and orders its uses after the preceding s_waitcnt
+__device__ __forceinline__ void pin(AFrag& a) { asm volatile("" : "+v"(a.lo), "+v"(a.hi)); }
+
+template <bool FULL>
+__device__ __forceinline__ AFrag load_afrag(const GemmParams& p, int64_t row, int k) {
+    if constexpr (FULL) {
+        const float* ptr = p.a + row * p.K + k;
+        return AFrag{gload16(ptr), gload16(ptr + 4)};
+    } else {  // out-of-range rows / k read a valid address (row 0 of the matrix) and are zeroed after the wait
+        const bool ok_lo = row < p.M && k < p.K;
+        const bool ok_hi = row < p.M && k + 4 < p.K;
+        return AFrag{gload16(p.a + (ok_lo ? row * p.K + k : 0)), gload16(p.a + (ok_hi ? row * p.K + k + 4 : 0))};
+    }
+}
+
+__device__ __forceinline__ void split_afrag(const AFrag& a, bf16x8 (&out)[3]) {
+    uint2 l[3], u[3];
+    split4(make_float4(a.lo[0], a.lo[1], a.lo[2], a.lo[3]), l[0], l[1], l[2]);
+    split4(make_float4(a.hi[0], a.hi[1], a.hi[2], a.hi[3]), u[0], u[1], u[2]);
+#pragma unroll
+    for (int q = 0; q < 3; ++q) out[q] = __builtin_bit_cast(bf16x8, make_uint4(l[q].x, l[q].y, u[q].x, u[q].y));
+}
+
+template <int EPI, bool FULL>
+__global__ __launch_bounds__(kThreads, 2) void mlp_gemm_x6r_kernel(GemmParams p, const uint4* __restrict__ bimg) {
+    __shared__ __attribute__((aligned(16))) char ring[kRB][kX6ChunkB];
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int h = lane >> 5;
+    const int l32 = lane & 31;
+    const int64_t row0 = static_cast<int64_t>(blockIdx.x) * kBMR;
+    const int64_t wrow0 = row0 + 32 * wave;
+#ifdef RSLRL_STAMPS
+    uint64_t st0 = __builtin_amdgcn_s_memrealtime();
+    uint64_t ct0 = __builtin_amdgcn_s_memtime();
+#endif
+    const int64_t arow = wrow0 + l32;
+    const int nchunks = (p.K + kKC - 1) / kKC;
+
+    f32x16 acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = f32x16{};
+
+    AFrag ar[kRB];
+    auto issue = [&](int c, AFrag& dst) {  // chunk min(c, n-1): B -> ring slot c % kRB, A -> dst
+        const int cc = min(c, nchunks - 1);
+        load_b_lds(bimg, cc, ring[c % kRB]);
+        dst = load_afrag<FULL>(p, arow, cc * kKC + 8 * h);
+    };
+    // prologue: chunks 0 .. kD-1 in flight
+#pragma unroll
+    for (int d = 0; d < kD; ++d) issue(d, ar[d]);
+    // steady state, unrolled by kRB so every ring index is static: at chunk c issue c + kD (into the slot
+    // chunk c - 1 used; every wave passed the barrier at the top of compute(c) after reading it), then
+    // compute c
+    for (int c0 = 0; c0 < nchunks; c0 += kRB) {
+#pragma unroll
+        for (int u = 0; u < kRB; ++u) {
+            const int c = c0 + u;
+            if (c < nchunks) {
+                // chunk c's loads are older than the 5 * (kD - 1) issued after them; the barrier also
+                // tells every wave that slot (c - 1) % kRB has been read by all
+                asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(5 * (kD - 1)) : "memory");
+                AFrag& a = ar[u];
+                pin(a);
+                issue(c + kD, ar[(u + kD) % kRB]);
+                if constexpr (!FULL) {
+                    const int k = c * kKC + 8 * h;
+                    if (!(arow < p.M && k < p.K)) a.lo = f32x4{0.f, 0.f, 0.f, 0.f};
+                    if (!(arow < p.M && k + 4 < p.K)) a.hi = f32x4{0.f, 0.f, 0.f, 0.f};
+                }
+                bf16x8 af[3];
+                split_afrag(a, af);
+                const char* b = ring[c % kRB];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    bf16x8 bf[3];
+#pragma unroll
+                    for (int q = 0; q < 3; ++q) bf[q] = read_frag(b + q * kX6PlaneB, j * 32 + l32, h);
+                    acc[j] = mfma_x6(af, bf, acc[j]);
+                }
+            }
+        }
+    }
+    // drain: the surplus (clamped) loads must land before their registers are reused
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int u = 0; u < kRB; ++u) pin(ar[u]);
+
+    // epilogue: the wave's 32 rows x 256 columns as a 1 x 8 tile grid
+    const bool full = (row0 + kBMR <= p.M) && (p.N == kBN);
+    f32x16 acc2[1][8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc2[0][j] = acc[j];
+    float colpart[8];
+#ifdef RSLRL_STAMPS
+    uint64_t st1 = __builtin_amdgcn_s_memrealtime();
+    uint64_t ct1 = __builtin_amdgcn_s_memtime();
+#endif
+    epilogue_tiles<EPI, 1, 8>(p, acc2, wrow0, 0, full, colpart);
+#ifdef RSLRL_STAMPS
+    {
+        uint64_t st2 = __builtin_amdgcn_s_memrealtime();
+        uint32_t hw, xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        if (threadIdx.x == 0 || threadIdx.x == 448) {
+            uint64_t* o = g_stamps + (static_cast<int64_t>(blockIdx.x) * 2 + (threadIdx.x ? 1 : 0)) * 6;
+            o[0] = st0; o[1] = st1; o[2] = st2; o[3] = (static_cast<uint64_t>(xcc) << 32) | hw;
+            o[4] = ct0; o[5] = ct1;
+        }
+    }
+#endif
+    if constexpr (EPI == kEpiEluGrad) {
+        // per-column sums of each 128-row tile = waves 4t .. 4t+3, combined in wave order through LDS
+        float* red = reinterpret_cast<float*>(ring[0]);  // 8 waves x 256 floats
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const float s2 = colpart[j] + __shfl_xor(colpart[j], 32, 64);
+            if (h == 0) red[wave * kBN + j * 32 + l32] = s2;
         }
         __syncthreads();
-        // column-major partials [N][tiles]: the fold then reads each column contiguously
-        for (int col = threadIdx.x; col < p.N && col < kBN; col += kThreads)
-            p.colsum[static_cast<int64_t>(col) * gridDim.x + blockIdx.x] = colred[0][col] + colred[1][col];
+        for (int e = threadIdx.x; e < 2 * kBN; e += kThreads) {
+            const int half = e / kBN, col = e % kBN;
+            const int64_t t = 2 * static_cast<int64_t>(blockIdx.x) + half;
+            if (col < p.N && t < p.ctiles) {
+                const float* r = red + 4 * half * kBN + col;
+                p.colsum[static_cast<int64_t>(col) * p.ctiles + t] = ((r[0] + r[kBN]) + r[2 * kBN]) + r[3 * kBN];
+            }
+        }
     }
 }
 
@@ -236,15 +681,53 @@ int dgrad_occupancy() {  // tuning knob: RSLRL_DGRAD_OCC=2|4 (default 4)
     return v;
 }
 
+int x6_tile() {  // tuning knob: RSLRL_X6_TILE=128|256|reg (default 128)
+    static const int v = [] {
+        const char* e = std::getenv("RSLRL_X6_TILE");
+        if (e && std::string(e) == "reg") return 1;
+        return (e && std::atoi(e) == 256) ? 256 : 128;
+    }();
+    return v;
+}
+
+// bimage == nullptr: exact f32 MFMA main loop on p.bw; otherwise the split-bf16 main loop on the image.
 template <int EPI>
-int launch(const GemmParams& p, hipStream_t st) {
+int launch(const GemmParams& p, const void* bimage, hipStream_t st) {
     const int64_t tiles = ceil_div(p.M, kBM);
     if (tiles > INT32_MAX) return RSLRL_E_INVALID_ARGUMENT;
     const dim3 g(static_cast<unsigned>(tiles)), b(kThreads);
-    if (EPI == kEpiEluGrad && dgrad_occupancy() == 2)
+    if (bimage) {
+        const uint4* img = static_cast<const uint4*>(bimage);
+        if (x6_tile() == 1) {
+            const dim3 gr(static_cast<unsigned>(ceil_div(p.M, kBMR)));
+            if (p.M % kBMR == 0 && p.K % kKC == 0)
+                hipLaunchKernelGGL((mlp_gemm_x6r_kernel<EPI, true>), gr, b, 0, st, p, img);
+            else
+                hipLaunchKernelGGL((mlp_gemm_x6r_kernel<EPI, false>), gr, b, 0, st, p, img);
+        } else if (x6_tile() == 256) {
+            const dim3 g6(static_cast<unsigned>(ceil_div(p.M, 256)));
+            if (p.M % 256 == 0 && p.K % kKC == 0)
+                hipLaunchKernelGGL((mlp_gemm_x6_kernel<EPI, true, 256>), g6, b, 0, st, p, img);
+            else
+                hipLaunchKernelGGL((mlp_gemm_x6_kernel<EPI, false, 256>), g6, b, 0, st, p, img);
+        } else {
+            // a short reduction (the dgrad of the 12- / 1-wide output layer: one chunk) is bound by the
+            // epilogue's h loads, which want the registers of the 2-waves-per-SIMD allocation
+            const bool short_k = EPI == kEpiEluGrad && p.K <= 2 * kKC;
+            const bool fullm = p.M % 128 == 0 && p.K % kKC == 0;
+            if (short_k) {
+                if (fullm) hipLaunchKernelGGL((mlp_gemm_x6_kernel<EPI, true, 128, 2>), g, b, 0, st, p, img);
+                else hipLaunchKernelGGL((mlp_gemm_x6_kernel<EPI, false, 128, 2>), g, b, 0, st, p, img);
+            } else {
+                if (fullm) hipLaunchKernelGGL((mlp_gemm_x6_kernel<EPI, true, 128>), g, b, 0, st, p, img);
+                else hipLaunchKernelGGL((mlp_gemm_x6_kernel<EPI, false, 128>), g, b, 0, st, p, img);
+            }
+        }
+    } else if (EPI == kEpiEluGrad && dgrad_occupancy() == 2) {
         hipLaunchKernelGGL((mlp_gemm_kernel<EPI, 2>), g, b, 0, st, p);
-    else
+    } else {
         hipLaunchKernelGGL((mlp_gemm_kernel<EPI, 4>), g, b, 0, st, p);
+    }
     return launch_status();
 }
 
@@ -255,28 +738,56 @@ using namespace rslrl;
 
 extern "C" int64_t rslrl_linear_tiles(int64_t M) { return ceil_div(M, kBM); }
 
+extern "C" size_t rslrl_linear_bimage_bytes(int32_t depth) {
+    return depth < 1 ? 0 : static_cast<size_t>(ceil_div(static_cast<int64_t>(depth), kKC)) * kX6ChunkB;
+}
+
+extern "C" int rslrl_linear_prepare_bimages(const rslrl_bimage_desc_t* descs, int32_t n, rslrl_stream_t stream) {
+    if (!descs || n < 1 || n > kMaxImages) return RSLRL_E_INVALID_ARGUMENT;
+    BImageBatch batch{};
+    int max_chunks = 0;
+    for (int i = 0; i < n; ++i) {
+        const rslrl_bimage_desc_t& d = descs[i];
+        if (!d.src || !d.image || d.rows < 1 || d.rows > kBN || d.depth < 1 || d.depth > (1 << 24))
+            return RSLRL_E_INVALID_ARGUMENT;
+        if (reinterpret_cast<uintptr_t>(d.image) & 15) return RSLRL_E_MISALIGNED;
+        batch.d[i] = d;
+        max_chunks = std::max(max_chunks, static_cast<int>(ceil_div(static_cast<int64_t>(d.depth), kKC)));
+    }
+    const dim3 grid(static_cast<unsigned>(ceil_div(max_chunks * kBN * 2, kBlock)), static_cast<unsigned>(n));
+    hipLaunchKernelGGL(bimage_kernel, grid, dim3(kBlock), 0, reinterpret_cast<hipStream_t>(stream), batch);
+    return launch_status();
+}
+
+extern "C" int rslrl_linear_prepare_bimage(const float* src, int32_t rows, int32_t depth, int32_t transposed,
+                                           void* image, rslrl_stream_t stream) {
+    const rslrl_bimage_desc_t d{src, image, rows, depth, transposed ? 1 : 0, 0};
+    return rslrl_linear_prepare_bimages(&d, 1, stream);
+}
+
 extern "C" int rslrl_linear_fwd(const float* x, int64_t M, int32_t K, const float* weight, int32_t N,
-                                const float* bias, int32_t activation, float* y, rslrl_stream_t stream) {
+                                const float* bias, int32_t activation, float* y, const void* bimage,
+                                rslrl_stream_t stream) {
     if (M < 0 || K < 1 || N < 1 || N > kBN || (K & 3) || K > INT32_MAX / 2) return RSLRL_E_INVALID_ARGUMENT;
     if (M == 0) return RSLRL_OK;
-    if (!x || !weight || !bias || !y) return RSLRL_E_INVALID_ARGUMENT;
-    if (!aligned16(x) || !aligned16(weight)) return RSLRL_E_MISALIGNED;
+    if (!x || (!weight && !bimage) || !bias || !y) return RSLRL_E_INVALID_ARGUMENT;
+    if (!aligned16(x) || (!bimage && !aligned16(weight)) || (bimage && !aligned16(bimage))) return RSLRL_E_MISALIGNED;
     if (activation != 0 && activation != 1) return RSLRL_E_UNSUPPORTED;
-    GemmParams p{x, weight, bias, nullptr, y, nullptr, M, K, N};
+    GemmParams p{x, weight, bias, nullptr, y, nullptr, M, K, N, 0};
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    return activation ? launch<kEpiBiasElu>(p, st) : launch<kEpiBias>(p, st);
+    return activation ? launch<kEpiBiasElu>(p, bimage, st) : launch<kEpiBias>(p, bimage, st);
 }
 
 extern "C" int rslrl_linear_dgrad_elu(const float* dz, int64_t M, int32_t Nred, const float* weight_t, int32_t K,
-                                      const float* h, float* dz_prev, float* colsum_partials,
+                                      const float* h, float* dz_prev, float* colsum_partials, const void* bimage,
                                       rslrl_stream_t stream) {
     if (M < 0 || Nred < 1 || K < 1 || K > kBN || (Nred & 3)) return RSLRL_E_INVALID_ARGUMENT;
     if (M == 0) return RSLRL_OK;
-    if (!dz || !weight_t || !h || !dz_prev || !colsum_partials) return RSLRL_E_INVALID_ARGUMENT;
-    if (!aligned16(dz) || !aligned16(weight_t)) return RSLRL_E_MISALIGNED;
+    if (!dz || (!weight_t && !bimage) || !h || !dz_prev || !colsum_partials) return RSLRL_E_INVALID_ARGUMENT;
+    if (!aligned16(dz) || (!bimage && !aligned16(weight_t)) || (bimage && !aligned16(bimage))) return RSLRL_E_MISALIGNED;
     // GEMM view: A = dZ [M, Nred], Bw = W^T [K, Nred] -> C = dZ W [M, K]
-    GemmParams p{dz, weight_t, nullptr, h, dz_prev, colsum_partials, M, Nred, K};
-    return launch<kEpiEluGrad>(p, reinterpret_cast<hipStream_t>(stream));
+    GemmParams p{dz, weight_t, nullptr, h, dz_prev, colsum_partials, M, Nred, K, ceil_div(M, kBM)};
+    return launch<kEpiEluGrad>(p, bimage, reinterpret_cast<hipStream_t>(stream));
 }
 
 extern "C" int rslrl_column_sum_fold(const float* partials, int64_t tiles, int32_t N, float* out,

@@ -1,0 +1,248 @@
+// Weight gradient of the actor/critic MLP layers on the split-bf16 ("x6") MFMA path:
+//   dW[n][k] = sum_m dZ[m][n] X[m][k]        dZ [M, N] (layer output grad), X [M, K] (layer input)
+// the autograd backward of nn.Linear's weight (rsl_rl/networks/mlp.py:106-114 layers; the reference runs
+// it as one cuBLAS GEMM per layer).  M is the mini-batch (393216 rows at C3); N, K <= 256.
+//
+// Split-K over M: workgroup s reduces rows [s * rows_per, (s + 1) * rows_per) into a full TN x 256 tile
+// of partial sums ([S][N][K] fp32), wgrad_fold_kernel adds the S partials in a fixed order in fp64 ->
+// deterministic.  Both operands are consumed along their row index m, which is the MFMA reduction
+// index, so each is staged in its natural [m][col] layout (coalesced float4 loads, split into three bf16
+// planes while staged) and read back column-wise with ds_read_b64_tr_b16 (MI355X_MICROARCH.md §LDS;
+// cdna_hip_programming.md T10): lane 4q+p of each 16-lane group addresses row q, columns 4p..4p+3 of a
+// 4-row block and receives its own column's 4 rows -- exactly a 32x32x16 operand fragment half.
+//
+// LDS image per buffer and operand: 3 planes x [16 m][COLS bf16]; on 512-B rows the 16-B chunks of row m
+// are XOR-permuted by 4 (m & 3), which makes the transposed reads (4 rows x 64 B per 32-lane half) and
+// the staging stores (ds_write_b64, 128 contiguous bytes per 16 lanes) bank-conflict free; 64-B rows
+// (TN = 32) need no permutation.
+#include <algorithm>
+
+#include "common.h"
+#include "x6_split.h"
+
+namespace rslrl {
+namespace {
+
+constexpr int kThreadsW = 512;
+constexpr int kMC = 16;  // rows of m per chunk (one MFMA k step)
+constexpr int kTK = 256;
+
+using s16x4 = __attribute__((ext_vector_type(4))) short;
+
+struct WgradParams {
+    const float* dz;  // [M, N]
+    const float* x;   // [M, K]
+    float* part;      // [S, N, K]
+    int64_t M;
+    int64_t rows_per;  // multiple of kMC
+    int N;
+    int K;
+};
+
+template <int COLS>
+__device__ __forceinline__ int swz(int m, int col) {  // byte offset of (m, col), col % 4 == 0, within a plane
+    constexpr int rowb = COLS * 2;
+    if constexpr (rowb >= 512) return rowb * m + 16 * ((col >> 3) ^ (4 * (m & 3))) + 8 * ((col >> 2) & 1);
+    return rowb * m + 2 * col;
+}
+
+// stage one operand chunk: rows m0.. m0+15 (global rows < m_end valid), columns < ncols valid
+template <int COLS, bool FULL>
+__device__ __forceinline__ void load_tile(const float* __restrict__ src, int ld, int64_t m0, int64_t m_end,
+                                          int ncols, float4 (&v)[(kMC * COLS / 4 + kThreadsW - 1) / kThreadsW]) {
+    constexpr int units = kMC * COLS / 4;
+    constexpr int per = (units + kThreadsW - 1) / kThreadsW;
+#pragma unroll
+    for (int i = 0; i < per; ++i) {
+        const int u = threadIdx.x + kThreadsW * i;
+        const int m = u / (COLS / 4);
+        const int c = 4 * (u % (COLS / 4));
+        const int64_t row = m0 + m;
+        if constexpr (FULL) {
+            v[i] = (units % kThreadsW == 0 || u < units)
+                       ? *reinterpret_cast<const float4*>(src + row * ld + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+        } else {
+            const bool ok = (units % kThreadsW == 0 || u < units) && row < m_end && c < ncols;
+            const float4 t = *reinterpret_cast<const float4*>(src + (ok ? row * ld + c : 0));
+            v[i] = ok ? t : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    }
+}
+
+template <int COLS>
+__device__ __forceinline__ void store_tile(const float4 (&v)[(kMC * COLS / 4 + kThreadsW - 1) / kThreadsW],
+                                           char* __restrict__ img) {
+    constexpr int units = kMC * COLS / 4;
+    constexpr int per = (units + kThreadsW - 1) / kThreadsW;
+    constexpr int plane = kMC * COLS * 2;
+#pragma unroll
+    for (int i = 0; i < per; ++i) {
+        const int u = threadIdx.x + kThreadsW * i;
+        if (units % kThreadsW == 0 || u < units) {
+            const int m = u / (COLS / 4);
+            const int c = 4 * (u % (COLS / 4));
+            uint2 p0, p1, p2;
+            split4(v[i], p0, p1, p2);
+            const int off = swz<COLS>(m, c);
+            *reinterpret_cast<uint2*>(img + off) = p0;
+            *reinterpret_cast<uint2*>(img + plane + off) = p1;
+            *reinterpret_cast<uint2*>(img + 2 * plane + off) = p2;
+        }
+    }
+}
+
+// 32x32x16 operand fragment of columns [cb, cb + 32) (all 16 rows) of one plane, via two transposed reads
+template <int COLS>
+__device__ __forceinline__ bf16x8 read_frag_tr(const char* __restrict__ plane, int cb) {
+    const int lane = threadIdx.x & 63;
+    const int g = lane >> 4;
+    const int q = (lane >> 2) & 3;
+    const int p = lane & 3;
+    const int col = cb + 16 * (g & 1) + 4 * p;
+    const int m = 8 * (g >> 1) + q;
+    typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(plane + swz<COLS>(m, col)));
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(plane + swz<COLS>(m + 4, col)));
+    const __attribute__((ext_vector_type(8))) short v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, v);
+}
+
+// TN = rows of dW per workgroup (256: waves 2 (n) x 4 (k), wave tile 128 x 64; 32: waves 1 x 8, 32 x 32)
+template <int TN, bool FULL>
+__global__ __launch_bounds__(kThreadsW, 2) void wgrad_x6_kernel(WgradParams p) {
+    constexpr int WN = TN == 256 ? 2 : 1;
+    constexpr int WK = 8 / WN;
+    constexpr int I = TN / WN / 32;
+    constexpr int J = kTK / WK / 32;
+    constexpr int planeA = kMC * TN * 2;
+    constexpr int planeB = kMC * kTK * 2;
+    constexpr int bufBytes = 3 * planeA + 3 * planeB;
+    constexpr int perA = (kMC * TN / 4 + kThreadsW - 1) / kThreadsW;
+    constexpr int perB = (kMC * kTK / 4 + kThreadsW - 1) / kThreadsW;
+    __shared__ __attribute__((aligned(16))) char lds[2][bufBytes];
+
+    const int wave = threadIdx.x >> 6;
+    const int wn = wave / WK;
+    const int wk = wave % WK;
+    const int64_t m_begin = static_cast<int64_t>(blockIdx.x) * p.rows_per;
+    const int64_t m_end = m_begin + p.rows_per < p.M ? m_begin + p.rows_per : p.M;
+    const int nchunks = static_cast<int>((m_end - m_begin + kMC - 1) / kMC);
+
+    f32x16 acc[I][J];
+#pragma unroll
+    for (int i = 0; i < I; ++i)
+#pragma unroll
+        for (int j = 0; j < J; ++j) acc[i][j] = f32x16{};
+
+    float4 va[perA], vb[perB];
+    if (nchunks > 0) {
+        load_tile<TN, FULL>(p.dz, p.N, m_begin, m_end, p.N, va);
+        load_tile<kTK, FULL>(p.x, p.K, m_begin, m_end, p.K, vb);
+        store_tile<TN>(va, lds[0]);
+        store_tile<kTK>(vb, lds[0] + 3 * planeA);
+    }
+    __syncthreads();
+    for (int c = 0; c < nchunks; ++c) {
+        const int buf = c & 1;
+        const bool more = c + 1 < nchunks;
+        if (more) {
+            const int64_t m0 = m_begin + static_cast<int64_t>(c + 1) * kMC;
+            load_tile<TN, FULL>(p.dz, p.N, m0, m_end, p.N, va);
+            load_tile<kTK, FULL>(p.x, p.K, m0, m_end, p.K, vb);
+        }
+        const char* a_img = lds[buf];
+        const char* b_img = lds[buf] + 3 * planeA;
+        bf16x8 bf[J][3];
+#pragma unroll
+        for (int j = 0; j < J; ++j)
+#pragma unroll
+            for (int q = 0; q < 3; ++q) bf[j][q] = read_frag_tr<kTK>(b_img + q * planeB, wk * (J * 32) + j * 32);
+#pragma unroll
+        for (int i = 0; i < I; ++i) {
+            bf16x8 af[3];
+#pragma unroll
+            for (int q = 0; q < 3; ++q) af[q] = read_frag_tr<TN>(a_img + q * planeA, wn * (I * 32) + i * 32);
+#pragma unroll
+            for (int j = 0; j < J; ++j) acc[i][j] = mfma_x6(af, bf[j], acc[i][j]);
+        }
+        if (more) {
+            store_tile<TN>(va, lds[buf ^ 1]);
+            store_tile<kTK>(vb, lds[buf ^ 1] + 3 * planeA);
+        }
+        __syncthreads();
+    }
+
+    // partial tile -> part[s][n][k]; C/D map: col (k) = lane & 31, row (n) = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
+    const int lane = threadIdx.x & 63;
+    const int l32 = lane & 31;
+    const int h = lane >> 5;
+    float* out = p.part + static_cast<int64_t>(blockIdx.x) * p.N * p.K;
+#pragma unroll
+    for (int i = 0; i < I; ++i)
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+            const int k = wk * (J * 32) + j * 32 + l32;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int n = wn * (I * 32) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                if (n < p.N && k < p.K) out[n * p.K + k] = acc[i][j][r];
+            }
+        }
+}
+
+// dW[e] = sum over s of part[s][e] (e < N * K), fp64 in slice order
+__global__ __launch_bounds__(kBlock) void wgrad_fold_kernel(const float* __restrict__ part, int S, int NK,
+                                                            float* __restrict__ out) {
+    const int e = blockIdx.x * kBlock + threadIdx.x;
+    if (e >= NK) return;
+    double s = 0.0;
+    for (int i = 0; i < S; ++i) s += static_cast<double>(part[static_cast<int64_t>(i) * NK + e]);
+    out[e] = static_cast<float>(s);
+}
+
+int64_t wgrad_slices(int64_t M) {  // one workgroup per CU-slot, at least 4 chunks each
+    const int64_t chunks = ceil_div(M, kMC);
+    return std::max<int64_t>(1, std::min<int64_t>(512, chunks / 4));
+}
+
+int64_t wgrad_rows_per(int64_t M) { return ceil_div(ceil_div(M, wgrad_slices(M)), kMC) * kMC; }
+
+}  // namespace
+}  // namespace rslrl
+
+using namespace rslrl;
+
+extern "C" size_t rslrl_linear_wgrad_workspace_bytes(int64_t M, int32_t N, int32_t K) {
+    if (M < 1 || N < 1 || K < 1) return 0;
+    const int64_t S = ceil_div(M, wgrad_rows_per(M));
+    return static_cast<size_t>(S) * N * K * sizeof(float);
+}
+
+extern "C" int rslrl_linear_wgrad(const float* dz, const float* x, int64_t M, int32_t N, int32_t K, float* dw,
+                                  void* workspace, size_t workspace_bytes, rslrl_stream_t stream) {
+    if (M < 1 || N < 1 || K < 1 || N > 256 || K > kTK || (N & 3) || (K & 3)) return RSLRL_E_INVALID_ARGUMENT;
+    if (!dz || !x || !dw || !workspace) return RSLRL_E_INVALID_ARGUMENT;
+    if ((reinterpret_cast<uintptr_t>(dz) | reinterpret_cast<uintptr_t>(x)) & 15) return RSLRL_E_MISALIGNED;
+    const int64_t rows_per = wgrad_rows_per(M);
+    const int64_t S = ceil_div(M, rows_per);
+    if (workspace_bytes < static_cast<size_t>(S) * N * K * sizeof(float)) return RSLRL_E_WORKSPACE_TOO_SMALL;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    WgradParams p{dz, x, static_cast<float*>(workspace), M, rows_per, N, K};
+    bool full = (M % rows_per == 0) && K == kTK;  // and N == TN, checked per branch
+    const dim3 g(static_cast<unsigned>(S)), b(kThreadsW);
+    if (N <= 32) {
+        full = full && N == 32;
+        if (full) hipLaunchKernelGGL((wgrad_x6_kernel<32, true>), g, b, 0, st, p);
+        else hipLaunchKernelGGL((wgrad_x6_kernel<32, false>), g, b, 0, st, p);
+    } else {
+        full = full && N == 256;
+        if (full) hipLaunchKernelGGL((wgrad_x6_kernel<256, true>), g, b, 0, st, p);
+        else hipLaunchKernelGGL((wgrad_x6_kernel<256, false>), g, b, 0, st, p);
+    }
+    int rc = launch_status();
+    if (rc) return rc;
+    const int NK = N * K;
+    hipLaunchKernelGGL(wgrad_fold_kernel, dim3(static_cast<unsigned>(ceil_div(NK, kBlock))), dim3(kBlock), 0, st,
+                       static_cast<const float*>(workspace), static_cast<int>(S), NK, dw);
+    return launch_status();
+}

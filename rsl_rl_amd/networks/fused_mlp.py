@@ -16,7 +16,10 @@ fp32 MFMA accumulation order differs from hipBLASLt's at fp32 epsilon; tests/tes
 
 from __future__ import annotations
 
+import contextlib
 import ctypes
+import os
+import weakref
 
 import torch
 import torch.nn as nn
@@ -32,32 +35,139 @@ def _stream(t):
     return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
 
 
-def linear_fwd(x, w, b, elu: bool):
+GEMM_F32 = 0  # v_mfma_f32_32x32x2_f32: exact f32 fma chain
+GEMM_X6 = 1   # fp32 split into 3 bf16 planes, 6 bf16 MFMA products, fp32 accumulation (default)
+_mode = GEMM_F32 if os.environ.get("RSLRL_GEMM_MODE", "x6") == "f32" else GEMM_X6
+
+
+def set_gemm_mode(mode: int) -> int:
+    """Select the arithmetic of the fused GEMMs (GEMM_F32 | GEMM_X6); returns the previous mode.  The
+    initial mode comes from RSLRL_GEMM_MODE=f32|x6 (default x6)."""
+    global _mode
+    if mode not in (GEMM_F32, GEMM_X6):
+        raise ValueError(f"unknown GEMM mode {mode}")
+    prev, _mode = _mode, mode
+    return prev
+
+
+# B-operand images (include/rslrl_amd.h rslrl_linear_prepare_bimages).  Weights can change in place without
+# moving their version counter (fused Adam does not bump it), so images are rebuilt on every use except
+# inside a frozen_weights() scope, where the caller promises the weights do not change (the rollout).
+_frozen_depth = 0
+_bimage_cache: dict = {}
+
+
+@contextlib.contextmanager
+def frozen_weights():
+    """Scope in which B images of weights are built once and reused (the rollout of on_policy_runner)."""
+    global _frozen_depth
+    _frozen_depth += 1
+    try:
+        yield
+    finally:
+        _frozen_depth -= 1
+        if _frozen_depth == 0:
+            _bimage_cache.clear()
+
+
+def bimages(specs):
+    """Images for [(w, transposed), ...]: transposed=False -> B = w ([N, K]), True -> B = w^T.  One launch
+    for every image not already cached in a frozen_weights() scope."""
+    out = [None] * len(specs)
+    todo = []
+    for i, (w, tr) in enumerate(specs):
+        rows, depth = (w.shape[1], w.shape[0]) if tr else (w.shape[0], w.shape[1])
+        key = (w.data_ptr(), tr, rows, depth)
+        if _frozen_depth:
+            hit = _bimage_cache.get(key)
+            if hit is not None and hit[0]() is w:
+                out[i] = hit[1]
+                continue
+        todo.append((i, w, tr, rows, depth, key))
+    if not todo:
+        return out
+    L = _lib.lib()
+    sizes = [L.rslrl_linear_bimage_bytes(depth) // 4 for (_, _, _, _, depth, _) in todo]
+    buf = torch.empty(sum(sizes), dtype=torch.float32, device=todo[0][1].device)
+    for start in range(0, len(todo), _lib.MAX_BIMAGES):
+        part = todo[start:start + _lib.MAX_BIMAGES]
+        descs = (_lib.BImageDesc * len(part))()
+        off = sum(sizes[:start])
+        keep = []
+        for d, (i, w, tr, rows, depth, key), n in zip(descs, part, sizes[start:start + len(part)]):
+            src = w.detach()
+            src = src if src.is_contiguous() else src.contiguous()
+            keep.append(src)
+            img = buf[off:off + n]
+            off += n
+            d.src, d.image, d.rows, d.depth, d.transposed = src.data_ptr(), img.data_ptr(), rows, depth, int(tr)
+            out[i] = img
+            if _frozen_depth:
+                _bimage_cache[key] = (weakref.ref(w), img)
+        rc = L.rslrl_linear_prepare_bimages(descs, len(part), _stream(buf))
+        _lib.check(rc, "rslrl_linear_prepare_bimages")
+    return out
+
+
+def bimage(w, transposed: bool):
+    return bimages([(w, transposed)])[0]
+
+
+def linear_fwd(x, w, b, elu: bool, img=None):
+    """act(x w^T + b); img: B image of w (x6 arithmetic) or None (exact f32 MFMA)."""
     M, K = x.shape
     N = w.shape[0]
     y = torch.empty(M, N, device=x.device, dtype=torch.float32)
     rc = _lib.lib().rslrl_linear_fwd(x.data_ptr(), M, K, w.data_ptr(), N, b.data_ptr(), 1 if elu else 0,
-                                     y.data_ptr(), _stream(x))
+                                     y.data_ptr(), img.data_ptr() if img is not None else None, _stream(x))
     _lib.check(rc, "rslrl_linear_fwd")
     return y
 
 
-def linear_dgrad_elu(dz, w, h):
-    """(dz @ w) * ELU'(h) and its column sums; w is the layer weight [N, K] (dz [M, N], h [M, K])."""
+def linear_dgrad_elu(dz, w, h, img=None):
+    """(dz @ w) * ELU'(h) and its column sums; w is the layer weight [N, K] (dz [M, N], h [M, K]); img: B image
+    of w^T (x6 arithmetic) or None (exact f32 MFMA)."""
     M, N = dz.shape
     K = w.shape[1]
-    wt = w.t().contiguous()  # [K, N]: the kernel's B operand rows are the output columns
+    wt = w.t().contiguous() if img is None else w  # [K, N]: the f32 kernel's B operand rows are the output columns
     L = _lib.lib()
     tiles = L.rslrl_linear_tiles(M)
     out = torch.empty(M, K, device=dz.device, dtype=torch.float32)
     part = torch.empty(K, tiles, device=dz.device, dtype=torch.float32)
     rc = L.rslrl_linear_dgrad_elu(dz.data_ptr(), M, N, wt.data_ptr(), K, h.data_ptr(), out.data_ptr(),
-                                  part.data_ptr(), _stream(dz))
+                                  part.data_ptr(), img.data_ptr() if img is not None else None, _stream(dz))
     _lib.check(rc, "rslrl_linear_dgrad_elu")
     db = torch.empty(K, device=dz.device, dtype=torch.float32)
     rc = L.rslrl_column_sum_fold(part.data_ptr(), tiles, K, db.data_ptr(), _stream(dz))
     _lib.check(rc, "rslrl_column_sum_fold")
     return out, db
+
+
+def linear_wgrad(dz, x):
+    """dz^T x ([N, K]) on the x6 weight-gradient kernel; dz [M, N], x [M, K], N, K <= 256 and 4-aligned."""
+    M, N = dz.shape
+    K = x.shape[1]
+    L = _lib.lib()
+    nbytes = L.rslrl_linear_wgrad_workspace_bytes(M, N, K)
+    ws = torch.empty(nbytes // 4, dtype=torch.float32, device=dz.device)
+    dw = torch.empty(N, K, dtype=torch.float32, device=dz.device)
+    rc = L.rslrl_linear_wgrad(dz.data_ptr(), x.data_ptr(), M, N, K, dw.data_ptr(), ws.data_ptr(), nbytes,
+                              _stream(dz))
+    _lib.check(rc, "rslrl_linear_wgrad")
+    return dw
+
+
+def _weight_grad(dz, x, x6: bool):
+    # the x6 weight-gradient kernel computes full 256 x 256 tiles: it pays off (and is deterministic with
+    # a smaller error than the batched fp32 GEMM) for the square hidden layers; the narrow first / output
+    # layers stay on the split-K batched GEMM (networks/linear.py), which is faster there
+    if x6 and dz.shape[1] > 32 and x.shape[1] > 64 and dz.shape[1] <= MAX_WIDTH and x.shape[1] <= MAX_WIDTH \
+            and x.shape[1] % 4 == 0:
+        pad = (-dz.shape[1]) % 4
+        if pad:  # the critic's 1-wide output
+            return linear_wgrad(F.pad(dz, (0, pad)), x)[: dz.shape[1]]
+        return linear_wgrad(dz, x)
+    return _splitk_weight_grad(dz, x)
 
 
 class FusedMLPFunction(torch.autograd.Function):
@@ -68,9 +178,15 @@ class FusedMLPFunction(torch.autograd.Function):
         ws, bs = params[0::2], params[1::2]
         hs = [x]
         h = x
-        for w, b in zip(ws[:-1], bs[:-1]):
-            h = linear_fwd(h, w, b, elu=True)
+        x6 = _mode == GEMM_X6
+        nh = len(ws) - 1
+        # forward images of the hidden layers + (for backward) the transposed images of layers 1..L-1
+        imgs = bimages([(w, False) for w in ws[:-1]] + [(w, True) for w in ws[1:]]) if x6 else [None] * (2 * nh)
+        for w, b, img in zip(ws[:-1], bs[:-1], imgs[:nh]):
+            h = linear_fwd(h, w, b, elu=True, img=img)
             hs.append(h)
+        ctx.dgrad_imgs = [None] + imgs[nh:]  # index l: image of W_l^T
+        ctx.x6 = x6
         y = F.linear(h, ws[-1], bs[-1])
         ctx.save_for_backward(*hs, *params)
         ctx.n_layers = len(ws)
@@ -88,18 +204,21 @@ class FusedMLPFunction(torch.autograd.Function):
         grads_b[L - 1] = dz.sum(0)
         for l in range(L - 1, -1, -1):
             h_in = hs[l]
-            grads_w[l] = _splitk_weight_grad(dz, h_in) if ctx.needs_input_grad[1 + 2 * l] else None
+            grads_w[l] = _weight_grad(dz, h_in, ctx.x6) if ctx.needs_input_grad[1 + 2 * l] else None
             if l == 0:
                 dx = dz.mm(ws[0]) if ctx.needs_input_grad[0] else None
                 break
             # dZ_{l-1} = (dZ_l W_l) * ELU'(H_{l-1}), db_{l-1} = column sums; a reduction width that is not a
-            # multiple of 4 (the critic's 1-wide output) is zero-padded to the next multiple
+            # multiple of 4 (the critic's 1-wide output) is zero-padded to the next multiple (the x6 image
+            # zero-fills the weight side itself)
             w = ws[l]
+            img = ctx.dgrad_imgs[l]
             pad = (-dz.shape[1]) % 4
             if pad:
                 dz = F.pad(dz, (0, pad))
-                w = F.pad(w, (0, 0, 0, pad))
-            dz, grads_b[l - 1] = linear_dgrad_elu(dz, w, h_in)
+                if img is None:
+                    w = F.pad(w, (0, 0, 0, pad))
+            dz, grads_b[l - 1] = linear_dgrad_elu(dz, w, h_in, img)
         out = [dx]
         for gw, gb in zip(grads_w, grads_b):
             out += [gw, gb]
@@ -137,8 +256,9 @@ def fused_mlp_forward(mlp: nn.Sequential, x: torch.Tensor) -> torch.Tensor:
         y = FusedMLPFunction.apply(x, *params)
     else:
         h = x
-        for m in linears[:-1]:
-            h = linear_fwd(h, m.weight, m.bias, elu=True)
+        imgs = bimages([(m.weight, False) for m in linears[:-1]]) if _mode == GEMM_X6 else [None] * (len(linears) - 1)
+        for m, img in zip(linears[:-1], imgs):
+            h = linear_fwd(h, m.weight, m.bias, elu=True, img=img)
         y = F.linear(h, linears[-1].weight, linears[-1].bias)
     for m in mlp:
         if isinstance(m, nn.Unflatten):

@@ -25,6 +25,7 @@ import torch
 import rsl_rl_amd
 from rsl_rl_amd.algorithms import PPO  # noqa: F401  (resolved by class_name)
 from rsl_rl_amd.env import VecEnv
+from rsl_rl_amd.networks import fused_mlp
 from rsl_rl_amd.modules import ActorCritic, resolve_rnd_config, resolve_symmetry_config  # noqa: F401
 from rsl_rl_amd.utils import resolve_obs_groups, store_code_state
 
@@ -97,7 +98,7 @@ class OnPolicyRunner:
         tot_iter = start_iter + num_learning_iterations
         for it in range(start_iter, tot_iter):
             start = time.time()
-            with torch.inference_mode():
+            with torch.inference_mode(), fused_mlp.frozen_weights():
                 for _ in range(self.num_steps_per_env):
                     actions = self.alg.act(obs)
                     obs, rewards, dones, extras = self.env.step(actions.to(self.env.device))

@@ -59,11 +59,17 @@ def test_argument_validation_without_gpu():
 
 def test_linear_abi_rejects_bad_shapes():
     L = _lib.lib()
-    assert L.rslrl_linear_fwd(8, 10, 6, 8, 16, 8, 1, 8, None) == -1  # K % 4 != 0
-    assert L.rslrl_linear_fwd(8, 10, 8, 8, 300, 8, 1, 8, None) == -1  # N > 256
-    assert L.rslrl_linear_fwd(8, 0, 8, 8, 16, 8, 1, 8, None) == 0  # empty batch
-    assert L.rslrl_linear_dgrad_elu(8, 10, 6, 8, 16, 8, 8, 8, None) == -1  # Nred % 4 != 0
+    assert L.rslrl_linear_fwd(8, 10, 6, 8, 16, 8, 1, 8, None, None) == -1  # K % 4 != 0
+    assert L.rslrl_linear_fwd(8, 10, 8, 8, 300, 8, 1, 8, None, None) == -1  # N > 256
+    assert L.rslrl_linear_fwd(8, 0, 8, 8, 16, 8, 1, 8, None, None) == 0  # empty batch
+    assert L.rslrl_linear_fwd(16, 10, 8, None, 16, 16, 1, 16, None, None) == -1  # no weight and no image
+    assert L.rslrl_linear_fwd(16, 10, 8, None, 16, 16, 1, 16, 24, None) == -4  # misaligned image
+    assert L.rslrl_linear_dgrad_elu(8, 10, 6, 8, 16, 8, 8, 8, None, None) == -1  # Nred % 4 != 0
     assert L.rslrl_linear_tiles(393216) == 3072
+    assert L.rslrl_linear_bimage_bytes(256) == 16 * 3 * 256 * 32  # 16 chunks x 3 planes x 256 rows x 32 B
+    assert L.rslrl_linear_bimage_bytes(12) == 3 * 256 * 32
+    assert L.rslrl_linear_prepare_bimage(16, 300, 16, 0, 16, None) == -1  # rows > 256
+    assert L.rslrl_linear_prepare_bimage(16, 16, 16, 0, 8, None) == -4  # misaligned image
 
 
 def test_randperm_rejects_bad_state():
