@@ -190,19 +190,42 @@ __global__ __launch_bounds__(kThreadsW, 2) void wgrad_x6_kernel(WgradParams p) {
         }
 }
 
-// dW[e] = sum over s of part[s][e] (e < N * K), fp64 in slice order
+// dW[e] = sum over s of part[s][e] (e < N * K), fp64, fixed order: thread (g, c) of a 256-thread block
+// sums slices s = g (mod 4) of the float4 column group c (unrolled so several loads are in flight), then
+// the four group sums are added in g order through LDS.  One block per 256 outputs.
 __global__ __launch_bounds__(kBlock) void wgrad_fold_kernel(const float* __restrict__ part, int S, int NK,
                                                             float* __restrict__ out) {
-    const int e = blockIdx.x * kBlock + threadIdx.x;
-    if (e >= NK) return;
-    double s = 0.0;
-    for (int i = 0; i < S; ++i) s += static_cast<double>(part[static_cast<int64_t>(i) * NK + e]);
-    out[e] = static_cast<float>(s);
+    __shared__ double red[4][64][4];
+    const int g = threadIdx.x >> 6;
+    const int c = threadIdx.x & 63;
+    const int e0 = blockIdx.x * 256 + 4 * c;  // NK % 4 == 0 (K % 4 == 0)
+    double a[4] = {0.0, 0.0, 0.0, 0.0};
+    if (e0 < NK) {
+        const float4* src = reinterpret_cast<const float4*>(part + e0);
+        const int64_t stride = NK / 4;
+        int s = g;
+#pragma unroll 8
+        for (; s < S; s += 4) {
+            const float4 v = src[static_cast<int64_t>(s) * stride];
+            a[0] += v.x; a[1] += v.y; a[2] += v.z; a[3] += v.w;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) red[g][c][k] = a[k];
+    __syncthreads();
+    if (g == 0 && e0 < NK) {
+        float4 r;
+        r.x = static_cast<float>(((red[0][c][0] + red[1][c][0]) + red[2][c][0]) + red[3][c][0]);
+        r.y = static_cast<float>(((red[0][c][1] + red[1][c][1]) + red[2][c][1]) + red[3][c][1]);
+        r.z = static_cast<float>(((red[0][c][2] + red[1][c][2]) + red[2][c][2]) + red[3][c][2]);
+        r.w = static_cast<float>(((red[0][c][3] + red[1][c][3]) + red[2][c][3]) + red[3][c][3]);
+        *reinterpret_cast<float4*>(out + e0) = r;
+    }
 }
 
-int64_t wgrad_slices(int64_t M) {  // one workgroup per CU-slot, at least 4 chunks each
+int64_t wgrad_slices(int64_t M) {  // one workgroup per CU (98 KiB of LDS each), at least 4 chunks each
     const int64_t chunks = ceil_div(M, kMC);
-    return std::max<int64_t>(1, std::min<int64_t>(512, chunks / 4));
+    return std::max<int64_t>(1, std::min<int64_t>(256, chunks / 4));
 }
 
 int64_t wgrad_rows_per(int64_t M) { return ceil_div(ceil_div(M, wgrad_slices(M)), kMC) * kMC; }
@@ -242,7 +265,7 @@ extern "C" int rslrl_linear_wgrad(const float* dz, const float* x, int64_t M, in
     int rc = launch_status();
     if (rc) return rc;
     const int NK = N * K;
-    hipLaunchKernelGGL(wgrad_fold_kernel, dim3(static_cast<unsigned>(ceil_div(NK, kBlock))), dim3(kBlock), 0, st,
+    hipLaunchKernelGGL(wgrad_fold_kernel, dim3(static_cast<unsigned>(ceil_div(NK, 256))), dim3(kBlock), 0, st,
                        static_cast<const float*>(workspace), static_cast<int>(S), NK, dw);
     return launch_status();
 }

@@ -9,9 +9,15 @@ import csv
 import re
 
 FAMILIES = [
-    ("mlp_gemm<fwd bias+ELU>", r"mlp_gemm_kernel<1"),
-    ("mlp_gemm<fwd bias>", r"mlp_gemm_kernel<0"),
-    ("mlp_gemm<dgrad ELU'>", r"mlp_gemm_kernel<2"),
+    ("x6 gemm<fwd bias+ELU>", r"mlp_gemm_x6r?_kernel<1"),
+    ("x6 gemm<fwd bias>", r"mlp_gemm_x6r?_kernel<0"),
+    ("x6 gemm<dgrad ELU'>", r"mlp_gemm_x6r?_kernel<2"),
+    ("x6 wgrad", r"wgrad_x6_kernel"),
+    ("wgrad fold", r"wgrad_fold_kernel"),
+    ("bimage", r"bimage_kernel"),
+    ("f32 gemm<fwd bias+ELU>", r"mlp_gemm_kernel<1"),
+    ("f32 gemm<fwd bias>", r"mlp_gemm_kernel<0"),
+    ("f32 gemm<dgrad ELU'>", r"mlp_gemm_kernel<2"),
     ("colsum_fold", r"colsum_fold"),
     ("ppo_loss", r"ppo_loss_kernel"),
     ("gae_scan", r"gae_scan_kernel"),
