@@ -198,6 +198,67 @@ size_t rslrl_linear_wgrad_workspace_bytes(int64_t M, int32_t N, int32_t K);
 int rslrl_linear_wgrad(const float* dz, const float* x, int64_t M, int32_t N, int32_t K, float* dw, void* workspace,
                        size_t workspace_bytes, rslrl_stream_t stream);
 
+/* ------------------------------------------------------------------------------------------------
+ * Rollout-side record: for environment step t, in one launch,
+ *   logp   = sum_a Normal(mu, sigma).log_prob(actions)           (actor_critic.py:150-151, ppo.py:135)
+ *   r_int  = rnd_weight * || target(s) - predictor(s) ||_2       (rnd.py:113-135; optional)
+ *   reward = (rewards + extra_reward + r_int) + gamma * (values * time_outs)   (ppo.py:147-164)
+ * and writes storage row t: obs groups, actions, reward, uint8(dones), values, logp, mu, sigma
+ * (rollout_storage.py:77-103).  out_* point at row t of each [T, N, d] buffer (contiguous [N, d]).
+ * RND nets: Linear(in -> hidden) + ELU + Linear(hidden -> out), in, hidden <= 64, out <= 8, packed per
+ * net as [W1 (hidden x in) | b1 | W2 (out x hidden) | b2]; optional state normalisation
+ * (s - mean) / (std + eps).  dones / time_outs dtype: RSLRL_DTYPE_*; time_outs may be NULL.
+ * ----------------------------------------------------------------------------------------------*/
+#define RSLRL_DTYPE_F32 0
+#define RSLRL_DTYPE_U8 1 /* also bool */
+#define RSLRL_DTYPE_I32 2
+#define RSLRL_DTYPE_I64 3
+#define RSLRL_ROLLOUT_MAX_OBS 4
+typedef struct {
+    const float* src;
+    float* dst;
+    int64_t row_floats; /* % 4 == 0, both 16-byte aligned */
+} rslrl_obs_copy_t;
+typedef struct {
+    int64_t N;
+    int32_t A;
+    int32_t sigma_mode; /* 0: sigma [A] shared; 1: [N, A] */
+    const float* actions;
+    const float* mu;
+    const float* sigma;
+    const float* values;
+    const float* rewards;
+    const void* dones;
+    int32_t dones_dtype;
+    int32_t time_outs_dtype;
+    const void* time_outs;
+    float gamma;
+    float rnd_weight;
+    const float* extra_reward; /* optional [N], added before the RND reward */
+    const float* rnd_obs;      /* RND state rows (row stride rnd_obs_stride) */
+    int64_t rnd_obs_stride;
+    int32_t rnd_in;
+    int32_t rnd_hidden;
+    int32_t rnd_out;
+    float rnd_state_eps;
+    const float* rnd_target; /* NULL: no RND */
+    const float* rnd_predictor;
+    const float* rnd_state_mean; /* NULL: no state normalisation */
+    const float* rnd_state_std;
+    float* intrinsic_out; /* optional [N] */
+    int32_t n_obs;
+    int32_t reserved;
+    rslrl_obs_copy_t obs[RSLRL_ROLLOUT_MAX_OBS];
+    float* out_actions;
+    float* out_rewards;
+    uint8_t* out_dones;
+    float* out_values;
+    float* out_logp;
+    float* out_mu;
+    float* out_sigma;
+} rslrl_rollout_args_t;
+int rslrl_rollout_record(const rslrl_rollout_args_t* args /* host struct */, rslrl_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -235,3 +235,58 @@ def ppo_loss(mu, sigma, values, actions, old_logp, advantages, target_values, re
     dsig = g_var * f32(2) * sigma - g_lp / sigma + np.repeat(g_ent[:, None], A, axis=1) / sigma
     out.update(dmu=dmu.astype(f32), dsigma=dsig.astype(f32), dV=dV.astype(f32), dlogp=g_logp)
     return out
+
+
+# --------------------------------------------------------------------------------------------------
+# rollout-side record: act's log-prob + process_env_step's reward + RND (ppo.py:129-169, rnd.py:113-135)
+# --------------------------------------------------------------------------------------------------
+def normal_log_prob_sum(actions, mu, sigma):
+    """torch.distributions.Normal(mu, sigma).log_prob(actions).sum(-1) (normal.py) in fp32:
+    -((x - mu) ** 2) / (2 * var) - log(sigma) - log(sqrt(2 pi)), summed over the last axis in order."""
+    x, m = actions.astype(f32), mu.astype(f32)
+    s = np.broadcast_to(sigma.astype(f32), x.shape)
+    d = (x - m).astype(f32)
+    num = (-(d * d)).astype(f32)
+    den = (f32(2.0) * (s * s).astype(f32)).astype(f32)
+    t = ((num / den).astype(f32) - np.log(s).astype(f32)).astype(f32) - f32(math.log(math.sqrt(2 * math.pi)))
+    t = t.astype(f32)
+    out = np.zeros(x.shape[:-1], f32)
+    for a in range(x.shape[-1]):
+        out = (out + t[..., a]).astype(f32)
+    return out
+
+
+def _elu(z):
+    return np.where(z > 0, z, np.expm1(z.astype(np.float64)).astype(f32)).astype(f32)
+
+
+def mlp_forward(x, layers):
+    """Linear/ELU stack in fp64 accumulation rounded per layer (a GEMM-class fp32 result)."""
+    h = x.astype(f32)
+    for i, (w, b) in enumerate(layers):
+        h = (h.astype(np.float64) @ w.astype(np.float64).T + b.astype(np.float64)).astype(f32)
+        if i + 1 < len(layers):
+            h = _elu(h)
+    return h
+
+
+def rnd_intrinsic(state, target_layers, predictor_layers, weight, state_mean=None, state_std=None, eps=1e-2):
+    """weight * || target(s) - predictor(s) ||_2 with s optionally (s - mean) / (std + eps)."""
+    s = state.astype(f32)
+    if state_mean is not None:
+        s = ((s - state_mean.astype(f32)).astype(f32) / (state_std.astype(f32) + f32(eps)).astype(f32)).astype(f32)
+    d = (mlp_forward(s, target_layers) - mlp_forward(s, predictor_layers)).astype(f32)
+    ss = np.zeros(d.shape[0], f32)
+    for q in range(d.shape[1]):
+        ss = (ss + (d[:, q] * d[:, q]).astype(f32)).astype(f32)
+    return (np.sqrt(ss).astype(f32) * f32(weight)).astype(f32)
+
+
+def step_reward(rewards, values, time_outs, gamma, intrinsic=None):
+    """(rewards + intrinsic) + gamma * (values * time_outs)  (ppo.py:147-164)."""
+    r = rewards.astype(f32).copy()
+    if intrinsic is not None:
+        r = (r + intrinsic.astype(f32)).astype(f32)
+    if time_outs is not None:
+        r = (r + (f32(gamma) * (values.reshape(-1).astype(f32) * time_outs.astype(f32)).astype(f32)).astype(f32))
+    return r.astype(f32)

@@ -41,6 +41,7 @@ EXPORTED_SYMBOLS = (
     "rslrl_column_sum_fold",
     "rslrl_linear_wgrad_workspace_bytes",
     "rslrl_linear_wgrad",
+    "rslrl_rollout_record",
 )
 
 MAX_GATHER_FIELDS = 16
@@ -65,6 +66,54 @@ class BImageDesc(ctypes.Structure):
 
 
 MAX_BIMAGES = 16
+
+DTYPE_F32, DTYPE_U8, DTYPE_I32, DTYPE_I64 = 0, 1, 2, 3
+ROLLOUT_MAX_OBS = 4
+
+
+class ObsCopy(ctypes.Structure):
+    _fields_ = [("src", ctypes.c_void_p), ("dst", ctypes.c_void_p), ("row_floats", ctypes.c_int64)]
+
+
+class RolloutArgs(ctypes.Structure):
+    _fields_ = [
+        ("N", ctypes.c_int64),
+        ("A", ctypes.c_int32),
+        ("sigma_mode", ctypes.c_int32),
+        ("actions", ctypes.c_void_p),
+        ("mu", ctypes.c_void_p),
+        ("sigma", ctypes.c_void_p),
+        ("values", ctypes.c_void_p),
+        ("rewards", ctypes.c_void_p),
+        ("dones", ctypes.c_void_p),
+        ("dones_dtype", ctypes.c_int32),
+        ("time_outs_dtype", ctypes.c_int32),
+        ("time_outs", ctypes.c_void_p),
+        ("gamma", ctypes.c_float),
+        ("rnd_weight", ctypes.c_float),
+        ("extra_reward", ctypes.c_void_p),
+        ("rnd_obs", ctypes.c_void_p),
+        ("rnd_obs_stride", ctypes.c_int64),
+        ("rnd_in", ctypes.c_int32),
+        ("rnd_hidden", ctypes.c_int32),
+        ("rnd_out", ctypes.c_int32),
+        ("rnd_state_eps", ctypes.c_float),
+        ("rnd_target", ctypes.c_void_p),
+        ("rnd_predictor", ctypes.c_void_p),
+        ("rnd_state_mean", ctypes.c_void_p),
+        ("rnd_state_std", ctypes.c_void_p),
+        ("intrinsic_out", ctypes.c_void_p),
+        ("n_obs", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
+        ("obs", ObsCopy * ROLLOUT_MAX_OBS),
+        ("out_actions", ctypes.c_void_p),
+        ("out_rewards", ctypes.c_void_p),
+        ("out_dones", ctypes.c_void_p),
+        ("out_values", ctypes.c_void_p),
+        ("out_logp", ctypes.c_void_p),
+        ("out_mu", ctypes.c_void_p),
+        ("out_sigma", ctypes.c_void_p),
+    ]
 
 
 class PPOLossArgs(ctypes.Structure):
@@ -141,6 +190,8 @@ def _declare(L):
     L.rslrl_linear_wgrad_workspace_bytes.argtypes = [I64, I32, I32]
     L.rslrl_linear_wgrad.restype = ctypes.c_int
     L.rslrl_linear_wgrad.argtypes = [P, P, I64, I32, I32, P, P, SZ, P]
+    L.rslrl_rollout_record.restype = ctypes.c_int
+    L.rslrl_rollout_record.argtypes = [ctypes.POINTER(RolloutArgs), P]
     L.rslrl_column_sum_fold.restype = ctypes.c_int
     L.rslrl_column_sum_fold.argtypes = [P, I64, I32, P, P]
 

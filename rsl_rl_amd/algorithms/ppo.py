@@ -151,26 +151,79 @@ class PPO:
             self.transition.hidden_states = self.policy.get_hidden_states()
         self.transition.actions = self.policy.act(obs).detach()
         self.transition.values = self.policy.evaluate(obs).detach()
-        self.transition.actions_log_prob = self.policy.get_actions_log_prob(self.transition.actions).detach()
         self.transition.action_mean = self.policy.action_mean.detach()
         self.transition.action_sigma = self.policy.action_std.detach()
         self.transition.observations = obs
+        if not self._fused_rollout():
+            self.transition.actions_log_prob = self.policy.get_actions_log_prob(self.transition.actions).detach()
+        # else: the log-prob is computed by the fused record kernel in process_env_step
         return self.transition.actions
+
+    def _fused_rollout(self) -> bool:
+        return self.storage is not None and self.storage.fused_record_ok(self.transition)
+
+    def _rnd_fused_args(self, obs):
+        """Arguments of the RND part of the fused record, or None when the RND module is not of the fused
+        form (one hidden ELU layer <= 64 wide, <= 8 outputs, no reward normalisation)."""
+        rnd = self.rnd
+        if rnd is None or rnd.reward_normalization:
+            return None
+        nets = []
+        for mlp in (rnd.target, rnd.predictor):
+            mods = [m for m in mlp]
+            lin = [m for m in mods if isinstance(m, torch.nn.Linear)]
+            if (len(mods) != 3 or len(lin) != 2 or not isinstance(mods[1], torch.nn.ELU) or mods[1].alpha != 1.0
+                    or lin[0].in_features > 64 or lin[0].out_features > 64 or lin[1].out_features > 8):
+                return None
+            nets.append(lin)
+        if nets[0][0].out_features != nets[1][0].out_features:
+            return None
+        groups = rnd.obs_groups["rnd_state"]
+        state = obs[groups[0]] if len(groups) == 1 else torch.cat([obs[g] for g in groups], dim=-1)
+        # weight schedule (rnd.py:128-132), evaluated on the host as the reference does
+        rnd.update_counter += 1
+        if rnd.weight_scheduler is not None:
+            rnd.weight = rnd.weight_scheduler(step=rnd.update_counter, **rnd.weight_scheduler_params)
+        else:
+            rnd.weight = rnd.initial_weight
+        args = {"obs": state, "hidden": nets[0][0].out_features, "out": nets[0][1].out_features,
+                "target": kernels.pack_rnd_net(rnd.target), "predictor": kernels.pack_rnd_net(rnd.predictor),
+                "weight": rnd.weight}
+        if rnd.state_normalization:
+            sn = rnd.state_normalizer
+            args.update(state_mean=sn._mean, state_std=sn._std, state_eps=sn.eps)
+        return args
 
     def process_env_step(self, obs, rewards, dones, extras):
         self.policy.update_normalization(obs)
         if self.rnd:
             self.rnd.update_normalization(obs)
-        self.transition.rewards = rewards.clone()
-        self.transition.dones = dones
-        if self.rnd:
-            self.intrinsic_rewards = self.rnd.get_intrinsic_reward(obs)
-            self.transition.rewards += self.intrinsic_rewards
-        if "time_outs" in extras:  # bootstrap on time-outs (ppo.py:161-164)
-            self.transition.rewards += self.gamma * torch.squeeze(
-                self.transition.values * extras["time_outs"].unsqueeze(1).to(self.device), 1
-            )
-        self.storage.add_transitions(self.transition)
+        time_outs = extras.get("time_outs") if isinstance(extras, dict) else None
+        if self._fused_rollout():
+            # ppo.py:142-169 + rollout_storage.py:77-103 + rnd.py:113-135 in one launch
+            rnd_args = self._rnd_fused_args(obs) if self.rnd else None
+            extra = None
+            if self.rnd and rnd_args is None:  # RND of a form the kernel does not evaluate: PyTorch, then fused add
+                extra = self.rnd.get_intrinsic_reward(obs)
+                self.intrinsic_rewards = extra
+            elif rnd_args is not None:
+                self.intrinsic_rewards = torch.empty(rewards.shape[0], dtype=torch.float32, device=rewards.device)
+            if time_outs is not None:
+                time_outs = time_outs.to(self.device)
+            self.storage.add_transition_fused(self.transition, rewards, dones, time_outs, self.gamma,
+                                              extra_reward=extra, rnd=rnd_args,
+                                              intrinsic_out=self.intrinsic_rewards if rnd_args is not None else None)
+        else:
+            self.transition.rewards = rewards.clone()
+            self.transition.dones = dones
+            if self.rnd:
+                self.intrinsic_rewards = self.rnd.get_intrinsic_reward(obs)
+                self.transition.rewards += self.intrinsic_rewards
+            if time_outs is not None:  # bootstrap on time-outs (ppo.py:161-164)
+                self.transition.rewards += self.gamma * torch.squeeze(
+                    self.transition.values * time_outs.unsqueeze(1).to(self.device), 1
+                )
+            self.storage.add_transitions(self.transition)
         self.transition.clear()
         self.policy.reset(dones)
 

@@ -1,0 +1,213 @@
+// Rollout-side fusion: one launch per environment step replaces the tail of
+// PPO.act + PPO.process_env_step + RolloutStorage.add_transitions + RND.get_intrinsic_reward:
+//
+//   logp      = sum_a Normal(mu, sigma).log_prob(actions)          actor_critic.py:150-151 (act, ppo.py:135)
+//   r_int     = weight * || target(s) - predictor(s) ||_2          rnd.py:113-135 (s = normalised RND state)
+//   reward    = (rewards + r_int) + gamma * (values * time_outs)   ppo.py:147-164
+//   storage[t] <- obs groups, actions, reward, uint8(dones), values, logp, mu, sigma (expanded)
+//                                                                   rollout_storage.py:77-103
+//
+// Two index spaces share the grid: the first `copy_blocks` workgroups stream the row-contiguous slabs
+// (observation groups, actions, mu, sigma) with 16-byte accesses; the rest run one thread per env for
+// the per-row work (log-prob over A, the two RND MLPs from LDS-resident weights, the reward arithmetic).
+// Every fp32 operation of the reference expressions is issued separately in the reference's order
+// (__f*_rn), except the RND MLP dot products (fmaf chain, fp32 GEMM-class rounding) and the sum over
+// actions (sequential; torch's reduction order is unspecified).
+#include <algorithm>
+
+#include "common.h"
+
+namespace rslrl {
+namespace {
+
+constexpr int kMaxRndIn = 64;
+constexpr int kMaxRndHidden = 64;
+constexpr int kMaxRndOut = 8;
+constexpr int kMaxA = 64;
+
+struct RndNet {  // packed layout of rslrl_rollout_args_t::rnd_target / rnd_predictor
+    const float* w1;  // [H, in]
+    const float* b1;  // [H]
+    const float* w2;  // [Q, H]
+    const float* b2;  // [Q]
+};
+
+__device__ __forceinline__ float load_flag(const void* p, int dtype, int64_t i) {
+    switch (dtype) {
+        case RSLRL_DTYPE_U8: return static_cast<float>(static_cast<const uint8_t*>(p)[i]);
+        case RSLRL_DTYPE_I32: return static_cast<float>(static_cast<const int32_t*>(p)[i]);
+        case RSLRL_DTYPE_I64: return static_cast<float>(static_cast<const int64_t*>(p)[i]);
+        default: return static_cast<const float*>(p)[i];
+    }
+}
+
+// RND MLP forward for one state row held in registers: in -> H (ELU) -> Q, weights in LDS
+__device__ __forceinline__ void rnd_forward(const float* __restrict__ w, int in, int H, int Q, const float (&x)[kMaxRndIn],
+                                            float (&y)[kMaxRndOut]) {
+    const float* w1 = w;
+    const float* b1 = w1 + H * in;
+    const float* w2 = b1 + H;
+    const float* b2 = w2 + Q * H;
+#pragma unroll
+    for (int q = 0; q < kMaxRndOut; ++q) y[q] = 0.f;
+    for (int hh = 0; hh < H; ++hh) {
+        float z = 0.f;
+        const float* wr = w1 + hh * in;
+#pragma unroll
+        for (int i = 0; i < kMaxRndIn; ++i)
+            if (i < in) z = fmaf(wr[i], x[i], z);
+        z = __fadd_rn(z, b1[hh]);
+        const float a = z > 0.f ? z : expm1f(z);  // ELU, alpha 1 (torch: expm1)
+#pragma unroll
+        for (int q = 0; q < kMaxRndOut; ++q)
+            if (q < Q) y[q] = fmaf(w2[q * H + hh], a, y[q]);
+    }
+#pragma unroll
+    for (int q = 0; q < kMaxRndOut; ++q)
+        if (q < Q) y[q] = __fadd_rn(y[q], b2[q]);
+}
+
+__global__ __launch_bounds__(kBlock) void rollout_record_kernel(rslrl_rollout_args_t a, int copy_blocks) {
+    extern __shared__ float lds_w[];  // RND target then predictor weights
+    const int64_t N = a.N;
+    if (static_cast<int>(blockIdx.x) < copy_blocks) {
+        // ---- slab copies: obs groups [N, d], actions / mu [N, A], sigma expanded [N, A]
+        const int64_t tid = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+        const int64_t stride = static_cast<int64_t>(copy_blocks) * kBlock;
+        for (int g = 0; g < a.n_obs; ++g) {
+            const int64_t n4 = N * a.obs[g].row_floats / 4;  // row_floats % 4 == 0 checked on the host
+            const float4* s = reinterpret_cast<const float4*>(a.obs[g].src);
+            float4* d = reinterpret_cast<float4*>(a.obs[g].dst);
+            for (int64_t i = tid; i < n4; i += stride) d[i] = s[i];
+        }
+        const int64_t na = N * a.A;
+        if ((a.A & 3) == 0) {
+            const int64_t n4 = na / 4;
+            const float4* sa = reinterpret_cast<const float4*>(a.actions);
+            const float4* sm = reinterpret_cast<const float4*>(a.mu);
+            float4* da = reinterpret_cast<float4*>(a.out_actions);
+            float4* dm = reinterpret_cast<float4*>(a.out_mu);
+            float4* ds = reinterpret_cast<float4*>(a.out_sigma);
+            const float4* ss = reinterpret_cast<const float4*>(a.sigma);
+            const int a4 = a.A / 4;
+            for (int64_t i = tid; i < n4; i += stride) {
+                da[i] = sa[i];
+                dm[i] = sm[i];
+                ds[i] = a.sigma_mode ? ss[i] : ss[i % a4];
+            }
+        } else {
+            for (int64_t i = tid; i < na; i += stride) {
+                a.out_actions[i] = a.actions[i];
+                a.out_mu[i] = a.mu[i];
+                a.out_sigma[i] = a.sigma_mode ? a.sigma[i] : a.sigma[i % a.A];
+            }
+        }
+        return;
+    }
+
+    // ---- per-env work
+    const bool rnd = a.rnd_target != nullptr;
+    if (rnd) {
+        const int nw = a.rnd_hidden * a.rnd_in + a.rnd_hidden + a.rnd_out * a.rnd_hidden + a.rnd_out;
+        for (int i = threadIdx.x; i < nw; i += kBlock) {
+            lds_w[i] = a.rnd_target[i];
+            lds_w[nw + i] = a.rnd_predictor[i];
+        }
+        __syncthreads();
+    }
+    const int64_t n = static_cast<int64_t>(blockIdx.x - copy_blocks) * kBlock + threadIdx.x;
+    if (n >= N) return;
+
+    // log-prob of the action under Normal(mu, sigma): torch's
+    //   -((x - mu) ** 2) / (2 * var) - log(sigma) - log(sqrt(2 pi)),  var = sigma ** 2, summed over A
+    const float c = 0.918938533204672742f;  // math.log(math.sqrt(2 * math.pi)) rounded to fp32
+    float lp = 0.f;
+    const float* xr = a.actions + n * a.A;
+    const float* mr = a.mu + n * a.A;
+    const float* sr = a.sigma_mode ? a.sigma + n * a.A : a.sigma;
+    for (int j = 0; j < a.A; ++j) {
+        const float s = sr[j];
+        const float d = __fsub_rn(xr[j], mr[j]);
+        const float num = -__fmul_rn(d, d);
+        const float den = __fmul_rn(2.f, __fmul_rn(s, s));
+        const float t = __fsub_rn(__fsub_rn(__fdiv_rn(num, den), logf(s)), c);
+        lp = __fadd_rn(lp, t);
+    }
+
+    float reward = a.rewards[n];
+    if (a.extra_reward) reward = __fadd_rn(reward, a.extra_reward[n]);
+    if (rnd) {
+        float x[kMaxRndIn];
+        const float* sx = a.rnd_obs + n * a.rnd_obs_stride;
+#pragma unroll
+        for (int i = 0; i < kMaxRndIn; ++i) {
+            float v = i < a.rnd_in ? sx[i] : 0.f;
+            if (a.rnd_state_mean && i < a.rnd_in)  // (x - mean) / (std + eps), normalization.py forward
+                v = __fdiv_rn(__fsub_rn(v, a.rnd_state_mean[i]), __fadd_rn(a.rnd_state_std[i], a.rnd_state_eps));
+            x[i] = v;
+        }
+        const int nw = a.rnd_hidden * a.rnd_in + a.rnd_hidden + a.rnd_out * a.rnd_hidden + a.rnd_out;
+        float yt[kMaxRndOut], yp[kMaxRndOut];
+        rnd_forward(lds_w, a.rnd_in, a.rnd_hidden, a.rnd_out, x, yt);
+        rnd_forward(lds_w + nw, a.rnd_in, a.rnd_hidden, a.rnd_out, x, yp);
+        float ss = 0.f;
+#pragma unroll
+        for (int q = 0; q < kMaxRndOut; ++q)
+            if (q < a.rnd_out) {
+                const float d = __fsub_rn(yt[q], yp[q]);
+                ss = __fadd_rn(ss, __fmul_rn(d, d));
+            }
+        const float r_int = __fmul_rn(__fsqrt_rn(ss), a.rnd_weight);
+        if (a.intrinsic_out) a.intrinsic_out[n] = r_int;
+        reward = __fadd_rn(reward, r_int);
+    }
+    const float v = a.values[n];
+    if (a.time_outs) reward = __fadd_rn(reward, __fmul_rn(a.gamma, __fmul_rn(v, load_flag(a.time_outs, a.time_outs_dtype, n))));
+
+    a.out_rewards[n] = reward;
+    a.out_values[n] = v;
+    a.out_logp[n] = lp;
+    a.out_dones[n] = load_flag(a.dones, a.dones_dtype, n) != 0.f ? 1 : 0;
+}
+
+}  // namespace
+}  // namespace rslrl
+
+using namespace rslrl;
+
+extern "C" int rslrl_rollout_record(const rslrl_rollout_args_t* args, rslrl_stream_t stream) {
+    if (!args) return RSLRL_E_INVALID_ARGUMENT;
+    const rslrl_rollout_args_t& a = *args;
+    if (a.N < 0 || a.A < 1 || a.A > kMaxA || a.n_obs < 0 || a.n_obs > RSLRL_ROLLOUT_MAX_OBS) return RSLRL_E_INVALID_ARGUMENT;
+    if (a.N == 0) return RSLRL_OK;
+    if (!a.actions || !a.mu || !a.sigma || !a.values || !a.rewards || !a.dones || !a.out_actions || !a.out_rewards ||
+        !a.out_dones || !a.out_values || !a.out_logp || !a.out_mu || !a.out_sigma)
+        return RSLRL_E_INVALID_ARGUMENT;
+    for (int g = 0; g < a.n_obs; ++g) {
+        if (!a.obs[g].src || !a.obs[g].dst || a.obs[g].row_floats < 1 || (a.obs[g].row_floats & 3))
+            return RSLRL_E_INVALID_ARGUMENT;
+        if ((reinterpret_cast<uintptr_t>(a.obs[g].src) | reinterpret_cast<uintptr_t>(a.obs[g].dst)) & 15)
+            return RSLRL_E_MISALIGNED;
+    }
+    if ((a.A & 3) == 0 && ((reinterpret_cast<uintptr_t>(a.actions) | reinterpret_cast<uintptr_t>(a.mu) |
+                            reinterpret_cast<uintptr_t>(a.sigma) | reinterpret_cast<uintptr_t>(a.out_actions) |
+                            reinterpret_cast<uintptr_t>(a.out_mu) | reinterpret_cast<uintptr_t>(a.out_sigma)) & 15))
+        return RSLRL_E_MISALIGNED;
+    size_t lds = 0;
+    if (a.rnd_target) {
+        if (!a.rnd_predictor || !a.rnd_obs || a.rnd_in < 1 || a.rnd_in > kMaxRndIn || a.rnd_hidden < 1 ||
+            a.rnd_hidden > kMaxRndHidden || a.rnd_out < 1 || a.rnd_out > kMaxRndOut)
+            return RSLRL_E_UNSUPPORTED;
+        if ((a.rnd_state_mean == nullptr) != (a.rnd_state_std == nullptr)) return RSLRL_E_INVALID_ARGUMENT;
+        const int nw = a.rnd_hidden * a.rnd_in + a.rnd_hidden + a.rnd_out * a.rnd_hidden + a.rnd_out;
+        lds = 2 * static_cast<size_t>(nw) * sizeof(float);
+    }
+    int64_t copy_elems = a.N * a.A;
+    for (int g = 0; g < a.n_obs; ++g) copy_elems += a.N * a.obs[g].row_floats;
+    const int copy_blocks = static_cast<int>(std::min<int64_t>(1024, std::max<int64_t>(1, ceil_div(copy_elems / 4, kBlock * 4))));
+    const int64_t row_blocks = ceil_div(a.N, kBlock);
+    if (row_blocks + copy_blocks > INT32_MAX) return RSLRL_E_INVALID_ARGUMENT;
+    hipLaunchKernelGGL(rollout_record_kernel, dim3(static_cast<unsigned>(copy_blocks + row_blocks)), dim3(kBlock), lds,
+                       reinterpret_cast<hipStream_t>(stream), a, copy_blocks);
+    return launch_status();
+}

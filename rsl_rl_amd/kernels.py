@@ -21,6 +21,7 @@ __all__ = [
     "gather_rows",
     "ppo_loss_fwd_bwd",
     "PPOLossFunction",
+    "rollout_record",
 ]
 
 
@@ -308,3 +309,88 @@ class PPOLossFunction(torch.autograd.Function):
     def backward(ctx, g_loss, g_stats):
         gmu, gsig, gv = ctx.saved_tensors
         return (gmu * g_loss, gsig * g_loss, gv * g_loss) + (None,) * 13
+
+
+# --------------------------------------------------------------------------------------------------
+# rollout-side record (include/rslrl_amd.h rslrl_rollout_record)
+# --------------------------------------------------------------------------------------------------
+_DTYPE_CODES = {torch.float32: _lib.DTYPE_F32, torch.uint8: _lib.DTYPE_U8, torch.bool: _lib.DTYPE_U8,
+                torch.int32: _lib.DTYPE_I32, torch.int64: _lib.DTYPE_I64}
+
+
+def _flag_array(t, n):
+    """(tensor, dtype code) for a [N] / [N, 1] flag array, converted only if its dtype is not native."""
+    t = t.reshape(n)
+    if t.dtype not in _DTYPE_CODES:
+        t = t.float()
+    if not t.is_contiguous():
+        t = t.contiguous()
+    return t, _DTYPE_CODES[t.dtype]
+
+
+def pack_rnd_net(mlp) -> torch.Tensor:
+    """[W1 | b1 | W2 | b2] of a Linear-ELU-Linear MLP (the layout rslrl_rollout_record reads)."""
+    lin = [m for m in mlp if isinstance(m, torch.nn.Linear)]
+    return torch.cat([lin[0].weight.reshape(-1), lin[0].bias, lin[1].weight.reshape(-1), lin[1].bias]).detach()
+
+
+def rollout_record(step, *, obs_pairs, actions, mu, sigma, values, rewards, dones, time_outs, gamma,
+                   out_actions, out_rewards, out_dones, out_values, out_logp, out_mu, out_sigma,
+                   extra_reward=None, rnd=None, intrinsic_out=None):
+    """One launch for the transition of env step `step` (ppo.py:142-169 + rollout_storage.py:77-103).
+
+    obs_pairs: [(src [N, d], dst [N, d]), ...] observation groups to store.  rnd: None or a dict with
+    keys obs [N, in], target / predictor (packed, pack_rnd_net), hidden, out, weight, and optionally
+    state_mean / state_std / state_eps.  Returns nothing; all outputs are written in place."""
+    _require_device(actions, mu, values, rewards)
+    N, A = actions.shape
+    L = _lib.lib()
+    a = _lib.RolloutArgs()
+    a.N, a.A = N, A
+    sigma = sigma.detach()
+    a.sigma_mode = 1 if sigma.dim() == 2 else 0
+    keep = []
+
+    def c(t):
+        t = t.detach()
+        t = t if t.is_contiguous() else t.contiguous()
+        keep.append(t)
+        return t.data_ptr()
+
+    a.actions, a.mu, a.sigma, a.values, a.rewards = c(actions), c(mu), c(sigma), c(values), c(rewards.reshape(N))
+    d, a.dones_dtype = _flag_array(dones, N)
+    keep.append(d)
+    a.dones = d.data_ptr()
+    if time_outs is not None:
+        to, a.time_outs_dtype = _flag_array(time_outs, N)
+        keep.append(to)
+        a.time_outs = to.data_ptr()
+    a.gamma = float(gamma)
+    if extra_reward is not None:
+        a.extra_reward = c(extra_reward.reshape(N))
+    if rnd is not None:
+        ro = rnd["obs"]
+        if ro.stride(-1) != 1:
+            ro = ro.contiguous()
+        keep.append(ro)
+        a.rnd_obs, a.rnd_obs_stride = ro.data_ptr(), ro.stride(0)
+        a.rnd_in, a.rnd_hidden, a.rnd_out = ro.shape[1], rnd["hidden"], rnd["out"]
+        a.rnd_target, a.rnd_predictor = c(rnd["target"]), c(rnd["predictor"])
+        a.rnd_weight = float(rnd["weight"])
+        if rnd.get("state_mean") is not None:
+            a.rnd_state_mean = c(rnd["state_mean"].reshape(-1))
+            a.rnd_state_std = c(rnd["state_std"].reshape(-1))
+            a.rnd_state_eps = float(rnd["state_eps"])
+        if intrinsic_out is not None:
+            a.intrinsic_out = intrinsic_out.data_ptr()
+    if len(obs_pairs) > _lib.ROLLOUT_MAX_OBS:
+        raise ValueError(f"at most {_lib.ROLLOUT_MAX_OBS} observation groups")
+    a.n_obs = len(obs_pairs)
+    for i, (src, dst) in enumerate(obs_pairs):
+        a.obs[i].src, a.obs[i].dst, a.obs[i].row_floats = c(src), dst.data_ptr(), src.shape[-1]
+    a.out_actions, a.out_rewards, a.out_dones = out_actions.data_ptr(), out_rewards.data_ptr(), out_dones.data_ptr()
+    a.out_values, a.out_logp = out_values.data_ptr(), out_logp.data_ptr()
+    a.out_mu, a.out_sigma = out_mu.data_ptr(), out_sigma.data_ptr()
+    rc = L.rslrl_rollout_record(ctypes.byref(a), _stream(actions.device))
+    _lib.check(rc, "rslrl_rollout_record")
+    return keep  # the caller may hold these until the stream has consumed them (torch's allocator is stream-ordered)

@@ -100,6 +100,43 @@ class RolloutStorage:
         self._save_hidden_states(transition.hidden_states)
         self.step += 1
 
+    def fused_record_ok(self, transition) -> bool:
+        """The fused rollout record (kernels.rollout_record) covers the RL transition of a feed-forward
+        policy on a ROCm device: A <= 64 and fp32 policy outputs."""
+        a = transition.actions
+        return (self.training_type == "rl" and a is not None and a.is_cuda and a.dim() == 2
+                and a.dtype == torch.float32 and a.shape[1] <= 64 and transition.hidden_states in (None, (None, None))
+                and len(self.actions_shape) == 1)
+
+    def add_transition_fused(self, transition, rewards, dones, time_outs, gamma, extra_reward=None, rnd=None,
+                             intrinsic_out=None):
+        """add_transitions + the reward arithmetic of PPO.process_env_step in one launch
+        (rollout_storage.py:77-103, ppo.py:147-164): row t receives the observation groups, actions,
+        (rewards + extra + r_int) + gamma * values * time_outs, uint8(dones), values, log-prob, mu, sigma."""
+        if self.step >= self.num_transitions_per_env:
+            raise OverflowError("Rollout buffer overflow! You should call clear() before adding new transitions.")
+        t = self.step
+        pairs = []
+        for k, dst in self.observations.items():
+            src = transition.observations[k]
+            ok = (src.dtype == torch.float32 and src.is_cuda and src.dim() == 2 and src.shape[-1] % 4 == 0
+                  and src.is_contiguous() and src.data_ptr() % 16 == 0 and dst[t].data_ptr() % 16 == 0
+                  and len(pairs) < 4)
+            if ok:
+                pairs.append((src, dst[t]))
+            else:
+                dst[t].copy_(src)
+        sigma = transition.action_sigma
+        if sigma.dim() == 2 and sigma.stride(0) == 0:  # Normal's expand of a shared [A] std
+            sigma = sigma[0]
+        kernels.rollout_record(
+            t, obs_pairs=pairs, actions=transition.actions, mu=transition.action_mean, sigma=sigma,
+            values=transition.values, rewards=rewards, dones=dones, time_outs=time_outs, gamma=gamma,
+            out_actions=self.actions[t], out_rewards=self.rewards[t], out_dones=self.dones[t],
+            out_values=self.values[t], out_logp=self.actions_log_prob[t], out_mu=self.mu[t], out_sigma=self.sigma[t],
+            extra_reward=extra_reward, rnd=rnd, intrinsic_out=intrinsic_out)
+        self.step += 1
+
     def _save_hidden_states(self, hidden_states):
         if hidden_states is None or hidden_states == (None, None):
             return

@@ -446,12 +446,85 @@ def make_update_c1(PPO, ActorCritic, RolloutStorage):
     return m
 
 
+# --------------------------------------------------------------------------------------------------
+# rollout side: act + process_env_step + add_transitions + RND (ppo.py:129-169, rollout_storage.py:77-103,
+# rnd.py:113-135) -- the inputs of each step, the transition act() produced, and the storage after T steps
+# --------------------------------------------------------------------------------------------------
+ROLLOUT_CASES = [
+    # name, N, O, A, T, rnd_cfg (None: no RND), p(time_out), dones dtype, seed
+    ("rnd_c5like", 300, 48, 12, 3,
+     dict(weight=1.0 * 0.02, num_outputs=1, predictor_hidden_dims=[-1], target_hidden_dims=[-1]), 0.3, "int64", 7),
+    ("rnd_statenorm_q3", 130, 16, 4, 3,
+     dict(weight=0.5, num_outputs=3, predictor_hidden_dims=[32], target_hidden_dims=[32], state_normalization=True,
+          weight_schedule={"mode": "step", "final_step": 2, "final_value": 0.25}), 0.2, "bool", 8),
+    ("plain_timeouts", 257, 16, 4, 2, None, 0.5, "float", 9),
+]
+
+
+def make_rollout(PPO, ActorCritic, RolloutStorage):
+    meta = {}
+    for name, N, O, A, T, rnd_cfg, p_to, dt, seed in ROLLOUT_CASES:
+        torch.manual_seed(seed)
+        obs0 = {"policy": torch.zeros(N, O)}
+        groups = {"policy": ["policy"], "critic": ["policy"], "rnd_state": ["policy"]}
+        pol = ActorCritic(obs0, groups, A, actor_hidden_dims=[64, 64], critic_hidden_dims=[64, 64])
+        cfg = None
+        if rnd_cfg is not None:
+            cfg = dict(rnd_cfg, num_states=O, obs_groups=groups)
+        alg = PPO(pol, device="cpu", rnd_cfg=cfg)
+        alg.init_storage("rl", N, T, obs0, [A])
+        arrays = {f"init/{k}": f32(v) for k, v in pol.state_dict().items()}
+        if alg.rnd is not None:
+            arrays.update({f"rnd_init/{k}": f32(v) for k, v in alg.rnd.state_dict().items()})
+        g = torch.Generator().manual_seed(seed + 1)
+        obs = torch.randn(N, O, generator=g)
+        for t in range(T):
+            with torch.inference_mode():
+                alg.act({"policy": obs})
+                tr = alg.transition
+                arrays[f"step{t}/obs"] = f32(obs)
+                for k in ("actions", "values", "actions_log_prob", "action_mean", "action_sigma"):
+                    arrays[f"step{t}/{k}"] = f32(getattr(tr, k))
+                nobs = torch.randn(N, O, generator=g)
+                rew = torch.randn(N, generator=g)
+                d = torch.rand(N, generator=g) < 0.1
+                dones = {"int64": d.long(), "bool": d, "float": d.float()}[dt]
+                to = (torch.rand(N, generator=g) < p_to).float()
+                arrays[f"step{t}/next_obs"] = f32(nobs)
+                arrays[f"step{t}/rewards"] = f32(rew)
+                arrays[f"step{t}/dones"] = d.numpy().astype(np.uint8)
+                arrays[f"step{t}/time_outs"] = f32(to)
+                alg.process_env_step({"policy": nobs}, rew, dones, {"time_outs": to})
+                if alg.rnd is not None:
+                    arrays[f"step{t}/intrinsic"] = f32(alg.intrinsic_rewards)
+                    arrays[f"step{t}/rnd_weight"] = np.float32(alg.rnd.weight)
+                obs = nobs
+        st = alg.storage
+        for k in ("rewards", "values", "actions_log_prob", "mu", "sigma", "actions"):
+            arrays[f"storage/{k}"] = f32(getattr(st, k))
+        arrays["storage/dones"] = st.dones.numpy().copy()
+        arrays["storage/obs_policy"] = f32(st.observations["policy"])
+        np.savez_compressed(os.path.join(HERE, f"rollout_{name}.npz"), **arrays)
+        meta[name] = {"N": N, "O": O, "A": A, "T": T, "rnd_cfg": rnd_cfg, "dones_dtype": dt, "gamma": alg.gamma,
+                      "p_time_out": p_to, "actor_hidden": [64, 64]}
+    return meta
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reference", default=os.environ.get("RSL_RL_REFERENCE", "/root/reference"))
+    ap.add_argument("--only", choices=["rollout"], help="regenerate one fixture family, keep the rest")
     args = ap.parse_args()
     torch.set_num_threads(4)
     PPO, ActorCritic, RolloutStorage = import_reference(args.reference)
+    if args.only == "rollout":
+        with open(os.path.join(HERE, "golden.json")) as f:
+            meta = json.load(f)
+        meta["rollout"] = make_rollout(PPO, ActorCritic, RolloutStorage)
+        with open(os.path.join(HERE, "golden.json"), "w") as f:
+            json.dump(meta, f, indent=1, sort_keys=True)
+        print("wrote rollout fixtures")
+        return
     meta = {
         "generator": "tests/golden/make_golden.py",
         "reference": "rsl-rl-lib 3.1.0 (kaixi287/rsl_rl snapshot 2025-10-17)",
@@ -461,6 +534,7 @@ def main():
         "minibatch": make_minibatch(RolloutStorage),
         "loss": make_loss(PPO, ActorCritic, RolloutStorage),
         "update_c1": make_update_c1(PPO, ActorCritic, RolloutStorage),
+        "rollout": make_rollout(PPO, ActorCritic, RolloutStorage),
     }
     with open(os.path.join(HERE, "golden.json"), "w") as f:
         json.dump(meta, f, indent=1, sort_keys=True)

@@ -103,3 +103,33 @@ def test_loss_and_gradients(golden_meta):
             if m["num_batches"] == 1:
                 for k in ("surrogate", "value_function", "entropy"):
                     assert abs(o[k] - m["loss_dict"][k]) <= 1e-5 * abs(m["loss_dict"][k]) + 1e-7, (name, k)
+
+
+# ---------------------------------------------------------------------------------------------------
+# rollout side (ppo.py:129-169, rnd.py:113-135) -- oracle vs the reference's captured rollout
+# ---------------------------------------------------------------------------------------------------
+def _rnd_layers(z, prefix, net):
+    keys = sorted({k.rsplit(".", 1)[0] for k in z.files if k.startswith(f"{prefix}{net}.")},
+                  key=lambda k: int(k.rsplit(".", 1)[1]))
+    return [(z[k + ".weight"], z[k + ".bias"]) for k in keys]
+
+
+@pytest.mark.parametrize("case", ["rnd_c5like", "rnd_statenorm_q3", "plain_timeouts"])
+def test_oracle_rollout_record(case, golden_meta):
+    from oracle import ppo_oracle as po
+    m = golden_meta["rollout"][case]
+    z = np.load(golden_path(f"rollout_{case}.npz"))
+    T = m["T"]
+    for t in range(T):
+        lp = po.normal_log_prob_sum(z[f"step{t}/actions"], z[f"step{t}/action_mean"], z[f"step{t}/action_sigma"])
+        np.testing.assert_allclose(lp, z[f"step{t}/actions_log_prob"], rtol=2e-6, atol=2e-6)
+        intr = None
+        if m["rnd_cfg"] is not None:
+            if not m["rnd_cfg"].get("state_normalization"):  # (normaliser statistics evolve: GPU test)
+                ours = po.rnd_intrinsic(z[f"step{t}/next_obs"], _rnd_layers(z, "rnd_init/", "target"),
+                                        _rnd_layers(z, "rnd_init/", "predictor"), z[f"step{t}/rnd_weight"])
+                np.testing.assert_allclose(ours, z[f"step{t}/intrinsic"], rtol=1e-5, atol=1e-6)
+            intr = z[f"step{t}/intrinsic"]  # the reward composition itself is checked bit-exactly
+        r = po.step_reward(z[f"step{t}/rewards"], z[f"step{t}/values"], z[f"step{t}/time_outs"], m["gamma"], intr)
+        np.testing.assert_array_equal(r, z["storage/rewards"][t, :, 0])
+        np.testing.assert_array_equal(z["storage/dones"][t, :, 0], z[f"step{t}/dones"])
