@@ -31,6 +31,10 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+BF16_MFMA_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA at 2.4 GHz (MI355X_MICROARCH.md)
+X6_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 6  # fp32-equivalent peak of the 6-product split-bf16 GEMMs
+FP32_MFMA_PEAK_TFLOPS = 157.3
+HOT_PATH = ("gae_scan", "adv_normalize", "gather_rows", "ppo_loss", "rollout_record")
 # per-launch HBM traffic of the hot-path kernels from rocprofv3 FETCH_SIZE / WRITE_SIZE passes over this same
 # bench command (scripts/pmc_summary.py; raw counters next to it).  PMC passes serialise and slow the
 # run, so they are collected separately and the committed summary is reported here.
@@ -46,9 +50,9 @@ def pmc_traffic(kernel):
         return None, None
 
 
-def train_cfg(args):
+def train_cfg(args, rnd=False):
     hidden = [args.hidden] * args.layers
-    return {
+    cfg = {
         "num_steps_per_env": args.num_steps_per_env,
         "save_interval": 10**9,
         "obs_groups": {"policy": ["policy"], "critic": ["policy"]},
@@ -60,6 +64,35 @@ def train_cfg(args):
                       "use_clipped_value_loss": True, "desired_kl": 0.01, "entropy_coef": 0.01, "gamma": 0.99,
                       "lam": 0.95, "max_grad_norm": 1.0, "normalize_advantage_per_mini_batch": False},
     }
+    if rnd:  # config C5: RND weight 1.0 (x step_dt), 1 output, hidden [-1], no normalisation
+        cfg["obs_groups"]["rnd_state"] = ["policy"]
+        cfg["algorithm"]["rnd_cfg"] = {"weight": 1.0, "num_outputs": 1, "predictor_hidden_dims": [-1],
+                                       "target_hidden_dims": [-1], "learning_rate": 1e-3,
+                                       "state_normalization": False, "reward_normalization": False}
+    return cfg
+
+
+def time_runner(args, device, rank, *, rnd=False, steps=3, warmup=1):
+    """Iterations/s of a fresh runner (for the secondary configurations; world size 1 only)."""
+    from rsl_rl_amd.env import SyntheticVecEnv
+    from rsl_rl_amd.runners import OnPolicyRunner
+
+    torch.manual_seed(1)
+    env = SyntheticVecEnv(args.num_envs, args.num_obs, args.num_actions, device=device, seed=rank)
+    with contextlib.redirect_stdout(sys.stderr):
+        runner = OnPolicyRunner(env, train_cfg(args, rnd=rnd), log_dir=None, device=device)
+        runner.learn(warmup)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        runner.learn(steps)
+        torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    stats = {k: round(v, 4) for k, v in runner.last_iteration_stats.items() if k != "loss_dict"}
+    del runner, env
+    torch.cuda.empty_cache()
+    T, N = args.num_steps_per_env, args.num_envs
+    return {"value": round(T * N * steps / el, 1), "unit": "env-steps/s", "steps": steps, "warmup": warmup,
+            "ms_per_step": round(el / steps * 1e3, 3), "phases_last_iter": stats}
 
 
 def cpu_baseline(args):
@@ -99,6 +132,7 @@ def main():
     ap.add_argument("--layers", type=int, default=3)
     ap.add_argument("--cpu-sample-envs", type=int, default=8192)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extra", action="store_true", help="skip the secondary configurations (C5, f32 GEMMs)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -135,6 +169,12 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     kernels.timer.enabled = False
+    # one more iteration with the MLP GEMM launches timed (kept out of the headline timing: ~470 event
+    # pairs per iteration would add host overhead to the launch-bound rollout)
+    kernels.timer.mlp_enabled = True
+    runner.learn(1)
+    torch.cuda.synchronize()
+    kernels.timer.mlp_enabled = False
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -144,14 +184,21 @@ def main():
     value = T * N * world * K / elapsed
     prof = kernels.timer.summary()
     hot = {}
+    mlp = {}
     for name, s in prof.items():
-        hot[name] = {
-            "launches_per_step": s["launches"] / K,
+        ent = {
+            "launches_per_step": s["launches"] / (1 if name.startswith("linear_") else K),
             "mean_us": round(s["mean_ms"] * 1e3, 2),
-            "ms_per_step": round(s["total_ms"] / K, 4),
+            "ms_per_step": round(s["total_ms"] / (1 if name.startswith("linear_") else K), 4),
             "algorithmic_bytes_per_launch": int(s["bytes_per_launch"]),
             "achieved_GBps": round(s["bytes_per_launch"] / (s["mean_ms"] * 1e-3) / 1e9, 1),
         }
+        if name in HOT_PATH:
+            hot[name] = ent
+        elif name.startswith("linear_"):
+            ent["flops_per_launch"] = int(s["flops_per_launch"])
+            ent["achieved_TFLOPs"] = round(s["flops_per_launch"] / (s["mean_ms"] * 1e-3) / 1e12, 1)
+            mlp[name] = ent
     hot_ms = sum(h["ms_per_step"] for h in hot.values())
     dominant = max(hot, key=lambda k: hot[k]["ms_per_step"]) if hot else None
     roofline = None
@@ -162,6 +209,19 @@ def main():
                     "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": traffic, "traffic_source": traffic_src,
                     "algorithmic_bytes_per_launch": hot[dominant]["algorithmic_bytes_per_launch"],
                     "mean_launch_us": hot[dominant]["mean_us"]}
+    roofline_mlp = None
+    from rsl_rl_amd.networks import fused_mlp
+    x6 = fused_mlp._mode == fused_mlp.GEMM_X6
+    if mlp:
+        dm = max(mlp, key=lambda k: mlp[k]["ms_per_step"])
+        ach = mlp[dm]["achieved_TFLOPs"]
+        peak = X6_PEAK_TFLOPS if x6 else FP32_MFMA_PEAK_TFLOPS
+        roofline_mlp = {"kernel": dm, "bound": "mfma", "achieved": ach, "peak": round(peak, 1), "unit": "TFLOP/s",
+                        "frac": round(ach / peak, 4), "traffic": None,
+                        "flops_per_launch": mlp[dm]["flops_per_launch"], "mean_launch_us": mlp[dm]["mean_us"],
+                        "arithmetic": "x6 split-bf16 (fp32-class, DESIGN.md s5); peak = bf16 dense / 6" if x6
+                        else "fp32 MFMA", "fp32_mfma_peak": FP32_MFMA_PEAK_TFLOPS,
+                        "mlp_ms_per_step": round(sum(e["ms_per_step"] for e in mlp.values()), 3)}
 
     out = {
         "metric": "PPO env-steps/sec (rollout+GAE+update) at N=65536 envs, 1->8 MI355X",
@@ -175,6 +235,7 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "fp32",
+        "gemm_arithmetic": "x6 split-bf16 MFMA, fp32-class error (DESIGN.md s5)" if x6 else "fp32 MFMA",
         "data": "synthetic (SyntheticVecEnv: obs/reward ~ N(0,1), dones ~ Bernoulli(0.02); random-init weights)",
         "config": {
             "workload": f"C3: {N} envs/GPU x T={T}, obs {args.num_obs}, act {args.num_actions}, "
@@ -187,11 +248,23 @@ def main():
             "parallelism": f"dp{world} (env shards, RCCL grad all-reduce per mini-batch)",
         },
         "roofline": roofline,
+        "roofline_mlp": roofline_mlp,
+        "mlp_kernels": mlp,
         "hot_path": {"kernels": hot, "ms_per_step": round(hot_ms, 4),
                      "env_steps_per_s": round(T * N / (hot_ms * 1e-3), 1) if hot_ms else None},
         "phases_last_iter": {k: round(v, 4) for k, v in runner.last_iteration_stats.items() if k != "loss_dict"},
         "cpu_baseline": None,
     }
+    if world == 1 and not args.no_extra:
+        del runner, env
+        torch.cuda.empty_cache()
+        extra = {"C5_rnd": time_runner(args, device, rank, rnd=True)}
+        extra["C5_rnd"]["workload"] = "C3 + RND (predictor/target 48->48->1 ELU, weight 1.0 x step_dt, fused record)"
+        prev = fused_mlp.set_gemm_mode(fused_mlp.GEMM_F32)
+        extra["C3_fp32_mfma"] = time_runner(args, device, rank)
+        extra["C3_fp32_mfma"]["workload"] = "C3 with the exact-fp32 MFMA GEMM kernels (RSLRL_GEMM_MODE=f32)"
+        fused_mlp.set_gemm_mode(prev)
+        out["extra_configs"] = extra
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args)
     if rank == 0:

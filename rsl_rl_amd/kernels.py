@@ -76,16 +76,19 @@ class KernelTimer:
 
     def __init__(self):
         self.enabled = False
+        self.mlp_enabled = False  # the (many) MLP GEMM launches are timed separately from the hot path
         self.spans = defaultdict(list)
         self.bytes = defaultdict(list)
+        self.flops = defaultdict(list)
 
     def reset(self):
         self.spans.clear()
         self.bytes.clear()
+        self.flops.clear()
 
     @contextlib.contextmanager
-    def span(self, name: str, device: torch.device, algorithmic_bytes: int):
-        if not self.enabled:
+    def span(self, name: str, device: torch.device, algorithmic_bytes: int, flops: int = 0):
+        if not (self.mlp_enabled if name.startswith("linear_") else self.enabled):
             yield
             return
         stream = torch.cuda.current_stream(device)
@@ -96,6 +99,7 @@ class KernelTimer:
         end.record(stream)
         self.spans[name].append((start, end))
         self.bytes[name].append(algorithmic_bytes)
+        self.flops[name].append(flops)
 
     def summary(self):
         """name -> {launches, mean_ms, total_ms, bytes_per_launch}; synchronises the events."""
@@ -107,6 +111,7 @@ class KernelTimer:
                 "mean_ms": sum(ms) / len(ms),
                 "total_ms": sum(ms),
                 "bytes_per_launch": sum(self.bytes[name]) / len(self.bytes[name]),
+                "flops_per_launch": sum(self.flops[name]) / len(self.flops[name]),
             }
         return out
 
@@ -391,6 +396,11 @@ def rollout_record(step, *, obs_pairs, actions, mu, sigma, values, rewards, done
     a.out_actions, a.out_rewards, a.out_dones = out_actions.data_ptr(), out_rewards.data_ptr(), out_dones.data_ptr()
     a.out_values, a.out_logp = out_values.data_ptr(), out_logp.data_ptr()
     a.out_mu, a.out_sigma = out_mu.data_ptr(), out_sigma.data_ptr()
-    rc = L.rslrl_rollout_record(ctypes.byref(a), _stream(actions.device))
+    # algorithmic bytes per env (SURVEY §8d style): obs groups in+out, actions/mu in+out, sigma out (+in if
+    # per row), values/rewards/dones/time-outs in, reward/value/log-prob/done out
+    obs_b = sum(8 * src.shape[-1] for src, _ in obs_pairs)
+    per_env = obs_b + 4 * A * (5 + a.sigma_mode) + 4 + 4 + d.element_size() + 4 + (4 if time_outs is not None else 0) + 13
+    with timer.span("rollout_record", actions.device, per_env * N):
+        rc = L.rslrl_rollout_record(ctypes.byref(a), _stream(actions.device))
     _lib.check(rc, "rslrl_rollout_record")
     return keep  # the caller may hold these until the stream has consumed them (torch's allocator is stream-ordered)

@@ -26,6 +26,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import _lib
+from ..kernels import timer
 from .linear import _splitk_weight_grad
 
 MAX_WIDTH = 256
@@ -118,8 +119,9 @@ def linear_fwd(x, w, b, elu: bool, img=None):
     M, K = x.shape
     N = w.shape[0]
     y = torch.empty(M, N, device=x.device, dtype=torch.float32)
-    rc = _lib.lib().rslrl_linear_fwd(x.data_ptr(), M, K, w.data_ptr(), N, b.data_ptr(), 1 if elu else 0,
-                                     y.data_ptr(), img.data_ptr() if img is not None else None, _stream(x))
+    with timer.span(f"linear_fwd[M={M},K={K},N={N}]", x.device, 4 * M * (K + N), 2 * M * K * N):
+        rc = _lib.lib().rslrl_linear_fwd(x.data_ptr(), M, K, w.data_ptr(), N, b.data_ptr(), 1 if elu else 0,
+                                         y.data_ptr(), img.data_ptr() if img is not None else None, _stream(x))
     _lib.check(rc, "rslrl_linear_fwd")
     return y
 
@@ -134,8 +136,9 @@ def linear_dgrad_elu(dz, w, h, img=None):
     tiles = L.rslrl_linear_tiles(M)
     out = torch.empty(M, K, device=dz.device, dtype=torch.float32)
     part = torch.empty(K, tiles, device=dz.device, dtype=torch.float32)
-    rc = L.rslrl_linear_dgrad_elu(dz.data_ptr(), M, N, wt.data_ptr(), K, h.data_ptr(), out.data_ptr(),
-                                  part.data_ptr(), img.data_ptr() if img is not None else None, _stream(dz))
+    with timer.span(f"linear_dgrad[M={M},Nred={N},K={K}]", dz.device, 4 * M * (N + 2 * K), 2 * M * K * N):
+        rc = L.rslrl_linear_dgrad_elu(dz.data_ptr(), M, N, wt.data_ptr(), K, h.data_ptr(), out.data_ptr(),
+                                      part.data_ptr(), img.data_ptr() if img is not None else None, _stream(dz))
     _lib.check(rc, "rslrl_linear_dgrad_elu")
     db = torch.empty(K, device=dz.device, dtype=torch.float32)
     rc = L.rslrl_column_sum_fold(part.data_ptr(), tiles, K, db.data_ptr(), _stream(dz))
@@ -151,8 +154,9 @@ def linear_wgrad(dz, x):
     nbytes = L.rslrl_linear_wgrad_workspace_bytes(M, N, K)
     ws = torch.empty(nbytes // 4, dtype=torch.float32, device=dz.device)
     dw = torch.empty(N, K, dtype=torch.float32, device=dz.device)
-    rc = L.rslrl_linear_wgrad(dz.data_ptr(), x.data_ptr(), M, N, K, dw.data_ptr(), ws.data_ptr(), nbytes,
-                              _stream(dz))
+    with timer.span(f"linear_wgrad[M={M},N={N},K={K}]", dz.device, 4 * M * (N + K), 2 * M * K * N):
+        rc = L.rslrl_linear_wgrad(dz.data_ptr(), x.data_ptr(), M, N, K, dw.data_ptr(), ws.data_ptr(), nbytes,
+                                  _stream(dz))
     _lib.check(rc, "rslrl_linear_wgrad")
     return dw
 
