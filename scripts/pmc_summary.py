@@ -21,8 +21,15 @@ SHORT = {
     "adv_normalize_kernel": "adv_normalize",
     "moments_kernel": "moments",
     "gather_rows_kernel": "gather_rows",
+    "rollout_record_kernel": "rollout_record",
+    "mlp_gemm_x6_kernel<1": "x6_fwd_elu",
+    "mlp_gemm_x6_kernel<2": "x6_dgrad_elu",
+    "wgrad_x6_kernel": "x6_wgrad",
+    "wgrad_fold_kernel": "wgrad_fold",
     "__amd_rocclr_copyBuffer": "copyBuffer",
 }
+# kernels launched at several shapes are keyed "<short>@grid=<threads>"
+BY_GRID = {"x6_fwd_elu", "x6_dgrad_elu", "x6_wgrad", "wgrad_fold"}
 
 
 def load(d, counter):
@@ -35,6 +42,8 @@ def load(d, counter):
                 continue
             name = next((v for k, v in SHORT.items() if k in r["Kernel_Name"]), None)
             if name:
+                if name in BY_GRID:
+                    name = f"{name}@grid={r['Grid_Size']}"
                 out[name].append(float(r["Counter_Value"]))
     return out
 
