@@ -259,6 +259,26 @@ typedef struct {
 } rslrl_rollout_args_t;
 int rslrl_rollout_record(const rslrl_rollout_args_t* args /* host struct */, rslrl_stream_t stream);
 
+/* ------------------------------------------------------------------------------------------------
+ * Running normalisers, rsl_rl/networks/normalization.py.
+ *   rslrl_normalizer_update: EmpiricalNormalization.update (:44-66) of the running (mean, var, std, count)
+ *     [D] fp32 buffers (count: device int64) with the batch x [N, D] (row stride row_stride); no-op when
+ *     until >= 0 and count >= until (tested on the device).  Workspace: rslrl_normalizer_workspace_bytes.
+ *   rslrl_normalizer_apply: y [N, D] = (x - mean) / (std + eps)  (forward, :40-42).
+ *   rslrl_reward_normalize: EmpiricalDiscountedVariationNormalization.forward (:84-99) over rewards [N]:
+ *     when training, disc_avg = first ? r : disc_avg * gamma + r, then the update above with D = 1; then
+ *     out = r / std if std > 0 else r.
+ * ----------------------------------------------------------------------------------------------*/
+size_t rslrl_normalizer_workspace_bytes(int64_t N, int32_t D);
+int rslrl_normalizer_update(const float* x, int64_t N, int32_t D, int64_t row_stride, float* mean, float* var,
+                            float* std, int64_t* count, int64_t until, void* workspace, size_t workspace_bytes,
+                            rslrl_stream_t stream);
+int rslrl_normalizer_apply(const float* x, int64_t N, int32_t D, int64_t row_stride, const float* mean,
+                           const float* std, float eps, float* y, rslrl_stream_t stream);
+int rslrl_reward_normalize(const float* rewards, int64_t N, float gamma, float* disc_avg, int32_t first, float* mean,
+                           float* var, float* std, int64_t* count, int64_t until, int32_t training, float* out,
+                           void* workspace, size_t workspace_bytes, rslrl_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -290,3 +290,28 @@ def step_reward(rewards, values, time_outs, gamma, intrinsic=None):
     if time_outs is not None:
         r = (r + (f32(gamma) * (values.reshape(-1).astype(f32) * time_outs.astype(f32)).astype(f32)).astype(f32))
     return r.astype(f32)
+
+
+# --------------------------------------------------------------------------------------------------
+# running normalisers (networks/normalization.py:44-99)
+# --------------------------------------------------------------------------------------------------
+def normalizer_update(x, mean, var, count, until=None):
+    """One EmpiricalNormalization.update: fp64 batch moments, then the reference's fp32 update order.
+    Returns (mean, var, std, count) (the inputs unchanged once count >= until)."""
+    if until is not None and count >= until:
+        return mean, var, np.sqrt(var).astype(f32), count
+    n = x.shape[0]
+    count = count + n
+    rate = f32(f32(n) / f32(count))
+    xd = x.astype(np.float64)
+    mean_x = xd.mean(0).astype(f32)
+    var_x = np.maximum((xd * xd).mean(0) - xd.mean(0) ** 2, 0.0).astype(f32)
+    delta = (mean_x - mean).astype(f32)
+    mean_new = (mean + (rate * delta).astype(f32)).astype(f32)
+    inner = ((var_x - var).astype(f32) + (delta * (mean_x - mean_new).astype(f32)).astype(f32)).astype(f32)
+    var_new = (var + (rate * inner).astype(f32)).astype(f32)
+    return mean_new, var_new, np.sqrt(var_new).astype(f32), count
+
+
+def normalizer_apply(x, mean, std, eps=1e-2):
+    return ((x.astype(f32) - mean).astype(f32) / (std + f32(eps)).astype(f32)).astype(f32)

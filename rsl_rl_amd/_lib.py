@@ -42,6 +42,10 @@ EXPORTED_SYMBOLS = (
     "rslrl_linear_wgrad_workspace_bytes",
     "rslrl_linear_wgrad",
     "rslrl_rollout_record",
+    "rslrl_normalizer_workspace_bytes",
+    "rslrl_normalizer_update",
+    "rslrl_normalizer_apply",
+    "rslrl_reward_normalize",
 )
 
 MAX_GATHER_FIELDS = 16
@@ -190,6 +194,14 @@ def _declare(L):
     L.rslrl_linear_wgrad_workspace_bytes.argtypes = [I64, I32, I32]
     L.rslrl_linear_wgrad.restype = ctypes.c_int
     L.rslrl_linear_wgrad.argtypes = [P, P, I64, I32, I32, P, P, SZ, P]
+    L.rslrl_normalizer_workspace_bytes.restype = SZ
+    L.rslrl_normalizer_workspace_bytes.argtypes = [I64, I32]
+    L.rslrl_normalizer_update.restype = ctypes.c_int
+    L.rslrl_normalizer_update.argtypes = [P, I64, I32, I64, P, P, P, P, I64, P, SZ, P]
+    L.rslrl_normalizer_apply.restype = ctypes.c_int
+    L.rslrl_normalizer_apply.argtypes = [P, I64, I32, I64, P, P, F, P, P]
+    L.rslrl_reward_normalize.restype = ctypes.c_int
+    L.rslrl_reward_normalize.argtypes = [P, I64, F, P, I32, P, P, P, P, I64, I32, P, P, SZ, P]
     L.rslrl_rollout_record.restype = ctypes.c_int
     L.rslrl_rollout_record.argtypes = [ctypes.POINTER(RolloutArgs), P]
     L.rslrl_column_sum_fold.restype = ctypes.c_int

@@ -1,14 +1,34 @@
 """Running observation / reward normalisers (rsl_rl/networks/normalization.py).
 
 Same buffers (_mean, _var, _std, count) and update rule as the reference so checkpoints load into
-either implementation.  Fusing the per-step moment update into the rollout-side kernel is listed as a
-"next" item in SURVEY.md §8f.
+either implementation.  On a ROCm device the update, the forward and the reward normaliser run on the
+HIP kernels of csrc/normalizer.hip (fp64 batch moments, the reference's fp32
+update order, the `until` limit tested on the device -- no host synchronisation); CPU modules (e.g. an
+exported inference policy) keep the PyTorch expressions.
 """
 
 from __future__ import annotations
 
 import torch
 from torch import nn
+
+from .. import _lib
+
+
+def _stream(t):
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+class _WS:
+    bufs: dict = {}
+
+    @classmethod
+    def get(cls, device, nbytes):
+        b = cls.bufs.get(device)
+        if b is None or b.numel() < nbytes:
+            b = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=device)
+            cls.bufs[device] = b
+        return b
 
 
 class EmpiricalNormalization(nn.Module):
@@ -32,12 +52,30 @@ class EmpiricalNormalization(nn.Module):
         return self._std.squeeze(0).clone()
 
     def forward(self, x):
+        if x.is_cuda and x.dim() == 2 and x.dtype == torch.float32 and x.stride(-1) == 1:
+            N, D = x.shape
+            y = torch.empty(N, D, dtype=torch.float32, device=x.device)
+            rc = _lib.lib().rslrl_normalizer_apply(x.data_ptr(), N, D, x.stride(0), self._mean.data_ptr(),
+                                                   self._std.data_ptr(), float(self.eps), y.data_ptr(), _stream(x))
+            _lib.check(rc, "rslrl_normalizer_apply")
+            return y
         return (x - self._mean) / (self._std + self.eps)
 
     @torch.jit.unused
     def update(self, x):
         """Chan et al. parallel-moments merge of the batch into the running (mean, var)."""
         if not self.training:
+            return
+        if x.is_cuda and x.dim() == 2 and x.dtype == torch.float32 and x.stride(-1) == 1 and x.shape[1] <= 256:
+            N, D = x.shape
+            L = _lib.lib()
+            nbytes = L.rslrl_normalizer_workspace_bytes(N, D)
+            ws = _WS.get(x.device, nbytes)
+            until = -1 if self.until is None else int(self.until)
+            rc = L.rslrl_normalizer_update(x.data_ptr(), N, D, x.stride(0), self._mean.data_ptr(), self._var.data_ptr(),
+                                           self._std.data_ptr(), self.count.data_ptr(), until, ws.data_ptr(), nbytes,
+                                           _stream(x))
+            _lib.check(rc, "rslrl_normalizer_update")
             return
         if self.until is not None and self.count >= self.until:
             return
@@ -65,6 +103,25 @@ class EmpiricalDiscountedVariationNormalization(nn.Module):
         self.disc_avg = _DiscountedAverage(gamma)
 
     def forward(self, rew):
+        en = self.emp_norm
+        if rew.is_cuda and rew.dim() == 1 and rew.dtype == torch.float32 and rew.is_contiguous():
+            N = rew.shape[0]
+            first = self.disc_avg.avg is None
+            if self.training and first:
+                self.disc_avg.avg = torch.empty_like(rew)
+            L = _lib.lib()
+            nbytes = L.rslrl_normalizer_workspace_bytes(N, 1)
+            ws = _WS.get(rew.device, nbytes)
+            out = torch.empty_like(rew)
+            until = -1 if en.until is None else int(en.until)
+            avg = self.disc_avg.avg
+            rc = L.rslrl_reward_normalize(rew.data_ptr(), N, float(self.disc_avg.gamma),
+                                          avg.data_ptr() if avg is not None else None, int(first),
+                                          en._mean.data_ptr(), en._var.data_ptr(), en._std.data_ptr(),
+                                          en.count.data_ptr(), until, int(self.training), out.data_ptr(),
+                                          ws.data_ptr(), nbytes, _stream(rew))
+            _lib.check(rc, "rslrl_reward_normalize")
+            return out
         if self.training:
             self.emp_norm.update(self.disc_avg.update(rew))
         if self.emp_norm._std > 0:

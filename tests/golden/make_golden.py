@@ -510,20 +510,53 @@ def make_rollout(PPO, ActorCritic, RolloutStorage):
     return meta
 
 
+# --------------------------------------------------------------------------------------------------
+# normalisers (networks/normalization.py): a sequence of updates with an `until` limit, forward outputs,
+# and the discounted reward normaliser over several steps
+# --------------------------------------------------------------------------------------------------
+def make_normalizer(ref_path):
+    sys.path.insert(0, ref_path)
+    from rsl_rl.networks.normalization import EmpiricalDiscountedVariationNormalization, EmpiricalNormalization
+
+    g = torch.Generator().manual_seed(77)
+    arrays = {}
+    norm = EmpiricalNormalization(shape=[7], until=2500)
+    norm.train()
+    for k in range(4):  # 1000 rows each: the 4th update is skipped (count 3000 >= 2500)
+        x = torch.randn(1000, 7, generator=g) * torch.linspace(0.5, 3.0, 7) + torch.linspace(-2.0, 5.0, 7)
+        norm.update(x)
+        arrays[f"obs/x{k}"] = f32(x)
+        arrays[f"obs/mean{k}"], arrays[f"obs/var{k}"] = f32(norm._mean), f32(norm._var)
+        arrays[f"obs/std{k}"], arrays[f"obs/count{k}"] = f32(norm._std), np.int64(norm.count.item())
+        arrays[f"obs/y{k}"] = f32(norm(x))
+    rn = EmpiricalDiscountedVariationNormalization(shape=[], gamma=0.99)
+    rn.train()
+    for k in range(5):
+        r = torch.randn(300, generator=g) * 2.0 + 0.5
+        out = rn(r)
+        arrays[f"rew/r{k}"], arrays[f"rew/out{k}"] = f32(r), f32(out)
+        arrays[f"rew/std{k}"], arrays[f"rew/avg{k}"] = f32(rn.emp_norm._std), f32(rn.disc_avg.avg)
+    np.savez_compressed(os.path.join(HERE, "normalizer.npz"), **arrays)
+    return {"obs_updates": 4, "until": 2500, "reward_steps": 5, "gamma": 0.99}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reference", default=os.environ.get("RSL_RL_REFERENCE", "/root/reference"))
-    ap.add_argument("--only", choices=["rollout"], help="regenerate one fixture family, keep the rest")
+    ap.add_argument("--only", choices=["rollout", "normalizer"], help="regenerate one fixture family, keep the rest")
     args = ap.parse_args()
     torch.set_num_threads(4)
     PPO, ActorCritic, RolloutStorage = import_reference(args.reference)
-    if args.only == "rollout":
+    if args.only:
         with open(os.path.join(HERE, "golden.json")) as f:
             meta = json.load(f)
-        meta["rollout"] = make_rollout(PPO, ActorCritic, RolloutStorage)
+        if args.only == "rollout":
+            meta["rollout"] = make_rollout(PPO, ActorCritic, RolloutStorage)
+        else:
+            meta["normalizer"] = make_normalizer(args.reference)
         with open(os.path.join(HERE, "golden.json"), "w") as f:
             json.dump(meta, f, indent=1, sort_keys=True)
-        print("wrote rollout fixtures")
+        print("wrote", args.only, "fixtures")
         return
     meta = {
         "generator": "tests/golden/make_golden.py",
@@ -535,6 +568,7 @@ def main():
         "loss": make_loss(PPO, ActorCritic, RolloutStorage),
         "update_c1": make_update_c1(PPO, ActorCritic, RolloutStorage),
         "rollout": make_rollout(PPO, ActorCritic, RolloutStorage),
+        "normalizer": make_normalizer(args.reference),
     }
     with open(os.path.join(HERE, "golden.json"), "w") as f:
         json.dump(meta, f, indent=1, sort_keys=True)

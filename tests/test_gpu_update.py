@@ -99,3 +99,32 @@ def test_runner_end_to_end(cuda_device, tmp_path):
     for k, v in runner2.alg.policy.state_dict().items():
         assert torch.equal(v, sd[k]), k
     assert runner2.current_learning_iteration == runner.current_learning_iteration
+
+
+@pytest.mark.parametrize("reward_norm", [False, True])
+def test_runner_with_normalizers_and_rnd(cuda_device, reward_norm):
+    """Observation normalisers on, RND (fused into the rollout record, or -- with reward normalisation --
+    evaluated in PyTorch and added by the record kernel), state-dependent std: the whole loop runs and
+    the normalisers' running statistics are updated on the device."""
+    torch.manual_seed(1)
+    env = SyntheticVecEnv(1024, 48, 12, device=cuda_device, seed=3, timeout_prob=0.1)
+    cfg = {
+        "num_steps_per_env": 8, "save_interval": 10**9,
+        "obs_groups": {"policy": ["policy"], "critic": ["policy"], "rnd_state": ["policy"]},
+        "policy": {"class_name": "ActorCritic", "actor_hidden_dims": [256, 256], "critic_hidden_dims": [256, 256],
+                   "activation": "elu", "init_noise_std": 1.0, "actor_obs_normalization": True,
+                   "critic_obs_normalization": True},
+        "algorithm": {"class_name": "PPO", "num_learning_epochs": 2, "num_mini_batches": 2,
+                      "rnd_cfg": {"weight": 1.0, "num_outputs": 1, "predictor_hidden_dims": [-1],
+                                  "target_hidden_dims": [-1], "learning_rate": 1e-3, "state_normalization": True,
+                                  "reward_normalization": reward_norm}},
+    }
+    runner = OnPolicyRunner(env, cfg, log_dir=None, device=str(cuda_device))
+    runner.learn(2)
+    s = runner.last_iteration_stats
+    assert all(np.isfinite(v) for v in s["loss_dict"].values())
+    n = runner.alg.policy.actor_obs_normalizer
+    assert n.count.item() == 2 * 8 * 1024
+    assert torch.isfinite(n._mean).all() and (n._std > 0).all()
+    assert runner.alg.rnd.state_normalizer.count.item() == 2 * 8 * 1024
+    assert torch.isfinite(runner.alg.intrinsic_rewards).all()

@@ -133,3 +133,28 @@ def test_oracle_rollout_record(case, golden_meta):
         r = po.step_reward(z[f"step{t}/rewards"], z[f"step{t}/values"], z[f"step{t}/time_outs"], m["gamma"], intr)
         np.testing.assert_array_equal(r, z["storage/rewards"][t, :, 0])
         np.testing.assert_array_equal(z["storage/dones"][t, :, 0], z[f"step{t}/dones"])
+
+
+def test_oracle_normalizer(golden_meta):
+    """EmpiricalNormalization / EmpiricalDiscountedVariationNormalization (normalization.py:44-99) vs the
+    reference's captured sequence (fp64 moments here vs torch's fp32 reductions: rtol 1e-5)."""
+    from oracle import ppo_oracle as po
+    z = np.load(golden_path("normalizer.npz"))
+    m = golden_meta["normalizer"]
+    mean, var, count = np.zeros(7, np.float32), np.ones(7, np.float32), 0
+    for k in range(m["obs_updates"]):
+        mean, var, std, count = po.normalizer_update(z[f"obs/x{k}"], mean, var, count, until=m["until"])
+        assert count == int(z[f"obs/count{k}"])
+        np.testing.assert_allclose(mean, z[f"obs/mean{k}"][0], rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(var, z[f"obs/var{k}"][0], rtol=1e-5)
+        np.testing.assert_allclose(std, z[f"obs/std{k}"][0], rtol=1e-5)
+        np.testing.assert_allclose(po.normalizer_apply(z[f"obs/x{k}"], z[f"obs/mean{k}"][0], z[f"obs/std{k}"][0]),
+                                   z[f"obs/y{k}"], rtol=0, atol=0)  # the forward itself is bit-exact
+    mean, var, count, avg = np.zeros(1, np.float32), np.ones(1, np.float32), 0, None
+    for k in range(m["reward_steps"]):
+        r = z[f"rew/r{k}"]
+        avg = r.copy() if avg is None else (avg * np.float32(m["gamma"]) + r).astype(np.float32)
+        np.testing.assert_array_equal(avg, z[f"rew/avg{k}"])
+        mean, var, std, count = po.normalizer_update(avg[:, None], mean, var, count)
+        np.testing.assert_allclose(std, z[f"rew/std{k}"], rtol=1e-5)
+        np.testing.assert_allclose((r / z[f"rew/std{k}"]).astype(np.float32), z[f"rew/out{k}"], rtol=0, atol=0)
