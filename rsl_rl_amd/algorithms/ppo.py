@@ -50,11 +50,11 @@ def adapt_learning_rate_device(lr: torch.Tensor, kl_mean: torch.Tensor, desired_
     kl_mean the fp32 KL; the comparisons happen in fp32 against fp32(2 * kl*) / fp32(kl* / 2), exactly as
     the reference's `tensor > python_float` does."""
     kl = kl_mean.reshape(())
-    hi = torch.tensor(desired_kl * 2.0, dtype=kl.dtype, device=kl.device)
-    lo = torch.tensor(desired_kl / 2.0, dtype=kl.dtype, device=kl.device)
+    # Python-float operands: torch compares a fp32 tensor with a wrapped scalar in fp32, like the reference,
+    # and no threshold tensor has to be copied to the device (a pageable copy would synchronise)
     down = torch.clamp(lr / 1.5, min=1e-5)
     up = torch.clamp(lr * 1.5, max=1e-2)
-    return torch.where(kl > hi, down, torch.where((kl < lo) & (kl > 0.0), up, lr))
+    return torch.where(kl > desired_kl * 2.0, down, torch.where((kl < desired_kl / 2.0) & (kl > 0.0), up, lr))
 
 
 class PPO:
@@ -306,6 +306,7 @@ class PPO:
         # device-resident lr (needs an optimizer that takes a tensor lr: fused / capturable Adam)
         device_lr = adaptive and dev.type == "cuda" and self._optimizer_takes_tensor_lr()
         lr_dev = torch.tensor(self.learning_rate, dtype=torch.float64, device=dev) if device_lr else None
+        stat_idx = torch.tensor([kernels.STATS_VALUE, kernels.STATS_SURROGATE, kernels.STATS_ENTROPY], device=dev)
 
         generator = self.storage.mini_batch_generator(self.num_mini_batches, self.num_learning_epochs)
         for (
@@ -371,7 +372,7 @@ class PPO:
                 self.rnd_optimizer.step()
 
             # loss statistics stay on the device (ppo.py:387-395)
-            sums[0:3] += stats[[kernels.STATS_VALUE, kernels.STATS_SURROGATE, kernels.STATS_ENTROPY]].double()
+            sums[0:3] += stats.index_select(0, stat_idx).double()
             if self.rnd:
                 sums[3] += rnd_loss.detach().double()
 
