@@ -126,7 +126,12 @@ class ActorCritic(nn.Module):
     def act(self, obs, **kwargs):
         obs = self.actor_obs_normalizer(self.get_actor_obs(obs))
         self.update_distribution(obs)
-        return self.distribution.sample()
+        # = self.distribution.sample(): torch.normal(loc, scale) draws normal_(0, 1) and applies
+        # .mul_(scale).add_(loc) -- the same values from the same generator stream -- but first checks
+        # scale.min() >= 0 with a device-to-host read that stalls the launch queue every env step
+        loc, scale = self.distribution.loc, self.distribution.scale
+        with torch.no_grad():
+            return torch.empty_like(loc).normal_().mul_(scale).add_(loc)
 
     def act_inference(self, obs):
         obs = self.actor_obs_normalizer(self.get_actor_obs(obs))

@@ -110,3 +110,17 @@ def test_rollout_record_kernel_direct(cuda_device):
         np.testing.assert_allclose(c(lp[:, 0]), po.normal_log_prob_sum(c(actions), c(mu), c(sigma)), rtol=2e-6, atol=2e-6)
         ref_r = po.step_reward(c(rewards), c(values), c(to) if to is not None else None, 0.97, c(extra))
         np.testing.assert_array_equal(c(r[:, 0]), ref_r)
+
+
+def test_act_sampling_equals_torch_normal(cuda_device):
+    """ActorCritic.act draws normal_(0, 1) * scale + loc itself (skipping torch.normal's host-synchronising
+    std >= 0 check); the values are those of Normal(loc, scale).sample() for the same generator state."""
+    torch.manual_seed(0)
+    pol = ActorCritic({"policy": torch.zeros(8, 16)}, {"policy": ["policy"], "critic": ["policy"]}, 4,
+                      actor_hidden_dims=[32], critic_hidden_dims=[32]).to(cuda_device)
+    obs = {"policy": torch.randn(5000, 16, device=cuda_device)}
+    state = torch.cuda.get_rng_state()
+    ours = pol.act(obs)
+    torch.cuda.set_rng_state(state)
+    ref = pol.distribution.sample()
+    assert torch.equal(ours, ref)
