@@ -307,6 +307,7 @@ class PPO:
         device_lr = adaptive and dev.type == "cuda" and self._optimizer_takes_tensor_lr()
         lr_dev = torch.tensor(self.learning_rate, dtype=torch.float64, device=dev) if device_lr else None
         stat_idx = torch.tensor([kernels.STATS_VALUE, kernels.STATS_SURROGATE, kernels.STATS_ENTROPY], device=dev)
+        trainable = self._trainable_params()
 
         generator = self.storage.mini_batch_generator(self.num_mini_batches, self.num_learning_epochs)
         for (
@@ -353,8 +354,11 @@ class PPO:
                 target_embedding = self.rnd.target(rnd_state_batch).detach()
                 rnd_loss = nn.functional.mse_loss(predicted_embedding, target_embedding)
 
-            # backward through the MLPs (ppo.py:367-372) into the flat gradient buffer
-            self._bind_flat_grads()
+            # backward through the MLPs (ppo.py:367-372).  The gradients start as None (the reference's
+            # optimizer.zero_grad() default, set_to_none): autograd then adopts each freshly computed gradient
+            # as .grad instead of launching one accumulate-add per parameter
+            for p in trainable:
+                p.grad = None
             outs, grads = [mean, value_batch], [g_mean, g_value]
             if sigma.requires_grad:
                 outs.append(sigma)
@@ -425,9 +429,6 @@ class PPO:
         all_params = self.policy.parameters()
         if self.rnd:
             all_params = chain(all_params, self.rnd.parameters())
-        offset = 0
-        for p in all_params:
-            if p.grad is not None:
-                n = p.numel()
-                p.grad.data.copy_(all_grads[offset:offset + n].view_as(p.grad.data))
-                offset += n
+        # copy back (ppo.py:464-469) as one multi-tensor copy
+        dst = [p.grad.data for p in all_params if p.grad is not None]
+        torch._foreach_copy_(dst, [g.view_as(d) for g, d in zip(all_grads.split([d.numel() for d in dst]), dst)])
