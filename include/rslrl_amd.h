@@ -195,6 +195,21 @@ int rslrl_column_sum_fold(const float* partials, int64_t tiles, int32_t N, float
  * rows are split over workgroups whose partial tiles go to the workspace
  * (rslrl_linear_wgrad_workspace_bytes) and are added in a fixed order in fp64: deterministic. */
 size_t rslrl_linear_wgrad_workspace_bytes(int64_t M, int32_t N, int32_t K);
+/* out[NK] = sum over s < S of partials[s][NK] in fp64, in an order fixed by (S, NK) (NK % 4 == 0; 16-byte
+ * aligned).  Many slices over few columns fold in two stages through an fp64 workspace of
+ * rslrl_fold_partials_workspace_bytes(S, NK) bytes (0: none needed, workspace may be NULL). */
+size_t rslrl_fold_partials_workspace_bytes(int64_t S, int64_t NK);
+int rslrl_fold_partials(const float* partials, int64_t S, int64_t NK, float* out, void* workspace,
+                        size_t workspace_bytes, rslrl_stream_t stream);
+
+/* Output-layer backward in one x6 launch (Nred <= 16, % 4 == 0): rslrl_linear_dgrad_elu's outputs plus this
+ * layer's weight gradient dW[Nred, K] = dz^T h as per-128-row-tile partials
+ * [rslrl_linear_tiles(M)][Nred][K] (rslrl_linear_dgrad_wgrad_partial_bytes), folded by rslrl_fold_partials.
+ * The reference runs these as three autograd GEMM/elementwise steps over the same h (mlp.py:106-114). */
+size_t rslrl_linear_dgrad_wgrad_partial_bytes(int64_t M, int32_t Nred, int32_t K);
+int rslrl_linear_dgrad_elu_wgrad(const float* dz, int64_t M, int32_t Nred, int32_t K, const float* h, float* dz_prev,
+                                 float* colsum_partials, const void* bimage, float* wgrad_partials,
+                                 rslrl_stream_t stream);
 int rslrl_linear_wgrad(const float* dz, const float* x, int64_t M, int32_t N, int32_t K, float* dw, void* workspace,
                        size_t workspace_bytes, rslrl_stream_t stream);
 

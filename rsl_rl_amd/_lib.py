@@ -41,6 +41,10 @@ EXPORTED_SYMBOLS = (
     "rslrl_column_sum_fold",
     "rslrl_linear_wgrad_workspace_bytes",
     "rslrl_linear_wgrad",
+    "rslrl_fold_partials_workspace_bytes",
+    "rslrl_fold_partials",
+    "rslrl_linear_dgrad_wgrad_partial_bytes",
+    "rslrl_linear_dgrad_elu_wgrad",
     "rslrl_rollout_record",
     "rslrl_normalizer_workspace_bytes",
     "rslrl_normalizer_update",
@@ -192,6 +196,14 @@ def _declare(L):
     L.rslrl_linear_dgrad_elu.argtypes = [P, I64, I32, P, I32, P, P, P, P, P]
     L.rslrl_linear_wgrad_workspace_bytes.restype = SZ
     L.rslrl_linear_wgrad_workspace_bytes.argtypes = [I64, I32, I32]
+    L.rslrl_fold_partials.restype = ctypes.c_int
+    L.rslrl_fold_partials.argtypes = [P, I64, I64, P, P, SZ, P]
+    L.rslrl_fold_partials_workspace_bytes.restype = SZ
+    L.rslrl_fold_partials_workspace_bytes.argtypes = [I64, I64]
+    L.rslrl_linear_dgrad_wgrad_partial_bytes.restype = SZ
+    L.rslrl_linear_dgrad_wgrad_partial_bytes.argtypes = [I64, I32, I32]
+    L.rslrl_linear_dgrad_elu_wgrad.restype = ctypes.c_int
+    L.rslrl_linear_dgrad_elu_wgrad.argtypes = [P, I64, I32, I32, P, P, P, P, P, P]
     L.rslrl_linear_wgrad.restype = ctypes.c_int
     L.rslrl_linear_wgrad.argtypes = [P, P, I64, I32, I32, P, P, SZ, P]
     L.rslrl_normalizer_workspace_bytes.restype = SZ

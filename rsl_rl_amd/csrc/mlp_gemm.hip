@@ -37,7 +37,10 @@ constexpr int kPad = 2;
 constexpr int kLd = kKC + kPad;  // LDS row stride (floats)
 constexpr int kThreads = 512;
 
-enum Epilogue { kEpiBias = 0, kEpiBiasElu = 1, kEpiEluGrad = 2 };
+// kEpiEluGradWgrad: kEpiEluGrad for a short reduction (Nred <= 16, one chunk: the output layer) that also
+// accumulates that layer's weight gradient dZ^T H from the same H tile (x6 path only)
+enum Epilogue { kEpiBias = 0, kEpiBiasElu = 1, kEpiEluGrad = 2, kEpiEluGradWgrad = 3 };
+constexpr int kMaxWgradRows = 16;
 
 struct GemmParams {
     const float* a;    // [M, K] row-major (lda = K)
@@ -50,6 +53,7 @@ struct GemmParams {
     int K;
     int N;
     int64_t ctiles;    // dgrad: columns of colsum (= rslrl_linear_tiles(M), 128-row tiles)
+    float* wpart;      // kEpiEluGradWgrad: per-tile weight-gradient partials [tiles][K][N]
 };
 
 // global -> registers for one K chunk: A: 128 x 16 floats = 512 float4 (1 per thread); B: 256 x 16 = 1024
@@ -116,16 +120,18 @@ __device__ __forceinline__ float elu_neg(float v) {
 // col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5).  Tiles are processed in order b = J i + j;
 // for the ELU' epilogue the 16 h values of tile b + 1 are loaded before tile b is finished, so no h load
 // waits alone.  colpart[j] returns this lane's sum over its rows of column wcol0 + 32 j + (lane & 31).
-template <int EPI, int I, int J, bool FULLT>
+template <int EPI, int I, int J, bool FULLT, int NR>
 __device__ __forceinline__ void epilogue_tiles_impl(const GemmParams& p, f32x16 (&acc)[I][J], int64_t wrow0,
-                                                    int wcol0, float (&colpart)[J]) {
+                                                    int wcol0, float (&colpart)[J], const float* dzo, int dzo_row0,
+                                                    f32x2 (&wacc)[NR]) {
     constexpr bool full = FULLT;
+    constexpr bool GRAD = EPI == kEpiEluGrad || EPI == kEpiEluGradWgrad;
     const int lane = threadIdx.x & 63;
     const int h = lane >> 5;
     const int l32 = lane & 31;
 #pragma unroll
     for (int j = 0; j < J; ++j) colpart[j] = 0.f;
-    float hcur[16], hnext[16];
+    float hcur[16], hnext[16], hsave[16];
     auto load_h = [&](int b, float (&dst)[16]) {
         const int i = b / J, j = b % J;
         const int col = wcol0 + j * 32 + l32;
@@ -137,17 +143,17 @@ __device__ __forceinline__ void epilogue_tiles_impl(const GemmParams& p, f32x16 
             dst[r] = (full || (rbase + roff < p.M && col < p.N)) ? hp[static_cast<int64_t>(roff) * p.N] : 0.f;
         }
     };
-    if constexpr (EPI == kEpiEluGrad) load_h(0, hcur);
+    if constexpr (GRAD) load_h(0, hcur);
 #pragma unroll
     for (int b = 0; b < I * J; ++b) {
         const int i = b / J, j = b % J;
-        if constexpr (EPI == kEpiEluGrad) {
+        if constexpr (GRAD) {
             if (b + 1 < I * J) load_h(b + 1, hnext);
         }
         const int col = wcol0 + j * 32 + l32;
         const bool col_ok = col < p.N;
         float bias = 0.f;
-        if constexpr (EPI != kEpiEluGrad) bias = col_ok ? p.bias[col] : 0.f;
+        if constexpr (!GRAD) bias = col_ok ? p.bias[col] : 0.f;
         const int64_t rbase = wrow0 + i * 32 + 4 * h;
         float* cp = p.c + rbase * p.N + col;
 #pragma unroll
@@ -160,7 +166,7 @@ __device__ __forceinline__ void epilogue_tiles_impl(const GemmParams& p, f32x16 
                 } else if constexpr (EPI == kEpiBiasElu) {
                     v = v + bias;
                     v = v > 0.f ? v : elu_neg(v);  // torch ELU, alpha = 1
-                } else {
+                } else {  // kEpiEluGrad / kEpiEluGradWgrad
                     const float hv = hcur[r];  // ELU'(z) = 1 if z > 0 else hv + 1
                     v = hv > 0.f ? v : v * (hv + 1.f);
                     colpart[j] += v;
@@ -170,7 +176,32 @@ __device__ __forceinline__ void epilogue_tiles_impl(const GemmParams& p, f32x16 
                 __builtin_nontemporal_store(v, cp + static_cast<int64_t>(roff) * p.N);
             }
         }
-        if constexpr (EPI == kEpiEluGrad) {
+        if constexpr (EPI == kEpiEluGradWgrad) {
+            // dW[o][col] += dZ[row][o] * H[row][col] over this lane's 16 rows (H = 0 outside the matrix); the two
+            // column tiles of row tile i share each dZ read and one packed FMA (v_pk_fma_f32)
+            static_assert(J == 2, "the fused weight gradient pairs the wave's two column tiles");
+            if (j == 0) {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) hsave[r] = hcur[r];
+            } else {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int roff = (r & 3) + 8 * (r >> 2);
+                    const float4* d =
+                        reinterpret_cast<const float4*>(dzo + (dzo_row0 + i * 32 + 4 * h + roff) * kMaxWgradRows);
+                    const f32x2 hh = {hsave[r], hcur[r]};
+#pragma unroll
+                    for (int o4 = 0; o4 < NR / 4; ++o4) {
+                        const float4 dv = d[o4];
+                        wacc[4 * o4 + 0] = __builtin_elementwise_fma(f32x2{dv.x, dv.x}, hh, wacc[4 * o4 + 0]);
+                        wacc[4 * o4 + 1] = __builtin_elementwise_fma(f32x2{dv.y, dv.y}, hh, wacc[4 * o4 + 1]);
+                        wacc[4 * o4 + 2] = __builtin_elementwise_fma(f32x2{dv.z, dv.z}, hh, wacc[4 * o4 + 2]);
+                        wacc[4 * o4 + 3] = __builtin_elementwise_fma(f32x2{dv.w, dv.w}, hh, wacc[4 * o4 + 3]);
+                    }
+                }
+            }
+        }
+        if constexpr (GRAD) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) hcur[r] = hnext[r];
         }
@@ -182,11 +213,25 @@ __device__ __forceinline__ void epilogue_tiles_impl(const GemmParams& p, f32x16 
 // vmcnt(0) before each store (64 serialised stores per wave: the epilogue ran 3x longer).
 template <int EPI, int I, int J>
 __device__ __forceinline__ void epilogue_tiles(const GemmParams& p, f32x16 (&acc)[I][J], int64_t wrow0, int wcol0,
-                                               bool full, float (&colpart)[J]) {
+                                               bool full, float (&colpart)[J], const float* dzo = nullptr,
+                                               int dzo_row0 = 0) {
+    f32x2 wacc[1];  // unused (no weight-gradient accumulation)
     if (full)
-        epilogue_tiles_impl<EPI, I, J, true>(p, acc, wrow0, wcol0, colpart);
+        epilogue_tiles_impl<EPI, I, J, true, 1>(p, acc, wrow0, wcol0, colpart, dzo, dzo_row0, wacc);
     else
-        epilogue_tiles_impl<EPI, I, J, false>(p, acc, wrow0, wcol0, colpart);
+        epilogue_tiles_impl<EPI, I, J, false, 1>(p, acc, wrow0, wcol0, colpart, dzo, dzo_row0, wacc);
+}
+
+template <int EPI, int I, int J, int NR>
+__device__ __forceinline__ void epilogue_tiles_w(const GemmParams& p, f32x16 (&acc)[I][J], int64_t wrow0, int wcol0,
+                                                 bool full, float (&colpart)[J], const float* dzo, int dzo_row0,
+                                                 f32x2 (&wacc)[NR]) {
+#pragma unroll
+    for (int o = 0; o < NR; ++o) wacc[o] = f32x2{0.f, 0.f};
+    if (full)
+        epilogue_tiles_impl<EPI, I, J, true, NR>(p, acc, wrow0, wcol0, colpart, dzo, dzo_row0, wacc);
+    else
+        epilogue_tiles_impl<EPI, I, J, false, NR>(p, acc, wrow0, wcol0, colpart, dzo, dzo_row0, wacc);
 }
 
 // f32 kernel epilogue: 128-row tile, waves 2 (m) x 4 (n) of 64 x 64; column sums over the tile's 128 rows
@@ -392,11 +437,12 @@ __device__ __forceinline__ bf16x8 read_frag(const char* __restrict__ plane, int 
     return __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(plane + swz(row, h)));
 }
 
-// BM = 128: waves 2 (M) x 4 (N) of 64 x 64 (2 x 2 MFMA tiles), two workgroups per CU.
-// BM = 256: waves 2 x 4 of 128 x 64 (4 x 2 MFMA tiles), one workgroup per CU.
-template <int EPI, bool FULL, int BM, int MINW = (BM == 128 ? 4 : 2)>
-__global__ __launch_bounds__(kThreads, MINW) void mlp_gemm_x6_kernel(GemmParams p,
-                                                                                 const uint4* __restrict__ bimg) {
+// 128 rows x 256 columns per workgroup: waves 2 (M) x 4 (N) of 64 x 64 (2 x 2 MFMA tiles); MINW = 4:
+// two workgroups per CU (<= 128 VGPRs), 2: one (the register-hungrier short-K dgrad epilogues).
+// NR: rows of the fused weight gradient (kEpiEluGradWgrad: Nred rounded up to 4; otherwise unused).
+template <int EPI, bool FULL, int MINW, int NR = 4>
+__global__ __launch_bounds__(kThreads, MINW) void mlp_gemm_x6_kernel(GemmParams p, const uint4* __restrict__ bimg) {
+    constexpr int BM = kBM;
     constexpr int I = BM / 64;
     constexpr int planeA = BM * kX6RowB;
     constexpr int bufBytes = 3 * planeA + kX6ChunkB;
@@ -458,7 +504,55 @@ __global__ __launch_bounds__(kThreads, MINW) void mlp_gemm_x6_kernel(GemmParams 
     uint64_t st1 = __builtin_amdgcn_s_memrealtime();
     uint64_t ct1 = __builtin_amdgcn_s_memtime();
 #endif
-    epilogue_tiles<EPI, I, 2>(p, acc, row0 + wm * (BM / 2), wn * 64, full, colpart);
+    if constexpr (EPI == kEpiEluGradWgrad) {
+        // one chunk (K <= 16): buffer 0 holds the tile's dZ planes; rebuild the fp32 rows (p0 + p1 + p2 is
+        // exact) into buffer 1 as [128][16] for the weight-gradient accumulation
+        float* dzo = reinterpret_cast<float*>(lds[1]);
+        {
+            const int r = threadIdx.x >> 2, q = threadIdx.x & 3;
+            const int off = swz(r, q >> 1) + 8 * (q & 1);
+            const uint2 p0 = *reinterpret_cast<const uint2*>(lds[0] + off);
+            const uint2 p1 = *reinterpret_cast<const uint2*>(lds[0] + planeA + off);
+            const uint2 p2 = *reinterpret_cast<const uint2*>(lds[0] + 2 * planeA + off);
+            auto lo = [](uint32_t w) { return __uint_as_float(w << 16); };
+            auto hi = [](uint32_t w) { return __uint_as_float(w & 0xffff0000u); };
+            float4 v;
+            v.x = (lo(p0.x) + lo(p1.x)) + lo(p2.x);
+            v.y = (hi(p0.x) + hi(p1.x)) + hi(p2.x);
+            v.z = (lo(p0.y) + lo(p1.y)) + lo(p2.y);
+            v.w = (hi(p0.y) + hi(p1.y)) + hi(p2.y);
+            *reinterpret_cast<float4*>(dzo + r * kMaxWgradRows + 4 * q) = v;
+        }
+        __syncthreads();
+        f32x2 wacc[NR];
+        epilogue_tiles_w<EPI, I, 2, NR>(p, acc, row0 + wm * (BM / 2), wn * 64, full, colpart, dzo, wm * (BM / 2), wacc);
+        // per-tile partial dW[o][col]: lane halves (rows 4h..) by shuffle, then the two wave rows in a fixed
+        // order through LDS (the B region of buffer 0 is free after the main loop)
+        float* red = reinterpret_cast<float*>(lds[0] + 3 * planeA);  // [16][256]
+#pragma unroll
+        for (int o = 0; o < NR; ++o)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) wacc[o][j] += __shfl_xor(wacc[o][j], 32, 64);
+        if (wm == 0 && h == 0) {
+#pragma unroll
+            for (int o = 0; o < NR; ++o)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) red[o * kBN + wn * 64 + j * 32 + l32] = wacc[o][j];
+        }
+        __syncthreads();
+        if (wm == 1 && h == 0) {
+            float* out = p.wpart + static_cast<int64_t>(blockIdx.x) * p.K * p.N;
+#pragma unroll
+            for (int o = 0; o < NR; ++o)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    const int col = wn * 64 + j * 32 + l32;
+                    if (o < p.K && col < p.N) out[o * p.N + col] = red[o * kBN + col] + wacc[o][j];
+                }
+        }
+    } else {
+        epilogue_tiles<EPI, I, 2>(p, acc, row0 + wm * (BM / 2), wn * 64, full, colpart);
+    }
 #ifdef RSLRL_STAMPS
     {
         uint64_t st2 = __builtin_amdgcn_s_memrealtime();
@@ -473,189 +567,21 @@ __global__ __launch_bounds__(kThreads, MINW) void mlp_gemm_x6_kernel(GemmParams 
         }
     }
 #endif
-    if constexpr (EPI == kEpiEluGrad) {
-        // column sums over the tile's rows -> colsum[col][128-row tile].  BM = 256: each wave row (wm) is
-        // one 128-row tile; BM = 128: the two wave rows are combined (fixed order) through LDS.
+    if constexpr (EPI == kEpiEluGrad || EPI == kEpiEluGradWgrad) {
+        // column sums over the tile's 128 rows -> colsum[col][tile]: lanes l and l + 32 hold the two row
+        // halves of a column, the two wave rows (wm) are combined in a fixed order through LDS
         const int64_t tiles = p.ctiles;
         float s[2];
 #pragma unroll
         for (int j = 0; j < 2; ++j) s[j] = colpart[j] + __shfl_xor(colpart[j], 32, 64);
-        if constexpr (BM == 256) {
-            const int64_t t = 2 * static_cast<int64_t>(blockIdx.x) + wm;
+        float* colred = reinterpret_cast<float*>(lds[0]);
+        __syncthreads();  // the LDS tiles are no longer read
 #pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const int col = wn * 64 + j * 32 + l32;
-                if (h == 0 && col < p.N && t < tiles) p.colsum[static_cast<int64_t>(col) * tiles + t] = s[j];
-            }
-        } else {
-            float* colred = reinterpret_cast<float*>(lds[0]);
-            __syncthreads();  // the LDS tiles are no longer read
-#pragma unroll
-            for (int j = 0; j < 2; ++j)
-                if (h == 0) colred[wm * kBN + wn * 64 + j * 32 + l32] = s[j];
-            __syncthreads();
-            for (int col = threadIdx.x; col < p.N && col < kBN; col += kThreads)
-                p.colsum[static_cast<int64_t>(col) * tiles + blockIdx.x] = colred[col] + colred[kBN + col];
-        }
-    }
-}
-
-// ---- x6 with register-resident A ("x6r").  Each wave owns 32 rows x all 256 columns (8 MFMA tiles):
-// it loads its A fragments straight from HBM into registers (lane (r, h) reads row r, k 8h..8h+7 of the
-// chunk: two 16-B loads), splits them in registers and feeds the MFMAs -- A never touches LDS and needs
-// no barrier.  Only B (the weight image, shared by the 8 waves) goes through LDS, in a ring of kRB
-// chunk slots filled by global_load_lds.  Both streams run kD = kRB - 1 chunks ahead: the A loads are
-// issued as inline asm so the compiler does not drain them at every barrier (it waits vmcnt(0) for
-// ordinary loads whenever an LDS-DMA is in flight); the kernel counts vmcnt itself.  Per chunk and wave
-// the issue order is fixed: 3 global_load_lds (B) then 2 global_load_dwordx4 (A), so "chunk c has
-// landed" is vmcnt(5 * (kD - 1)) once the loads of chunks up to c + kD - 1 are issued.
-constexpr int kD = 2;
-constexpr int kRB = kD + 1;
-constexpr int kBMR = 256;
-
-using f32x4 = __attribute__((ext_vector_type(4))) float;
-
-struct AFrag {
-    f32x4 lo, hi;  // k 8h .. 8h+3, 8h+4 .. 8h+7 of row r
-};
-
-__device__ __forceinline__ f32x4 gload16(const float* ptr) {
-    f32x4 v;
-    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(ptr) : "memory");
-    return v;
-}
-
-// keeps v live and orders its uses after the preceding s_waitcnt
-__device__ __forceinline__ void pin(AFrag& a) { asm volatile("" : "+v"(a.lo), "+v"(a.hi)); }
-
-template <bool FULL>
-__device__ __forceinline__ AFrag load_afrag(const GemmParams& p, int64_t row, int k) {
-    if constexpr (FULL) {
-        const float* ptr = p.a + row * p.K + k;
-        return AFrag{gload16(ptr), gload16(ptr + 4)};
-    } else {  // out-of-range rows / k read a valid address (row 0 of the matrix) and are zeroed after the wait
-        const bool ok_lo = row < p.M && k < p.K;
-        const bool ok_hi = row < p.M && k + 4 < p.K;
-        return AFrag{gload16(p.a + (ok_lo ? row * p.K + k : 0)), gload16(p.a + (ok_hi ? row * p.K + k + 4 : 0))};
-    }
-}
-
-__device__ __forceinline__ void split_afrag(const AFrag& a, bf16x8 (&out)[3]) {
-    uint2 l[3], u[3];
-    split4(make_float4(a.lo[0], a.lo[1], a.lo[2], a.lo[3]), l[0], l[1], l[2]);
-    split4(make_float4(a.hi[0], a.hi[1], a.hi[2], a.hi[3]), u[0], u[1], u[2]);
-#pragma unroll
-    for (int q = 0; q < 3; ++q) out[q] = __builtin_bit_cast(bf16x8, make_uint4(l[q].x, l[q].y, u[q].x, u[q].y));
-}
-
-template <int EPI, bool FULL>
-__global__ __launch_bounds__(kThreads, 2) void mlp_gemm_x6r_kernel(GemmParams p, const uint4* __restrict__ bimg) {
-    __shared__ __attribute__((aligned(16))) char ring[kRB][kX6ChunkB];
-    const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
-    const int h = lane >> 5;
-    const int l32 = lane & 31;
-    const int64_t row0 = static_cast<int64_t>(blockIdx.x) * kBMR;
-    const int64_t wrow0 = row0 + 32 * wave;
-#ifdef RSLRL_STAMPS
-    uint64_t st0 = __builtin_amdgcn_s_memrealtime();
-    uint64_t ct0 = __builtin_amdgcn_s_memtime();
-#endif
-    const int64_t arow = wrow0 + l32;
-    const int nchunks = (p.K + kKC - 1) / kKC;
-
-    f32x16 acc[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[j] = f32x16{};
-
-    AFrag ar[kRB];
-    auto issue = [&](int c, AFrag& dst) {  // chunk min(c, n-1): B -> ring slot c % kRB, A -> dst
-        const int cc = min(c, nchunks - 1);
-        load_b_lds(bimg, cc, ring[c % kRB]);
-        dst = load_afrag<FULL>(p, arow, cc * kKC + 8 * h);
-    };
-    // prologue: chunks 0 .. kD-1 in flight
-#pragma unroll
-    for (int d = 0; d < kD; ++d) issue(d, ar[d]);
-    // steady state, unrolled by kRB so every ring index is static: at chunk c issue c + kD (into the slot
-    // chunk c - 1 used; every wave passed the barrier at the top of compute(c) after reading it), then
-    // compute c
-    for (int c0 = 0; c0 < nchunks; c0 += kRB) {
-#pragma unroll
-        for (int u = 0; u < kRB; ++u) {
-            const int c = c0 + u;
-            if (c < nchunks) {
-                // chunk c's loads are older than the 5 * (kD - 1) issued after them; the barrier also
-                // tells every wave that slot (c - 1) % kRB has been read by all
-                asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(5 * (kD - 1)) : "memory");
-                AFrag& a = ar[u];
-                pin(a);
-                issue(c + kD, ar[(u + kD) % kRB]);
-                if constexpr (!FULL) {
-                    const int k = c * kKC + 8 * h;
-                    if (!(arow < p.M && k < p.K)) a.lo = f32x4{0.f, 0.f, 0.f, 0.f};
-                    if (!(arow < p.M && k + 4 < p.K)) a.hi = f32x4{0.f, 0.f, 0.f, 0.f};
-                }
-                bf16x8 af[3];
-                split_afrag(a, af);
-                const char* b = ring[c % kRB];
-#pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    bf16x8 bf[3];
-#pragma unroll
-                    for (int q = 0; q < 3; ++q) bf[q] = read_frag(b + q * kX6PlaneB, j * 32 + l32, h);
-                    acc[j] = mfma_x6(af, bf, acc[j]);
-                }
-            }
-        }
-    }
-    // drain: the surplus (clamped) loads must land before their registers are reused
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-    for (int u = 0; u < kRB; ++u) pin(ar[u]);
-
-    // epilogue: the wave's 32 rows x 256 columns as a 1 x 8 tile grid
-    const bool full = (row0 + kBMR <= p.M) && (p.N == kBN);
-    f32x16 acc2[1][8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc2[0][j] = acc[j];
-    float colpart[8];
-#ifdef RSLRL_STAMPS
-    uint64_t st1 = __builtin_amdgcn_s_memrealtime();
-    uint64_t ct1 = __builtin_amdgcn_s_memtime();
-#endif
-    epilogue_tiles<EPI, 1, 8>(p, acc2, wrow0, 0, full, colpart);
-#ifdef RSLRL_STAMPS
-    {
-        uint64_t st2 = __builtin_amdgcn_s_memrealtime();
-        uint32_t hw, xcc;
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-        if (threadIdx.x == 0 || threadIdx.x == 448) {
-            uint64_t* o = g_stamps + (static_cast<int64_t>(blockIdx.x) * 2 + (threadIdx.x ? 1 : 0)) * 6;
-            o[0] = st0; o[1] = st1; o[2] = st2; o[3] = (static_cast<uint64_t>(xcc) << 32) | hw;
-            o[4] = ct0; o[5] = ct1;
-        }
-    }
-#endif
-    if constexpr (EPI == kEpiEluGrad) {
-        // per-column sums of each 128-row tile = waves 4t .. 4t+3, combined in wave order through LDS
-        float* red = reinterpret_cast<float*>(ring[0]);  // 8 waves x 256 floats
+        for (int j = 0; j < 2; ++j)
+            if (h == 0) colred[wm * kBN + wn * 64 + j * 32 + l32] = s[j];
         __syncthreads();
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const float s2 = colpart[j] + __shfl_xor(colpart[j], 32, 64);
-            if (h == 0) red[wave * kBN + j * 32 + l32] = s2;
-        }
-        __syncthreads();
-        for (int e = threadIdx.x; e < 2 * kBN; e += kThreads) {
-            const int half = e / kBN, col = e % kBN;
-            const int64_t t = 2 * static_cast<int64_t>(blockIdx.x) + half;
-            if (col < p.N && t < p.ctiles) {
-                const float* r = red + 4 * half * kBN + col;
-                p.colsum[static_cast<int64_t>(col) * p.ctiles + t] = ((r[0] + r[kBN]) + r[2 * kBN]) + r[3 * kBN];
-            }
-        }
+        for (int col = threadIdx.x; col < p.N && col < kBN; col += kThreads)
+            p.colsum[static_cast<int64_t>(col) * tiles + blockIdx.x] = colred[col] + colred[kBN + col];
     }
 }
 
@@ -681,15 +607,6 @@ int dgrad_occupancy() {  // tuning knob: RSLRL_DGRAD_OCC=2|4 (default 4)
     return v;
 }
 
-int x6_tile() {  // tuning knob: RSLRL_X6_TILE=128|256|reg (default 128)
-    static const int v = [] {
-        const char* e = std::getenv("RSLRL_X6_TILE");
-        if (e && std::string(e) == "reg") return 1;
-        return (e && std::atoi(e) == 256) ? 256 : 128;
-    }();
-    return v;
-}
-
 // bimage == nullptr: exact f32 MFMA main loop on p.bw; otherwise the split-bf16 main loop on the image.
 template <int EPI>
 int launch(const GemmParams& p, const void* bimage, hipStream_t st) {
@@ -698,31 +615,31 @@ int launch(const GemmParams& p, const void* bimage, hipStream_t st) {
     const dim3 g(static_cast<unsigned>(tiles)), b(kThreads);
     if (bimage) {
         const uint4* img = static_cast<const uint4*>(bimage);
-        if (x6_tile() == 1) {
-            const dim3 gr(static_cast<unsigned>(ceil_div(p.M, kBMR)));
-            if (p.M % kBMR == 0 && p.K % kKC == 0)
-                hipLaunchKernelGGL((mlp_gemm_x6r_kernel<EPI, true>), gr, b, 0, st, p, img);
-            else
-                hipLaunchKernelGGL((mlp_gemm_x6r_kernel<EPI, false>), gr, b, 0, st, p, img);
-        } else if (x6_tile() == 256) {
-            const dim3 g6(static_cast<unsigned>(ceil_div(p.M, 256)));
-            if (p.M % 256 == 0 && p.K % kKC == 0)
-                hipLaunchKernelGGL((mlp_gemm_x6_kernel<EPI, true, 256>), g6, b, 0, st, p, img);
-            else
-                hipLaunchKernelGGL((mlp_gemm_x6_kernel<EPI, false, 256>), g6, b, 0, st, p, img);
-        } else {
-            // a short reduction (the dgrad of the 12- / 1-wide output layer: one chunk) is bound by the
-            // epilogue's h loads, which want the registers of the 2-waves-per-SIMD allocation
-            const bool short_k = EPI == kEpiEluGrad && p.K <= 2 * kKC;
-            const bool fullm = p.M % 128 == 0 && p.K % kKC == 0;
-            if (short_k) {
-                if (fullm) hipLaunchKernelGGL((mlp_gemm_x6_kernel<EPI, true, 128, 2>), g, b, 0, st, p, img);
-                else hipLaunchKernelGGL((mlp_gemm_x6_kernel<EPI, false, 128, 2>), g, b, 0, st, p, img);
-            } else {
-                if (fullm) hipLaunchKernelGGL((mlp_gemm_x6_kernel<EPI, true, 128>), g, b, 0, st, p, img);
-                else hipLaunchKernelGGL((mlp_gemm_x6_kernel<EPI, false, 128>), g, b, 0, st, p, img);
+        // a short reduction (the dgrad of the 12- / 1-wide output layer: one chunk) is bound by the
+        // epilogue's h loads, which want the registers of the 2-waves-per-SIMD allocation
+        const bool short_k = EPI != kEpiBias && EPI != kEpiBiasElu && p.K <= 2 * kKC;
+        const bool fullm = p.M % kBM == 0 && p.K % kKC == 0;
+        if constexpr (EPI == kEpiEluGradWgrad) {  // K = Nred in {4, 8, 12, 16}
+            auto go = [&](auto nr) {
+                constexpr int NR = decltype(nr)::value;
+                if (fullm) hipLaunchKernelGGL((mlp_gemm_x6_kernel<EPI, true, 2, NR>), g, b, 0, st, p, img);
+                else hipLaunchKernelGGL((mlp_gemm_x6_kernel<EPI, false, 2, NR>), g, b, 0, st, p, img);
+            };
+            switch (p.K) {
+                case 4: go(std::integral_constant<int, 4>{}); break;
+                case 8: go(std::integral_constant<int, 8>{}); break;
+                case 12: go(std::integral_constant<int, 12>{}); break;
+                default: go(std::integral_constant<int, 16>{}); break;
             }
+        } else if (short_k) {
+            if (fullm) hipLaunchKernelGGL((mlp_gemm_x6_kernel<EPI, true, 2>), g, b, 0, st, p, img);
+            else hipLaunchKernelGGL((mlp_gemm_x6_kernel<EPI, false, 2>), g, b, 0, st, p, img);
+        } else {
+            if (fullm) hipLaunchKernelGGL((mlp_gemm_x6_kernel<EPI, true, 4>), g, b, 0, st, p, img);
+            else hipLaunchKernelGGL((mlp_gemm_x6_kernel<EPI, false, 4>), g, b, 0, st, p, img);
         }
+    } else if constexpr (EPI == kEpiEluGradWgrad) {
+        return RSLRL_E_UNSUPPORTED;  // x6 path only
     } else if (EPI == kEpiEluGrad && dgrad_occupancy() == 2) {
         hipLaunchKernelGGL((mlp_gemm_kernel<EPI, 2>), g, b, 0, st, p);
     } else {
@@ -773,7 +690,7 @@ extern "C" int rslrl_linear_fwd(const float* x, int64_t M, int32_t K, const floa
     if (!x || (!weight && !bimage) || !bias || !y) return RSLRL_E_INVALID_ARGUMENT;
     if (!aligned16(x) || (!bimage && !aligned16(weight)) || (bimage && !aligned16(bimage))) return RSLRL_E_MISALIGNED;
     if (activation != 0 && activation != 1) return RSLRL_E_UNSUPPORTED;
-    GemmParams p{x, weight, bias, nullptr, y, nullptr, M, K, N, 0};
+    GemmParams p{x, weight, bias, nullptr, y, nullptr, M, K, N, 0, nullptr};
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     return activation ? launch<kEpiBiasElu>(p, bimage, st) : launch<kEpiBias>(p, bimage, st);
 }
@@ -786,8 +703,24 @@ extern "C" int rslrl_linear_dgrad_elu(const float* dz, int64_t M, int32_t Nred, 
     if (!dz || (!weight_t && !bimage) || !h || !dz_prev || !colsum_partials) return RSLRL_E_INVALID_ARGUMENT;
     if (!aligned16(dz) || (!bimage && !aligned16(weight_t)) || (bimage && !aligned16(bimage))) return RSLRL_E_MISALIGNED;
     // GEMM view: A = dZ [M, Nred], Bw = W^T [K, Nred] -> C = dZ W [M, K]
-    GemmParams p{dz, weight_t, nullptr, h, dz_prev, colsum_partials, M, Nred, K, ceil_div(M, kBM)};
+    GemmParams p{dz, weight_t, nullptr, h, dz_prev, colsum_partials, M, Nred, K, ceil_div(M, kBM), nullptr};
     return launch<kEpiEluGrad>(p, bimage, reinterpret_cast<hipStream_t>(stream));
+}
+
+extern "C" size_t rslrl_linear_dgrad_wgrad_partial_bytes(int64_t M, int32_t Nred, int32_t K) {
+    if (M < 1 || Nred < 1 || K < 1) return 0;
+    return static_cast<size_t>(ceil_div(M, kBM)) * Nred * K * sizeof(float);
+}
+
+extern "C" int rslrl_linear_dgrad_elu_wgrad(const float* dz, int64_t M, int32_t Nred, int32_t K, const float* h,
+                                            float* dz_prev, float* colsum_partials, const void* bimage,
+                                            float* wgrad_partials, rslrl_stream_t stream) {
+    if (M < 0 || Nred < 1 || Nred > kMaxWgradRows || K < 1 || K > kBN || (Nred & 3)) return RSLRL_E_INVALID_ARGUMENT;
+    if (M == 0) return RSLRL_OK;
+    if (!dz || !h || !dz_prev || !colsum_partials || !bimage || !wgrad_partials) return RSLRL_E_INVALID_ARGUMENT;
+    if (!aligned16(dz) || !aligned16(bimage)) return RSLRL_E_MISALIGNED;
+    GemmParams p{dz, nullptr, nullptr, h, dz_prev, colsum_partials, M, Nred, K, ceil_div(M, kBM), wgrad_partials};
+    return launch<kEpiEluGradWgrad>(p, bimage, reinterpret_cast<hipStream_t>(stream));
 }
 
 extern "C" int rslrl_column_sum_fold(const float* partials, int64_t tiles, int32_t N, float* out,

@@ -4,7 +4,7 @@
 // it as one cuBLAS GEMM per layer).  M is the mini-batch (393216 rows at C3); N, K <= 256.
 //
 // Split-K over M: workgroup s reduces rows [s * rows_per, (s + 1) * rows_per) into a full TN x 256 tile
-// of partial sums ([S][N][K] fp32), wgrad_fold_kernel adds the S partials in a fixed order in fp64 ->
+// of partial sums ([S][N][K] fp32), fold_kernel adds the S partials in a fixed order in fp64 ->
 // deterministic.  Both operands are consumed along their row index m, which is the MFMA reduction
 // index, so each is staged in its natural [m][col] layout (coalesced float4 loads, split into three bf16
 // planes while staged) and read back column-wise with ds_read_b64_tr_b16 (MI355X_MICROARCH.md §LDS;
@@ -193,34 +193,62 @@ __global__ __launch_bounds__(kThreadsW, 2) void wgrad_x6_kernel(WgradParams p) {
 // dW[e] = sum over s of part[s][e] (e < N * K), fp64, fixed order: thread (g, c) of a 256-thread block
 // sums slices s = g (mod 4) of the float4 column group c (unrolled so several loads are in flight), then
 // the four group sums are added in g order through LDS.  One block per 256 outputs.
-__global__ __launch_bounds__(kBlock) void wgrad_fold_kernel(const float* __restrict__ part, int S, int NK,
-                                                            float* __restrict__ out) {
+// out[e] = sum of part[s][e] over the slices s of group blockIdx.y (per slices each) in a fixed order: four
+// interleaved fp64 accumulator groups (s % 4), combined ((g0 + g1) + g2) + g3.  IN is float (partials) or
+// double (stage-1 group sums); OUT is double (stage 1 of a two-stage fold) or float (final).
+template <typename IN, typename OUT>
+__global__ __launch_bounds__(kBlock) void fold_kernel(const IN* __restrict__ part, int S, int per, int NK,
+                                                      OUT* __restrict__ out) {
     __shared__ double red[4][64][4];
     const int g = threadIdx.x >> 6;
     const int c = threadIdx.x & 63;
     const int e0 = blockIdx.x * 256 + 4 * c;  // NK % 4 == 0 (K % 4 == 0)
+    const int s0 = blockIdx.y * per;
+    const int s1 = min(S, s0 + per);
     double a[4] = {0.0, 0.0, 0.0, 0.0};
     if (e0 < NK) {
-        const float4* src = reinterpret_cast<const float4*>(part + e0);
-        const int64_t stride = NK / 4;
-        int s = g;
+        const IN* src = part + e0;
 #pragma unroll 8
-        for (; s < S; s += 4) {
-            const float4 v = src[static_cast<int64_t>(s) * stride];
-            a[0] += v.x; a[1] += v.y; a[2] += v.z; a[3] += v.w;
+        for (int s = s0 + g; s < s1; s += 4) {
+            const IN* q = src + static_cast<int64_t>(s) * NK;
+            if constexpr (sizeof(IN) == 4) {
+                const float4 v = *reinterpret_cast<const float4*>(q);
+                a[0] += v.x; a[1] += v.y; a[2] += v.z; a[3] += v.w;
+            } else {
+                const double2 v0 = reinterpret_cast<const double2*>(q)[0];
+                const double2 v1 = reinterpret_cast<const double2*>(q)[1];
+                a[0] += v0.x; a[1] += v0.y; a[2] += v1.x; a[3] += v1.y;
+            }
         }
     }
 #pragma unroll
     for (int k = 0; k < 4; ++k) red[g][c][k] = a[k];
     __syncthreads();
     if (g == 0 && e0 < NK) {
-        float4 r;
-        r.x = static_cast<float>(((red[0][c][0] + red[1][c][0]) + red[2][c][0]) + red[3][c][0]);
-        r.y = static_cast<float>(((red[0][c][1] + red[1][c][1]) + red[2][c][1]) + red[3][c][1]);
-        r.z = static_cast<float>(((red[0][c][2] + red[1][c][2]) + red[2][c][2]) + red[3][c][2]);
-        r.w = static_cast<float>(((red[0][c][3] + red[1][c][3]) + red[2][c][3]) + red[3][c][3]);
-        *reinterpret_cast<float4*>(out + e0) = r;
+        double r[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) r[k] = ((red[0][c][k] + red[1][c][k]) + red[2][c][k]) + red[3][c][k];
+        OUT* dst = out + static_cast<int64_t>(blockIdx.y) * NK + e0;
+        if constexpr (sizeof(OUT) == 4) {
+            *reinterpret_cast<float4*>(dst) =
+                make_float4(static_cast<float>(r[0]), static_cast<float>(r[1]), static_cast<float>(r[2]),
+                            static_cast<float>(r[3]));
+        } else {
+            reinterpret_cast<double2*>(dst)[0] = make_double2(r[0], r[1]);
+            reinterpret_cast<double2*>(dst)[1] = make_double2(r[2], r[3]);
+        }
     }
+}
+
+// Two-stage fold when one pass would leave the chip idle (few columns, many slices -- e.g. the output
+// layer's per-tile partials: 3072 slices x 3072 columns): stage 1 sums groups of kFoldPer slices into fp64
+// [G][NK], stage 2 sums the G groups.  The order is fixed by (S, NK) alone: deterministic.
+constexpr int kFoldPer = 64;
+
+int64_t fold_groups(int64_t S, int64_t NK) {
+    const int64_t cols = ceil_div(NK, 256);
+    if (S <= kFoldPer || cols >= 256) return 1;
+    return ceil_div(S, kFoldPer);
 }
 
 int64_t wgrad_slices(int64_t M) {  // one workgroup per CU (98 KiB of LDS each), at least 4 chunks each
@@ -239,6 +267,37 @@ extern "C" size_t rslrl_linear_wgrad_workspace_bytes(int64_t M, int32_t N, int32
     if (M < 1 || N < 1 || K < 1) return 0;
     const int64_t S = ceil_div(M, wgrad_rows_per(M));
     return static_cast<size_t>(S) * N * K * sizeof(float);
+}
+
+extern "C" size_t rslrl_fold_partials_workspace_bytes(int64_t S, int64_t NK) {
+    if (S < 1 || NK < 1) return 0;
+    const int64_t G = fold_groups(S, NK);
+    return G > 1 ? static_cast<size_t>(G) * NK * sizeof(double) : 0;
+}
+
+extern "C" int rslrl_fold_partials(const float* partials, int64_t S, int64_t NK, float* out, void* workspace,
+                                   size_t workspace_bytes, rslrl_stream_t stream) {
+    if (!partials || !out || S < 1 || S > INT32_MAX || NK < 4 || NK > INT32_MAX || (NK & 3)) return RSLRL_E_INVALID_ARGUMENT;
+    if ((reinterpret_cast<uintptr_t>(partials) | reinterpret_cast<uintptr_t>(out)) & 15) return RSLRL_E_MISALIGNED;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const unsigned cols = static_cast<unsigned>(ceil_div(NK, 256));
+    const int64_t G = fold_groups(S, NK);
+    if (G == 1) {
+        hipLaunchKernelGGL((fold_kernel<float, float>), dim3(cols), dim3(kBlock), 0, st, partials,
+                           static_cast<int>(S), static_cast<int>(S), static_cast<int>(NK), out);
+        return launch_status();
+    }
+    if (!workspace) return RSLRL_E_INVALID_ARGUMENT;
+    if (reinterpret_cast<uintptr_t>(workspace) & 15) return RSLRL_E_MISALIGNED;
+    if (workspace_bytes < static_cast<size_t>(G) * NK * sizeof(double)) return RSLRL_E_WORKSPACE_TOO_SMALL;
+    double* ws = static_cast<double*>(workspace);
+    hipLaunchKernelGGL((fold_kernel<float, double>), dim3(cols, static_cast<unsigned>(G)), dim3(kBlock), 0, st,
+                       partials, static_cast<int>(S), kFoldPer, static_cast<int>(NK), ws);
+    int rc = launch_status();
+    if (rc) return rc;
+    hipLaunchKernelGGL((fold_kernel<double, float>), dim3(cols), dim3(kBlock), 0, st, static_cast<const double*>(ws),
+                       static_cast<int>(G), static_cast<int>(G), static_cast<int>(NK), out);
+    return launch_status();
 }
 
 extern "C" int rslrl_linear_wgrad(const float* dz, const float* x, int64_t M, int32_t N, int32_t K, float* dw,
@@ -265,7 +324,7 @@ extern "C" int rslrl_linear_wgrad(const float* dz, const float* x, int64_t M, in
     int rc = launch_status();
     if (rc) return rc;
     const int NK = N * K;
-    hipLaunchKernelGGL(wgrad_fold_kernel, dim3(static_cast<unsigned>(ceil_div(NK, 256))), dim3(kBlock), 0, st,
-                       static_cast<const float*>(workspace), static_cast<int>(S), NK, dw);
+    hipLaunchKernelGGL((fold_kernel<float, float>), dim3(static_cast<unsigned>(ceil_div(NK, 256))), dim3(kBlock), 0,
+                       st, static_cast<const float*>(workspace), static_cast<int>(S), static_cast<int>(S), NK, dw);
     return launch_status();
 }

@@ -36,6 +36,7 @@ def _stream(t):
     return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
 
 
+_FUSE_OUT = os.environ.get("RSLRL_FUSE_OUT", "1") == "1"
 GEMM_F32 = 0  # v_mfma_f32_32x32x2_f32: exact f32 fma chain
 GEMM_X6 = 1   # fp32 split into 3 bf16 planes, 6 bf16 MFMA products, fp32 accumulation (default)
 _mode = GEMM_F32 if os.environ.get("RSLRL_GEMM_MODE", "x6") == "f32" else GEMM_X6
@@ -146,6 +147,31 @@ def linear_dgrad_elu(dz, w, h, img=None):
     return out, db
 
 
+def linear_dgrad_elu_wgrad(dz, w, h, img):
+    """Output-layer backward in one launch (x6; dz [M, Nred <= 16, % 4]): ((dz @ w) * ELU'(h), its column sums,
+    dz^T h).  w is the layer weight [Nred, K] (only its image is read)."""
+    M, N = dz.shape
+    K = h.shape[1]
+    L = _lib.lib()
+    tiles = L.rslrl_linear_tiles(M)
+    out = torch.empty(M, K, device=dz.device, dtype=torch.float32)
+    part = torch.empty(K, tiles, device=dz.device, dtype=torch.float32)
+    wpart = torch.empty(tiles, N, K, device=dz.device, dtype=torch.float32)
+    with timer.span(f"linear_dgrad_wgrad[M={M},Nred={N},K={K}]", dz.device, 4 * M * (N + 2 * K), 4 * M * K * N):
+        rc = L.rslrl_linear_dgrad_elu_wgrad(dz.data_ptr(), M, N, K, h.data_ptr(), out.data_ptr(), part.data_ptr(),
+                                            img.data_ptr(), wpart.data_ptr(), _stream(dz))
+    _lib.check(rc, "rslrl_linear_dgrad_elu_wgrad")
+    db = torch.empty(K, device=dz.device, dtype=torch.float32)
+    rc = L.rslrl_column_sum_fold(part.data_ptr(), tiles, K, db.data_ptr(), _stream(dz))
+    _lib.check(rc, "rslrl_column_sum_fold")
+    dw = torch.empty(N, K, device=dz.device, dtype=torch.float32)
+    nbytes = L.rslrl_fold_partials_workspace_bytes(tiles, N * K)
+    ws = torch.empty(max(nbytes, 16) // 8, dtype=torch.float64, device=dz.device)
+    rc = L.rslrl_fold_partials(wpart.data_ptr(), tiles, N * K, dw.data_ptr(), ws.data_ptr(), nbytes, _stream(dz))
+    _lib.check(rc, "rslrl_fold_partials")
+    return out, db, dw
+
+
 def linear_wgrad(dz, x):
     """dz^T x ([N, K]) on the x6 weight-gradient kernel; dz [M, N], x [M, K], N, K <= 256 and 4-aligned."""
     M, N = dz.shape
@@ -208,6 +234,15 @@ class FusedMLPFunction(torch.autograd.Function):
         grads_b[L - 1] = dz.sum(0)
         for l in range(L - 1, -1, -1):
             h_in = hs[l]
+            fuse_w = (_FUSE_OUT and ctx.x6 and l == L - 1 and l > 0 and dz.shape[1] <= 16 and h_in.shape[1] <= MAX_WIDTH
+                      and ctx.needs_input_grad[1 + 2 * l])
+            if fuse_w:  # output layer: dgrad + ELU' + bias grad + weight grad over one read of h (one launch)
+                nred = dz.shape[1]
+                pad = (-nred) % 4
+                dzp = F.pad(dz, (0, pad)) if pad else dz
+                dz, grads_b[l - 1], dw = linear_dgrad_elu_wgrad(dzp, ws[l], h_in, ctx.dgrad_imgs[l])
+                grads_w[l] = dw[:nred]
+                continue
             grads_w[l] = _weight_grad(dz, h_in, ctx.x6) if ctx.needs_input_grad[1 + 2 * l] else None
             if l == 0:
                 dx = dz.mm(ws[0]) if ctx.needs_input_grad[0] else None

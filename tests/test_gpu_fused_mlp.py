@@ -5,6 +5,7 @@ k-order differs from hipBLASLt's at fp32 epsilon."""
 import pytest
 import torch
 
+from rsl_rl_amd import _lib
 from rsl_rl_amd.networks import MLP
 from rsl_rl_amd.networks import fused_mlp
 from rsl_rl_amd.networks.fused_mlp import bimage, fusable_structure, linear_dgrad_elu, linear_fwd
@@ -189,3 +190,40 @@ def test_linear_wgrad(M, N, K, cuda_device):
     rms = lambda a: (a.double() - ref).square().mean().sqrt().item()  # noqa: E731
     assert rms(ours) <= 2.0 * rms(t32) + 1e-12, (rms(ours), rms(t32))
     _close(ours, ref.float(), 1e-5)
+
+
+@pytest.mark.parametrize("M,N,K", [(393216, 12, 256), (5000, 4, 256), (3001, 16, 64), (128, 8, 48)])
+def test_linear_dgrad_elu_wgrad(M, N, K, cuda_device):
+    """Fused output-layer backward (one x6 launch): dz_prev and the bias grad as linear_dgrad_elu, and the
+    layer's weight gradient dz^T h, vs fp64 (fp32-class: 2e-5 of the max, the sum runs over M rows)."""
+    torch.manual_seed(M + N)
+    dz = torch.randn(M, N, device=cuda_device)
+    w = torch.randn(N, K, device=cuda_device) / N ** 0.5
+    h = torch.nn.functional.elu(torch.randn(M, K, device=cuda_device))
+    out, db, dw = fused_mlp.linear_dgrad_elu_wgrad(dz, w, h, bimage(w, True))
+    d = dz.double().mm(w.double())
+    ref = torch.where(h > 0, d, d * (h.double() + 1))
+    _close(out, ref.float())
+    _close(db, ref.sum(0).float(), 1e-4)
+    _close(dw, dz.double().t().mm(h.double()).float(), 2e-5)
+    out2, db2, dw2 = fused_mlp.linear_dgrad_elu_wgrad(dz, w, h, bimage(w, True))
+    assert torch.equal(dw, dw2) and torch.equal(db, db2)  # deterministic
+
+
+@pytest.mark.parametrize("S,NK", [(1, 4), (7, 100), (256, 65536), (3072, 3072), (3072, 1024), (129, 20)])
+def test_fold_partials(S, NK, cuda_device):
+    """rslrl_fold_partials (one- and two-stage) vs an fp64 sum; bitwise repeatable."""
+    L = _lib.lib()
+    torch.manual_seed(S + NK)
+    part = torch.randn(S, NK, device=cuda_device)
+    nbytes = L.rslrl_fold_partials_workspace_bytes(S, NK)
+    ws = torch.empty(max(nbytes, 16) // 8, dtype=torch.float64, device=cuda_device)
+    outs = []
+    for _ in range(2):
+        out = torch.empty(NK, device=cuda_device)
+        _lib.check(L.rslrl_fold_partials(part.data_ptr(), S, NK, out.data_ptr(), ws.data_ptr(), nbytes,
+                                         torch.cuda.current_stream().cuda_stream), "fold")
+        outs.append(out)
+    ref = part.double().sum(0)
+    assert torch.allclose(outs[0].double(), ref, rtol=1e-6, atol=1e-6)
+    assert torch.equal(outs[0], outs[1])
