@@ -13,8 +13,9 @@
 //
 // LDS image per buffer and operand: 3 planes x [16 m][COLS bf16]; on 512-B rows the 16-B chunks of row m
 // are XOR-permuted by 4 (m & 3), which makes the transposed reads (4 rows x 64 B per 32-lane half) and
-// the staging stores (ds_write_b64, 128 contiguous bytes per 16 lanes) bank-conflict free; 64-B rows
-// (TN = 32) need no permutation.
+// the staging stores (ds_write_b64, 128 contiguous bytes per 16 lanes) bank-conflict free; on 128-B rows
+// (TN = 64) rows 2, 3 (mod 4) swap their 64-B halves, which separates the banks of the four rows a 32-lane
+// transposed read spans; 64-B rows (TN = 32) need no permutation.
 #include <algorithm>
 
 #include "common.h"
@@ -43,6 +44,7 @@ template <int COLS>
 __device__ __forceinline__ int swz(int m, int col) {  // byte offset of (m, col), col % 4 == 0, within a plane
     constexpr int rowb = COLS * 2;
     if constexpr (rowb >= 512) return rowb * m + 16 * ((col >> 3) ^ (4 * (m & 3))) + 8 * ((col >> 2) & 1);
+    if constexpr (rowb == 128) return rowb * m + 16 * ((col >> 3) ^ (4 * ((m >> 1) & 1))) + 8 * ((col >> 2) & 1);
     return rowb * m + 2 * col;
 }
 
@@ -107,10 +109,11 @@ __device__ __forceinline__ bf16x8 read_frag_tr(const char* __restrict__ plane, i
     return __builtin_bit_cast(bf16x8, v);
 }
 
-// TN = rows of dW per workgroup (256: waves 2 (n) x 4 (k), wave tile 128 x 64; 32: waves 1 x 8, 32 x 32)
+// TN = rows of dW per workgroup (256: waves 2 (n) x 4 (k), wave tile 128 x 64; 64: waves 2 x 4, 32 x 64;
+// 32: waves 1 x 8, 32 x 32)
 template <int TN, bool FULL>
 __global__ __launch_bounds__(kThreadsW, 2) void wgrad_x6_kernel(WgradParams p) {
-    constexpr int WN = TN == 256 ? 2 : 1;
+    constexpr int WN = TN == 32 ? 1 : 2;
     constexpr int WK = 8 / WN;
     constexpr int I = TN / WN / 32;
     constexpr int J = kTK / WK / 32;
@@ -251,28 +254,33 @@ int64_t fold_groups(int64_t S, int64_t NK) {
     return ceil_div(S, kFoldPer);
 }
 
-int64_t wgrad_slices(int64_t M) {  // one workgroup per CU (98 KiB of LDS each), at least 4 chunks each
+// one workgroup per CU for the 256-row tiles (98 KiB of LDS each); the 32 / 64-row tiles (<= 60 KiB) run two
+// per CU, so twice as many slices keep 16 waves per CU in flight; at least 4 chunks per slice
+int64_t wgrad_slices(int64_t M, int N) {
     const int64_t chunks = ceil_div(M, kMC);
-    return std::max<int64_t>(1, std::min<int64_t>(256, chunks / 4));
+    const int64_t max_slices = N <= 64 ? 512 : 256;
+    return std::max<int64_t>(1, std::min<int64_t>(max_slices, chunks / 4));
 }
 
-int64_t wgrad_rows_per(int64_t M) { return ceil_div(ceil_div(M, wgrad_slices(M)), kMC) * kMC; }
+int64_t wgrad_rows_per(int64_t M, int N) { return ceil_div(ceil_div(M, wgrad_slices(M, N)), kMC) * kMC; }
 
 }  // namespace
 }  // namespace rslrl
 
 using namespace rslrl;
 
-extern "C" size_t rslrl_linear_wgrad_workspace_bytes(int64_t M, int32_t N, int32_t K) {
-    if (M < 1 || N < 1 || K < 1) return 0;
-    const int64_t S = ceil_div(M, wgrad_rows_per(M));
-    return static_cast<size_t>(S) * N * K * sizeof(float);
-}
-
 extern "C" size_t rslrl_fold_partials_workspace_bytes(int64_t S, int64_t NK) {
     if (S < 1 || NK < 1) return 0;
     const int64_t G = fold_groups(S, NK);
     return G > 1 ? static_cast<size_t>(G) * NK * sizeof(double) : 0;
+}
+
+// workspace: the [S][N][K] partials, then the fold's fp64 group sums
+extern "C" size_t rslrl_linear_wgrad_workspace_bytes(int64_t M, int32_t N, int32_t K) {
+    if (M < 1 || N < 1 || K < 1) return 0;
+    const int64_t S = ceil_div(M, wgrad_rows_per(M, N));
+    const size_t part = static_cast<size_t>(S) * N * K * sizeof(float);
+    return part + rslrl_fold_partials_workspace_bytes(S, static_cast<int64_t>(N) * K);
 }
 
 extern "C" int rslrl_fold_partials(const float* partials, int64_t S, int64_t NK, float* out, void* workspace,
@@ -305,9 +313,10 @@ extern "C" int rslrl_linear_wgrad(const float* dz, const float* x, int64_t M, in
     if (M < 1 || N < 1 || K < 1 || N > 256 || K > kTK || (N & 3) || (K & 3)) return RSLRL_E_INVALID_ARGUMENT;
     if (!dz || !x || !dw || !workspace) return RSLRL_E_INVALID_ARGUMENT;
     if ((reinterpret_cast<uintptr_t>(dz) | reinterpret_cast<uintptr_t>(x)) & 15) return RSLRL_E_MISALIGNED;
-    const int64_t rows_per = wgrad_rows_per(M);
+    const int64_t rows_per = wgrad_rows_per(M, N);
     const int64_t S = ceil_div(M, rows_per);
-    if (workspace_bytes < static_cast<size_t>(S) * N * K * sizeof(float)) return RSLRL_E_WORKSPACE_TOO_SMALL;
+    const size_t part_bytes = static_cast<size_t>(S) * N * K * sizeof(float);  // 16-byte multiple (N, K % 4)
+    if (workspace_bytes < rslrl_linear_wgrad_workspace_bytes(M, N, K)) return RSLRL_E_WORKSPACE_TOO_SMALL;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     WgradParams p{dz, x, static_cast<float*>(workspace), M, rows_per, N, K};
     bool full = (M % rows_per == 0) && K == kTK;  // and N == TN, checked per branch
@@ -316,6 +325,10 @@ extern "C" int rslrl_linear_wgrad(const float* dz, const float* x, int64_t M, in
         full = full && N == 32;
         if (full) hipLaunchKernelGGL((wgrad_x6_kernel<32, true>), g, b, 0, st, p);
         else hipLaunchKernelGGL((wgrad_x6_kernel<32, false>), g, b, 0, st, p);
+    } else if (N <= 64) {
+        full = full && N == 64;
+        if (full) hipLaunchKernelGGL((wgrad_x6_kernel<64, true>), g, b, 0, st, p);
+        else hipLaunchKernelGGL((wgrad_x6_kernel<64, false>), g, b, 0, st, p);
     } else {
         full = full && N == 256;
         if (full) hipLaunchKernelGGL((wgrad_x6_kernel<256, true>), g, b, 0, st, p);
@@ -323,8 +336,6 @@ extern "C" int rslrl_linear_wgrad(const float* dz, const float* x, int64_t M, in
     }
     int rc = launch_status();
     if (rc) return rc;
-    const int NK = N * K;
-    hipLaunchKernelGGL((fold_kernel<float, float>), dim3(static_cast<unsigned>(ceil_div(NK, 256))), dim3(kBlock), 0,
-                       st, static_cast<const float*>(workspace), static_cast<int>(S), static_cast<int>(S), NK, dw);
-    return launch_status();
+    return rslrl_fold_partials(static_cast<const float*>(workspace), S, static_cast<int64_t>(N) * K, dw,
+                               static_cast<char*>(workspace) + part_bytes, workspace_bytes - part_bytes, stream);
 }

@@ -188,9 +188,14 @@ def linear_wgrad(dz, x):
 
 
 def _weight_grad(dz, x, x6: bool):
-    # the x6 weight-gradient kernel computes full 256 x 256 tiles: it pays off (and is deterministic with
-    # a smaller error than the batched fp32 GEMM) for the square hidden layers; the narrow first / output
-    # layers stay on the split-K batched GEMM (networks/linear.py), which is faster there
+    # the x6 weight-gradient kernel computes TN x 256 tiles (TN = 32, 64 or 256 rows of its first operand):
+    # the square hidden layers run it as dz^T x; the first layer (input width <= 64) as (x^T dz)^T on the
+    # 64-row tiles; the narrow output layers stay on the split-K batched GEMM (networks/linear.py) unless
+    # their backward is fused (linear_dgrad_elu_wgrad)
+    if x6 and dz.shape[1] > 64 and x.shape[1] <= 64 and dz.shape[1] <= MAX_WIDTH and dz.shape[1] % 4 == 0:
+        pad = (-x.shape[1]) % 4
+        xp = F.pad(x, (0, pad)) if pad else x
+        return linear_wgrad(xp, dz)[: x.shape[1]].t().contiguous()
     if x6 and dz.shape[1] > 32 and x.shape[1] > 64 and dz.shape[1] <= MAX_WIDTH and x.shape[1] <= MAX_WIDTH \
             and x.shape[1] % 4 == 0:
         pad = (-dz.shape[1]) % 4

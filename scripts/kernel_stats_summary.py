@@ -12,8 +12,9 @@ FAMILIES = [
     ("x6 gemm<fwd bias+ELU>", r"mlp_gemm_x6r?_kernel<1"),
     ("x6 gemm<fwd bias>", r"mlp_gemm_x6r?_kernel<0"),
     ("x6 gemm<dgrad ELU'>", r"mlp_gemm_x6r?_kernel<2"),
+    ("x6 gemm<dgrad ELU' + wgrad>", r"mlp_gemm_x6_kernel<3"),
     ("x6 wgrad", r"wgrad_x6_kernel"),
-    ("wgrad fold", r"wgrad_fold_kernel"),
+    ("partials fold", r"wgrad_fold_kernel|fold_kernel<"),
     ("bimage", r"bimage_kernel"),
     ("f32 gemm<fwd bias+ELU>", r"mlp_gemm_kernel<1"),
     ("f32 gemm<fwd bias>", r"mlp_gemm_kernel<0"),

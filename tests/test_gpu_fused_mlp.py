@@ -175,7 +175,8 @@ def test_frozen_weights_scope_reuses_images(cuda_device):
         _close(a, _reference(mlp, x))
 
 
-@pytest.mark.parametrize("M,N,K", [(393216, 256, 256), (393216, 256, 48), (5000, 12, 256), (3001, 4, 256),
+@pytest.mark.parametrize("M,N,K", [(393216, 256, 256), (393216, 256, 48), (393216, 48, 256), (1000, 64, 256),
+                                   (777, 40, 200), (5000, 12, 256), (3001, 4, 256),
                                    (100, 256, 256), (16, 32, 64), (70000, 64, 128)])
 def test_linear_wgrad(M, N, K, cuda_device):
     """dW = dz^T x on the x6 weight-gradient kernel: fp32-class error against fp64 (RMS within 2x of torch's
@@ -227,3 +228,38 @@ def test_fold_partials(S, NK, cuda_device):
     ref = part.double().sum(0)
     assert torch.allclose(outs[0].double(), ref, rtol=1e-6, atol=1e-6)
     assert torch.equal(outs[0], outs[1])
+
+
+_X6S_CHECK = r"""
+import torch
+from rsl_rl_amd.networks import fused_mlp
+from rsl_rl_amd.networks.fused_mlp import bimage, linear_fwd
+fused_mlp.set_gemm_mode(fused_mlp.GEMM_X6)
+torch.manual_seed(0)
+dev = torch.device("cuda:0")
+for M, K, N, elu in [(65536, 256, 256, True), (65536, 48, 256, False), (1000, 16, 64, True), (333, 256, 128, True)]:
+    x = torch.randn(M, K, device=dev)
+    w = torch.randn(N, K, device=dev) / K ** 0.5
+    b = torch.randn(N, device=dev)
+    y = linear_fwd(x, w, b, elu, bimage(w, False))
+    z = x.double().mm(w.double().t()) + b.double()
+    ref = torch.nn.functional.elu(z) if elu else z
+    err = (y.double() - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 1e-6, (M, K, N, elu, err)
+    assert torch.equal(y, linear_fwd(x, w, b, elu, bimage(w, False)))
+print("ok")
+"""
+
+
+def test_x6_16x16_forward_opt_in(cuda_device):
+    """The opt-in 16x16x32 paired-x6 forward kernel (RSLRL_X6_SHAPE=16, read once per process: run in a child
+    process) vs fp64, full and ragged tiles, bitwise repeatable."""
+    import os
+    import subprocess
+    import sys
+
+    env = dict(os.environ, RSLRL_X6_SHAPE="16")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", _X6S_CHECK], env=env, cwd=root, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
