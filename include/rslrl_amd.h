@@ -31,7 +31,7 @@ extern "C" {
 
 typedef struct ihipStream_t* rslrl_stream_t; /* == hipStream_t */
 
-#define RSLRL_ABI_VERSION 2
+#define RSLRL_ABI_VERSION 3
 
 enum {
     RSLRL_OK = 0,
@@ -179,8 +179,10 @@ typedef struct {
     int32_t rows;
     int32_t depth;
     int32_t transposed;
-    int32_t reserved; /* 0 */
+    int32_t layout; /* RSLRL_BIMAGE_LAYOUT_GEMM (0) or RSLRL_BIMAGE_LAYOUT_OUT (1, see rslrl_linear_fwd_out) */
 } rslrl_bimage_desc_t;
+#define RSLRL_BIMAGE_LAYOUT_GEMM 0
+#define RSLRL_BIMAGE_LAYOUT_OUT 1
 #define RSLRL_MAX_BIMAGES 16
 int rslrl_linear_prepare_bimages(const rslrl_bimage_desc_t* descs, int32_t n, rslrl_stream_t stream);
 int rslrl_linear_fwd(const float* x, int64_t M, int32_t K, const float* weight, int32_t N, const float* bias,
@@ -189,6 +191,16 @@ int rslrl_linear_dgrad_elu(const float* dz, int64_t M, int32_t Nred, const float
                            const float* h, float* dz_prev, float* colsum_partials, const void* bimage,
                            rslrl_stream_t stream);
 int rslrl_column_sum_fold(const float* partials, int64_t tiles, int32_t N, float* out, rslrl_stream_t stream);
+
+/* Last hidden layer and output layer in one x6 launch (the MLP's final Linear, rsl_rl/networks/mlp.py:106-114,
+ * 1-32 outputs): h = ELU(x[M,K] W[N,K]^T + bias[N]) -- written to h_out[M,N] unless h_out is NULL (inference:
+ * the activation then never reaches HBM) -- and y[M,Nout] = h W_out[Nout,N]^T + out_bias[Nout].  bimage is W's
+ * image (layout 0); out_image (rslrl_linear_out_image_bytes() bytes) is W_out's image built with a descriptor
+ * {src = W_out, rows = Nout <= 32, depth = N, transposed = 0, layout = RSLRL_BIMAGE_LAYOUT_OUT}.  N % 4 == 0. */
+size_t rslrl_linear_out_image_bytes(void);
+int rslrl_linear_fwd_out(const float* x, int64_t M, int32_t K, const float* bias, int32_t N, const void* bimage,
+                         float* h_out, const float* out_bias, int32_t Nout, const void* out_image, float* y,
+                         rslrl_stream_t stream);
 
 /* Weight gradient of a linear layer on the x6 path: dw[N,K] = dz[M,N]^T x[M,K] (the autograd backward of
  * nn.Linear.weight; the reference's cuBLAS GEMM).  N, K <= 256 and % 4 == 0; dz, x 16-byte aligned.  The

@@ -18,7 +18,7 @@ import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 LIB_PATH = os.path.join(LIB_DIR, "librslrl_amd.so")
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 # symbols declared in include/rslrl_amd.h (tests/test_capi.py checks the header against this list)
 EXPORTED_SYMBOLS = (
@@ -39,6 +39,8 @@ EXPORTED_SYMBOLS = (
     "rslrl_linear_fwd",
     "rslrl_linear_dgrad_elu",
     "rslrl_column_sum_fold",
+    "rslrl_linear_out_image_bytes",
+    "rslrl_linear_fwd_out",
     "rslrl_linear_wgrad_workspace_bytes",
     "rslrl_linear_wgrad",
     "rslrl_fold_partials_workspace_bytes",
@@ -70,10 +72,12 @@ class GatherField(ctypes.Structure):
 
 class BImageDesc(ctypes.Structure):
     _fields_ = [("src", ctypes.c_void_p), ("image", ctypes.c_void_p), ("rows", ctypes.c_int32),
-                ("depth", ctypes.c_int32), ("transposed", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+                ("depth", ctypes.c_int32), ("transposed", ctypes.c_int32), ("layout", ctypes.c_int32)]
 
 
 MAX_BIMAGES = 16
+BIMAGE_LAYOUT_GEMM = 0
+BIMAGE_LAYOUT_OUT = 1
 
 DTYPE_F32, DTYPE_U8, DTYPE_I32, DTYPE_I64 = 0, 1, 2, 3
 ROLLOUT_MAX_OBS = 4
@@ -192,6 +196,10 @@ def _declare(L):
     L.rslrl_linear_prepare_bimages.restype = ctypes.c_int
     L.rslrl_linear_prepare_bimages.argtypes = [ctypes.POINTER(BImageDesc), I32, P]
     L.rslrl_linear_fwd.argtypes = [P, I64, I32, P, I32, P, I32, P, P, P]
+    L.rslrl_linear_out_image_bytes.restype = SZ
+    L.rslrl_linear_out_image_bytes.argtypes = []
+    L.rslrl_linear_fwd_out.restype = ctypes.c_int
+    L.rslrl_linear_fwd_out.argtypes = [P, I64, I32, P, I32, P, P, P, I32, P, P, P]
     L.rslrl_linear_dgrad_elu.restype = ctypes.c_int
     L.rslrl_linear_dgrad_elu.argtypes = [P, I64, I32, P, I32, P, P, P, P, P]
     L.rslrl_linear_wgrad_workspace_bytes.restype = SZ

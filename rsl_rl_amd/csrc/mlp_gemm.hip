@@ -39,8 +39,11 @@ constexpr int kThreads = 512;
 
 // kEpiEluGradWgrad: kEpiEluGrad for a short reduction (Nred <= 16, one chunk: the output layer) that also
 // accumulates that layer's weight gradient dZ^T H from the same H tile (x6 path only)
-enum Epilogue { kEpiBias = 0, kEpiBiasElu = 1, kEpiEluGrad = 2, kEpiEluGradWgrad = 3 };
+// kEpiBiasEluOut: kEpiBiasElu for the last hidden layer that also applies the (<= 32 wide) output layer to
+// the activation tile while it is in registers (x6 path only; the main loop computes C^T tiles)
+enum Epilogue { kEpiBias = 0, kEpiBiasElu = 1, kEpiEluGrad = 2, kEpiEluGradWgrad = 3, kEpiBiasEluOut = 4 };
 constexpr int kMaxWgradRows = 16;
+constexpr int kMaxOutWidth = 32;  // kEpiBiasEluOut
 
 struct GemmParams {
     const float* a;    // [M, K] row-major (lda = K)
@@ -54,6 +57,10 @@ struct GemmParams {
     int N;
     int64_t ctiles;    // dgrad: columns of colsum (= rslrl_linear_tiles(M), 128-row tiles)
     float* wpart;      // kEpiEluGradWgrad: per-tile weight-gradient partials [tiles][K][N]
+    const uint4* oimg;   // kEpiBiasEluOut: output-layer image (out_image_kernel layout)
+    const float* obias;  // kEpiBiasEluOut: output bias [nout]
+    float* y;            // kEpiBiasEluOut: output [M, nout]
+    int nout;            // kEpiBiasEluOut: output width <= 32
 };
 
 // global -> registers for one K chunk: A: 128 x 16 floats = 512 float4 (1 per thread); B: 256 x 16 = 1024
@@ -350,8 +357,37 @@ struct BImageBatch {
     rslrl_bimage_desc_t d[kMaxImages];
 };
 
+// Output-layer image (layout 1, rslrl_linear_fwd_out): for wave column group wn (64 columns), column tile j,
+// k step s, plane q, lane half h and output o: 8 bf16 of W_out[o][c], c = 64 wn + 32 j + 4 h + (t & 3) +
+// 8 (2 s + (t >> 2)), t < 8 -- the columns lane half h of the C^T epilogue holds in registers 8 s .. 8 s + 7.
+// Unit (16 B) index ((((wn * 2 + j) * 2 + s) * 3 + q) * 2 + h) * 32 + o; zero for o >= rows, c >= depth.
+constexpr int kOutImageUnits = 4 * 2 * 2 * 3 * 2 * 32;
+constexpr int kOutImageThreads = 4 * 2 * 2 * 2 * 32;
+
+__device__ __forceinline__ void out_image_thread(const rslrl_bimage_desc_t& dsc, int id) {
+    if (id >= kOutImageThreads) return;
+    const int o = id & 31, h = (id >> 5) & 1, s = (id >> 6) & 1, j = (id >> 7) & 1, wn = id >> 8;
+    float v[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+        const int c = wn * 64 + j * 32 + 4 * h + (t & 3) + 8 * (2 * s + (t >> 2));
+        v[t] = (o < dsc.rows && c < dsc.depth) ? dsc.src[static_cast<int64_t>(o) * dsc.depth + c] : 0.f;
+    }
+    uint2 lo[3], hi[3];
+    split4(make_float4(v[0], v[1], v[2], v[3]), lo[0], lo[1], lo[2]);
+    split4(make_float4(v[4], v[5], v[6], v[7]), hi[0], hi[1], hi[2]);
+    uint4* img = static_cast<uint4*>(dsc.image);
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+        img[((((wn * 2 + j) * 2 + s) * 3 + q) * 2 + h) * 32 + o] = make_uint4(lo[q].x, lo[q].y, hi[q].x, hi[q].y);
+}
+
 __global__ __launch_bounds__(kBlock) void bimage_kernel(BImageBatch batch) {
     const rslrl_bimage_desc_t& dsc = batch.d[blockIdx.y];
+    if (dsc.layout == RSLRL_BIMAGE_LAYOUT_OUT) {
+        out_image_thread(dsc, blockIdx.x * kBlock + threadIdx.x);
+        return;
+    }
     const int rows = dsc.rows, depth = dsc.depth;
     const float* __restrict__ src = dsc.src;
     const int nchunks = (depth + kKC - 1) / kKC;
@@ -492,7 +528,12 @@ __global__ __launch_bounds__(kThreads, MINW) void mlp_gemm_x6_kernel(GemmParams 
 #pragma unroll
             for (int q = 0; q < 3; ++q) af[q] = read_frag(a_lds + q * planeA, wm * (BM / 2) + i * 32 + l32, h);
 #pragma unroll
-            for (int j = 0; j < 2; ++j) acc[i][j] = mfma_x6(af, bf[j], acc[i][j]);
+            for (int j = 0; j < 2; ++j) {
+                if constexpr (EPI == kEpiBiasEluOut)  // C^T tile: the weight fragment is the MFMA's A operand
+                    acc[i][j] = mfma_x6(bf[j], af, acc[i][j]);
+                else
+                    acc[i][j] = mfma_x6(af, bf[j], acc[i][j]);
+            }
         }
         if (more) store_a_split<BM>(an, lds[buf ^ 1]);
         __syncthreads();  // also retires the global_load_lds of chunk c+1 (vmcnt(0))
@@ -549,6 +590,67 @@ __global__ __launch_bounds__(kThreads, MINW) void mlp_gemm_x6_kernel(GemmParams 
                     const int col = wn * 64 + j * 32 + l32;
                     if (o < p.K && col < p.N) out[o * p.N + col] = red[o * kBN + col] + wacc[o][j];
                 }
+        }
+    } else if constexpr (EPI == kEpiBiasEluOut) {
+        // C^T tiles: lane (l32, h) holds row l32 of the tile, columns (r & 3) + 8 (r >> 2) + 4 h (r < 16).
+        // h = ELU(acc + b) is stored (when wanted) as float4 column quads, split into bf16 planes in
+        // registers and multiplied by the output weight: Y'[o][row] = sum over this wave's 64 columns,
+        // 2 k steps of 16 per 32-column tile (lane half h carries columns {0-3, 8-11} + 4 h, then
+        // {16-19, 24-27} + 4 h; the image orders the weight the same way).  The four wn waves' partial
+        // Y' tiles are added in a fixed order through LDS.
+        float* red = reinterpret_cast<float*>(&lds[0][0]);  // [wm][wn][i][32 o][32 rows] fp32 = 64 KiB
+        const uint4* oimg = p.oimg + wn * (2 * 2 * 3 * 64);
+#pragma unroll
+        for (int i = 0; i < I; ++i) {
+            const int64_t row = row0 + wm * (BM / 2) + i * 32 + l32;
+            const bool row_ok = row < p.M;
+            f32x16 oacc = f32x16{};
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int cb = wn * 64 + j * 32 + 4 * h;
+                float v[16];
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const int col = cb + 8 * g;
+                    const bool col_ok = col < p.N;  // N % 4 == 0
+                    const float4 b4 = col_ok ? *reinterpret_cast<const float4*>(p.bias + col)
+                                             : make_float4(0.f, 0.f, 0.f, 0.f);
+                    float t[4] = {acc[i][j][4 * g] + b4.x, acc[i][j][4 * g + 1] + b4.y, acc[i][j][4 * g + 2] + b4.z,
+                                  acc[i][j][4 * g + 3] + b4.w};
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v[4 * g + e] = t[e] > 0.f ? t[e] : elu_neg(t[e]);
+                    if (p.c && row_ok && col_ok)
+                        *reinterpret_cast<float4*>(p.c + row * p.N + col) =
+                            make_float4(v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]);
+                }
+#pragma unroll
+                for (int s2 = 0; s2 < 2; ++s2) {
+                    bf16x8 vb[3], wa[3];
+                    uint2 lo[3], hi[3];
+                    split4(make_float4(v[8 * s2], v[8 * s2 + 1], v[8 * s2 + 2], v[8 * s2 + 3]), lo[0], lo[1], lo[2]);
+                    split4(make_float4(v[8 * s2 + 4], v[8 * s2 + 5], v[8 * s2 + 6], v[8 * s2 + 7]), hi[0], hi[1],
+                           hi[2]);
+#pragma unroll
+                    for (int q = 0; q < 3; ++q) {
+                        vb[q] = __builtin_bit_cast(bf16x8, make_uint4(lo[q].x, lo[q].y, hi[q].x, hi[q].y));
+                        wa[q] = __builtin_bit_cast(bf16x8, oimg[((j * 2 + s2) * 3 + q) * 64 + lane]);
+                    }
+                    oacc = mfma_x6(wa, vb, oacc);
+                }
+            }
+            float* rd = red + ((wm * 4 + wn) * I + i) * 1024;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) rd[((r & 3) + 8 * (r >> 2) + 4 * h) * 32 + l32] = oacc[r];
+        }
+        __syncthreads();
+        const int nout = p.nout;
+        for (int idx = threadIdx.x; idx < BM * nout; idx += kThreads) {
+            const int rl = idx / nout;
+            const int o = idx - rl * nout;
+            const float* b = red + (((rl >> 6) * 4) * I + ((rl & 63) >> 5)) * 1024 + o * 32 + (rl & 31);
+            const float sum = ((b[0] + b[I * 1024]) + b[2 * I * 1024]) + b[3 * I * 1024];
+            const int64_t row = row0 + rl;
+            if (row < p.M) p.y[row * nout + o] = sum + p.obias[o];
         }
     } else {
         epilogue_tiles<EPI, I, 2>(p, acc, row0 + wm * (BM / 2), wn * 64, full, colpart);
@@ -805,6 +907,33 @@ int dgrad_occupancy() {  // tuning knob: RSLRL_DGRAD_OCC=2|4 (default 4)
     return v;
 }
 
+// the opt-in 16x16x32 forward (RSLRL_X6_SHAPE=16); false: not taken
+template <int EPI>
+bool launch_x6s(const GemmParams& p, const uint4* img, bool fullm, dim3 g, hipStream_t st) {
+    if constexpr (EPI == kEpiBias || EPI == kEpiBiasElu) {
+        if (x6_shape() != 16 || (p.N & 3) || !aligned16(p.c) || !aligned16(p.bias)) return false;  // 16-B epilogue
+        const dim3 b(kThreads);
+        if (x6s_nontemporal()) {
+            if (fullm) hipLaunchKernelGGL((mlp_gemm_x6s_kernel<EPI, true, 4, true>), g, b, 0, st, p, img);
+            else hipLaunchKernelGGL((mlp_gemm_x6s_kernel<EPI, false, 4, true>), g, b, 0, st, p, img);
+        } else {
+            if (fullm) hipLaunchKernelGGL((mlp_gemm_x6s_kernel<EPI, true, 4, false>), g, b, 0, st, p, img);
+            else hipLaunchKernelGGL((mlp_gemm_x6s_kernel<EPI, false, 4, false>), g, b, 0, st, p, img);
+        }
+        return true;
+    } else {
+        return false;
+    }
+}
+
+int out_fwd_occupancy() {  // tuning knob: RSLRL_OUT_FWD_OCC=2|4 (default 4)
+    static const int v = [] {
+        const char* e = std::getenv("RSLRL_OUT_FWD_OCC");
+        return (e && std::atoi(e) == 2) ? 2 : 4;
+    }();
+    return v;
+}
+
 // bimage == nullptr: exact f32 MFMA main loop on p.bw; otherwise the split-bf16 main loop on the image.
 template <int EPI>
 int launch(const GemmParams& p, const void* bimage, hipStream_t st) {
@@ -829,30 +958,22 @@ int launch(const GemmParams& p, const void* bimage, hipStream_t st) {
                 case 12: go(std::integral_constant<int, 12>{}); break;
                 default: go(std::integral_constant<int, 16>{}); break;
             }
+        } else if constexpr (EPI == kEpiBiasEluOut) {
+            if (out_fwd_occupancy() == 2) {
+                if (fullm) hipLaunchKernelGGL((mlp_gemm_x6_kernel<EPI, true, 2>), g, b, 0, st, p, img);
+                else hipLaunchKernelGGL((mlp_gemm_x6_kernel<EPI, false, 2>), g, b, 0, st, p, img);
+            } else {
+                if (fullm) hipLaunchKernelGGL((mlp_gemm_x6_kernel<EPI, true, 4>), g, b, 0, st, p, img);
+                else hipLaunchKernelGGL((mlp_gemm_x6_kernel<EPI, false, 4>), g, b, 0, st, p, img);
+            }
         } else if (short_k) {
             if (fullm) hipLaunchKernelGGL((mlp_gemm_x6_kernel<EPI, true, 2>), g, b, 0, st, p, img);
             else hipLaunchKernelGGL((mlp_gemm_x6_kernel<EPI, false, 2>), g, b, 0, st, p, img);
-        } else if (x6_shape() == 16 && EPI != kEpiEluGrad && (p.N & 3) == 0 && aligned16(p.c) && (!p.h || aligned16(p.h)) &&
-                   (!p.bias || aligned16(p.bias))) {  // 16-byte epilogue accesses
-            auto go = [&](auto minw, auto nt) {
-                constexpr int W = decltype(minw)::value;
-                constexpr bool T = decltype(nt)::value;
-                if (fullm) hipLaunchKernelGGL((mlp_gemm_x6s_kernel<EPI, true, W, T>), g, b, 0, st, p, img);
-                else hipLaunchKernelGGL((mlp_gemm_x6s_kernel<EPI, false, W, T>), g, b, 0, st, p, img);
-            };
-            using W2 = std::integral_constant<int, 2>;
-            using W4 = std::integral_constant<int, 4>;
-            const bool nt = x6s_nontemporal();
-            if (EPI == kEpiEluGrad && dgrad_occupancy() == 2) {
-                if (nt) go(W2{}, std::true_type{}); else go(W2{}, std::false_type{});
-            } else {
-                if (nt) go(W4{}, std::true_type{}); else go(W4{}, std::false_type{});
-            }
-        } else {
+        } else if (!launch_x6s<EPI>(p, img, fullm, g, st)) {
             if (fullm) hipLaunchKernelGGL((mlp_gemm_x6_kernel<EPI, true, 4>), g, b, 0, st, p, img);
             else hipLaunchKernelGGL((mlp_gemm_x6_kernel<EPI, false, 4>), g, b, 0, st, p, img);
         }
-    } else if constexpr (EPI == kEpiEluGradWgrad) {
+    } else if constexpr (EPI == kEpiEluGradWgrad || EPI == kEpiBiasEluOut) {
         return RSLRL_E_UNSUPPORTED;  // x6 path only
     } else if (EPI == kEpiEluGrad && dgrad_occupancy() == 2) {
         hipLaunchKernelGGL((mlp_gemm_kernel<EPI, 2>), g, b, 0, st, p);
@@ -877,22 +998,31 @@ extern "C" int rslrl_linear_prepare_bimages(const rslrl_bimage_desc_t* descs, in
     if (!descs || n < 1 || n > kMaxImages) return RSLRL_E_INVALID_ARGUMENT;
     BImageBatch batch{};
     int max_chunks = 0;
+    int max_threads = 0;
     for (int i = 0; i < n; ++i) {
         const rslrl_bimage_desc_t& d = descs[i];
         if (!d.src || !d.image || d.rows < 1 || d.rows > kBN || d.depth < 1 || d.depth > (1 << 24))
             return RSLRL_E_INVALID_ARGUMENT;
         if (reinterpret_cast<uintptr_t>(d.image) & 15) return RSLRL_E_MISALIGNED;
+        if (d.layout == RSLRL_BIMAGE_LAYOUT_OUT) {
+            if (d.rows > kMaxOutWidth || d.depth > kBN || d.transposed) return RSLRL_E_INVALID_ARGUMENT;
+            max_threads = std::max(max_threads, kOutImageThreads);
+        } else if (d.layout == RSLRL_BIMAGE_LAYOUT_GEMM) {
+            max_chunks = std::max(max_chunks, static_cast<int>(ceil_div(static_cast<int64_t>(d.depth), kKC)));
+        } else {
+            return RSLRL_E_INVALID_ARGUMENT;
+        }
         batch.d[i] = d;
-        max_chunks = std::max(max_chunks, static_cast<int>(ceil_div(static_cast<int64_t>(d.depth), kKC)));
     }
-    const dim3 grid(static_cast<unsigned>(ceil_div(max_chunks * kBN * 2, kBlock)), static_cast<unsigned>(n));
+    max_threads = std::max(max_threads, max_chunks * kBN * 2);
+    const dim3 grid(static_cast<unsigned>(ceil_div(max_threads, kBlock)), static_cast<unsigned>(n));
     hipLaunchKernelGGL(bimage_kernel, grid, dim3(kBlock), 0, reinterpret_cast<hipStream_t>(stream), batch);
     return launch_status();
 }
 
 extern "C" int rslrl_linear_prepare_bimage(const float* src, int32_t rows, int32_t depth, int32_t transposed,
                                            void* image, rslrl_stream_t stream) {
-    const rslrl_bimage_desc_t d{src, image, rows, depth, transposed ? 1 : 0, 0};
+    const rslrl_bimage_desc_t d{src, image, rows, depth, transposed ? 1 : 0, RSLRL_BIMAGE_LAYOUT_GEMM};
     return rslrl_linear_prepare_bimages(&d, 1, stream);
 }
 
@@ -935,6 +1065,22 @@ extern "C" int rslrl_linear_dgrad_elu_wgrad(const float* dz, int64_t M, int32_t 
     if (!aligned16(dz) || !aligned16(bimage)) return RSLRL_E_MISALIGNED;
     GemmParams p{dz, nullptr, nullptr, h, dz_prev, colsum_partials, M, Nred, K, ceil_div(M, kBM), wgrad_partials};
     return launch<kEpiEluGradWgrad>(p, bimage, reinterpret_cast<hipStream_t>(stream));
+}
+
+extern "C" size_t rslrl_linear_out_image_bytes(void) { return static_cast<size_t>(kOutImageUnits) * 16; }
+
+extern "C" int rslrl_linear_fwd_out(const float* x, int64_t M, int32_t K, const float* bias, int32_t N,
+                                    const void* bimage, float* h_out, const float* out_bias, int32_t Nout,
+                                    const void* out_image, float* y, rslrl_stream_t stream) {
+    if (M < 0 || K < 1 || N < 1 || N > kBN || (K & 3) || (N & 3) || K > INT32_MAX / 2) return RSLRL_E_INVALID_ARGUMENT;
+    if (Nout < 1 || Nout > kMaxOutWidth) return RSLRL_E_INVALID_ARGUMENT;
+    if (M == 0) return RSLRL_OK;
+    if (!x || !bias || !bimage || !out_bias || !out_image || !y) return RSLRL_E_INVALID_ARGUMENT;
+    if (!aligned16(x) || !aligned16(bias) || !aligned16(bimage) || !aligned16(out_image) || (h_out && !aligned16(h_out)))
+        return RSLRL_E_MISALIGNED;
+    GemmParams p{x, nullptr, bias, nullptr, h_out, nullptr, M, K, N, 0, nullptr,
+                 static_cast<const uint4*>(out_image), out_bias, y, Nout};
+    return launch<kEpiBiasEluOut>(p, bimage, reinterpret_cast<hipStream_t>(stream));
 }
 
 extern "C" int rslrl_column_sum_fold(const float* partials, int64_t tiles, int32_t N, float* out,

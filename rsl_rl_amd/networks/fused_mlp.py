@@ -36,7 +36,8 @@ def _stream(t):
     return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
 
 
-_FUSE_OUT = os.environ.get("RSLRL_FUSE_OUT", "1") == "1"
+_FUSE_OUT = os.environ.get("RSLRL_FUSE_OUT", "1") == "1"  # output-layer backward in one launch
+_FUSE_OUT_FWD = os.environ.get("RSLRL_FUSE_OUT_FWD", "1") == "1"  # output-layer forward in the last hidden GEMM
 GEMM_F32 = 0  # v_mfma_f32_32x32x2_f32: exact f32 fma chain
 GEMM_X6 = 1   # fp32 split into 3 bf16 planes, 6 bf16 MFMA products, fp32 accumulation (default)
 _mode = GEMM_F32 if os.environ.get("RSLRL_GEMM_MODE", "x6") == "f32" else GEMM_X6
@@ -73,13 +74,16 @@ def frozen_weights():
 
 
 def bimages(specs):
-    """Images for [(w, transposed), ...]: transposed=False -> B = w ([N, K]), True -> B = w^T.  One launch
-    for every image not already cached in a frozen_weights() scope."""
+    """Images for [(w, transposed[, layout]), ...]: transposed=False -> B = w ([N, K]), True -> B = w^T;
+    layout _lib.BIMAGE_LAYOUT_OUT -> the output-layer image of linear_fwd_out.  One launch for every image not
+    already cached in a frozen_weights() scope."""
     out = [None] * len(specs)
     todo = []
-    for i, (w, tr) in enumerate(specs):
+    for i, spec in enumerate(specs):
+        w, tr = spec[0], spec[1]
+        layout = spec[2] if len(spec) > 2 else _lib.BIMAGE_LAYOUT_GEMM
         rows, depth = (w.shape[1], w.shape[0]) if tr else (w.shape[0], w.shape[1])
-        key = (w.data_ptr(), tr, rows, depth)
+        key = (w.data_ptr(), tr, rows, depth, layout)
         if _frozen_depth:
             hit = _bimage_cache.get(key)
             if hit is not None and hit[0]() is w:
@@ -89,7 +93,8 @@ def bimages(specs):
     if not todo:
         return out
     L = _lib.lib()
-    sizes = [L.rslrl_linear_bimage_bytes(depth) // 4 for (_, _, _, _, depth, _) in todo]
+    sizes = [(L.rslrl_linear_out_image_bytes() if key[4] == _lib.BIMAGE_LAYOUT_OUT else
+              L.rslrl_linear_bimage_bytes(depth)) // 4 for (_, _, _, _, depth, key) in todo]
     buf = torch.empty(sum(sizes), dtype=torch.float32, device=todo[0][1].device)
     for start in range(0, len(todo), _lib.MAX_BIMAGES):
         part = todo[start:start + _lib.MAX_BIMAGES]
@@ -103,6 +108,7 @@ def bimages(specs):
             img = buf[off:off + n]
             off += n
             d.src, d.image, d.rows, d.depth, d.transposed = src.data_ptr(), img.data_ptr(), rows, depth, int(tr)
+            d.layout = key[4]
             out[i] = img
             if _frozen_depth:
                 _bimage_cache[key] = (weakref.ref(w), img)
@@ -125,6 +131,33 @@ def linear_fwd(x, w, b, elu: bool, img=None):
                                          y.data_ptr(), img.data_ptr() if img is not None else None, _stream(x))
     _lib.check(rc, "rslrl_linear_fwd")
     return y
+
+
+MAX_OUT_WIDTH = 32
+
+
+def linear_fwd_out(x, w, b, img, w_out, b_out, out_img, store_h: bool):
+    """(h, y): h = ELU(x w^T + b) (None unless store_h) and y = h w_out^T + b_out in one x6 launch; img: B image
+    of w, out_img: the BIMAGE_LAYOUT_OUT image of w_out (<= 32 rows)."""
+    M, K = x.shape
+    N = w.shape[0]
+    nout = w_out.shape[0]
+    h = torch.empty(M, N, device=x.device, dtype=torch.float32) if store_h else None
+    y = torch.empty(M, nout, device=x.device, dtype=torch.float32)
+    flops = 2 * M * N * (K + nout)
+    with timer.span(f"linear_fwd_out[M={M},K={K},N={N},out={nout}]", x.device,
+                    4 * M * (K + nout + (N if store_h else 0)), flops):
+        rc = _lib.lib().rslrl_linear_fwd_out(x.data_ptr(), M, K, b.data_ptr(), N, img.data_ptr(),
+                                             h.data_ptr() if store_h else None, b_out.data_ptr(), nout,
+                                             out_img.data_ptr(), y.data_ptr(), _stream(x))
+    _lib.check(rc, "rslrl_linear_fwd_out")
+    return h, y
+
+
+def _fuse_out_fwd(ws) -> bool:
+    """The last hidden layer and the output layer run as one linear_fwd_out launch (x6 only)."""
+    return _FUSE_OUT_FWD and _mode == GEMM_X6 and len(ws) >= 2 and ws[-1].shape[0] <= MAX_OUT_WIDTH \
+        and ws[-1].shape[1] % 4 == 0
 
 
 def linear_dgrad_elu(dz, w, h, img=None):
@@ -215,14 +248,23 @@ class FusedMLPFunction(torch.autograd.Function):
         h = x
         x6 = _mode == GEMM_X6
         nh = len(ws) - 1
+        fuse_out = _fuse_out_fwd(ws)
         # forward images of the hidden layers + (for backward) the transposed images of layers 1..L-1
-        imgs = bimages([(w, False) for w in ws[:-1]] + [(w, True) for w in ws[1:]]) if x6 else [None] * (2 * nh)
-        for w, b, img in zip(ws[:-1], bs[:-1], imgs[:nh]):
-            h = linear_fwd(h, w, b, elu=True, img=img)
+        # [+ the output-layer image]
+        specs = [(w, False) for w in ws[:-1]] + [(w, True) for w in ws[1:]]
+        if fuse_out:
+            specs.append((ws[-1], False, _lib.BIMAGE_LAYOUT_OUT))
+        imgs = bimages(specs) if x6 else [None] * (2 * nh)
+        for l, (w, b, img) in enumerate(zip(ws[:-1], bs[:-1], imgs[:nh])):
+            if fuse_out and l == nh - 1:
+                h, y = linear_fwd_out(h, w, b, img, ws[-1], bs[-1], imgs[2 * nh], store_h=True)
+            else:
+                h = linear_fwd(h, w, b, elu=True, img=img)
             hs.append(h)
-        ctx.dgrad_imgs = [None] + imgs[nh:]  # index l: image of W_l^T
+        ctx.dgrad_imgs = [None] + imgs[nh:2 * nh]  # index l: image of W_l^T
         ctx.x6 = x6
-        y = F.linear(h, ws[-1], bs[-1])
+        if not fuse_out:
+            y = F.linear(h, ws[-1], bs[-1])
         ctx.save_for_backward(*hs, *params)
         ctx.n_layers = len(ws)
         return y
@@ -300,10 +342,21 @@ def fused_mlp_forward(mlp: nn.Sequential, x: torch.Tensor) -> torch.Tensor:
         y = FusedMLPFunction.apply(x, *params)
     else:
         h = x
-        imgs = bimages([(m.weight, False) for m in linears[:-1]]) if _mode == GEMM_X6 else [None] * (len(linears) - 1)
-        for m, img in zip(linears[:-1], imgs):
-            h = linear_fwd(h, m.weight, m.bias, elu=True, img=img)
-        y = F.linear(h, linears[-1].weight, linears[-1].bias)
+        nh = len(linears) - 1
+        ws = [m.weight for m in linears]
+        fuse_out = _fuse_out_fwd(ws)
+        specs = [(w, False) for w in ws[:-1]]
+        if fuse_out:
+            specs.append((ws[-1], False, _lib.BIMAGE_LAYOUT_OUT))
+        imgs = bimages(specs) if _mode == GEMM_X6 else [None] * nh
+        y = None
+        for l, (m, img) in enumerate(zip(linears[:-1], imgs)):
+            if fuse_out and l == nh - 1:  # the last activation never reaches HBM
+                _, y = linear_fwd_out(h, m.weight, m.bias, img, ws[-1], linears[-1].bias, imgs[nh], store_h=False)
+            else:
+                h = linear_fwd(h, m.weight, m.bias, elu=True, img=img)
+        if y is None:
+            y = F.linear(h, linears[-1].weight, linears[-1].bias)
     for m in mlp:
         if isinstance(m, nn.Unflatten):
             y = m(y)

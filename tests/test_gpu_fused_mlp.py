@@ -167,7 +167,10 @@ def test_frozen_weights_scope_reuses_images(cuda_device):
     x = torch.randn(1000, 48, device=cuda_device)
     with torch.inference_mode(), fused_mlp.frozen_weights():
         a = mlp(x)
-        assert len(fused_mlp._bimage_cache) == 2
+        # two hidden-layer images (+ the output-layer image when the output layer is fused into the last
+        # hidden layer's forward)
+        assert len(fused_mlp._bimage_cache) == 2 + int(fused_mlp._fuse_out_fwd([m.weight for m in mlp
+                                                                                 if isinstance(m, torch.nn.Linear)]))
         b = mlp(x)
     assert len(fused_mlp._bimage_cache) == 0
     assert torch.equal(a, b)
@@ -263,3 +266,28 @@ def test_x6_16x16_forward_opt_in(cuda_device):
     r = subprocess.run([sys.executable, "-c", _X6S_CHECK], env=env, cwd=root, capture_output=True, text=True,
                        timeout=300)
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
+
+
+@pytest.mark.parametrize("M,K,N,nout,store", [(393216, 256, 256, 12, True), (65536, 256, 256, 1, False),
+                                              (1000, 64, 128, 7, True), (333, 48, 256, 32, True),
+                                              (130, 256, 60, 3, False)])
+def test_linear_fwd_out(M, K, N, nout, store, cuda_device):
+    """Last hidden layer + output layer in one x6 launch: h = ELU(x W^T + b) (stored or not) and
+    y = h W_out^T + b_out vs fp64 (fp32-class: 1e-5 of the max), bitwise repeatable."""
+    torch.manual_seed(M + nout)
+    x = torch.randn(M, K, device=cuda_device)
+    w = torch.randn(N, K, device=cuda_device) / K ** 0.5
+    b = torch.randn(N, device=cuda_device) * 0.1
+    wo = torch.randn(nout, N, device=cuda_device) / N ** 0.5
+    bo = torch.randn(nout, device=cuda_device)
+    img, oimg = fused_mlp.bimages([(w, False), (wo, False, _lib.BIMAGE_LAYOUT_OUT)])
+    h, y = fused_mlp.linear_fwd_out(x, w, b, img, wo, bo, oimg, store_h=store)
+    href = torch.nn.functional.elu(x.double().mm(w.double().t()) + b.double())
+    yref = href.mm(wo.double().t()) + bo.double()
+    _close(y, yref.float())
+    if store:
+        _close(h, href.float())
+    else:
+        assert h is None
+    h2, y2 = fused_mlp.linear_fwd_out(x, w, b, img, wo, bo, oimg, store_h=store)
+    assert torch.equal(y, y2)
