@@ -43,7 +43,8 @@ constexpr int kThreads = 512;
 // the activation tile while it is in registers (x6 path only; the main loop computes C^T tiles)
 enum Epilogue { kEpiBias = 0, kEpiBiasElu = 1, kEpiEluGrad = 2, kEpiEluGradWgrad = 3, kEpiBiasEluOut = 4 };
 constexpr int kMaxWgradRows = 16;
-constexpr int kMaxOutWidth = 32;  // kEpiBiasEluOut
+constexpr int kMaxOutWidth = 32;     // kEpiBiasEluOut
+constexpr int kStagedOutWidth = 20;  // kEpiBiasEluOut: widths whose reduction tiles fit beside the h stage
 
 struct GemmParams {
     const float* a;    // [M, K] row-major (lda = K)
@@ -61,6 +62,7 @@ struct GemmParams {
     const float* obias;  // kEpiBiasEluOut: output bias [nout]
     float* y;            // kEpiBiasEluOut: output [M, nout]
     int nout;            // kEpiBiasEluOut: output width <= 32
+    int nt;              // kEpiBiasEluOut: streaming stores for h
 };
 
 // global -> registers for one K chunk: A: 128 x 16 floats = 512 float4 (1 per thread); B: 256 x 16 = 1024
@@ -361,8 +363,11 @@ struct BImageBatch {
 // k step s, plane q, lane half h and output o: 8 bf16 of W_out[o][c], c = 64 wn + 32 j + 4 h + (t & 3) +
 // 8 (2 s + (t >> 2)), t < 8 -- the columns lane half h of the C^T epilogue holds in registers 8 s .. 8 s + 7.
 // Unit (16 B) index ((((wn * 2 + j) * 2 + s) * 3 + q) * 2 + h) * 32 + o; zero for o >= rows, c >= depth.
-constexpr int kOutImageUnits = 4 * 2 * 2 * 3 * 2 * 32;
+// Followed by the same weights in fp32 for the VALU path (<= 4 outputs): 8 floats per (wn, j, s, h, o) at
+// unit kOutImagePlaneUnits + 2 ((((wn * 2 + j) * 2 + s) * 2 + h) * 32 + o).
+constexpr int kOutImagePlaneUnits = 4 * 2 * 2 * 3 * 2 * 32;
 constexpr int kOutImageThreads = 4 * 2 * 2 * 2 * 32;
+constexpr int kOutImageUnits = kOutImagePlaneUnits + 2 * kOutImageThreads;
 
 __device__ __forceinline__ void out_image_thread(const rslrl_bimage_desc_t& dsc, int id) {
     if (id >= kOutImageThreads) return;
@@ -380,6 +385,9 @@ __device__ __forceinline__ void out_image_thread(const rslrl_bimage_desc_t& dsc,
 #pragma unroll
     for (int q = 0; q < 3; ++q)
         img[((((wn * 2 + j) * 2 + s) * 3 + q) * 2 + h) * 32 + o] = make_uint4(lo[q].x, lo[q].y, hi[q].x, hi[q].y);
+    float4* f = reinterpret_cast<float4*>(img + kOutImagePlaneUnits) + 2 * id;
+    f[0] = make_float4(v[0], v[1], v[2], v[3]);
+    f[1] = make_float4(v[4], v[5], v[6], v[7]);
 }
 
 __global__ __launch_bounds__(kBlock) void bimage_kernel(BImageBatch batch) {
@@ -598,13 +606,21 @@ __global__ __launch_bounds__(kThreads, MINW) void mlp_gemm_x6_kernel(GemmParams 
         // 2 k steps of 16 per 32-column tile (lane half h carries columns {0-3, 8-11} + 4 h, then
         // {16-19, 24-27} + 4 h; the image orders the weight the same way).  The four wn waves' partial
         // Y' tiles are added in a fixed order through LDS.
-        float* red = reinterpret_cast<float*>(&lds[0][0]);  // [wm][wn][i][32 o][32 rows] fp32 = 64 KiB
+        // h leaves through a per-wave LDS stage (32 x 32 floats, float4 quads XOR-swizzled by (row >> 1) & 7):
+        // written as the C^T quads, read back as 8 rows x 128 B per instruction -> whole-line stores (direct
+        // C^T stores write 32-B pieces: +48 us per launch at M = 393216).  red: [wm][wn][i][o][32 rows].
+        const bool staged = p.c != nullptr && p.nout <= kStagedOutWidth;
+        const int red_rows = staged ? kStagedOutWidth : 32;
+        float* stage = reinterpret_cast<float*>(&lds[0][0]) + wave * 1024;
+        float* red = reinterpret_cast<float*>(&lds[0][0]) + (staged ? 8 * 1024 : 0);
         const uint4* oimg = p.oimg + wn * (2 * 2 * 3 * 64);
+        const bool valu = p.nout <= 4;  // the critic's value head: VALU dot products beat 32-row MFMA tiles
 #pragma unroll
         for (int i = 0; i < I; ++i) {
             const int64_t row = row0 + wm * (BM / 2) + i * 32 + l32;
             const bool row_ok = row < p.M;
             f32x16 oacc = f32x16{};
+            float oval[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
                 const int cb = wn * 64 + j * 32 + 4 * h;
@@ -619,9 +635,46 @@ __global__ __launch_bounds__(kThreads, MINW) void mlp_gemm_x6_kernel(GemmParams 
                                   acc[i][j][4 * g + 3] + b4.w};
 #pragma unroll
                     for (int e = 0; e < 4; ++e) v[4 * g + e] = t[e] > 0.f ? t[e] : elu_neg(t[e]);
-                    if (p.c && row_ok && col_ok)
-                        *reinterpret_cast<float4*>(p.c + row * p.N + col) =
-                            make_float4(v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]);
+                    const f32x4 hv = {v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]};
+                    if (staged) {
+                        *reinterpret_cast<f32x4*>(stage + l32 * 32 + 4 * ((2 * g + h) ^ ((l32 >> 1) & 7))) = hv;
+                    } else if (p.c && row_ok && col_ok) {
+                        *reinterpret_cast<f32x4*>(p.c + row * p.N + col) = hv;
+                    }
+                }
+                if (staged) {
+                    __builtin_amdgcn_wave_barrier();  // one wave's LDS accesses execute in order
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const int sr = 8 * k + (lane >> 3);
+                        const int cq = lane & 7;
+                        const f32x4 hv = *reinterpret_cast<const f32x4*>(stage + sr * 32 + 4 * (cq ^ ((sr >> 1) & 7)));
+                        const int64_t grow = row0 + wm * (BM / 2) + i * 32 + sr;
+                        const int gcol = wn * 64 + j * 32 + 4 * cq;
+                        if (grow < p.M && gcol < p.N) {
+                            f32x4* dst = reinterpret_cast<f32x4*>(p.c + grow * p.N + gcol);
+                            if (p.nt) __builtin_nontemporal_store(hv, dst);
+                            else *dst = hv;
+                        }
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                }
+                if (valu) {
+                    // <= 4 outputs: fp32 FMA chains over the lane's 16 columns (the image's fp32 copy)
+                    const float4* wf = reinterpret_cast<const float4*>(p.oimg + kOutImagePlaneUnits) +
+                                       2 * ((((wn * 2 + j) * 2) * 2 + h) * 32);
+#pragma unroll
+                    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+                        for (int o = 0; o < 4; ++o) {
+                            if (o >= p.nout) break;
+                            const float4* q = wf + 2 * (s2 * 64 + o);
+                            const float4 w0 = q[0], w1 = q[1];
+                            const float w[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+#pragma unroll
+                            for (int t = 0; t < 8; ++t) oval[o] = fmaf(v[8 * s2 + t], w[t], oval[o]);
+                        }
+                    continue;
                 }
 #pragma unroll
                 for (int s2 = 0; s2 < 2; ++s2) {
@@ -638,17 +691,29 @@ __global__ __launch_bounds__(kThreads, MINW) void mlp_gemm_x6_kernel(GemmParams 
                     oacc = mfma_x6(wa, vb, oacc);
                 }
             }
-            float* rd = red + ((wm * 4 + wn) * I + i) * 1024;
+            float* rd = red + ((wm * 4 + wn) * I + i) * red_rows * 32;
+            if (valu) {  // the two lane halves hold different columns of the same row
 #pragma unroll
-            for (int r = 0; r < 16; ++r) rd[((r & 3) + 8 * (r >> 2) + 4 * h) * 32 + l32] = oacc[r];
+                for (int o = 0; o < 4; ++o) {
+                    const float t = oval[o] + __shfl_xor(oval[o], 32, 64);
+                    if (h == 0 && o < p.nout) rd[o * 32 + l32] = t;
+                }
+            } else {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int o = (r & 3) + 8 * (r >> 2) + 4 * h;
+                    if (o < red_rows) rd[o * 32 + l32] = oacc[r];
+                }
+            }
         }
         __syncthreads();
         const int nout = p.nout;
         for (int idx = threadIdx.x; idx < BM * nout; idx += kThreads) {
             const int rl = idx / nout;
             const int o = idx - rl * nout;
-            const float* b = red + (((rl >> 6) * 4) * I + ((rl & 63) >> 5)) * 1024 + o * 32 + (rl & 31);
-            const float sum = ((b[0] + b[I * 1024]) + b[2 * I * 1024]) + b[3 * I * 1024];
+            const int tile = red_rows * 32;
+            const float* b = red + (((rl >> 6) * 4) * I + ((rl & 63) >> 5)) * tile + o * 32 + (rl & 31);
+            const float sum = ((b[0] + b[I * tile]) + b[2 * I * tile]) + b[3 * I * tile];
             const int64_t row = row0 + rl;
             if (row < p.M) p.y[row * nout + o] = sum + p.obias[o];
         }
@@ -699,8 +764,6 @@ __global__ __launch_bounds__(kThreads, MINW) void mlp_gemm_x6_kernel(GemmParams 
 // The MFMAs take the weight fragment as their A operand and the activation fragment as B, so they
 // produce C^T tiles: lane l holds row (l & 15) of its 16-row block and the four consecutive columns
 // 4 (l >> 4) .. +3 of its 16-column block -> 16-byte stores and h loads in the epilogue.  Wave tile 64 x 64.
-using f32x4 = __attribute__((ext_vector_type(4))) float;
-
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 
 template <int EPI, bool FULLT, bool NT>
@@ -926,6 +989,14 @@ bool launch_x6s(const GemmParams& p, const uint4* img, bool fullm, dim3 g, hipSt
     }
 }
 
+int out_fwd_nt() {  // tuning knob: RSLRL_OUT_FWD_NT=0|1
+    static const int v = [] {
+        const char* e = std::getenv("RSLRL_OUT_FWD_NT");
+        return (e && std::atoi(e) == 1) ? 1 : 0;
+    }();
+    return v;
+}
+
 int out_fwd_occupancy() {  // tuning knob: RSLRL_OUT_FWD_OCC=2|4 (default 4)
     static const int v = [] {
         const char* e = std::getenv("RSLRL_OUT_FWD_OCC");
@@ -1079,7 +1150,7 @@ extern "C" int rslrl_linear_fwd_out(const float* x, int64_t M, int32_t K, const 
     if (!aligned16(x) || !aligned16(bias) || !aligned16(bimage) || !aligned16(out_image) || (h_out && !aligned16(h_out)))
         return RSLRL_E_MISALIGNED;
     GemmParams p{x, nullptr, bias, nullptr, h_out, nullptr, M, K, N, 0, nullptr,
-                 static_cast<const uint4*>(out_image), out_bias, y, Nout};
+                 static_cast<const uint4*>(out_image), out_bias, y, Nout, out_fwd_nt()};
     return launch<kEpiBiasEluOut>(p, bimage, reinterpret_cast<hipStream_t>(stream));
 }
 
