@@ -1,17 +1,19 @@
-"""Actor/critic MLP forward + backward on the fused fp32 MFMA GEMMs.
+"""Actor/critic MLP forward + backward on fused MFMA GEMMs.
 
 For an `MLP` of Linear(+ELU) hidden blocks and a final Linear (rsl_rl/networks/mlp.py:59-114) this
 autograd Function runs
 
-    forward   H_l = ELU(H_{l-1} W_l^T + b_l)    one rslrl_linear_fwd launch per hidden layer
-              Y   = H_{L-1} W_L^T + b_L         F.linear (the 1-12 wide output layer suits hipBLASLt)
-    backward  dW_l = dZ_l^T H_{l-1}             split-K batched GEMM (networks/linear.py)
+    forward   H_l = ELU(H_{l-1} W_l^T + b_l)    one rslrl_linear_fwd launch per hidden layer; the last one
+              Y   = H_{L-1} W_L^T + b_L         also computes the (<= 32 wide) output layer from its
+                                                register tile (rslrl_linear_fwd_out)
+    backward  dW_l = dZ_l^T H_{l-1}             x6 split-K weight-gradient kernel (rslrl_linear_wgrad)
               dZ_{l-1} = (dZ_l W_l) * ELU'(H_{l-1}) and db_{l-1} = column sums of dZ_{l-1}
-                                                one rslrl_linear_dgrad_elu launch (+ a tiny fold)
+                                                one rslrl_linear_dgrad_elu launch (+ a tiny fold); for the
+                                                output layer together with its dW (rslrl_linear_dgrad_elu_wgrad)
 
 so the pre-activations and dH never reach HBM and the separate ELU / ELU-backward / bias-reduction
 kernels disappear.  Parameters, state_dict and the forward values are those of the nn.Sequential (the
-fp32 MFMA accumulation order differs from hipBLASLt's at fp32 epsilon; tests/test_gpu_fused_mlp.py).
+MFMA accumulation order differs from hipBLASLt's at fp32 epsilon; tests/test_gpu_fused_mlp.py).
 """
 
 from __future__ import annotations
