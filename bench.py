@@ -100,8 +100,8 @@ def cpu_baseline(args):
 
     threads = min(16, len(os.sched_getaffinity(0)))
     n = args.cpu_sample_envs
-    rate, secs = cpu_ppo.time_iterations(n, args.num_obs, args.num_actions, T=args.num_steps_per_env, iters=1,
-                                         warmup=1, threads=threads)
+    rate, secs, parts = cpu_ppo.time_iterations(n, args.num_obs, args.num_actions, T=args.num_steps_per_env,
+                                                iters=1, warmup=1, threads=threads, detail=True)
     model = ""
     try:
         with open("/proc/cpuinfo") as f:
@@ -113,6 +113,9 @@ def cpu_baseline(args):
         "unit": "env-steps/s",
         "cores": threads,
         "kind": "port",
+        # hot path (GAE + shuffle/gathers + loss) and update phase timed apart as well
+        "hot_path_env_steps_per_s": round(parts["hot_path"], 1),
+        "update_env_steps_per_s": round(parts["update"], 1),
         "sample": f"1 timed PPO iteration (+1 warmup) of the CPU oracle (oracle/cpu_ppo.py: torch-CPU MLPs + "
                   f"oracle GAE/randperm/gather/loss) at N={n} envs, T={args.num_steps_per_env}, obs {args.num_obs}, "
                   f"act {args.num_actions}, 3x256 MLP; {secs:.1f} s timed; {threads} threads; CPU: {model}",
@@ -253,6 +256,8 @@ def main():
         "hot_path": {"kernels": hot, "ms_per_step": round(hot_ms, 4),
                      "env_steps_per_s": round(T * N / (hot_ms * 1e-3), 1) if hot_ms else None},
         "phases_last_iter": {k: round(v, 4) for k, v in runner.last_iteration_stats.items() if k != "loss_dict"},
+        # end-to-end (value), update phase and hot path (above) reported apart
+        "update_env_steps_per_s": round(T * N * world / runner.last_iteration_stats["learn_time"], 1),
         "cpu_baseline": None,
     }
     if world == 1 and not args.no_extra:

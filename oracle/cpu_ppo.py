@@ -80,6 +80,7 @@ class CpuPPO:
 
     def update(self, buf, last_v):
         hp = self.hp
+        t0 = time.perf_counter()
         ret, adv = O.compute_returns(buf["values"], buf["rewards"], buf["dones"], last_v, hp["gamma"], hp["lam"])
         fields = {"obs": buf["obs"], "actions": buf["actions"], "values": buf["values"][..., None],
                   "advantages": adv[..., None], "returns": ret[..., None], "logp": buf["logp"][..., None],
@@ -87,14 +88,24 @@ class CpuPPO:
         perm, mb, new_state = O.minibatch_indices(self.N, self.T, self.M, torch.default_generator.get_state().numpy())
         torch.default_generator.set_state(torch.from_numpy(new_state))
         sums = np.zeros(3)
-        for b in O.minibatches(fields, perm, mb, self.M, self.E):
+        # hot path (GAE, shuffle + gathers, fused loss) timed apart from the MLPs / optimizer
+        hot = time.perf_counter() - t0
+        batches = O.minibatches(fields, perm, mb, self.M, self.E)
+        while True:
+            t0 = time.perf_counter()
+            b = next(batches, None)
+            hot += time.perf_counter() - t0
+            if b is None:
+                break
             obs = torch.from_numpy(b["obs"])
             mean = self.actor(obs)
             value = self.critic(obs)
+            t0 = time.perf_counter()
             out = O.ppo_loss(mean.detach().numpy(), np.broadcast_to(self.std.detach().numpy(), mean.shape),
                              value.detach().numpy(), b["actions"], b["logp"], b["advantages"], b["values"],
                              b["returns"], b["mu"], b["sigma"], clip_param=hp["clip"],
                              value_loss_coef=hp["value_coef"], entropy_coef=hp["entropy_coef"])
+            hot += time.perf_counter() - t0
             kl = out["kl_mean"]
             if kl > hp["desired_kl"] * 2.0:
                 self.lr = max(1e-5, self.lr / 1.5)
@@ -110,6 +121,7 @@ class CpuPPO:
             self.opt.step()
             sums += (out["value_function"], out["surrogate"], out["entropy"])
         n = self.E * self.M
+        self.hot_path_seconds = hot
         return {"value_function": sums[0] / n, "surrogate": sums[1] / n, "entropy": sums[2] / n}
 
     def iteration(self):
@@ -117,15 +129,25 @@ class CpuPPO:
         return self.update(buf, last_v)
 
 
-def time_iterations(num_envs, num_obs=48, num_actions=12, T=24, iters=1, warmup=1, threads=None):
-    """env-steps/s of `iters` full CPU iterations after `warmup` ones."""
+def time_iterations(num_envs, num_obs=48, num_actions=12, T=24, iters=1, warmup=1, threads=None, detail=False):
+    """env-steps/s of `iters` full CPU iterations after `warmup` ones (detail: also the hot-path-only rate,
+    GAE + shuffle/gathers + loss, and the update-phase rate)."""
     if threads:
         torch.set_num_threads(threads)
     ppo = CpuPPO(num_envs, num_obs, num_actions, T=T)
     for _ in range(warmup):
         ppo.iteration()
+    hot = upd = 0.0
     t0 = time.perf_counter()
     for _ in range(iters):
-        ppo.iteration()
+        buf, last_v = ppo.rollout()
+        t1 = time.perf_counter()
+        ppo.update(buf, last_v)
+        upd += time.perf_counter() - t1
+        hot += ppo.hot_path_seconds
     dt = time.perf_counter() - t0
-    return num_envs * T * iters / dt, dt
+    steps = num_envs * T * iters
+    if detail:
+        return steps / dt, dt, {"hot_path": steps / hot, "update": steps / upd, "hot_path_seconds": hot,
+                                "update_seconds": upd}
+    return steps / dt, dt
