@@ -16,7 +16,7 @@ inline int launch_status() {
     return e == hipSuccess ? RSLRL_OK : static_cast<int>(e);
 }
 
-inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+__host__ __device__ inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 

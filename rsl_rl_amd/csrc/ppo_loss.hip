@@ -15,7 +15,9 @@
 // Bytes per sample (sigma shared): read 4A (mu) + 4A (actions) + 8A (old mu, sigma) + 20 (old_logp,
 // adv, target V, returns, V), write 4A (d mu) + 4 (d V) = 20A + 24.
 
+#include <algorithm>
 #include <cstdlib>
+#include <string>
 
 #include "common.h"
 
@@ -350,6 +352,458 @@ __global__ __launch_bounds__(kBlock) void ppo_loss_kernel(LossParams p, double* 
     }
 }
 
+// ---- quad layout (A % 4 == 0, A <= 16): four lanes per sample ------------------------------------
+//
+// The lane-per-sample kernel above holds whole [A] rows per lane (182 VGPRs at A = 12: two waves per
+// SIMD) and each of its row loads covers 64 rows at a 48-byte stride.  Here a wave owns a tile of 64
+// samples and works on it in two layouts:
+//   row layout    (4 rounds of 16 samples): lane l holds actions [APL*(l&3), APL*(l&3)+APL) of sample
+//                 16*round + (l>>2) -- every row load / gradient store of a round is one contiguous
+//                 16*A*4-byte segment, and every per-action transcendental (KL log, division) is
+//                 evaluated once;
+//   sample layout (lane l = sample l): ratio, clipped surrogate, clipped value loss, their gradients,
+//                 coalesced scalar loads and the d/dV store.
+// log-prob partials are summed inside each quad (two DPP adds) and moved to the sample layout with
+// four ds_bpermute; d(loss)/d(log-prob) moves back the same way.  Per-element arithmetic is the same
+// expression sequence as the lane-per-sample kernel; only the summation order of the A log-prob terms
+// (three sequential, then a quad tree) and of the KL terms differs.
+//
+// Partials fold in two levels so that the grid can cover one tile per wave: groups of kFoldGroup
+// blocks (last arriver of a group folds the group, fixed order), then the last group folds the groups.
+
+constexpr int kFoldGroup = 64;
+constexpr int kQuadMaxBlocks = 256;  // one workgroup per CU; 6 tiles per wave at C3 (measured: 256 < 512 < 768 us)
+
+using rsrc_t = __amdgpu_buffer_rsrc_t;
+
+// Buffer resource over `bytes` bytes: loads past the end return 0 and stores past it are dropped, so
+// the tail tile needs no per-lane guards on its memory operations (only on what it accumulates).
+__device__ __forceinline__ rsrc_t make_rsrc(const void* ptr, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(ptr), 0, static_cast<int>(bytes), 0x00020000);
+}
+
+// APL consecutive fp32 values at byte offset `off` (dword-aligned; 16-/8-byte aligned for APL 4 / 2).
+// Elements are copied out as values first: hipcc 7.2 lowers __builtin_bit_cast of a vector-element
+// lvalue (x[k]) to a read of element 0.
+template <int APL>
+__device__ __forceinline__ void load_piece(rsrc_t r, uint32_t off, float (&v)[APL]) {
+    if constexpr (APL == 4) {
+        const auto x = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = __builtin_bit_cast(float, static_cast<unsigned>(x[k]));
+    } else if constexpr (APL == 3) {
+        const auto x = __builtin_amdgcn_raw_buffer_load_b96(r, off, 0, 0);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) v[k] = __builtin_bit_cast(float, static_cast<unsigned>(x[k]));
+    } else if constexpr (APL == 2) {
+        const auto x = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
+#pragma unroll
+        for (int k = 0; k < 2; ++k) v[k] = __builtin_bit_cast(float, static_cast<unsigned>(x[k]));
+    } else {
+        v[0] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+    }
+}
+
+template <int APL>
+__device__ __forceinline__ void store_piece(rsrc_t r, uint32_t off, const float (&v)[APL]) {
+    using u = unsigned int;
+    if constexpr (APL == 4) {
+        __attribute__((ext_vector_type(4))) u x;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) x[k] = __builtin_bit_cast(u, v[k]);
+        __builtin_amdgcn_raw_buffer_store_b128(x, r, off, 0, 0);
+    } else if constexpr (APL == 3) {
+        __attribute__((ext_vector_type(3))) u x;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) x[k] = __builtin_bit_cast(u, v[k]);
+        __builtin_amdgcn_raw_buffer_store_b96(x, r, off, 0, 0);
+    } else if constexpr (APL == 2) {
+        __attribute__((ext_vector_type(2))) u x;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) x[k] = __builtin_bit_cast(u, v[k]);
+        __builtin_amdgcn_raw_buffer_store_b64(x, r, off, 0, 0);
+    } else {
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(u, v[0]), r, off, 0, 0);
+    }
+}
+
+__device__ __forceinline__ float load_f32(rsrc_t r, uint32_t off) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+}
+
+// Sum over the 4 lanes of a quad (DPP quad_perm [1,0,3,2] then [2,3,0,1]); every lane of the quad
+// gets the same bits ((v0 + v1) + (v2 + v3), fp addition being commutative).
+__device__ __forceinline__ float quad_sum(float v) {
+    const float a = __fadd_rn(v, __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xB1,
+                                                                                      0xF, 0xF, false)));
+    return __fadd_rn(a, __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, a), 0x4E, 0xF,
+                                                                             0xF, false)));
+}
+
+// Fixed-order fold of `n` (<= 64) partials per column (column c at src[c * ld + r]) into out[c]:
+// 16 lanes per column, each adding rows l16, l16+16, l16+32, l16+48 in that order, then a 16-lane
+// butterfly.  Every load is issued before the first add, so the fold costs one memory round trip.
+// Loads use sc1 (bypass the non-coherent per-CU cache); the caller has acquired.
+template <int kMaxC>
+__device__ __forceinline__ void fold_columns(const double* __restrict__ src, int ld, int n, int ncols,
+                                             double* __restrict__ out) {
+    constexpr int kPasses = (kMaxC + 15) / 16;
+    const int l16 = threadIdx.x & 15;
+    const int cc = threadIdx.x >> 4;
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<double*>(src), 0, static_cast<int>(sizeof(double) * ncols * ld), 0x00020000);
+    double v[kPasses][4];
+#pragma unroll
+    for (int ps = 0; ps < kPasses; ++ps) {
+        const int c = ps * 16 + cc;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int r = l16 + 16 * i;
+            // out-of-range offsets read 0 through the buffer resource
+            const int off = (c < ncols && r < n) ? (c * ld + r) * 8 : 0x7ffffff0;
+            v[ps][i] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rsrc, off, 0, 16 /* sc1 */));
+        }
+    }
+#pragma unroll
+    for (int ps = 0; ps < kPasses; ++ps) {
+        double t = ((v[ps][0] + v[ps][1]) + v[ps][2]) + v[ps][3];
+#pragma unroll
+        for (int off = 8; off >= 1; off >>= 1) t += __shfl_xor(t, off, kWave);
+        const int c = ps * 16 + cc;
+        if (l16 == 0 && c < ncols) out[c] = t;
+    }
+}
+
+// Waves per SIMD the register budget is sized for (no spills at these bounds, hipcc 7.2): two tiles
+// (current + prefetched) of row pieces live per lane.
+constexpr int quad_waves(int apl, bool shared, bool kl) { return (apl == 1 && (shared || !kl)) ? 4 : 2; }
+
+template <int APL, bool SHARED, bool KL>
+__global__ __launch_bounds__(kBlock, quad_waves(APL, SHARED, KL)) void ppo_loss_quad_kernel(LossParams p, double* __restrict__ partials,
+                                                               unsigned* __restrict__ tickets, float value_loss_coef,
+                                                               float entropy_coef) {
+    constexpr int A = 4 * APL;
+    constexpr int kCols = kNumScalarCols + (SHARED ? A : 0);
+    __shared__ double wave_part[kBlock / kWave][kCols];
+    __shared__ double folded[kCols];
+    __shared__ int last_flag;
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wid = threadIdx.x / kWave;
+    const int q = lane & 3;
+    const int s16 = lane >> 2;
+    const int a0 = q * APL;
+
+    float c_s[APL], c_ls[APL], c_inv_den[APL], c_inv_s[APL], c_inv_s3[APL];
+    float ent_shared = 0.0f;
+    if constexpr (SHARED) {
+#pragma unroll
+        for (int k = 0; k < APL; ++k) {
+            const float s = p.sigma[a0 + k];
+            const float inv_s = 1.0f / s;
+            c_s[k] = s;
+            c_ls[k] = logf(s);
+            c_inv_den[k] = 1.0f / __fmul_rn(2.0f, __fmul_rn(s, s));
+            c_inv_s[k] = inv_s;
+            c_inv_s3[k] = inv_s * inv_s * inv_s;
+        }
+#pragma unroll
+        for (int a = 0; a < A; ++a) ent_shared = __fadd_rn(ent_shared, __fadd_rn(kEntC, logf(p.sigma[a])));
+    }
+    float adv_mean = 0.0f, adv_den = 1.0f;
+    if (p.normalize_adv) {
+        adv_mean = p.adv_stats[0];
+        adv_den = __fadd_rn(p.adv_stats[1], 1e-8f);  // ppo.py:223  (std + 1e-8)
+    }
+
+    float acc_surr = 0.0f, acc_value = 0.0f, acc_ent = 0.0f, acc_kl = 0.0f;
+    float acc_sig[APL];
+#pragma unroll
+    for (int k = 0; k < APL; ++k) acc_sig[k] = 0.0f;
+
+    // Buffer resources (byte extents < 2^31, checked by the host): rows of [B, A] operands share one
+    // 32-bit offset per round; mu / grad_mu / sigma rows use their own strides.
+    const uint32_t B32 = static_cast<uint32_t>(p.B);
+    const uint32_t rowA = static_cast<uint32_t>(A) * 4u;
+    const auto ext = [&](int64_t stride) { return static_cast<uint32_t>(((p.B - 1) * stride + A) * 4); };
+    const rsrc_t r_mu = make_rsrc(p.mu, ext(p.mu_stride));
+    const rsrc_t r_x = make_rsrc(p.actions, B32 * rowA);
+    const rsrc_t r_omu = make_rsrc(p.old_mu, B32 * rowA);
+    const rsrc_t r_osg = make_rsrc(p.old_sigma, B32 * rowA);
+    const rsrc_t r_sg = make_rsrc(p.sigma, SHARED ? rowA : ext(p.sigma_stride));
+    const rsrc_t r_gmu = make_rsrc(p.grad_mu, ext(p.grad_mu_stride));
+    const rsrc_t r_gsg = make_rsrc(p.grad_sigma, SHARED ? rowA : ext(p.grad_sigma_stride));
+    const rsrc_t r_ologp = make_rsrc(p.old_logp, B32 * 4u);
+    const rsrc_t r_adv = make_rsrc(p.adv, B32 * 4u);
+    const rsrc_t r_v = make_rsrc(p.values, B32 * 4u);
+    const rsrc_t r_tv = make_rsrc(p.target_values, B32 * 4u);
+    const rsrc_t r_ret = make_rsrc(p.returns, B32 * 4u);
+    const rsrc_t r_gv = make_rsrc(p.grad_values, B32 * 4u);
+    const uint32_t mu_row = static_cast<uint32_t>(p.mu_stride) * 4u;
+    const uint32_t gmu_row = static_cast<uint32_t>(p.grad_mu_stride) * 4u;
+    const uint32_t sg_row = static_cast<uint32_t>(p.sigma_stride) * 4u;
+    const uint32_t gsg_row = static_cast<uint32_t>(p.grad_sigma_stride) * 4u;
+    const uint32_t piece = static_cast<uint32_t>(a0) * 4u;
+
+    const uint32_t ntiles = static_cast<uint32_t>(ceil_div(p.B, kWave));
+    const uint32_t tstride = gridDim.x * (kBlock / kWave);
+    // Software pipeline over this wave's tiles: the next tile's loads are issued before the current
+    // tile is computed, so each wave keeps one tile (~13.5 KB at A = 12) in flight while it computes.
+    // A tile index past the end loads zeros through the buffer resources and is never computed.
+    struct TileIn {
+        float old_logp, adv, V, tv, R;
+        float mu[4][APL], x[4][APL], omu[4][APL], osg[4][APL], sr[4][APL];
+    };
+    const auto load_tile = [&](uint32_t tile, TileIn& t) {
+        const uint32_t base = tile * kWave;
+        const uint32_t is = base + lane;
+        t.old_logp = load_f32(r_ologp, is * 4u);
+        t.adv = load_f32(r_adv, is * 4u);
+        t.V = load_f32(r_v, is * 4u);
+        t.tv = load_f32(r_tv, is * 4u);
+        t.R = load_f32(r_ret, is * 4u);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t iq = base + 16 * j + s16;
+            load_piece<APL>(r_mu, iq * mu_row + piece, t.mu[j]);
+            load_piece<APL>(r_x, iq * rowA + piece, t.x[j]);
+            if constexpr (KL) {
+                load_piece<APL>(r_omu, iq * rowA + piece, t.omu[j]);
+                load_piece<APL>(r_osg, iq * rowA + piece, t.osg[j]);
+            }
+            if constexpr (!SHARED) load_piece<APL>(r_sg, iq * sg_row + piece, t.sr[j]);
+        }
+    };
+    uint32_t tile = blockIdx.x * (kBlock / kWave) + wid;
+    TileIn cur;
+    if (tile < ntiles) load_tile(tile, cur);
+    for (; tile < ntiles; tile += tstride) {
+        TileIn nxt;
+        load_tile(tile + tstride, nxt);
+        const uint32_t base = tile * kWave;
+        const uint32_t is = base + lane;
+        const bool vs = is < B32;
+        const float old_logp = cur.old_logp, V = cur.V, tv = cur.tv, R = cur.R;
+        float adv = cur.adv;
+        const auto& mu = cur.mu;
+        const auto& x = cur.x;
+        const auto& omu = cur.omu;
+        const auto& osg = cur.osg;
+        const auto& sr = cur.sr;
+
+        float d[4][APL], lp[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const bool vq = base + 16 * j + s16 < B32;
+            float lpart = 0.0f, klpart = 0.0f, entpart = 0.0f;
+#pragma unroll
+            for (int k = 0; k < APL; ++k) {
+                float s, ls, inv_den;
+                if constexpr (SHARED) {
+                    s = c_s[k];
+                    ls = c_ls[k];
+                    inv_den = c_inv_den[k];
+                } else {
+                    s = sr[j][k];
+                    ls = logf(s);
+                    inv_den = 1.0f / (2.0f * s * s);
+                    entpart += kEntC + ls;
+                }
+                const float dd = x[j][k] - mu[j][k];
+                d[j][k] = dd;
+                lpart += (-(dd * dd) * inv_den - ls) - kLogSqrt2Pi;
+                if constexpr (KL) {
+                    const float os = osg[j][k];
+                    const float dm = __fsub_rn(omu[j][k], mu[j][k]);
+                    const float t1 = logf(__fadd_rn(__fdiv_rn(s, os), 1.0e-5f));
+                    const float t2 = __fdiv_rn(__fadd_rn(__fmul_rn(os, os), __fmul_rn(dm, dm)),
+                                               __fmul_rn(2.0f, __fmul_rn(s, s)));
+                    klpart = __fadd_rn(klpart, __fsub_rn(__fadd_rn(t1, t2), 0.5f));
+                }
+            }
+            if (vq) {
+                acc_kl += klpart;
+                if constexpr (!SHARED) acc_ent += entpart;
+            }
+            lp[j] = quad_sum(lpart);
+        }
+
+        // ---- sample layout: lane l <- log-prob of sample base + l (quad l & 15 of round l >> 4)
+        const int src = (lane & 15) << 2;
+        const float l0 = __shfl(lp[0], src, kWave), l1 = __shfl(lp[1], src, kWave);
+        const float l2 = __shfl(lp[2], src, kWave), l3 = __shfl(lp[3], src, kWave);
+        const int rnd = lane >> 4;
+        const float logp = rnd == 0 ? l0 : (rnd == 1 ? l1 : (rnd == 2 ? l2 : l3));
+        // (lanes past B compute on zero-filled inputs; their results are masked here and their d/dV
+        // store is dropped by the buffer resource -- no branch, so the scalar loads issue with the rows)
+        if (p.normalize_adv) adv = __fdiv_rn(__fsub_rn(adv, adv_mean), adv_den);
+        // surrogate (ppo.py:297-302)
+        const float ratio = expf(logp - old_logp);
+        const float nadv = -adv;
+        const float surr = nadv * ratio;
+        const float rc = fminf(fmaxf(ratio, p.ratio_lo), p.ratio_hi);
+        const float surr_c = nadv * rc;
+        float g_s, g_sc;
+        max_grads(surr, surr_c, p.g_surr, g_s, g_sc);
+        const bool in_clip = (ratio >= p.ratio_lo) && (ratio <= p.ratio_hi);
+        const float g_ratio = g_s * nadv + (in_clip ? g_sc * nadv : 0.0f);
+        const float g_logp = vs ? g_ratio * ratio : 0.0f;
+        // value loss (ppo.py:305-313)
+        float vterm, dV;
+        if (p.clipped_value) {
+            const float dv = V - tv;
+            const float vc = tv + fminf(fmaxf(dv, -p.clip), p.clip);
+            const float e1 = V - R;
+            const float e2 = vc - R;
+            const float vl = e1 * e1;
+            const float vlc = e2 * e2;
+            vterm = fmaxf(vl, vlc);
+            float g1, g2;
+            max_grads(vl, vlc, p.g_value, g1, g2);
+            dV = 2.0f * g1 * e1;
+            if (dv >= -p.clip && dv <= p.clip) dV += 2.0f * g2 * e2;
+        } else {
+            const float e = R - V;
+            vterm = e * e;
+            dV = -2.0f * p.g_value * e;
+        }
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, dV), r_gv, is * 4u, 0, 0);
+        if (vs) {
+            acc_surr += fmaxf(surr, surr_c);
+            acc_value += vterm;
+            if constexpr (SHARED) acc_ent += ent_shared;
+        }
+
+        // ---- row layout again: d/dmu, d/dsigma from d(loss)/d(log-prob) of each round's sample
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const float gj = __shfl(g_logp, 16 * j + s16, kWave);
+            const uint32_t iq = base + 16 * j + s16;
+            float gmu[APL], gsg[APL];
+            const float g2 = 2.0f * gj;
+#pragma unroll
+            for (int k = 0; k < APL; ++k) {
+                float inv_den, inv_s, inv_s3;
+                if constexpr (SHARED) {
+                    inv_den = c_inv_den[k];
+                    inv_s = c_inv_s[k];
+                    inv_s3 = c_inv_s3[k];
+                } else {
+                    const float s = sr[j][k];
+                    inv_s = 1.0f / s;
+                    inv_den = 0.5f * inv_s * inv_s;
+                    inv_s3 = inv_s * inv_s * inv_s;
+                }
+                const float dd = d[j][k];
+                gmu[k] = g2 * dd * inv_den;
+                gsg[k] = gj * (dd * dd * inv_s3 - inv_s) + p.g_ent * inv_s;
+            }
+            store_piece<APL>(r_gmu, iq * gmu_row + piece, gmu);  // past B: dropped by the resource
+            if constexpr (SHARED) {
+                const bool vq = iq < B32;
+#pragma unroll
+                for (int k = 0; k < APL; ++k) acc_sig[k] += vq ? gsg[k] : 0.0f;
+            } else {
+                store_piece<APL>(r_gsg, iq * gsg_row + piece, gsg);
+            }
+        }
+        cur = nxt;
+    }
+
+    // ---- block partials: scalar columns by wave butterfly; sigma columns over lanes of equal q
+    {
+        const double vs_[kNumScalarCols] = {wave_sum(static_cast<double>(acc_surr)),
+                                             wave_sum(static_cast<double>(acc_value)),
+                                             wave_sum(static_cast<double>(acc_ent)),
+                                             wave_sum(static_cast<double>(acc_kl))};
+        if (lane == 0) {
+#pragma unroll
+            for (int c = 0; c < kNumScalarCols; ++c) wave_part[wid][c] = vs_[c];
+        }
+        if constexpr (SHARED) {
+#pragma unroll
+            for (int k = 0; k < APL; ++k) {
+                double v = static_cast<double>(acc_sig[k]);
+#pragma unroll
+                for (int off = 4; off < kWave; off <<= 1) v += __shfl_xor(v, off, kWave);
+                if (lane < 4) wave_part[wid][kNumScalarCols + a0 + k] = v;
+            }
+        }
+    }
+    __syncthreads();
+    const int nb = gridDim.x;
+    const int ng = static_cast<int>(ceil_div(nb, kFoldGroup));
+    double* gpart = partials + static_cast<int64_t>(kCols) * nb;  // [kCols][ng] group partials
+    if (threadIdx.x < kCols) {
+        double v = wave_part[0][threadIdx.x];
+#pragma unroll
+        for (int w = 1; w < kBlock / kWave; ++w) v += wave_part[w][threadIdx.x];
+        __hip_atomic_store(reinterpret_cast<unsigned long long*>(partials + static_cast<int64_t>(threadIdx.x) * nb +
+                                                                 blockIdx.x),
+                           __double_as_longlong(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    // level 1: the last arriver of this block's group folds the group's partials (fixed order)
+    const int g = blockIdx.x / kFoldGroup;
+    const int g0 = g * kFoldGroup;
+    const int gsz = min(kFoldGroup, nb - g0);
+    if (threadIdx.x == 0) {
+        const unsigned t = __hip_atomic_fetch_add(tickets + 1 + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = (t == static_cast<unsigned>(gsz) - 1);
+        if (last) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        last_flag = last;
+    }
+    __syncthreads();
+    if (!last_flag) return;
+    if (threadIdx.x == 0) __hip_atomic_store(tickets + 1 + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    fold_columns<kCols>(partials + g0, nb, gsz, kCols, folded);
+    __syncthreads();
+    if (ng > 1) {
+        if (threadIdx.x < kCols)
+            __hip_atomic_store(
+                reinterpret_cast<unsigned long long*>(gpart + static_cast<int64_t>(threadIdx.x) * ng + g),
+                __double_as_longlong(folded[threadIdx.x]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        // level 2: the last group folds the group partials
+        if (threadIdx.x == 0) {
+            const unsigned t = __hip_atomic_fetch_add(tickets, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int last = (t == static_cast<unsigned>(ng) - 1);
+            if (last) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            last_flag = last;
+        }
+        __syncthreads();
+        if (!last_flag) return;
+        fold_columns<kCols>(gpart, ng, ng, kCols, folded);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        const double Bd = static_cast<double>(p.B);
+        float* stats = p.stats;
+        stats[1] = static_cast<float>(folded[kColSurr] / Bd);
+        stats[2] = static_cast<float>(folded[kColValue] / Bd);
+        stats[3] = static_cast<float>(folded[kColEnt] / Bd);
+        stats[4] = static_cast<float>(folded[kColKl] / Bd);
+        stats[0] = __fsub_rn(__fadd_rn(stats[1], __fmul_rn(value_loss_coef, stats[2])),
+                             __fmul_rn(entropy_coef, stats[3]));
+        if (!p.normalize_adv) {
+            stats[5] = 0.0f;
+            stats[6] = 0.0f;
+        }
+        stats[7] = 0.0f;
+        __hip_atomic_store(tickets, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm (stream-ordered)
+    }
+    if constexpr (SHARED) {
+        if (threadIdx.x < A) p.grad_sigma[threadIdx.x] = static_cast<float>(folded[kNumScalarCols + threadIdx.x]);
+    }
+}
+
 // Per-mini-batch advantage statistics (ppo.py:221-223): moments -> (mean, unbiased std) in stats[5..6].
 __global__ __launch_bounds__(kBlock) void mb_moments_kernel(const float* __restrict__ x, int64_t n,
                                                             double2* __restrict__ partials) {
@@ -401,6 +855,39 @@ int loss_blocks(int64_t B) {
     return static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(ceil_div(B, kBlock), max_blocks())));
 }
 
+// Quad-layout grid: one 64-sample tile per wave up to kQuadMaxBlocks (RSLRL_LOSS_QUAD_MAX_BLOCKS overrides).
+int quad_blocks(int64_t B) {
+    static const int cap = [] {
+        const char* e = std::getenv("RSLRL_LOSS_QUAD_MAX_BLOCKS");
+        const int x = e ? std::atoi(e) : 0;
+        return x > 0 ? std::min(x, kFoldGroup * kFoldGroup) : kQuadMaxBlocks;
+    }();
+    return static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(ceil_div(B, kBlock), cap)));
+}
+
+// Kernel choice, read per call so tests can exercise both: RSLRL_LOSS_KERNEL=lane / quad forces one,
+// unset picks the quad kernel for a shared sigma (29 vs 32 us at C3) and the lane kernel for per-row
+// sigma (34 vs 36 us: the row layout's extra sigma stream costs more than it saves).
+bool use_quad(int sigma_mode) {
+    const char* e = std::getenv("RSLRL_LOSS_KERNEL");
+    if (e && std::string(e) == "lane") return false;
+    if (e && std::string(e) == "quad") return true;
+    return sigma_mode == 0;
+}
+
+template <int APL>
+void launch_quad(const LossParams& p, int nb, double* part, unsigned* tickets, float cv, float ce, hipStream_t st) {
+    const dim3 g(nb), b(kBlock);
+    if (p.sigma_mode == 0 && p.compute_kl)
+        hipLaunchKernelGGL((ppo_loss_quad_kernel<APL, true, true>), g, b, 0, st, p, part, tickets, cv, ce);
+    else if (p.sigma_mode == 0)
+        hipLaunchKernelGGL((ppo_loss_quad_kernel<APL, true, false>), g, b, 0, st, p, part, tickets, cv, ce);
+    else if (p.compute_kl)
+        hipLaunchKernelGGL((ppo_loss_quad_kernel<APL, false, true>), g, b, 0, st, p, part, tickets, cv, ce);
+    else
+        hipLaunchKernelGGL((ppo_loss_quad_kernel<APL, false, false>), g, b, 0, st, p, part, tickets, cv, ce);
+}
+
 template <int MAXA, bool EXACT>
 void launch_loss_exact(const LossParams& p, bool vec, int nb, double* part, unsigned* ticket, float cv, float ce,
                        hipStream_t st) {
@@ -425,8 +912,9 @@ void launch_loss(const LossParams& p, bool vec, int nb, double* part, unsigned* 
         launch_loss_exact<MAXA, false>(p, vec, nb, part, ticket, cv, ce, st);
 }
 
-// workspace layout: [ticket word | pad to 256 B][fp64 partials [cols][blocks] | pad][mini-batch moments]
-constexpr size_t kTicketBytes = 256;
+// workspace layout: [tickets: global word, then one per fold group | pad to 1 KiB]
+//                   [fp64 partials [cols][blocks], then group partials [cols][groups] | pad][mini-batch moments]
+constexpr size_t kTicketBytes = 1024;
 
 bool aligned16(const void* ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 15) == 0; }
 
@@ -437,8 +925,9 @@ using namespace rslrl;
 
 extern "C" size_t rslrl_ppo_loss_workspace_bytes(int64_t B, int32_t A) {
     const size_t cols = kNumScalarCols + static_cast<size_t>(A > 0 ? A : 0);
-    return kTicketBytes + align_up(sizeof(double) * cols * static_cast<size_t>(loss_blocks(B)), 256) +
-           sizeof(double2) * kMomentBlocks;
+    const size_t qb = static_cast<size_t>(quad_blocks(B));
+    const size_t slots = std::max(static_cast<size_t>(loss_blocks(B)), qb + static_cast<size_t>(ceil_div(qb, kFoldGroup)));
+    return kTicketBytes + align_up(sizeof(double) * cols * slots, 256) + sizeof(double2) * kMomentBlocks;
 }
 
 extern "C" int rslrl_ppo_loss_fwd_bwd(const rslrl_ppo_loss_args_t* a, void* workspace, size_t workspace_bytes,
@@ -458,10 +947,12 @@ extern "C" int rslrl_ppo_loss_fwd_bwd(const rslrl_ppo_loss_args_t* a, void* work
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     const int A = a->A;
     const int nb = loss_blocks(a->B);
+    const int nbq = quad_blocks(a->B);
+    const size_t slots = std::max<size_t>(nb, nbq + ceil_div(nbq, kFoldGroup));
     unsigned* ticket = static_cast<unsigned*>(workspace);
     double* part = reinterpret_cast<double*>(static_cast<char*>(workspace) + kTicketBytes);
     double2* mpart = reinterpret_cast<double2*>(static_cast<char*>(workspace) + kTicketBytes +
-                                                align_up(sizeof(double) * (kNumScalarCols + A) * nb, 256));
+                                                align_up(sizeof(double) * (kNumScalarCols + A) * slots, 256));
 
     LossParams p{};
     p.B = a->B;
@@ -512,6 +1003,18 @@ extern "C" int rslrl_ppo_loss_fwd_bwd(const rslrl_ppo_loss_args_t* a, void* work
         vec = vec && (a->sigma_stride % 4 == 0) && (a->grad_sigma_stride % 4 == 0) && aligned16(a->sigma) &&
               aligned16(a->grad_sigma);
     const float cv = a->value_loss_coef, ce = a->entropy_coef;
+    const int64_t max_row = std::max({a->mu_stride, a->grad_mu_stride, a->sigma_mode == 1 ? a->sigma_stride : 0,
+                                      a->sigma_mode == 1 ? a->grad_sigma_stride : 0, static_cast<int64_t>(A)});
+    const bool fits32 = a->B * max_row * 4 < (int64_t{1} << 31);  // 32-bit buffer offsets
+    if (vec && fits32 && A % 4 == 0 && A <= 16 && use_quad(a->sigma_mode)) {
+        switch (A / 4) {
+            case 1: launch_quad<1>(p, nbq, part, ticket, cv, ce, st); break;
+            case 2: launch_quad<2>(p, nbq, part, ticket, cv, ce, st); break;
+            case 3: launch_quad<3>(p, nbq, part, ticket, cv, ce, st); break;
+            default: launch_quad<4>(p, nbq, part, ticket, cv, ce, st); break;
+        }
+        return launch_status();
+    }
     if (A <= 4)
         launch_loss<4>(p, vec, nb, part, ticket, cv, ce, st);
     else if (A <= 8)

@@ -75,8 +75,13 @@ def test_golden_cases(golden_meta, cuda_device):
     (777, 33, True, {}),
     (300, 64, False, {"entropy_coef": 0.0}),
     (1, 4, True, {}),
+    (4097, 8, False, {}),
+    (70000, 4, True, {"compute_kl": False}),
 ])
-def test_random_vs_oracle(B, A, shared, kw, cuda_device):
+@pytest.mark.parametrize("kernel", ["quad", "lane"])
+def test_random_vs_oracle(B, A, shared, kw, kernel, cuda_device, monkeypatch):
+    # RSLRL_LOSS_KERNEL is read per call by the library (quad layout: A % 4 == 0 and A <= 16)
+    monkeypatch.setenv("RSLRL_LOSS_KERNEL", kernel)
     rng = np.random.default_rng(B + A)
     mu = rng.standard_normal((B, A), dtype=np.float32)
     sig_vec = rng.uniform(0.5, 1.5, A).astype(np.float32)
