@@ -33,6 +33,7 @@ if ROOT not in sys.path:
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA at 2.4 GHz (MI355X_MICROARCH.md)
 X6_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 6  # fp32-equivalent peak of the 6-product split-bf16 GEMMs
+H3_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 3  # ... of the 3-product split-fp16 GEMMs (fp16 MFMA = bf16 rate)
 FP32_MFMA_PEAK_TFLOPS = 157.3
 HOT_PATH = ("gae_scan", "adv_normalize", "gather_rows", "ppo_loss", "rollout_record")
 # per-launch HBM traffic of the hot-path kernels from rocprofv3 FETCH_SIZE / WRITE_SIZE passes over this same
@@ -214,16 +215,24 @@ def main():
                     "mean_launch_us": hot[dominant]["mean_us"]}
     roofline_mlp = None
     from rsl_rl_amd.networks import fused_mlp
-    x6 = fused_mlp._mode == fused_mlp.GEMM_X6
+    mode = fused_mlp._mode
+    arith_label = {fused_mlp.GEMM_H3: "h3 split-fp16 MFMA on the hidden layers (x6 split-bf16 on the first and "
+                                      "output layers), fp32-class error (DESIGN.md s5)",
+                   fused_mlp.GEMM_X6: "x6 split-bf16 MFMA, fp32-class error (DESIGN.md s5)",
+                   fused_mlp.GEMM_F32: "fp32 MFMA"}[mode]
     if mlp:
         dm = max(mlp, key=lambda k: mlp[k]["ms_per_step"])
         ach = mlp[dm]["achieved_TFLOPs"]
-        peak = X6_PEAK_TFLOPS if x6 else FP32_MFMA_PEAK_TFLOPS
+        if dm.endswith("/h3"):
+            peak, arith = H3_PEAK_TFLOPS, "h3 split-fp16 (fp32-class, DESIGN.md s5); peak = fp16 dense / 3"
+        elif mode != fused_mlp.GEMM_F32:
+            peak, arith = X6_PEAK_TFLOPS, "x6 split-bf16 (fp32-class, DESIGN.md s5); peak = bf16 dense / 6"
+        else:
+            peak, arith = FP32_MFMA_PEAK_TFLOPS, "fp32 MFMA"
         roofline_mlp = {"kernel": dm, "bound": "mfma", "achieved": ach, "peak": round(peak, 1), "unit": "TFLOP/s",
                         "frac": round(ach / peak, 4), "traffic": None,
                         "flops_per_launch": mlp[dm]["flops_per_launch"], "mean_launch_us": mlp[dm]["mean_us"],
-                        "arithmetic": "x6 split-bf16 (fp32-class, DESIGN.md s5); peak = bf16 dense / 6" if x6
-                        else "fp32 MFMA", "fp32_mfma_peak": FP32_MFMA_PEAK_TFLOPS,
+                        "arithmetic": arith, "fp32_mfma_peak": FP32_MFMA_PEAK_TFLOPS,
                         "mlp_ms_per_step": round(sum(e["ms_per_step"] for e in mlp.values()), 3)}
 
     out = {
@@ -238,7 +247,7 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "fp32",
-        "gemm_arithmetic": "x6 split-bf16 MFMA, fp32-class error (DESIGN.md s5)" if x6 else "fp32 MFMA",
+        "gemm_arithmetic": arith_label,
         "data": "synthetic (SyntheticVecEnv: obs/reward ~ N(0,1), dones ~ Bernoulli(0.02); random-init weights)",
         "config": {
             "workload": f"C3: {N} envs/GPU x T={T}, obs {args.num_obs}, act {args.num_actions}, "
@@ -268,6 +277,10 @@ def main():
         prev = fused_mlp.set_gemm_mode(fused_mlp.GEMM_F32)
         extra["C3_fp32_mfma"] = time_runner(args, device, rank)
         extra["C3_fp32_mfma"]["workload"] = "C3 with the exact-fp32 MFMA GEMM kernels (RSLRL_GEMM_MODE=f32)"
+        if prev != fused_mlp.GEMM_X6:
+            fused_mlp.set_gemm_mode(fused_mlp.GEMM_X6)
+            extra["C3_x6"] = time_runner(args, device, rank)
+            extra["C3_x6"]["workload"] = "C3 with every MLP GEMM on x6 split-bf16 (RSLRL_GEMM_MODE=x6)"
         fused_mlp.set_gemm_mode(prev)
         out["extra_configs"] = extra
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -31,7 +31,7 @@ extern "C" {
 
 typedef struct ihipStream_t* rslrl_stream_t; /* == hipStream_t */
 
-#define RSLRL_ABI_VERSION 3
+#define RSLRL_ABI_VERSION 4
 
 enum {
     RSLRL_OK = 0,
@@ -183,6 +183,7 @@ typedef struct {
 } rslrl_bimage_desc_t;
 #define RSLRL_BIMAGE_LAYOUT_GEMM 0
 #define RSLRL_BIMAGE_LAYOUT_OUT 1
+#define RSLRL_BIMAGE_LAYOUT_H3 2 /* h3 arithmetic (rslrl_linear_gemm): rslrl_linear_bimage_h3_bytes(depth) bytes */
 #define RSLRL_MAX_BIMAGES 16
 int rslrl_linear_prepare_bimages(const rslrl_bimage_desc_t* descs, int32_t n, rslrl_stream_t stream);
 int rslrl_linear_fwd(const float* x, int64_t M, int32_t K, const float* weight, int32_t N, const float* bias,
@@ -224,6 +225,59 @@ int rslrl_linear_dgrad_elu_wgrad(const float* dz, int64_t M, int32_t Nred, int32
                                  rslrl_stream_t stream);
 int rslrl_linear_wgrad(const float* dz, const float* x, int64_t M, int32_t N, int32_t K, float* dw, void* workspace,
                        size_t workspace_bytes, rslrl_stream_t stream);
+
+/* "h3" arithmetic and the generic entry point of the fused linear ops.
+ * h3: every fp32 operand x is scaled by a power of two s (max |s x| < 2^15) and split into two fp16 planes
+ * x0 + x1 (22 significant bits); three fp16 MFMA products a0b0 + a0b1 + a1b0 accumulate in fp32 and the
+ * result is divided by the scales (exact) -- half the MFMA work of x6 at an fp32 GEMM's normwise error
+ * (tests/test_gpu_h3.py measures it against fp64 next to torch's fp32 GEMM).  The A operand's scale comes
+ * from a_amax, a device scalar max |A| that A's producer wrote through amax_out (every op here can write
+ * one; the first layer's input has no producer and stays on x6); the B image (layout H3) carries a scale
+ * per row of B.
+ *   op                         A (a, [M, K])  output                      B image (rows = N, depth = K)
+ *   RSLRL_LINEAR_FWD[_ELU]     x              c = act(x W^T + bias) [M,N]  W [N, K]
+ *   RSLRL_LINEAR_DGRAD_ELU     dz             c = (dz W) * ELU'(h) [M,N]   W^T (transposed image of W [K, N])
+ *                                             + colsum_partials [N, rslrl_linear_tiles(M)]
+ *   RSLRL_LINEAR_DGRAD_ELU_WGRAD  (x6 only)   as rslrl_linear_dgrad_elu_wgrad (K = Nred <= 16)
+ *   RSLRL_LINEAR_FWD_OUT       x              c = h (nullable), y = h W_out^T + out_bias (rslrl_linear_fwd_out)
+ * amax_out (optional, not for FWD_OUT): max |c| over the output, published by the launch's last workgroup;
+ * needs amax_workspace (rslrl_amax_workspace_bytes(), zero-filled once; every launch leaves it zero; one
+ * workspace per stream).
+ * rslrl_linear_wgrad_ex: rslrl_linear_wgrad with arith = X6 | H3 (H3: dz_amax, x_amax = max |dz|, max |x|). */
+#define RSLRL_ARITH_X6 1
+#define RSLRL_ARITH_H3 2
+#define RSLRL_LINEAR_FWD 0
+#define RSLRL_LINEAR_FWD_ELU 1
+#define RSLRL_LINEAR_DGRAD_ELU 2
+#define RSLRL_LINEAR_DGRAD_ELU_WGRAD 3
+#define RSLRL_LINEAR_FWD_OUT 4
+typedef struct {
+    int32_t op;
+    int32_t arith;
+    const float* a;
+    const float* a_amax;
+    int64_t M;
+    int32_t K;
+    int32_t N;
+    const void* bimage;
+    const float* bias;
+    const float* h;
+    float* c;
+    float* colsum_partials;
+    float* wgrad_partials;
+    const void* out_image;
+    const float* out_bias;
+    float* y;
+    int32_t nout;
+    float* amax_out;
+    void* amax_workspace;
+} rslrl_linear_args_t;
+size_t rslrl_linear_bimage_h3_bytes(int32_t depth);
+size_t rslrl_amax_workspace_bytes(void);
+int rslrl_linear_gemm(const rslrl_linear_args_t* args /* host struct */, rslrl_stream_t stream);
+int rslrl_linear_wgrad_ex(const float* dz, const float* dz_amax, const float* x, const float* x_amax, int64_t M,
+                          int32_t N, int32_t K, int32_t arith, float* dw, void* workspace, size_t workspace_bytes,
+                          rslrl_stream_t stream);
 
 /* ------------------------------------------------------------------------------------------------
  * Rollout-side record: for environment step t, in one launch,

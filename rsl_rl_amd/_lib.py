@@ -17,8 +17,9 @@ import threading
 import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
-LIB_PATH = os.path.join(LIB_DIR, "librslrl_amd.so")
-ABI_VERSION = 3
+# RSLRL_AMD_LIB: an alternative in-tree build of the same library (A/B kernel experiments)
+LIB_PATH = os.environ.get("RSLRL_AMD_LIB") or os.path.join(LIB_DIR, "librslrl_amd.so")
+ABI_VERSION = 4
 
 # symbols declared in include/rslrl_amd.h (tests/test_capi.py checks the header against this list)
 EXPORTED_SYMBOLS = (
@@ -52,6 +53,10 @@ EXPORTED_SYMBOLS = (
     "rslrl_normalizer_update",
     "rslrl_normalizer_apply",
     "rslrl_reward_normalize",
+    "rslrl_linear_bimage_h3_bytes",
+    "rslrl_amax_workspace_bytes",
+    "rslrl_linear_gemm",
+    "rslrl_linear_wgrad_ex",
 )
 
 MAX_GATHER_FIELDS = 16
@@ -78,6 +83,35 @@ class BImageDesc(ctypes.Structure):
 MAX_BIMAGES = 16
 BIMAGE_LAYOUT_GEMM = 0
 BIMAGE_LAYOUT_OUT = 1
+BIMAGE_LAYOUT_H3 = 2
+
+ARITH_X6, ARITH_H3 = 1, 2
+LINEAR_FWD, LINEAR_FWD_ELU, LINEAR_DGRAD_ELU, LINEAR_DGRAD_ELU_WGRAD, LINEAR_FWD_OUT = 0, 1, 2, 3, 4
+
+
+class LinearArgs(ctypes.Structure):
+    """rslrl_linear_args_t (include/rslrl_amd.h)."""
+    _fields_ = [
+        ("op", ctypes.c_int32),
+        ("arith", ctypes.c_int32),
+        ("a", ctypes.c_void_p),
+        ("a_amax", ctypes.c_void_p),
+        ("M", ctypes.c_int64),
+        ("K", ctypes.c_int32),
+        ("N", ctypes.c_int32),
+        ("bimage", ctypes.c_void_p),
+        ("bias", ctypes.c_void_p),
+        ("h", ctypes.c_void_p),
+        ("c", ctypes.c_void_p),
+        ("colsum_partials", ctypes.c_void_p),
+        ("wgrad_partials", ctypes.c_void_p),
+        ("out_image", ctypes.c_void_p),
+        ("out_bias", ctypes.c_void_p),
+        ("y", ctypes.c_void_p),
+        ("nout", ctypes.c_int32),
+        ("amax_out", ctypes.c_void_p),
+        ("amax_workspace", ctypes.c_void_p),
+    ]
 
 DTYPE_F32, DTYPE_U8, DTYPE_I32, DTYPE_I64 = 0, 1, 2, 3
 ROLLOUT_MAX_OBS = 4
@@ -226,6 +260,14 @@ def _declare(L):
     L.rslrl_rollout_record.argtypes = [ctypes.POINTER(RolloutArgs), P]
     L.rslrl_column_sum_fold.restype = ctypes.c_int
     L.rslrl_column_sum_fold.argtypes = [P, I64, I32, P, P]
+    L.rslrl_linear_bimage_h3_bytes.restype = SZ
+    L.rslrl_linear_bimage_h3_bytes.argtypes = [I32]
+    L.rslrl_amax_workspace_bytes.restype = SZ
+    L.rslrl_amax_workspace_bytes.argtypes = []
+    L.rslrl_linear_gemm.restype = ctypes.c_int
+    L.rslrl_linear_gemm.argtypes = [ctypes.POINTER(LinearArgs), P]
+    L.rslrl_linear_wgrad_ex.restype = ctypes.c_int
+    L.rslrl_linear_wgrad_ex.argtypes = [P, P, P, P, I64, I32, I32, I32, P, P, SZ, P]
 
 
 def lib():

@@ -63,6 +63,9 @@ struct GemmParams {
     float* y;            // kEpiBiasEluOut: output [M, nout]
     int nout;            // kEpiBiasEluOut: output width <= 32
     int nt;              // kEpiBiasEluOut: streaming stores for h
+    const float* a_amax;  // h3: max |A| (device scalar written by A's producer) -> A's power-of-two scale
+    float* amax_out;      // optional: max |C| over the stored output (device scalar, for an h3 consumer)
+    unsigned* amax_ws;    // with amax_out: {running max bits, arrival ticket}, zero before and after the launch
 };
 
 // global -> registers for one K chunk: A: 128 x 16 floats = 512 float4 (1 per thread); B: 256 x 16 = 1024
@@ -132,7 +135,7 @@ __device__ __forceinline__ float elu_neg(float v) {
 template <int EPI, int I, int J, bool FULLT, int NR>
 __device__ __forceinline__ void epilogue_tiles_impl(const GemmParams& p, f32x16 (&acc)[I][J], int64_t wrow0,
                                                     int wcol0, float (&colpart)[J], const float* dzo, int dzo_row0,
-                                                    f32x2 (&wacc)[NR]) {
+                                                    f32x2 (&wacc)[NR], float& amx) {
     constexpr bool full = FULLT;
     constexpr bool GRAD = EPI == kEpiEluGrad || EPI == kEpiEluGradWgrad;
     const int lane = threadIdx.x & 63;
@@ -180,6 +183,7 @@ __device__ __forceinline__ void epilogue_tiles_impl(const GemmParams& p, f32x16 
                     v = hv > 0.f ? v : v * (hv + 1.f);
                     colpart[j] += v;
                 }
+                amx = fmaxf(amx, fabsf(v));
                 // streaming store: the outputs are not re-read by this kernel, and keeping them out of L2
                 // keeps the B image and the A stream resident (-7% kernel time measured)
                 __builtin_nontemporal_store(v, cp + static_cast<int64_t>(roff) * p.N);
@@ -222,25 +226,24 @@ __device__ __forceinline__ void epilogue_tiles_impl(const GemmParams& p, f32x16 
 // vmcnt(0) before each store (64 serialised stores per wave: the epilogue ran 3x longer).
 template <int EPI, int I, int J>
 __device__ __forceinline__ void epilogue_tiles(const GemmParams& p, f32x16 (&acc)[I][J], int64_t wrow0, int wcol0,
-                                               bool full, float (&colpart)[J], const float* dzo = nullptr,
-                                               int dzo_row0 = 0) {
+                                               bool full, float (&colpart)[J], float& amx) {
     f32x2 wacc[1];  // unused (no weight-gradient accumulation)
     if (full)
-        epilogue_tiles_impl<EPI, I, J, true, 1>(p, acc, wrow0, wcol0, colpart, dzo, dzo_row0, wacc);
+        epilogue_tiles_impl<EPI, I, J, true, 1>(p, acc, wrow0, wcol0, colpart, nullptr, 0, wacc, amx);
     else
-        epilogue_tiles_impl<EPI, I, J, false, 1>(p, acc, wrow0, wcol0, colpart, dzo, dzo_row0, wacc);
+        epilogue_tiles_impl<EPI, I, J, false, 1>(p, acc, wrow0, wcol0, colpart, nullptr, 0, wacc, amx);
 }
 
 template <int EPI, int I, int J, int NR>
 __device__ __forceinline__ void epilogue_tiles_w(const GemmParams& p, f32x16 (&acc)[I][J], int64_t wrow0, int wcol0,
                                                  bool full, float (&colpart)[J], const float* dzo, int dzo_row0,
-                                                 f32x2 (&wacc)[NR]) {
+                                                 f32x2 (&wacc)[NR], float& amx) {
 #pragma unroll
     for (int o = 0; o < NR; ++o) wacc[o] = f32x2{0.f, 0.f};
     if (full)
-        epilogue_tiles_impl<EPI, I, J, true, NR>(p, acc, wrow0, wcol0, colpart, dzo, dzo_row0, wacc);
+        epilogue_tiles_impl<EPI, I, J, true, NR>(p, acc, wrow0, wcol0, colpart, dzo, dzo_row0, wacc, amx);
     else
-        epilogue_tiles_impl<EPI, I, J, false, NR>(p, acc, wrow0, wcol0, colpart, dzo, dzo_row0, wacc);
+        epilogue_tiles_impl<EPI, I, J, false, NR>(p, acc, wrow0, wcol0, colpart, dzo, dzo_row0, wacc, amx);
 }
 
 // f32 kernel epilogue: 128-row tile, waves 2 (m) x 4 (n) of 64 x 64; column sums over the tile's 128 rows
@@ -256,7 +259,8 @@ __device__ __forceinline__ void epilogue(const GemmParams& p, f32x16 (&acc)[2][2
     const int l32 = lane & 31;
     const bool full = (row0 + kBM <= p.M) && (p.N == kBN);  // wave-uniform: no per-element bounds checks
     float colpart[2];
-    epilogue_tiles<EPI, 2, 2>(p, acc, row0 + wm * 64, wn * 64, full, colpart);
+    float amx = 0.f;
+    epilogue_tiles<EPI, 2, 2>(p, acc, row0 + wm * 64, wn * 64, full, colpart, amx);
     if constexpr (EPI == kEpiEluGrad) {
         __syncthreads();  // the LDS tiles are no longer read
 #pragma unroll
@@ -348,6 +352,10 @@ __device__ uint64_t* g_stamps;
 constexpr int kX6RowB = 32;
 constexpr int kX6PlaneB = kBN * kX6RowB;  // 8 KiB
 constexpr int kX6ChunkB = 3 * kX6PlaneB;  // 24 KiB: one chunk of the B image
+// h3 B image (RSLRL_BIMAGE_LAYOUT_H3): [chunk][2 fp16 planes][256 rows][32 B swizzled] of t_n B[n][k] (t_n a
+// power of two per row n from max_k |B[n][k]|), then 1 / t_n for the 256 rows (fp32).
+constexpr int kH3ChunkB = 2 * kX6PlaneB;
+__host__ __device__ inline int64_t h3_image_scales_offset(int depth) { return ((depth + kKC - 1) / kKC) * int64_t{kH3ChunkB}; }
 
 __device__ __forceinline__ int swz(int row, int half) { return row * kX6RowB + 16 * (half ^ ((row >> 3) & 1)); }
 
@@ -400,6 +408,40 @@ __global__ __launch_bounds__(kBlock) void bimage_kernel(BImageBatch batch) {
     const float* __restrict__ src = dsc.src;
     const int nchunks = (depth + kKC - 1) / kKC;
     const int id = blockIdx.x * kBlock + threadIdx.x;
+    if (dsc.layout == RSLRL_BIMAGE_LAYOUT_H3) {
+        // depth <= 256: the 16 chunks x 2 halves of row n are the 32 lanes of a half wave, so the row's max
+        // (-> its scale t_n) is a 32-lane shuffle reduction of the lanes' own 8 values
+        if (id >= kBN * 32) return;  // whole half waves exit together
+        const int n = id >> 5;
+        const int c = (id >> 1) & 15;
+        const int ph = id & 1;
+        const int lh = ph ^ ((n >> 3) & 1);
+        float v[8];
+        float m = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int k = 16 * c + 8 * lh + j;
+            v[j] = (n < rows && k < depth) ? src[dsc.transposed ? static_cast<int64_t>(k) * rows + n
+                                                                : static_cast<int64_t>(n) * depth + k]
+                                           : 0.f;
+            m = fmaxf(m, fabsf(v[j]));
+        }
+#pragma unroll
+        for (int off = 16; off >= 1; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 32));
+        const float t = h3_scale(m);
+        if (c < nchunks) {
+            uint2 lo[2], hi[2];
+            split4_h(make_float4(v[0] * t, v[1] * t, v[2] * t, v[3] * t), lo[0], lo[1]);
+            split4_h(make_float4(v[4] * t, v[5] * t, v[6] * t, v[7] * t), hi[0], hi[1]);
+            uint4* base = static_cast<uint4*>(dsc.image) + static_cast<int64_t>(c) * (kH3ChunkB / 16) +
+                          (n * kX6RowB + 16 * ph) / 16;
+#pragma unroll
+            for (int q = 0; q < 2; ++q) base[q * (kX6PlaneB / 16)] = make_uint4(lo[q].x, lo[q].y, hi[q].x, hi[q].y);
+        }
+        if (c == 0 && ph == 0)
+            reinterpret_cast<float*>(static_cast<char*>(dsc.image) + h3_image_scales_offset(depth))[n] = 1.f / t;
+        return;
+    }
     if (id >= nchunks * kBN * 2) return;
     const int c = id / (kBN * 2);
     const int n = (id >> 1) % kBN;
@@ -447,8 +489,9 @@ __device__ __forceinline__ AStage<BM> load_a(const GemmParams& p, int64_t row0, 
     return s;
 }
 
-template <int BM>
-__device__ __forceinline__ void store_a_split(const AStage<BM>& s, char* __restrict__ a_lds) {
+// PL planes (3: x6 bf16, 2: h3 fp16 of the operand scaled by sc, a power of two)
+template <int BM, int PL>
+__device__ __forceinline__ void store_a_split(const AStage<BM>& s, char* __restrict__ a_lds, float sc) {
     constexpr int plane = BM * kX6RowB;
 #pragma unroll
     for (int i = 0; i < BM / 128; ++i) {
@@ -456,40 +499,96 @@ __device__ __forceinline__ void store_a_split(const AStage<BM>& s, char* __restr
         const int q = u & 3;
         const int r = u >> 2;
         const int off = swz(r, q >> 1) + 8 * (q & 1);
-        uint2 w0, w1, w2;
-        split4(s.v[i], w0, w1, w2);
-        *reinterpret_cast<uint2*>(a_lds + off) = w0;
-        *reinterpret_cast<uint2*>(a_lds + plane + off) = w1;
-        *reinterpret_cast<uint2*>(a_lds + 2 * plane + off) = w2;
+        uint2 w[PL];
+        float4 v = s.v[i];
+        if constexpr (PL == 2) v = make_float4(v.x * sc, v.y * sc, v.z * sc, v.w * sc);
+        Arith<PL>::split(v, w);
+#pragma unroll
+        for (int q2 = 0; q2 < PL; ++q2) *reinterpret_cast<uint2*>(a_lds + q2 * plane + off) = w[q2];
     }
 }
 
-// B chunk c of the image -> LDS: 1536 16-B units, thread t copies units t, t + 512, t + 1024; the LDS
+// B chunk c of the image -> LDS: PL x 512 16-B units, thread t copies units t, t + 512, ...; the LDS
 // destination of a wave's global_load_lds is (wave-uniform base) + 16 * lane.
+template <int PL>
 __device__ __forceinline__ void load_b_lds(const uint4* __restrict__ img, int c, char* b_lds) {
     const int t = threadIdx.x;
-    const uint4* src = img + static_cast<int64_t>(c) * (kX6ChunkB / 16);
+    const uint4* src = img + static_cast<int64_t>(c) * (PL * kX6PlaneB / 16);
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
+    for (int i = 0; i < PL; ++i) {
         const int u = t + kThreads * i;
         __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + u),
                                          (__attribute__((address_space(3))) void*)(b_lds + 16 * (u & ~63)), 16, 0, 0);
     }
 }
 
-__device__ __forceinline__ bf16x8 read_frag(const char* __restrict__ plane, int row, int h) {
-    return __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(plane + swz(row, h)));
+template <typename F = bf16x8>
+__device__ __forceinline__ F read_frag(const char* __restrict__ plane, int row, int h) {
+    return __builtin_bit_cast(F, *reinterpret_cast<const uint4*>(plane + swz(row, h)));
+}
+
+
+// max |C| of a launch, without same-address contention: the workgroup's max (waves through LDS) goes to
+// one of kAmaxGroups group words (atomic max; non-negative floats order as their bits); the last workgroup
+// of each group (group ticket) forwards the group max to the global word, and the last group (global ticket)
+// publishes it to *amax_out.  Every word is re-armed to zero by its last reader.  amax_ws layout (u32):
+// [0, 64) group max, [64, 128) group tickets, 128 global max, 129 global ticket.
+// Ordering without fences: all of these are device-scope atomics (performed at the coherence point, not in
+// the per-XCD L2s) and each is waited for (vmcnt(0)) before the next one issues, so a ticket increment is
+// never visible before the max it follows.  An agent-scope release fence here would write back the L2 of
+// every XCD per workgroup (+150-200 us per launch measured).  Every thread of the workgroup calls this.
+constexpr int kAmaxGroups = 64;
+__device__ __forceinline__ void amax_commit(const GemmParams& p, float amx) {
+    if (!p.amax_out) return;  // uniform
+    __shared__ float wave_max[kThreads / 64];
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) amx = fmaxf(amx, __shfl_xor(amx, off, 64));
+    if ((threadIdx.x & 63) == 0) wave_max[threadIdx.x >> 6] = amx;
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    float m = wave_max[0];
+#pragma unroll
+    for (int w = 1; w < kThreads / 64; ++w) m = fmaxf(m, wave_max[w]);
+    unsigned* ws = p.amax_ws;
+    const unsigned nb = gridDim.x;
+    const unsigned g = blockIdx.x % kAmaxGroups;
+    const unsigned ng = nb < kAmaxGroups ? nb : kAmaxGroups;
+    const unsigned in_group = (nb - g + kAmaxGroups - 1) / kAmaxGroups;
+    auto amax_ = [](unsigned* a, unsigned v) {
+        __hip_atomic_fetch_max(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    };
+    auto ticket_ = [](unsigned* a) {
+        return __hip_atomic_fetch_add(a, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // returns: waited
+    };
+    auto load_ = [](unsigned* a) { return __hip_atomic_fetch_add(a, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+    auto clear_ = [](unsigned* a) { __hip_atomic_exchange(a, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+    amax_(ws + g, __float_as_uint(m));
+    if (ticket_(ws + kAmaxGroups + g) != in_group - 1) return;
+    const unsigned mg = load_(ws + g);
+    clear_(ws + g);
+    clear_(ws + kAmaxGroups + g);
+    amax_(ws + 2 * kAmaxGroups, mg);
+    if (ticket_(ws + 2 * kAmaxGroups + 1) != ng - 1) return;
+    const unsigned mall = load_(ws + 2 * kAmaxGroups);
+    *p.amax_out = __uint_as_float(mall);
+    clear_(ws + 2 * kAmaxGroups);
+    clear_(ws + 2 * kAmaxGroups + 1);
 }
 
 // 128 rows x 256 columns per workgroup: waves 2 (M) x 4 (N) of 64 x 64 (2 x 2 MFMA tiles); MINW = 4:
 // two workgroups per CU (<= 128 VGPRs), 2: one (the register-hungrier short-K dgrad epilogues).
 // NR: rows of the fused weight gradient (kEpiEluGradWgrad: Nred rounded up to 4; otherwise unused).
-template <int EPI, bool FULL, int MINW, int NR = 4>
+// PL: operand planes (3: x6 bf16 on a layout-0 image; 2: h3 fp16 on a layout-2 image, A scaled from *p.a_amax).
+template <int EPI, bool FULL, int MINW, int NR = 4, int PL = 3>
 __global__ __launch_bounds__(kThreads, MINW) void mlp_gemm_x6_kernel(GemmParams p, const uint4* __restrict__ bimg) {
+    static_assert(PL == 3 || EPI != kEpiEluGradWgrad, "the fused output-layer backward is x6 only");
+    using Frag = typename Arith<PL>::frag;
     constexpr int BM = kBM;
     constexpr int I = BM / 64;
     constexpr int planeA = BM * kX6RowB;
-    constexpr int bufBytes = 3 * planeA + kX6ChunkB;
+    // the fused output layer's epilogue (h stage + reduction tiles) needs the x6 main loop's 72 KiB
+    constexpr int bufBytes = EPI == kEpiBiasEluOut ? (3 * planeA + 3 * kX6PlaneB) : (PL * planeA + PL * kX6PlaneB);
     __shared__ __attribute__((aligned(16))) char lds[2][bufBytes];
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
@@ -512,43 +611,63 @@ __global__ __launch_bounds__(kThreads, MINW) void mlp_gemm_x6_kernel(GemmParams 
     // Pipeline: B of chunk c+1 is copied (global_load_lds) and A of chunk c+1 fetched into registers at
     // the start of chunk c; A is split into the other LDS buffer at its end.
     const int nchunks = (p.K + kKC - 1) / kKC;
-    load_b_lds(bimg, 0, lds[0] + 3 * planeA);
-    store_a_split<BM>(load_a<BM, FULL>(p, row0, 0), lds[0]);
+    const float sa = PL == 2 ? h3_scale(*p.a_amax) : 1.f;
+    load_b_lds<PL>(bimg, 0, lds[0] + PL * planeA);
+    store_a_split<BM, PL>(load_a<BM, FULL>(p, row0, 0), lds[0], sa);
     __syncthreads();
     for (int c = 0; c < nchunks; ++c) {
         const int buf = c & 1;
         const bool more = c + 1 < nchunks;
         AStage<BM> an;
         if (more) {  // the other buffer was last read in chunk c-1, and every wave passed the barrier after it
-            load_b_lds(bimg, c + 1, lds[buf ^ 1] + 3 * planeA);
+            load_b_lds<PL>(bimg, c + 1, lds[buf ^ 1] + PL * planeA);
             an = load_a<BM, FULL>(p, row0, (c + 1) * kKC);
         }
         const char* a_lds = lds[buf];
-        const char* b_lds = lds[buf] + 3 * planeA;
-        bf16x8 bf[2][3];
+        const char* b_lds = lds[buf] + PL * planeA;
+        Frag bf[2][PL];
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
-            for (int q = 0; q < 3; ++q) bf[j][q] = read_frag(b_lds + q * kX6PlaneB, wn * 64 + j * 32 + l32, h);
+            for (int q = 0; q < PL; ++q) bf[j][q] = read_frag<Frag>(b_lds + q * kX6PlaneB, wn * 64 + j * 32 + l32, h);
 #pragma unroll
         for (int i = 0; i < I; ++i) {
-            bf16x8 af[3];
+            Frag af[PL];
 #pragma unroll
-            for (int q = 0; q < 3; ++q) af[q] = read_frag(a_lds + q * planeA, wm * (BM / 2) + i * 32 + l32, h);
+            for (int q = 0; q < PL; ++q) af[q] = read_frag<Frag>(a_lds + q * planeA, wm * (BM / 2) + i * 32 + l32, h);
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
                 if constexpr (EPI == kEpiBiasEluOut)  // C^T tile: the weight fragment is the MFMA's A operand
-                    acc[i][j] = mfma_x6(bf[j], af, acc[i][j]);
+                    acc[i][j] = Arith<PL>::mfma(bf[j], af, acc[i][j]);
                 else
-                    acc[i][j] = mfma_x6(af, bf[j], acc[i][j]);
+                    acc[i][j] = Arith<PL>::mfma(af, bf[j], acc[i][j]);
             }
         }
-        if (more) store_a_split<BM>(an, lds[buf ^ 1]);
+        if (more) store_a_split<BM, PL>(an, lds[buf ^ 1], sa);
         __syncthreads();  // also retires the global_load_lds of chunk c+1 (vmcnt(0))
+    }
+    const float inv_sa = 1.f / sa;
+    if constexpr (PL == 2) {
+        // undo the operand scales: C[m][n] = acc / (s_a t_n), exact (powers of two)
+        const float* inv_t =
+            reinterpret_cast<const float*>(reinterpret_cast<const char*>(bimg) + h3_image_scales_offset(p.K));
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            if constexpr (EPI == kEpiBiasEluOut) {
+                // C^T tiles: unscaled column by column in the epilogue below (its bias loads)
+            } else {
+                const float f = inv_t[wn * 64 + j * 32 + l32] * inv_sa;
+#pragma unroll
+                for (int i = 0; i < I; ++i)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) acc[i][j][r] *= f;
+            }
+        }
     }
 
     const bool full = (row0 + BM <= p.M) && (p.N == kBN);
     float colpart[2];
+    float amx = 0.f;  // max |stored output| of this lane (amax_commit)
 #ifdef RSLRL_STAMPS
     uint64_t st1 = __builtin_amdgcn_s_memrealtime();
     uint64_t ct1 = __builtin_amdgcn_s_memtime();
@@ -574,7 +693,8 @@ __global__ __launch_bounds__(kThreads, MINW) void mlp_gemm_x6_kernel(GemmParams 
         }
         __syncthreads();
         f32x2 wacc[NR];
-        epilogue_tiles_w<EPI, I, 2, NR>(p, acc, row0 + wm * (BM / 2), wn * 64, full, colpart, dzo, wm * (BM / 2), wacc);
+        epilogue_tiles_w<EPI, I, 2, NR>(p, acc, row0 + wm * (BM / 2), wn * 64, full, colpart, dzo, wm * (BM / 2), wacc,
+                                        amx);
         // per-tile partial dW[o][col]: lane halves (rows 4h..) by shuffle, then the two wave rows in a fixed
         // order through LDS (the B region of buffer 0 is free after the main loop)
         float* red = reinterpret_cast<float*>(lds[0] + 3 * planeA);  // [16][256]
@@ -631,8 +751,20 @@ __global__ __launch_bounds__(kThreads, MINW) void mlp_gemm_x6_kernel(GemmParams 
                     const bool col_ok = col < p.N;  // N % 4 == 0
                     const float4 b4 = col_ok ? *reinterpret_cast<const float4*>(p.bias + col)
                                              : make_float4(0.f, 0.f, 0.f, 0.f);
-                    float t[4] = {acc[i][j][4 * g] + b4.x, acc[i][j][4 * g + 1] + b4.y, acc[i][j][4 * g + 2] + b4.z,
-                                  acc[i][j][4 * g + 3] + b4.w};
+                    float t[4] = {acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
+                    if constexpr (PL == 2) {  // h3: C = acc / (s_a t_n), exact
+                        const float4 f4 = *reinterpret_cast<const float4*>(
+                            reinterpret_cast<const float*>(reinterpret_cast<const char*>(bimg) +
+                                                           h3_image_scales_offset(p.K)) + col);
+                        t[0] *= f4.x * inv_sa;
+                        t[1] *= f4.y * inv_sa;
+                        t[2] *= f4.z * inv_sa;
+                        t[3] *= f4.w * inv_sa;
+                    }
+                    t[0] += b4.x;
+                    t[1] += b4.y;
+                    t[2] += b4.z;
+                    t[3] += b4.w;
 #pragma unroll
                     for (int e = 0; e < 4; ++e) v[4 * g + e] = t[e] > 0.f ? t[e] : elu_neg(t[e]);
                     const f32x4 hv = {v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]};
@@ -718,7 +850,7 @@ __global__ __launch_bounds__(kThreads, MINW) void mlp_gemm_x6_kernel(GemmParams 
             if (row < p.M) p.y[row * nout + o] = sum + p.obias[o];
         }
     } else {
-        epilogue_tiles<EPI, I, 2>(p, acc, row0 + wm * (BM / 2), wn * 64, full, colpart);
+        epilogue_tiles<EPI, I, 2>(p, acc, row0 + wm * (BM / 2), wn * 64, full, colpart, amx);
     }
 #ifdef RSLRL_STAMPS
     {
@@ -750,6 +882,7 @@ __global__ __launch_bounds__(kThreads, MINW) void mlp_gemm_x6_kernel(GemmParams 
         for (int col = threadIdx.x; col < p.N && col < kBN; col += kThreads)
             p.colsum[static_cast<int64_t>(col) * tiles + blockIdx.x] = colred[col] + colred[kBN + col];
     }
+    if constexpr (EPI != kEpiBiasEluOut) amax_commit(p, amx);
 }
 
 // ---- the same x6 GEMM on v_mfma_f32_16x16x32_bf16 ("paired" x6).  Under load the chip holds a higher
@@ -860,15 +993,15 @@ __global__ __launch_bounds__(kThreads, MINW) void mlp_gemm_x6s_kernel(GemmParams
         for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{};
 
     const int nchunks = (p.K + kKC - 1) / kKC;
-    load_b_lds(bimg, 0, lds[0] + 3 * planeA);
-    store_a_split<BM>(load_a<BM, FULL>(p, row0, 0), lds[0]);
+    load_b_lds<3>(bimg, 0, lds[0] + 3 * planeA);
+    store_a_split<BM, 3>(load_a<BM, FULL>(p, row0, 0), lds[0], 1.f);
     __syncthreads();
     for (int c = 0; c < nchunks; ++c) {
         const int buf = c & 1;
         const bool more = c + 1 < nchunks;
         AStage<BM> an;
         if (more) {
-            load_b_lds(bimg, c + 1, lds[buf ^ 1] + 3 * planeA);
+            load_b_lds<3>(bimg, c + 1, lds[buf ^ 1] + 3 * planeA);
             an = load_a<BM, FULL>(p, row0, (c + 1) * kKC);
         }
         const char* a_lds = lds[buf];
@@ -893,7 +1026,7 @@ __global__ __launch_bounds__(kThreads, MINW) void mlp_gemm_x6s_kernel(GemmParams
                 acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b2, af[i][1], acc[i][j], 0, 0, 0);
             }
         }
-        if (more) store_a_split<BM>(an, lds[buf ^ 1]);
+        if (more) store_a_split<BM, 3>(an, lds[buf ^ 1], 1.f);
         __syncthreads();
     }
 
@@ -974,7 +1107,8 @@ int dgrad_occupancy() {  // tuning knob: RSLRL_DGRAD_OCC=2|4 (default 4)
 template <int EPI>
 bool launch_x6s(const GemmParams& p, const uint4* img, bool fullm, dim3 g, hipStream_t st) {
     if constexpr (EPI == kEpiBias || EPI == kEpiBiasElu) {
-        if (x6_shape() != 16 || (p.N & 3) || !aligned16(p.c) || !aligned16(p.bias)) return false;  // 16-B epilogue
+        if (x6_shape() != 16 || (p.N & 3) || !aligned16(p.c) || !aligned16(p.bias) || p.amax_out)
+            return false;  // 16-B epilogue, no amax
         const dim3 b(kThreads);
         if (x6s_nontemporal()) {
             if (fullm) hipLaunchKernelGGL((mlp_gemm_x6s_kernel<EPI, true, 4, true>), g, b, 0, st, p, img);
@@ -1005,8 +1139,9 @@ int out_fwd_occupancy() {  // tuning knob: RSLRL_OUT_FWD_OCC=2|4 (default 4)
     return v;
 }
 
-// bimage == nullptr: exact f32 MFMA main loop on p.bw; otherwise the split-bf16 main loop on the image.
-template <int EPI>
+// bimage == nullptr: exact f32 MFMA main loop on p.bw; otherwise the split main loop on the image (PL = 3: x6
+// bf16 planes, layout-0 image; PL = 2: h3 fp16 planes, layout-2 image, A scaled from *p.a_amax).
+template <int EPI, int PL = 3>
 int launch(const GemmParams& p, const void* bimage, hipStream_t st) {
     const int64_t tiles = ceil_div(p.M, kBM);
     if (tiles > INT32_MAX) return RSLRL_E_INVALID_ARGUMENT;
@@ -1018,31 +1153,35 @@ int launch(const GemmParams& p, const void* bimage, hipStream_t st) {
         const bool short_k = EPI != kEpiBias && EPI != kEpiBiasElu && p.K <= 2 * kKC;
         const bool fullm = p.M % kBM == 0 && p.K % kKC == 0;
         if constexpr (EPI == kEpiEluGradWgrad) {  // K = Nred in {4, 8, 12, 16}
-            auto go = [&](auto nr) {
-                constexpr int NR = decltype(nr)::value;
-                if (fullm) hipLaunchKernelGGL((mlp_gemm_x6_kernel<EPI, true, 2, NR>), g, b, 0, st, p, img);
-                else hipLaunchKernelGGL((mlp_gemm_x6_kernel<EPI, false, 2, NR>), g, b, 0, st, p, img);
-            };
-            switch (p.K) {
-                case 4: go(std::integral_constant<int, 4>{}); break;
-                case 8: go(std::integral_constant<int, 8>{}); break;
-                case 12: go(std::integral_constant<int, 12>{}); break;
-                default: go(std::integral_constant<int, 16>{}); break;
+            if constexpr (PL != 3) {
+                return RSLRL_E_UNSUPPORTED;
+            } else {
+                auto go = [&](auto nr) {
+                    constexpr int NR = decltype(nr)::value;
+                    if (fullm) hipLaunchKernelGGL((mlp_gemm_x6_kernel<EPI, true, 2, NR>), g, b, 0, st, p, img);
+                    else hipLaunchKernelGGL((mlp_gemm_x6_kernel<EPI, false, 2, NR>), g, b, 0, st, p, img);
+                };
+                switch (p.K) {
+                    case 4: go(std::integral_constant<int, 4>{}); break;
+                    case 8: go(std::integral_constant<int, 8>{}); break;
+                    case 12: go(std::integral_constant<int, 12>{}); break;
+                    default: go(std::integral_constant<int, 16>{}); break;
+                }
             }
         } else if constexpr (EPI == kEpiBiasEluOut) {
             if (out_fwd_occupancy() == 2) {
-                if (fullm) hipLaunchKernelGGL((mlp_gemm_x6_kernel<EPI, true, 2>), g, b, 0, st, p, img);
-                else hipLaunchKernelGGL((mlp_gemm_x6_kernel<EPI, false, 2>), g, b, 0, st, p, img);
+                if (fullm) hipLaunchKernelGGL((mlp_gemm_x6_kernel<EPI, true, 2, 4, PL>), g, b, 0, st, p, img);
+                else hipLaunchKernelGGL((mlp_gemm_x6_kernel<EPI, false, 2, 4, PL>), g, b, 0, st, p, img);
             } else {
-                if (fullm) hipLaunchKernelGGL((mlp_gemm_x6_kernel<EPI, true, 4>), g, b, 0, st, p, img);
-                else hipLaunchKernelGGL((mlp_gemm_x6_kernel<EPI, false, 4>), g, b, 0, st, p, img);
+                if (fullm) hipLaunchKernelGGL((mlp_gemm_x6_kernel<EPI, true, 4, 4, PL>), g, b, 0, st, p, img);
+                else hipLaunchKernelGGL((mlp_gemm_x6_kernel<EPI, false, 4, 4, PL>), g, b, 0, st, p, img);
             }
         } else if (short_k) {
-            if (fullm) hipLaunchKernelGGL((mlp_gemm_x6_kernel<EPI, true, 2>), g, b, 0, st, p, img);
-            else hipLaunchKernelGGL((mlp_gemm_x6_kernel<EPI, false, 2>), g, b, 0, st, p, img);
-        } else if (!launch_x6s<EPI>(p, img, fullm, g, st)) {
-            if (fullm) hipLaunchKernelGGL((mlp_gemm_x6_kernel<EPI, true, 4>), g, b, 0, st, p, img);
-            else hipLaunchKernelGGL((mlp_gemm_x6_kernel<EPI, false, 4>), g, b, 0, st, p, img);
+            if (fullm) hipLaunchKernelGGL((mlp_gemm_x6_kernel<EPI, true, 2, 4, PL>), g, b, 0, st, p, img);
+            else hipLaunchKernelGGL((mlp_gemm_x6_kernel<EPI, false, 2, 4, PL>), g, b, 0, st, p, img);
+        } else if (PL != 3 || !launch_x6s<EPI>(p, img, fullm, g, st)) {
+            if (fullm) hipLaunchKernelGGL((mlp_gemm_x6_kernel<EPI, true, 4, 4, PL>), g, b, 0, st, p, img);
+            else hipLaunchKernelGGL((mlp_gemm_x6_kernel<EPI, false, 4, 4, PL>), g, b, 0, st, p, img);
         }
     } else if constexpr (EPI == kEpiEluGradWgrad || EPI == kEpiBiasEluOut) {
         return RSLRL_E_UNSUPPORTED;  // x6 path only
@@ -1065,6 +1204,10 @@ extern "C" size_t rslrl_linear_bimage_bytes(int32_t depth) {
     return depth < 1 ? 0 : static_cast<size_t>(ceil_div(static_cast<int64_t>(depth), kKC)) * kX6ChunkB;
 }
 
+extern "C" size_t rslrl_linear_bimage_h3_bytes(int32_t depth) {
+    return depth < 1 ? 0 : static_cast<size_t>(h3_image_scales_offset(depth)) + kBN * sizeof(float);
+}
+
 extern "C" int rslrl_linear_prepare_bimages(const rslrl_bimage_desc_t* descs, int32_t n, rslrl_stream_t stream) {
     if (!descs || n < 1 || n > kMaxImages) return RSLRL_E_INVALID_ARGUMENT;
     BImageBatch batch{};
@@ -1078,6 +1221,9 @@ extern "C" int rslrl_linear_prepare_bimages(const rslrl_bimage_desc_t* descs, in
         if (d.layout == RSLRL_BIMAGE_LAYOUT_OUT) {
             if (d.rows > kMaxOutWidth || d.depth > kBN || d.transposed) return RSLRL_E_INVALID_ARGUMENT;
             max_threads = std::max(max_threads, kOutImageThreads);
+        } else if (d.layout == RSLRL_BIMAGE_LAYOUT_H3) {
+            if (d.depth > kBN) return RSLRL_E_INVALID_ARGUMENT;
+            max_threads = std::max(max_threads, kBN * 32);
         } else if (d.layout == RSLRL_BIMAGE_LAYOUT_GEMM) {
             max_chunks = std::max(max_chunks, static_cast<int>(ceil_div(static_cast<int64_t>(d.depth), kKC)));
         } else {
@@ -1160,4 +1306,73 @@ extern "C" int rslrl_column_sum_fold(const float* partials, int64_t tiles, int32
     hipLaunchKernelGGL(colsum_fold_kernel, dim3(static_cast<unsigned>(N)), dim3(kBlock), 0,
                        reinterpret_cast<hipStream_t>(stream), partials, static_cast<int>(tiles), out);
     return launch_status();
+}
+
+extern "C" size_t rslrl_amax_workspace_bytes(void) { return 1024; }
+
+// One entry point for every fused linear op in either split arithmetic, with the h3 operand scales
+// (include/rslrl_amd.h rslrl_linear_args_t).
+extern "C" int rslrl_linear_gemm(const rslrl_linear_args_t* a, rslrl_stream_t stream) {
+    if (!a) return RSLRL_E_INVALID_ARGUMENT;
+    const int op = a->op;
+    const bool h3 = a->arith == RSLRL_ARITH_H3;
+    if (!h3 && a->arith != RSLRL_ARITH_X6) return RSLRL_E_INVALID_ARGUMENT;
+    if (a->M < 0 || a->K < 1 || a->N < 1 || a->N > kBN || (a->K & 3) || a->K > INT32_MAX / 2)
+        return RSLRL_E_INVALID_ARGUMENT;
+    if (a->M == 0) return RSLRL_OK;
+    if (!a->a || !a->bimage || (h3 && !a->a_amax)) return RSLRL_E_INVALID_ARGUMENT;
+    if (a->amax_out && !a->amax_workspace) return RSLRL_E_INVALID_ARGUMENT;
+    if (!aligned16(a->a) || !aligned16(a->bimage)) return RSLRL_E_MISALIGNED;
+    if (a->amax_out && op == RSLRL_LINEAR_FWD_OUT) return RSLRL_E_UNSUPPORTED;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    GemmParams p{};
+    p.a = a->a;
+    p.M = a->M;
+    p.K = a->K;
+    p.N = a->N;
+    p.a_amax = a->a_amax;
+    p.amax_out = a->amax_out;
+    p.amax_ws = static_cast<unsigned*>(a->amax_workspace);
+    switch (op) {
+        case RSLRL_LINEAR_FWD:
+        case RSLRL_LINEAR_FWD_ELU:
+            if (!a->bias || !a->c) return RSLRL_E_INVALID_ARGUMENT;
+            p.bias = a->bias;
+            p.c = a->c;
+            if (op == RSLRL_LINEAR_FWD_ELU)
+                return h3 ? launch<kEpiBiasElu, 2>(p, a->bimage, st) : launch<kEpiBiasElu, 3>(p, a->bimage, st);
+            return h3 ? launch<kEpiBias, 2>(p, a->bimage, st) : launch<kEpiBias, 3>(p, a->bimage, st);
+        case RSLRL_LINEAR_DGRAD_ELU:
+            if (!a->h || !a->c || !a->colsum_partials) return RSLRL_E_INVALID_ARGUMENT;
+            p.h = a->h;
+            p.c = a->c;
+            p.colsum = a->colsum_partials;
+            p.ctiles = ceil_div(a->M, kBM);
+            return h3 ? launch<kEpiEluGrad, 2>(p, a->bimage, st) : launch<kEpiEluGrad, 3>(p, a->bimage, st);
+        case RSLRL_LINEAR_DGRAD_ELU_WGRAD:
+            if (h3) return RSLRL_E_UNSUPPORTED;
+            if (a->K > kMaxWgradRows || !a->h || !a->c || !a->colsum_partials || !a->wgrad_partials)
+                return RSLRL_E_INVALID_ARGUMENT;
+            p.h = a->h;
+            p.c = a->c;
+            p.colsum = a->colsum_partials;
+            p.ctiles = ceil_div(a->M, kBM);
+            p.wpart = a->wgrad_partials;
+            return launch<kEpiEluGradWgrad, 3>(p, a->bimage, st);
+        case RSLRL_LINEAR_FWD_OUT:
+            if ((a->N & 3) || a->nout < 1 || a->nout > kMaxOutWidth || !a->bias || !a->out_bias || !a->out_image ||
+                !a->y)
+                return RSLRL_E_INVALID_ARGUMENT;
+            if (!aligned16(a->bias) || !aligned16(a->out_image) || (a->c && !aligned16(a->c))) return RSLRL_E_MISALIGNED;
+            p.bias = a->bias;
+            p.c = a->c;
+            p.oimg = static_cast<const uint4*>(a->out_image);
+            p.obias = a->out_bias;
+            p.y = a->y;
+            p.nout = a->nout;
+            p.nt = out_fwd_nt();
+            return h3 ? launch<kEpiBiasEluOut, 2>(p, a->bimage, st) : launch<kEpiBiasEluOut, 3>(p, a->bimage, st);
+        default:
+            return RSLRL_E_INVALID_ARGUMENT;
+    }
 }

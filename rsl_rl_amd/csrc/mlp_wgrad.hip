@@ -17,6 +17,7 @@
 // (TN = 64) rows 2, 3 (mod 4) swap their 64-B halves, which separates the banks of the four rows a 32-lane
 // transposed read spans; 64-B rows (TN = 32) need no permutation.
 #include <algorithm>
+#include <type_traits>
 
 #include "common.h"
 #include "x6_split.h"
@@ -38,6 +39,8 @@ struct WgradParams {
     int64_t rows_per;  // multiple of kMC
     int N;
     int K;
+    const float* dz_amax;  // h3 (PL = 2): max |dz|, max |x| -> the operands' power-of-two scales
+    const float* x_amax;
 };
 
 template <int COLS>
@@ -71,9 +74,9 @@ __device__ __forceinline__ void load_tile(const float* __restrict__ src, int ld,
     }
 }
 
-template <int COLS>
+template <int COLS, int PL>
 __device__ __forceinline__ void store_tile(const float4 (&v)[(kMC * COLS / 4 + kThreadsW - 1) / kThreadsW],
-                                           char* __restrict__ img) {
+                                           char* __restrict__ img, float sc) {
     constexpr int units = kMC * COLS / 4;
     constexpr int per = (units + kThreadsW - 1) / kThreadsW;
     constexpr int plane = kMC * COLS * 2;
@@ -83,19 +86,20 @@ __device__ __forceinline__ void store_tile(const float4 (&v)[(kMC * COLS / 4 + k
         if (units % kThreadsW == 0 || u < units) {
             const int m = u / (COLS / 4);
             const int c = 4 * (u % (COLS / 4));
-            uint2 p0, p1, p2;
-            split4(v[i], p0, p1, p2);
+            uint2 w[PL];
+            float4 x = v[i];
+            if constexpr (PL == 2) x = make_float4(x.x * sc, x.y * sc, x.z * sc, x.w * sc);
+            Arith<PL>::split(x, w);
             const int off = swz<COLS>(m, c);
-            *reinterpret_cast<uint2*>(img + off) = p0;
-            *reinterpret_cast<uint2*>(img + plane + off) = p1;
-            *reinterpret_cast<uint2*>(img + 2 * plane + off) = p2;
+#pragma unroll
+            for (int q = 0; q < PL; ++q) *reinterpret_cast<uint2*>(img + q * plane + off) = w[q];
         }
     }
 }
 
 // 32x32x16 operand fragment of columns [cb, cb + 32) (all 16 rows) of one plane, via two transposed reads
-template <int COLS>
-__device__ __forceinline__ bf16x8 read_frag_tr(const char* __restrict__ plane, int cb) {
+template <int COLS, typename F = bf16x8>
+__device__ __forceinline__ F read_frag_tr(const char* __restrict__ plane, int cb) {
     const int lane = threadIdx.x & 63;
     const int g = lane >> 4;
     const int q = (lane >> 2) & 3;
@@ -106,20 +110,21 @@ __device__ __forceinline__ bf16x8 read_frag_tr(const char* __restrict__ plane, i
     const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(plane + swz<COLS>(m, col)));
     const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(plane + swz<COLS>(m + 4, col)));
     const __attribute__((ext_vector_type(8))) short v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-    return __builtin_bit_cast(bf16x8, v);
+    return __builtin_bit_cast(F, v);
 }
 
 // TN = rows of dW per workgroup (256: waves 2 (n) x 4 (k), wave tile 128 x 64; 64: waves 2 x 4, 32 x 64;
 // 32: waves 1 x 8, 32 x 32)
-template <int TN, bool FULL>
+template <int TN, bool FULL, int PL = 3>
 __global__ __launch_bounds__(kThreadsW, 2) void wgrad_x6_kernel(WgradParams p) {
+    using Frag = typename Arith<PL>::frag;
     constexpr int WN = TN == 32 ? 1 : 2;
     constexpr int WK = 8 / WN;
     constexpr int I = TN / WN / 32;
     constexpr int J = kTK / WK / 32;
     constexpr int planeA = kMC * TN * 2;
     constexpr int planeB = kMC * kTK * 2;
-    constexpr int bufBytes = 3 * planeA + 3 * planeB;
+    constexpr int bufBytes = PL * planeA + PL * planeB;
     constexpr int perA = (kMC * TN / 4 + kThreadsW - 1) / kThreadsW;
     constexpr int perB = (kMC * kTK / 4 + kThreadsW - 1) / kThreadsW;
     __shared__ __attribute__((aligned(16))) char lds[2][bufBytes];
@@ -130,6 +135,8 @@ __global__ __launch_bounds__(kThreadsW, 2) void wgrad_x6_kernel(WgradParams p) {
     const int64_t m_begin = static_cast<int64_t>(blockIdx.x) * p.rows_per;
     const int64_t m_end = m_begin + p.rows_per < p.M ? m_begin + p.rows_per : p.M;
     const int nchunks = static_cast<int>((m_end - m_begin + kMC - 1) / kMC);
+    const float sa = PL == 2 ? h3_scale(*p.dz_amax) : 1.f;
+    const float sb = PL == 2 ? h3_scale(*p.x_amax) : 1.f;
 
     f32x16 acc[I][J];
 #pragma unroll
@@ -141,8 +148,8 @@ __global__ __launch_bounds__(kThreadsW, 2) void wgrad_x6_kernel(WgradParams p) {
     if (nchunks > 0) {
         load_tile<TN, FULL>(p.dz, p.N, m_begin, m_end, p.N, va);
         load_tile<kTK, FULL>(p.x, p.K, m_begin, m_end, p.K, vb);
-        store_tile<TN>(va, lds[0]);
-        store_tile<kTK>(vb, lds[0] + 3 * planeA);
+        store_tile<TN, PL>(va, lds[0], sa);
+        store_tile<kTK, PL>(vb, lds[0] + PL * planeA, sb);
     }
     __syncthreads();
     for (int c = 0; c < nchunks; ++c) {
@@ -154,23 +161,23 @@ __global__ __launch_bounds__(kThreadsW, 2) void wgrad_x6_kernel(WgradParams p) {
             load_tile<kTK, FULL>(p.x, p.K, m0, m_end, p.K, vb);
         }
         const char* a_img = lds[buf];
-        const char* b_img = lds[buf] + 3 * planeA;
-        bf16x8 bf[J][3];
+        const char* b_img = lds[buf] + PL * planeA;
+        Frag bf[J][PL];
 #pragma unroll
         for (int j = 0; j < J; ++j)
 #pragma unroll
-            for (int q = 0; q < 3; ++q) bf[j][q] = read_frag_tr<kTK>(b_img + q * planeB, wk * (J * 32) + j * 32);
+            for (int q = 0; q < PL; ++q) bf[j][q] = read_frag_tr<kTK, Frag>(b_img + q * planeB, wk * (J * 32) + j * 32);
 #pragma unroll
         for (int i = 0; i < I; ++i) {
-            bf16x8 af[3];
+            Frag af[PL];
 #pragma unroll
-            for (int q = 0; q < 3; ++q) af[q] = read_frag_tr<TN>(a_img + q * planeA, wn * (I * 32) + i * 32);
+            for (int q = 0; q < PL; ++q) af[q] = read_frag_tr<TN, Frag>(a_img + q * planeA, wn * (I * 32) + i * 32);
 #pragma unroll
-            for (int j = 0; j < J; ++j) acc[i][j] = mfma_x6(af, bf[j], acc[i][j]);
+            for (int j = 0; j < J; ++j) acc[i][j] = Arith<PL>::mfma(af, bf[j], acc[i][j]);
         }
         if (more) {
-            store_tile<TN>(va, lds[buf ^ 1]);
-            store_tile<kTK>(vb, lds[buf ^ 1] + 3 * planeA);
+            store_tile<TN, PL>(va, lds[buf ^ 1], sa);
+            store_tile<kTK, PL>(vb, lds[buf ^ 1] + PL * planeA, sb);
         }
         __syncthreads();
     }
@@ -179,6 +186,7 @@ __global__ __launch_bounds__(kThreadsW, 2) void wgrad_x6_kernel(WgradParams p) {
     const int lane = threadIdx.x & 63;
     const int l32 = lane & 31;
     const int h = lane >> 5;
+    const float unscale = PL == 2 ? (1.f / sa) * (1.f / sb) : 1.f;  // exact: powers of two
     float* out = p.part + static_cast<int64_t>(blockIdx.x) * p.N * p.K;
 #pragma unroll
     for (int i = 0; i < I; ++i)
@@ -188,7 +196,7 @@ __global__ __launch_bounds__(kThreadsW, 2) void wgrad_x6_kernel(WgradParams p) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int n = wn * (I * 32) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                if (n < p.N && k < p.K) out[n * p.K + k] = acc[i][j][r];
+                if (n < p.N && k < p.K) out[n * p.K + k] = PL == 2 ? acc[i][j][r] * unscale : acc[i][j][r];
             }
         }
 }
@@ -308,34 +316,44 @@ extern "C" int rslrl_fold_partials(const float* partials, int64_t S, int64_t NK,
     return launch_status();
 }
 
-extern "C" int rslrl_linear_wgrad(const float* dz, const float* x, int64_t M, int32_t N, int32_t K, float* dw,
-                                  void* workspace, size_t workspace_bytes, rslrl_stream_t stream) {
+extern "C" int rslrl_linear_wgrad_ex(const float* dz, const float* dz_amax, const float* x, const float* x_amax,
+                                     int64_t M, int32_t N, int32_t K, int32_t arith, float* dw, void* workspace,
+                                     size_t workspace_bytes, rslrl_stream_t stream) {
     if (M < 1 || N < 1 || K < 1 || N > 256 || K > kTK || (N & 3) || (K & 3)) return RSLRL_E_INVALID_ARGUMENT;
     if (!dz || !x || !dw || !workspace) return RSLRL_E_INVALID_ARGUMENT;
+    const bool h3 = arith == RSLRL_ARITH_H3;
+    if (!h3 && arith != RSLRL_ARITH_X6) return RSLRL_E_INVALID_ARGUMENT;
+    if (h3 && (!dz_amax || !x_amax)) return RSLRL_E_INVALID_ARGUMENT;
     if ((reinterpret_cast<uintptr_t>(dz) | reinterpret_cast<uintptr_t>(x)) & 15) return RSLRL_E_MISALIGNED;
     const int64_t rows_per = wgrad_rows_per(M, N);
     const int64_t S = ceil_div(M, rows_per);
     const size_t part_bytes = static_cast<size_t>(S) * N * K * sizeof(float);  // 16-byte multiple (N, K % 4)
     if (workspace_bytes < rslrl_linear_wgrad_workspace_bytes(M, N, K)) return RSLRL_E_WORKSPACE_TOO_SMALL;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    WgradParams p{dz, x, static_cast<float*>(workspace), M, rows_per, N, K};
+    WgradParams p{dz, x, static_cast<float*>(workspace), M, rows_per, N, K, dz_amax, x_amax};
     bool full = (M % rows_per == 0) && K == kTK;  // and N == TN, checked per branch
     const dim3 g(static_cast<unsigned>(S)), b(kThreadsW);
-    if (N <= 32) {
-        full = full && N == 32;
-        if (full) hipLaunchKernelGGL((wgrad_x6_kernel<32, true>), g, b, 0, st, p);
-        else hipLaunchKernelGGL((wgrad_x6_kernel<32, false>), g, b, 0, st, p);
-    } else if (N <= 64) {
-        full = full && N == 64;
-        if (full) hipLaunchKernelGGL((wgrad_x6_kernel<64, true>), g, b, 0, st, p);
-        else hipLaunchKernelGGL((wgrad_x6_kernel<64, false>), g, b, 0, st, p);
-    } else {
-        full = full && N == 256;
-        if (full) hipLaunchKernelGGL((wgrad_x6_kernel<256, true>), g, b, 0, st, p);
-        else hipLaunchKernelGGL((wgrad_x6_kernel<256, false>), g, b, 0, st, p);
-    }
+    auto go = [&](auto tn, auto pl) {
+        constexpr int TN = decltype(tn)::value, PL = decltype(pl)::value;
+        if (full && N == TN) hipLaunchKernelGGL((wgrad_x6_kernel<TN, true, PL>), g, b, 0, st, p);
+        else hipLaunchKernelGGL((wgrad_x6_kernel<TN, false, PL>), g, b, 0, st, p);
+    };
+    using I32 = std::integral_constant<int, 32>;
+    using I64 = std::integral_constant<int, 64>;
+    using I256 = std::integral_constant<int, 256>;
+    using P2 = std::integral_constant<int, 2>;
+    using P3 = std::integral_constant<int, 3>;
+    if (N <= 32) h3 ? go(I32{}, P2{}) : go(I32{}, P3{});
+    else if (N <= 64) h3 ? go(I64{}, P2{}) : go(I64{}, P3{});
+    else h3 ? go(I256{}, P2{}) : go(I256{}, P3{});
     int rc = launch_status();
     if (rc) return rc;
     return rslrl_fold_partials(static_cast<const float*>(workspace), S, static_cast<int64_t>(N) * K, dw,
                                static_cast<char*>(workspace) + part_bytes, workspace_bytes - part_bytes, stream);
+}
+
+extern "C" int rslrl_linear_wgrad(const float* dz, const float* x, int64_t M, int32_t N, int32_t K, float* dw,
+                                  void* workspace, size_t workspace_bytes, rslrl_stream_t stream) {
+    return rslrl_linear_wgrad_ex(dz, nullptr, x, nullptr, M, N, K, RSLRL_ARITH_X6, dw, workspace, workspace_bytes,
+                                 stream);
 }

@@ -41,18 +41,49 @@ def _stream(t):
 _FUSE_OUT = os.environ.get("RSLRL_FUSE_OUT", "1") == "1"  # output-layer backward in one launch
 _FUSE_OUT_FWD = os.environ.get("RSLRL_FUSE_OUT_FWD", "1") == "1"  # output-layer forward in the last hidden GEMM
 GEMM_F32 = 0  # v_mfma_f32_32x32x2_f32: exact f32 fma chain
-GEMM_X6 = 1   # fp32 split into 3 bf16 planes, 6 bf16 MFMA products, fp32 accumulation (default)
-_mode = GEMM_F32 if os.environ.get("RSLRL_GEMM_MODE", "x6") == "f32" else GEMM_X6
+GEMM_X6 = 1   # fp32 split into 3 bf16 planes, 6 bf16 MFMA products, fp32 accumulation
+GEMM_H3 = 2   # hidden-layer GEMMs on 2 fp16 planes of power-of-two scaled operands, 3 fp16 MFMA products
+#               (include/rslrl_amd.h rslrl_linear_gemm); the first layer (input without a producer max) and
+#               the output layer stay on x6
+_MODE_NAMES = {"f32": GEMM_F32, "x6": GEMM_X6, "h3": GEMM_H3}
+_mode = _MODE_NAMES.get(os.environ.get("RSLRL_GEMM_MODE", "h3"), GEMM_H3)
 
 
 def set_gemm_mode(mode: int) -> int:
-    """Select the arithmetic of the fused GEMMs (GEMM_F32 | GEMM_X6); returns the previous mode.  The
-    initial mode comes from RSLRL_GEMM_MODE=f32|x6 (default x6)."""
+    """Select the arithmetic of the fused GEMMs (GEMM_F32 | GEMM_X6 | GEMM_H3); returns the previous mode.  The
+    initial mode comes from RSLRL_GEMM_MODE=f32|x6|h3."""
     global _mode
-    if mode not in (GEMM_F32, GEMM_X6):
+    if mode not in (GEMM_F32, GEMM_X6, GEMM_H3):
         raise ValueError(f"unknown GEMM mode {mode}")
     prev, _mode = _mode, mode
     return prev
+
+
+def _split() -> bool:
+    """A split-precision MFMA mode (x6 or h3): B operands come from images."""
+    return _mode in (GEMM_X6, GEMM_H3)
+
+
+_amax_ws: dict = {}
+
+
+def _amax_workspace(device):
+    """Per-device {max bits, ticket} words of the amax reduction (zero once; every launch leaves them zero)."""
+    ws = _amax_ws.get(device)
+    if ws is None:
+        n = max(_lib.lib().rslrl_amax_workspace_bytes() // 4, 4)
+        ws = torch.zeros(n, dtype=torch.int32, device=device)
+        _amax_ws[device] = ws
+    return ws
+
+
+def _amax(t):
+    """max |t| as a 1-element device tensor (for an h3 operand whose producer did not publish one)."""
+    return t.detach().abs().amax().reshape(1).float()
+
+
+def _ptr(t):
+    return t.data_ptr() if t is not None else None
 
 
 # B-operand images (include/rslrl_amd.h rslrl_linear_prepare_bimages).  Weights can change in place without
@@ -95,8 +126,15 @@ def bimages(specs):
     if not todo:
         return out
     L = _lib.lib()
-    sizes = [(L.rslrl_linear_out_image_bytes() if key[4] == _lib.BIMAGE_LAYOUT_OUT else
-              L.rslrl_linear_bimage_bytes(depth)) // 4 for (_, _, _, _, depth, key) in todo]
+
+    def nbytes(depth, layout):
+        if layout == _lib.BIMAGE_LAYOUT_OUT:
+            return L.rslrl_linear_out_image_bytes()
+        if layout == _lib.BIMAGE_LAYOUT_H3:
+            return L.rslrl_linear_bimage_h3_bytes(depth)
+        return L.rslrl_linear_bimage_bytes(depth)
+
+    sizes = [nbytes(depth, key[4]) // 4 for (_, _, _, _, depth, key) in todo]
     buf = torch.empty(sum(sizes), dtype=torch.float32, device=todo[0][1].device)
     for start in range(0, len(todo), _lib.MAX_BIMAGES):
         part = todo[start:start + _lib.MAX_BIMAGES]
@@ -121,6 +159,32 @@ def bimages(specs):
 
 def bimage(w, transposed: bool):
     return bimages([(w, transposed)])[0]
+
+
+def _gemm(op, arith, a, a_amax, N, img, *, bias=None, h=None, c=None, colsum=None, wpart=None, out_img=None,
+          out_bias=None, y=None, nout=0, amax_out=None):
+    M, K = a.shape
+    args = _lib.LinearArgs(op, arith, a.data_ptr(), _ptr(a_amax), M, K, N, img.data_ptr(), _ptr(bias), _ptr(h), _ptr(c),
+                           _ptr(colsum), _ptr(wpart), _ptr(out_img), _ptr(out_bias), _ptr(y), nout, _ptr(amax_out),
+                           _ptr(_amax_workspace(a.device)) if amax_out is not None else None)
+    rc = _lib.lib().rslrl_linear_gemm(ctypes.byref(args), _stream(a))
+    _lib.check(rc, "rslrl_linear_gemm")
+
+
+def _tag(arith):
+    """Timer-span suffix of the h3 launches (bench.py prices them against the 3-product peak)."""
+    return "/h3" if arith == _lib.ARITH_H3 else ""
+
+
+def linear_fwd_ex(x, b, N: int, elu: bool, img, arith, x_amax=None, want_amax=False):
+    """(act(x W^T + b), max |y| or None) on the split MFMA path (arith _lib.ARITH_X6 with a layout-0 image, or
+    ARITH_H3 with a layout-H3 image and x_amax = max |x| as a device scalar)."""
+    M, K = x.shape
+    y = torch.empty(M, N, device=x.device, dtype=torch.float32)
+    amax = torch.empty(1, device=x.device, dtype=torch.float32) if want_amax else None
+    with timer.span(f"linear_fwd[M={M},K={K},N={N}]{_tag(arith)}", x.device, 4 * M * (K + N), 2 * M * K * N):
+        _gemm(_lib.LINEAR_FWD_ELU if elu else _lib.LINEAR_FWD, arith, x, x_amax, N, img, bias=b, c=y, amax_out=amax)
+    return y, amax
 
 
 def linear_fwd(x, w, b, elu: bool, img=None):
@@ -156,9 +220,22 @@ def linear_fwd_out(x, w, b, img, w_out, b_out, out_img, store_h: bool):
     return h, y
 
 
+def linear_fwd_out_ex(x, b, N: int, img, arith, x_amax, b_out, out_img, store_h: bool):
+    """linear_fwd_out with the hidden GEMM in either split arithmetic (see linear_fwd_ex)."""
+    M, K = x.shape
+    nout = b_out.shape[0]
+    h = torch.empty(M, N, device=x.device, dtype=torch.float32) if store_h else None
+    y = torch.empty(M, nout, device=x.device, dtype=torch.float32)
+    with timer.span(f"linear_fwd_out[M={M},K={K},N={N},out={nout}]{_tag(arith)}", x.device,
+                    4 * M * (K + nout + (N if store_h else 0)), 2 * M * N * (K + nout)):
+        _gemm(_lib.LINEAR_FWD_OUT, arith, x, x_amax, N, img, bias=b, c=h, out_img=out_img, out_bias=b_out, y=y,
+              nout=nout)
+    return h, y
+
+
 def _fuse_out_fwd(ws) -> bool:
-    """The last hidden layer and the output layer run as one linear_fwd_out launch (x6 only)."""
-    return _FUSE_OUT_FWD and _mode == GEMM_X6 and len(ws) >= 2 and ws[-1].shape[0] <= MAX_OUT_WIDTH \
+    """The last hidden layer and the output layer run as one linear_fwd_out launch (split modes only)."""
+    return _FUSE_OUT_FWD and _split() and len(ws) >= 2 and ws[-1].shape[0] <= MAX_OUT_WIDTH \
         and ws[-1].shape[1] % 4 == 0
 
 
@@ -182,7 +259,26 @@ def linear_dgrad_elu(dz, w, h, img=None):
     return out, db
 
 
-def linear_dgrad_elu_wgrad(dz, w, h, img):
+def linear_dgrad_elu_ex(dz, h, img, arith, dz_amax=None, want_amax=False):
+    """((dz W) * ELU'(h), its column sums, max |out| or None) on the split path; img: the B image of W^T in the
+    layout of arith (see linear_fwd_ex)."""
+    M, N = dz.shape
+    K = h.shape[1]
+    L = _lib.lib()
+    tiles = L.rslrl_linear_tiles(M)
+    out = torch.empty(M, K, device=dz.device, dtype=torch.float32)
+    part = torch.empty(K, tiles, device=dz.device, dtype=torch.float32)
+    amax = torch.empty(1, device=dz.device, dtype=torch.float32) if want_amax else None
+    with timer.span(f"linear_dgrad[M={M},Nred={N},K={K}]{_tag(arith)}", dz.device, 4 * M * (N + 2 * K),
+                    2 * M * K * N):
+        _gemm(_lib.LINEAR_DGRAD_ELU, arith, dz, dz_amax, K, img, h=h, c=out, colsum=part, amax_out=amax)
+    db = torch.empty(K, device=dz.device, dtype=torch.float32)
+    rc = L.rslrl_column_sum_fold(part.data_ptr(), tiles, K, db.data_ptr(), _stream(dz))
+    _lib.check(rc, "rslrl_column_sum_fold")
+    return out, db, amax
+
+
+def linear_dgrad_elu_wgrad(dz, w, h, img, want_amax=False):
     """Output-layer backward in one launch (x6; dz [M, Nred <= 16, % 4]): ((dz @ w) * ELU'(h), its column sums,
     dz^T h).  w is the layer weight [Nred, K] (only its image is read)."""
     M, N = dz.shape
@@ -192,10 +288,10 @@ def linear_dgrad_elu_wgrad(dz, w, h, img):
     out = torch.empty(M, K, device=dz.device, dtype=torch.float32)
     part = torch.empty(K, tiles, device=dz.device, dtype=torch.float32)
     wpart = torch.empty(tiles, N, K, device=dz.device, dtype=torch.float32)
+    amax = torch.empty(1, device=dz.device, dtype=torch.float32) if want_amax else None
     with timer.span(f"linear_dgrad_wgrad[M={M},Nred={N},K={K}]", dz.device, 4 * M * (N + 2 * K), 4 * M * K * N):
-        rc = L.rslrl_linear_dgrad_elu_wgrad(dz.data_ptr(), M, N, K, h.data_ptr(), out.data_ptr(), part.data_ptr(),
-                                            img.data_ptr(), wpart.data_ptr(), _stream(dz))
-    _lib.check(rc, "rslrl_linear_dgrad_elu_wgrad")
+        _gemm(_lib.LINEAR_DGRAD_ELU_WGRAD, _lib.ARITH_X6, dz, None, K, img, h=h, c=out, colsum=part, wpart=wpart,
+              amax_out=amax)
     db = torch.empty(K, device=dz.device, dtype=torch.float32)
     rc = L.rslrl_column_sum_fold(part.data_ptr(), tiles, K, db.data_ptr(), _stream(dz))
     _lib.check(rc, "rslrl_column_sum_fold")
@@ -204,29 +300,35 @@ def linear_dgrad_elu_wgrad(dz, w, h, img):
     ws = torch.empty(max(nbytes, 16) // 8, dtype=torch.float64, device=dz.device)
     rc = L.rslrl_fold_partials(wpart.data_ptr(), tiles, N * K, dw.data_ptr(), ws.data_ptr(), nbytes, _stream(dz))
     _lib.check(rc, "rslrl_fold_partials")
+    if want_amax:
+        return out, db, dw, amax
     return out, db, dw
 
 
-def linear_wgrad(dz, x):
-    """dz^T x ([N, K]) on the x6 weight-gradient kernel; dz [M, N], x [M, K], N, K <= 256 and 4-aligned."""
+def linear_wgrad(dz, x, arith=_lib.ARITH_X6, dz_amax=None, x_amax=None):
+    """dz^T x ([N, K]) on the split weight-gradient kernel (x6, or h3 with max |dz|, max |x| as device scalars);
+    dz [M, N], x [M, K], N, K <= 256 and 4-aligned."""
     M, N = dz.shape
     K = x.shape[1]
     L = _lib.lib()
     nbytes = L.rslrl_linear_wgrad_workspace_bytes(M, N, K)
     ws = torch.empty(nbytes // 4, dtype=torch.float32, device=dz.device)
     dw = torch.empty(N, K, dtype=torch.float32, device=dz.device)
-    with timer.span(f"linear_wgrad[M={M},N={N},K={K}]", dz.device, 4 * M * (N + K), 2 * M * K * N):
-        rc = L.rslrl_linear_wgrad(dz.data_ptr(), x.data_ptr(), M, N, K, dw.data_ptr(), ws.data_ptr(), nbytes,
-                                  _stream(dz))
-    _lib.check(rc, "rslrl_linear_wgrad")
+    if arith == _lib.ARITH_H3:
+        dz_amax = _amax(dz) if dz_amax is None else dz_amax
+        x_amax = _amax(x) if x_amax is None else x_amax
+    with timer.span(f"linear_wgrad[M={M},N={N},K={K}]{_tag(arith)}", dz.device, 4 * M * (N + K), 2 * M * K * N):
+        rc = L.rslrl_linear_wgrad_ex(dz.data_ptr(), _ptr(dz_amax), x.data_ptr(), _ptr(x_amax), M, N, K, arith,
+                                     dw.data_ptr(), ws.data_ptr(), nbytes, _stream(dz))
+    _lib.check(rc, "rslrl_linear_wgrad_ex")
     return dw
 
 
-def _weight_grad(dz, x, x6: bool):
-    # the x6 weight-gradient kernel computes TN x 256 tiles (TN = 32, 64 or 256 rows of its first operand):
-    # the square hidden layers run it as dz^T x; the first layer (input width <= 64) as (x^T dz)^T on the
-    # 64-row tiles; the narrow output layers stay on the split-K batched GEMM (networks/linear.py) unless
-    # their backward is fused (linear_dgrad_elu_wgrad)
+def _weight_grad(dz, x, x6: bool, h3=False, dz_amax=None, x_amax=None):
+    # the split weight-gradient kernel computes TN x 256 tiles (TN = 32, 64 or 256 rows of its first operand):
+    # the square hidden layers run it as dz^T x (h3 when both operands come from h3-layer producers); the first
+    # layer (input width <= 64) as (x^T dz)^T on the 64-row tiles (x6); the narrow output layers stay on the
+    # split-K batched GEMM (networks/linear.py) unless their backward is fused (linear_dgrad_elu_wgrad)
     if x6 and dz.shape[1] > 64 and x.shape[1] <= 64 and dz.shape[1] <= MAX_WIDTH and dz.shape[1] % 4 == 0:
         pad = (-x.shape[1]) % 4
         xp = F.pad(x, (0, pad)) if pad else x
@@ -236,8 +338,58 @@ def _weight_grad(dz, x, x6: bool):
         pad = (-dz.shape[1]) % 4
         if pad:  # the critic's 1-wide output
             return linear_wgrad(F.pad(dz, (0, pad)), x)[: dz.shape[1]]
+        if h3:
+            return linear_wgrad(dz, x, _lib.ARITH_H3, dz_amax, x_amax)
         return linear_wgrad(dz, x)
     return _splitk_weight_grad(dz, x)
+
+
+def _plan(ws):
+    """Per-layer arithmetic of a forward/backward pass in the current mode: returns (split, h3 flags per linear
+    layer l, fuse_out).  h3[l]: layer l's hidden GEMMs (forward; weight gradient; input gradient) run on h3 --
+    every layer whose input is a hidden activation, except the output layer (x6: its narrow GEMMs are
+    memory-bound and its fused backward is an x6 kernel)."""
+    split = _split()
+    nh = len(ws) - 1
+    h3 = [_mode == GEMM_H3 and 0 < l < nh for l in range(len(ws))]
+    return split, h3, _fuse_out_fwd(ws)
+
+
+def _forward_images(ws, h3, fuse_out, backward: bool):
+    nh = len(ws) - 1
+    lay = lambda l: _lib.BIMAGE_LAYOUT_H3 if h3[l] else _lib.BIMAGE_LAYOUT_GEMM  # noqa: E731
+    specs = [(w, False, lay(l)) for l, w in enumerate(ws[:-1])]
+    if backward:  # transposed images of layers 1..L-1 for the input gradients
+        specs += [(w, True, lay(l)) for l, w in enumerate(ws) if l > 0]
+    if fuse_out:
+        specs.append((ws[-1], False, _lib.BIMAGE_LAYOUT_OUT))
+    imgs = bimages(specs)
+    fwd = imgs[:nh]
+    dgrad = [None] + imgs[nh:2 * nh] if backward else None
+    out = imgs[-1] if fuse_out else None
+    return fwd, dgrad, out
+
+
+def _hidden_forward(x, ws, bs, h3, fuse_out, fwd_imgs, out_img, keep: bool):
+    """Hidden layers (+ the fused output layer).  Returns (hs, amaxes, y): hs[l] = input of linear l (only
+    stored when keep), amaxes[l] = max |hs[l]| when an h3 consumer needs it, y = output (None unless fused)."""
+    nh = len(ws) - 1
+    arith = lambda l: _lib.ARITH_H3 if h3[l] else _lib.ARITH_X6  # noqa: E731
+    hs, amaxes = [x], [None]
+    h, y = x, None
+    for l in range(nh):
+        # max |H_{l+1}| is needed when linear l+1 (a hidden layer) is h3: its forward, and in backward its
+        # weight gradient
+        want = l + 1 < nh and h3[l + 1]
+        if fuse_out and l == nh - 1:
+            h, y = linear_fwd_out_ex(h, bs[l], ws[l].shape[0], fwd_imgs[l], arith(l), amaxes[l], bs[-1], out_img,
+                                     store_h=keep)
+            amax = None
+        else:
+            h, amax = linear_fwd_ex(h, bs[l], ws[l].shape[0], True, fwd_imgs[l], arith(l), amaxes[l], want)
+        hs.append(h)
+        amaxes.append(amax)
+    return hs, amaxes, y
 
 
 class FusedMLPFunction(torch.autograd.Function):
@@ -246,27 +398,23 @@ class FusedMLPFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, *params):
         ws, bs = params[0::2], params[1::2]
-        hs = [x]
-        h = x
-        x6 = _mode == GEMM_X6
+        split, h3, fuse_out = _plan(ws)
         nh = len(ws) - 1
-        fuse_out = _fuse_out_fwd(ws)
-        # forward images of the hidden layers + (for backward) the transposed images of layers 1..L-1
-        # [+ the output-layer image]
-        specs = [(w, False) for w in ws[:-1]] + [(w, True) for w in ws[1:]]
-        if fuse_out:
-            specs.append((ws[-1], False, _lib.BIMAGE_LAYOUT_OUT))
-        imgs = bimages(specs) if x6 else [None] * (2 * nh)
-        for l, (w, b, img) in enumerate(zip(ws[:-1], bs[:-1], imgs[:nh])):
-            if fuse_out and l == nh - 1:
-                h, y = linear_fwd_out(h, w, b, img, ws[-1], bs[-1], imgs[2 * nh], store_h=True)
-            else:
-                h = linear_fwd(h, w, b, elu=True, img=img)
-            hs.append(h)
-        ctx.dgrad_imgs = [None] + imgs[nh:2 * nh]  # index l: image of W_l^T
-        ctx.x6 = x6
-        if not fuse_out:
-            y = F.linear(h, ws[-1], bs[-1])
+        if split:
+            fwd_imgs, dgrad_imgs, out_img = _forward_images(ws, h3, fuse_out, backward=True)
+            hs, amaxes, y = _hidden_forward(x, ws, bs, h3, fuse_out, fwd_imgs, out_img, keep=True)
+        else:
+            hs, amaxes, h = [x], [None] * (nh + 1), x
+            for l in range(nh):
+                h = linear_fwd(h, ws[l], bs[l], elu=True)
+                hs.append(h)
+            dgrad_imgs, y = [None] * (nh + 1), None
+        if y is None:
+            y = F.linear(hs[-1], ws[-1], bs[-1])
+        ctx.dgrad_imgs = dgrad_imgs  # index l: image of W_l^T
+        ctx.amaxes = amaxes
+        ctx.h3 = h3
+        ctx.x6 = split
         ctx.save_for_backward(*hs, *params)
         ctx.n_layers = len(ws)
         return y
@@ -277,9 +425,11 @@ class FusedMLPFunction(torch.autograd.Function):
         saved = ctx.saved_tensors
         hs, params = saved[:L], saved[L:]
         ws = params[0::2]
+        h3 = ctx.h3
         grads_w = [None] * L
         grads_b = [None] * L
         dz = dy.contiguous()
+        dz_amax = None
         grads_b[L - 1] = dz.sum(0)
         for l in range(L - 1, -1, -1):
             h_in = hs[l]
@@ -289,10 +439,14 @@ class FusedMLPFunction(torch.autograd.Function):
                 nred = dz.shape[1]
                 pad = (-nred) % 4
                 dzp = F.pad(dz, (0, pad)) if pad else dz
-                dz, grads_b[l - 1], dw = linear_dgrad_elu_wgrad(dzp, ws[l], h_in, ctx.dgrad_imgs[l])
+                want = l - 1 > 0 and h3[l - 1]
+                res = linear_dgrad_elu_wgrad(dzp, ws[l], h_in, ctx.dgrad_imgs[l], want_amax=want)
+                dz, grads_b[l - 1], dw = res[:3]
+                dz_amax = res[3] if want else None
                 grads_w[l] = dw[:nred]
                 continue
-            grads_w[l] = _weight_grad(dz, h_in, ctx.x6) if ctx.needs_input_grad[1 + 2 * l] else None
+            if ctx.needs_input_grad[1 + 2 * l]:
+                grads_w[l] = _weight_grad(dz, h_in, ctx.x6, h3[l], dz_amax, ctx.amaxes[l])
             if l == 0:
                 dx = dz.mm(ws[0]) if ctx.needs_input_grad[0] else None
                 break
@@ -306,7 +460,16 @@ class FusedMLPFunction(torch.autograd.Function):
                 dz = F.pad(dz, (0, pad))
                 if img is None:
                     w = F.pad(w, (0, 0, 0, pad))
-            dz, grads_b[l - 1] = linear_dgrad_elu(dz, w, h_in, img)
+            if h3[l]:
+                want = l - 1 > 0 and h3[l - 1]
+                dz_amax = _amax(dz) if dz_amax is None else dz_amax
+                dz, grads_b[l - 1], dz_amax = linear_dgrad_elu_ex(dz, h_in, img, _lib.ARITH_H3, dz_amax, want)
+            elif img is not None:
+                want = l - 1 > 0 and h3[l - 1]
+                dz, grads_b[l - 1], dz_amax = linear_dgrad_elu_ex(dz, h_in, img, _lib.ARITH_X6, None, want)
+            else:
+                dz, grads_b[l - 1] = linear_dgrad_elu(dz, w, h_in, None)
+                dz_amax = None
         out = [dx]
         for gw, gb in zip(grads_w, grads_b):
             out += [gw, gb]
@@ -343,20 +506,17 @@ def fused_mlp_forward(mlp: nn.Sequential, x: torch.Tensor) -> torch.Tensor:
     if torch.is_grad_enabled() and any(p.requires_grad for p in params + [x]):
         y = FusedMLPFunction.apply(x, *params)
     else:
-        h = x
-        nh = len(linears) - 1
         ws = [m.weight for m in linears]
-        fuse_out = _fuse_out_fwd(ws)
-        specs = [(w, False) for w in ws[:-1]]
-        if fuse_out:
-            specs.append((ws[-1], False, _lib.BIMAGE_LAYOUT_OUT))
-        imgs = bimages(specs) if _mode == GEMM_X6 else [None] * nh
-        y = None
-        for l, (m, img) in enumerate(zip(linears[:-1], imgs)):
-            if fuse_out and l == nh - 1:  # the last activation never reaches HBM
-                _, y = linear_fwd_out(h, m.weight, m.bias, img, ws[-1], linears[-1].bias, imgs[nh], store_h=False)
-            else:
-                h = linear_fwd(h, m.weight, m.bias, elu=True, img=img)
+        bs = [m.bias for m in linears]
+        split, h3, fuse_out = _plan(ws)
+        if split:  # the last activation never reaches HBM when the output layer is fused
+            fwd_imgs, _, out_img = _forward_images(ws, h3, fuse_out, backward=False)
+            hs, _, y = _hidden_forward(x, ws, bs, h3, fuse_out, fwd_imgs, out_img, keep=False)
+            h = hs[-1]
+        else:
+            h, y = x, None
+            for m in linears[:-1]:
+                h = linear_fwd(h, m.weight, m.bias, elu=True)
         if y is None:
             y = F.linear(h, linears[-1].weight, linears[-1].bias)
     for m in mlp:

@@ -1,5 +1,5 @@
 set -e
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_gpu_loss.py tests/test_gpu_update.py -x -q --timeout 120 --timeout-method thread > gpurun_out/loss_tests.log 2>&1
-timeout -k 10 120 python scripts/hotpath_microbench.py --only loss,loss_perrow --iters 200 > gpurun_out/mb_auto.json
-RSLRL_LOSS_KERNEL=lane timeout -k 10 120 python scripts/hotpath_microbench.py --only loss,loss_perrow --iters 200 > gpurun_out/mb_lane.json
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
+timeout -k 10 500 python bench.py > gpurun_out/bench_default.json 2> gpurun_out/bench_default.err

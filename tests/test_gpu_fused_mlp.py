@@ -19,9 +19,9 @@ def _close(a, b, tol=TOL):
     assert (a - b).abs().max().item() <= tol * b.abs().max().item() + 1e-12, (a - b).abs().max().item()
 
 
-@pytest.fixture(params=["x6", "f32"])
+@pytest.fixture(params=["x6", "f32", "h3"])
 def gemm_mode(request):
-    prev = fused_mlp.set_gemm_mode(fused_mlp.GEMM_X6 if request.param == "x6" else fused_mlp.GEMM_F32)
+    prev = fused_mlp.set_gemm_mode(fused_mlp._MODE_NAMES[request.param])
     yield request.param
     fused_mlp.set_gemm_mode(prev)
 
@@ -43,7 +43,7 @@ def test_linear_fwd(M, K, N, elu, gemm_mode, cuda_device):
     ref = torch.nn.functional.linear(x, w, b)
     if elu:
         ref = torch.nn.functional.elu(ref)
-    _close(linear_fwd(x, w, b, elu, bimage(w, False) if gemm_mode == "x6" else None), ref)
+    _close(linear_fwd(x, w, b, elu, bimage(w, False) if gemm_mode != "f32" else None), ref)
 
 
 @pytest.mark.parametrize("M,N,K", [(393216, 256, 256), (5000, 12, 256), (1000, 64, 64), (300, 48, 48)])
@@ -52,7 +52,7 @@ def test_linear_dgrad_elu(M, N, K, gemm_mode, cuda_device):
     dz = torch.randn(M, N, device=cuda_device)
     w = torch.randn(N, K, device=cuda_device) / N ** 0.5
     h = torch.nn.functional.elu(torch.randn(M, K, device=cuda_device))
-    out, db = linear_dgrad_elu(dz, w, h, bimage(w, True) if gemm_mode == "x6" else None)
+    out, db = linear_dgrad_elu(dz, w, h, bimage(w, True) if gemm_mode != "f32" else None)
     ref = dz.mm(w)
     ref = torch.where(h > 0, ref, ref * (h + 1))
     _close(out, ref)
