@@ -66,6 +66,7 @@ struct GemmParams {
     const float* a_amax;  // h3: max |A| (device scalar written by A's producer) -> A's power-of-two scale
     float* amax_out;      // optional: max |C| over the stored output (device scalar, for an h3 consumer)
     unsigned* amax_ws;    // with amax_out: {running max bits, arrival ticket}, zero before and after the launch
+    int deep;             // h3, K = 256: the unrolled look-ahead main loop (h3_deep_loop)
 };
 
 // global -> registers for one K chunk: A: 128 x 16 floats = 512 float4 (1 per thread); B: 256 x 16 = 1024
@@ -538,6 +539,12 @@ __device__ __forceinline__ F read_frag(const char* __restrict__ plane, int row, 
 // never visible before the max it follows.  An agent-scope release fence here would write back the L2 of
 // every XCD per workgroup (+150-200 us per launch measured).  Every thread of the workgroup calls this.
 constexpr int kAmaxGroups = 64;
+#ifndef RSLRL_H3_DEPTH
+#define RSLRL_H3_DEPTH 2
+#endif
+constexpr int kH3Depth = RSLRL_H3_DEPTH;  // A look-ahead (chunks) of the unrolled h3 main loop
+constexpr int kH3DeepDefault = (1 << RSLRL_LINEAR_FWD) | (1 << RSLRL_LINEAR_FWD_ELU) | (1 << RSLRL_LINEAR_DGRAD_ELU) |
+                               (1 << RSLRL_LINEAR_FWD_OUT);
 __device__ __forceinline__ void amax_commit(const GemmParams& p, float amx) {
     if (!p.amax_out) return;  // uniform
     __shared__ float wave_max[kThreads / 64];
@@ -576,6 +583,98 @@ __device__ __forceinline__ void amax_commit(const GemmParams& p, float amx) {
     clear_(ws + 2 * kAmaxGroups + 1);
 }
 
+// h3 main loop for a compile-time chunk count (K = 16 NCH, full tiles), fully unrolled so the A operand can be
+// fetched D chunks ahead into registers (sa_[k % D] holds chunk k) -- the one-chunk look-ahead of the generic
+// loop leaves each chunk waiting out an HBM load latency.  The B image chunk goes through registers as well
+// (16-byte loads + ds_write_b128, one chunk ahead): with a global_load_lds DMA in flight the compiler waits
+// vmcnt(0) before every LDS read (it cannot tell the DMA's buffer from the one being read), which would drain
+// the A look-ahead every chunk.  Per chunk c: read every fragment of chunk c, write A(c+1) and B(c+1) into the
+// other buffer, fetch A(c+1+D) and B(c+2), MFMAs, barrier (LDS writes only: lgkmcnt(0)).
+template <int PL>
+struct BStage {
+    uint4 u[PL];
+};
+
+template <int PL>
+__device__ __forceinline__ BStage<PL> load_b_regs(const uint4* __restrict__ img, int c) {
+    const uint4* src = img + static_cast<int64_t>(c) * (PL * kX6PlaneB / 16);
+    BStage<PL> b;
+#pragma unroll
+    for (int i = 0; i < PL; ++i) b.u[i] = src[threadIdx.x + kThreads * i];
+    return b;
+}
+
+template <int PL>
+__device__ __forceinline__ void store_b_regs(BStage<PL>& b, char* b_lds) {
+#pragma unroll
+    for (int i = 0; i < PL; ++i) {
+        asm volatile("" : "+v"(b.u[i].x), "+v"(b.u[i].y), "+v"(b.u[i].z), "+v"(b.u[i].w));
+        *reinterpret_cast<uint4*>(b_lds + 16 * (threadIdx.x + kThreads * i)) = b.u[i];
+    }
+}
+
+template <int EPI, int BM, int PL, int NCH, int D, typename Frag>
+__device__ __forceinline__ void h3_deep_loop(const GemmParams& p, int64_t row0, const uint4* __restrict__ bimg,
+                                             char* (&lds)[2], f32x16 (&acc)[BM / 64][2], float sa, int wm,
+                                             int wn, int l32, int h) {
+    constexpr int I = BM / 64;
+    constexpr int planeA = BM * kX6RowB;
+    AStage<BM> sa_[D];
+    BStage<PL> sb;
+    {
+        BStage<PL> b0 = load_b_regs<PL>(bimg, 0);
+        store_b_regs<PL>(b0, lds[0] + PL * planeA);
+    }
+    store_a_split<BM, PL>(load_a<BM, true>(p, row0, 0), lds[0], sa);
+#pragma unroll
+    for (int d = 1; d <= D; ++d)
+        if (d < NCH) sa_[d % D] = load_a<BM, true>(p, row0, d * kKC);
+    if (NCH > 1) sb = load_b_regs<PL>(bimg, 1);
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+        const char* a_lds = lds[c & 1];
+        const char* b_lds = lds[c & 1] + PL * planeA;
+        Frag bf[2][PL], af[I][PL];
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int q = 0; q < PL; ++q) bf[j][q] = read_frag<Frag>(b_lds + q * kX6PlaneB, wn * 64 + j * 32 + l32, h);
+#pragma unroll
+        for (int i = 0; i < I; ++i)
+#pragma unroll
+            for (int q = 0; q < PL; ++q) af[i][q] = read_frag<Frag>(a_lds + q * planeA, wm * (BM / 2) + i * 32 + l32, h);
+        if (c + 1 < NCH) {  // buffer (c+1)&1 was last read in chunk c-1; every wave passed the barrier after it
+            // pin the use of the prefetched registers here: otherwise the scheduler hoists the scaling
+            // multiply right behind the load and the wave waits out the look-ahead right away
+#pragma unroll
+            for (int u = 0; u < BM / 128; ++u) {
+                float4& v = sa_[(c + 1) % D].v[u];
+                asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w));
+            }
+            store_a_split<BM, PL>(sa_[(c + 1) % D], lds[(c + 1) & 1], sa);
+            store_b_regs<PL>(sb, lds[(c + 1) & 1] + PL * planeA);
+            if (c + 1 + D < NCH) sa_[(c + 1) % D] = load_a<BM, true>(p, row0, (c + 1 + D) * kKC);
+            if (c + 2 < NCH) sb = load_b_regs<PL>(bimg, c + 2);
+        }
+#pragma unroll
+        for (int i = 0; i < I; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                if constexpr (EPI == kEpiBiasEluOut)
+                    acc[i][j] = Arith<PL>::mfma(bf[j], af[i], acc[i][j]);
+                else
+                    acc[i][j] = Arith<PL>::mfma(af[i], bf[j], acc[i][j]);
+            }
+        // only LDS writes to retire (lgkmcnt); __syncthreads' release fence would also wait vmcnt(0) and drain
+        // the look-ahead every chunk
+        if (c + 1 < NCH)
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        else
+            __syncthreads();  // the epilogue may reuse the LDS
+    }
+}
+
 // 128 rows x 256 columns per workgroup: waves 2 (M) x 4 (N) of 64 x 64 (2 x 2 MFMA tiles); MINW = 4:
 // two workgroups per CU (<= 128 VGPRs), 2: one (the register-hungrier short-K dgrad epilogues).
 // NR: rows of the fused weight gradient (kEpiEluGradWgrad: Nred rounded up to 4; otherwise unused).
@@ -587,9 +686,16 @@ __global__ __launch_bounds__(kThreads, MINW) void mlp_gemm_x6_kernel(GemmParams 
     constexpr int BM = kBM;
     constexpr int I = BM / 64;
     constexpr int planeA = BM * kX6RowB;
-    // the fused output layer's epilogue (h stage + reduction tiles) needs the x6 main loop's 72 KiB
-    constexpr int bufBytes = EPI == kEpiBiasEluOut ? (3 * planeA + 3 * kX6PlaneB) : (PL * planeA + PL * kX6PlaneB);
-    __shared__ __attribute__((aligned(16))) char lds[2][bufBytes];
+    // the fused output layer's epilogue needs 40 KiB per buffer (h stage in one, reduction tiles in the other)
+    constexpr int bufBytes = EPI == kEpiBiasEluOut ? 40960 : (PL * planeA + PL * kX6PlaneB);
+    static_assert(bufBytes >= PL * planeA + PL * kX6PlaneB, "LDS buffer");
+    // two LDS objects, not one [2][bytes] array: the waitcnt pass can then tell a DMA into one buffer from
+    // reads of the other (distinct alias scopes) where the buffer index is a compile-time constant
+    __shared__ __attribute__((aligned(16))) char lds_b0[bufBytes];
+    __shared__ __attribute__((aligned(16))) char lds_b1[bufBytes];
+    char* lds[2];
+    lds[0] = lds_b0;
+    lds[1] = lds_b1;
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int wm = wave >> 2;  // rows wm * BM / 2
@@ -608,44 +714,85 @@ __global__ __launch_bounds__(kThreads, MINW) void mlp_gemm_x6_kernel(GemmParams 
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
 
+    const float sa = PL == 2 ? h3_scale(*p.a_amax) : 1.f;
+    bool deep = false;
+    if constexpr (PL == 2 && FULL) {
+        if (p.K == 16 * kKC && p.deep) {
+            h3_deep_loop<EPI, BM, PL, 16, kH3Depth, Frag>(p, row0, bimg, lds, acc, sa, wm, wn, l32, h);
+            deep = true;
+        }
+    }
     // Pipeline: B of chunk c+1 is copied (global_load_lds) and A of chunk c+1 fetched into registers at
     // the start of chunk c; A is split into the other LDS buffer at its end.
-    const int nchunks = (p.K + kKC - 1) / kKC;
-    const float sa = PL == 2 ? h3_scale(*p.a_amax) : 1.f;
+    const int nchunks = deep ? 0 : (p.K + kKC - 1) / kKC;
+    if (!deep) {
     load_b_lds<PL>(bimg, 0, lds[0] + PL * planeA);
     store_a_split<BM, PL>(load_a<BM, FULL>(p, row0, 0), lds[0], sa);
     __syncthreads();
     for (int c = 0; c < nchunks; ++c) {
         const int buf = c & 1;
         const bool more = c + 1 < nchunks;
-        AStage<BM> an;
-        if (more) {  // the other buffer was last read in chunk c-1, and every wave passed the barrier after it
-            load_b_lds<PL>(bimg, c + 1, lds[buf ^ 1] + PL * planeA);
-            an = load_a<BM, FULL>(p, row0, (c + 1) * kKC);
-        }
         const char* a_lds = lds[buf];
         const char* b_lds = lds[buf] + PL * planeA;
+        AStage<BM> an;
         Frag bf[2][PL];
+        if constexpr (PL == 2) {
+            // h3: every fragment of the chunk is read before the next chunk's loads issue -- the compiler
+            // cannot tell the global_load_lds destination (the other buffer) from this one and waits
+            // vmcnt(0) before any LDS read that follows it, which would expose the loads' full latency
+            Frag af[I][PL];
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+            for (int j = 0; j < 2; ++j)
 #pragma unroll
-            for (int q = 0; q < PL; ++q) bf[j][q] = read_frag<Frag>(b_lds + q * kX6PlaneB, wn * 64 + j * 32 + l32, h);
+                for (int q = 0; q < PL; ++q)
+                    bf[j][q] = read_frag<Frag>(b_lds + q * kX6PlaneB, wn * 64 + j * 32 + l32, h);
 #pragma unroll
-        for (int i = 0; i < I; ++i) {
-            Frag af[PL];
+            for (int i = 0; i < I; ++i)
 #pragma unroll
-            for (int q = 0; q < PL; ++q) af[q] = read_frag<Frag>(a_lds + q * planeA, wm * (BM / 2) + i * 32 + l32, h);
+                for (int q = 0; q < PL; ++q)
+                    af[i][q] = read_frag<Frag>(a_lds + q * planeA, wm * (BM / 2) + i * 32 + l32, h);
+            if (more) {  // the other buffer was last read in chunk c-1, and every wave passed the barrier after it
+                load_b_lds<PL>(bimg, c + 1, lds[buf ^ 1] + PL * planeA);
+                an = load_a<BM, FULL>(p, row0, (c + 1) * kKC);
+            }
 #pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                if constexpr (EPI == kEpiBiasEluOut)  // C^T tile: the weight fragment is the MFMA's A operand
-                    acc[i][j] = Arith<PL>::mfma(bf[j], af, acc[i][j]);
-                else
-                    acc[i][j] = Arith<PL>::mfma(af, bf[j], acc[i][j]);
+            for (int i = 0; i < I; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    if constexpr (EPI == kEpiBiasEluOut)  // C^T tile: the weight fragment is the MFMA's A operand
+                        acc[i][j] = Arith<PL>::mfma(bf[j], af[i], acc[i][j]);
+                    else
+                        acc[i][j] = Arith<PL>::mfma(af[i], bf[j], acc[i][j]);
+                }
+        } else {
+            if (more) {  // the other buffer was last read in chunk c-1, and every wave passed the barrier after it
+                load_b_lds<PL>(bimg, c + 1, lds[buf ^ 1] + PL * planeA);
+                an = load_a<BM, FULL>(p, row0, (c + 1) * kKC);
+            }
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int q = 0; q < PL; ++q)
+                    bf[j][q] = read_frag<Frag>(b_lds + q * kX6PlaneB, wn * 64 + j * 32 + l32, h);
+#pragma unroll
+            for (int i = 0; i < I; ++i) {
+                Frag af[PL];
+#pragma unroll
+                for (int q = 0; q < PL; ++q)
+                    af[q] = read_frag<Frag>(a_lds + q * planeA, wm * (BM / 2) + i * 32 + l32, h);
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    if constexpr (EPI == kEpiBiasEluOut)  // C^T tile: the weight fragment is the MFMA's A operand
+                        acc[i][j] = Arith<PL>::mfma(bf[j], af, acc[i][j]);
+                    else
+                        acc[i][j] = Arith<PL>::mfma(af, bf[j], acc[i][j]);
+                }
             }
         }
         if (more) store_a_split<BM, PL>(an, lds[buf ^ 1], sa);
         __syncthreads();  // also retires the global_load_lds of chunk c+1 (vmcnt(0))
     }
+    }  // !deep
     const float inv_sa = 1.f / sa;
     if constexpr (PL == 2) {
         // undo the operand scales: C[m][n] = acc / (s_a t_n), exact (powers of two)
@@ -731,8 +878,13 @@ __global__ __launch_bounds__(kThreads, MINW) void mlp_gemm_x6_kernel(GemmParams 
         // C^T stores write 32-B pieces: +48 us per launch at M = 393216).  red: [wm][wn][i][o][32 rows].
         const bool staged = p.c != nullptr && p.nout <= kStagedOutWidth;
         const int red_rows = staged ? kStagedOutWidth : 32;
-        float* stage = reinterpret_cast<float*>(&lds[0][0]) + wave * 1024;
-        float* red = reinterpret_cast<float*>(&lds[0][0]) + (staged ? 8 * 1024 : 0);
+        // stage: buffer 0 (32 KiB); red: [wm][wn][i][o][32] in buffer 1 when staged (<= 40 KiB), else wave row wm
+        // in buffer wm (32 KiB each)
+        float* stage = reinterpret_cast<float*>(lds[0]) + wave * 1024;
+        const int tile = red_rows * 32;
+        auto red_of = [&](int w) {
+            return staged ? reinterpret_cast<float*>(lds[1]) + w * 4 * I * tile : reinterpret_cast<float*>(lds[w]);
+        };
         const uint4* oimg = p.oimg + wn * (2 * 2 * 3 * 64);
         const bool valu = p.nout <= 4;  // the critic's value head: VALU dot products beat 32-row MFMA tiles
 #pragma unroll
@@ -823,7 +975,7 @@ __global__ __launch_bounds__(kThreads, MINW) void mlp_gemm_x6_kernel(GemmParams 
                     oacc = mfma_x6(wa, vb, oacc);
                 }
             }
-            float* rd = red + ((wm * 4 + wn) * I + i) * red_rows * 32;
+            float* rd = red_of(wm) + (wn * I + i) * tile;
             if (valu) {  // the two lane halves hold different columns of the same row
 #pragma unroll
                 for (int o = 0; o < 4; ++o) {
@@ -843,8 +995,7 @@ __global__ __launch_bounds__(kThreads, MINW) void mlp_gemm_x6_kernel(GemmParams 
         for (int idx = threadIdx.x; idx < BM * nout; idx += kThreads) {
             const int rl = idx / nout;
             const int o = idx - rl * nout;
-            const int tile = red_rows * 32;
-            const float* b = red + (((rl >> 6) * 4) * I + ((rl & 63) >> 5)) * tile + o * 32 + (rl & 31);
+            const float* b = red_of(rl >> 6) + ((rl & 63) >> 5) * tile + o * 32 + (rl & 31);
             const float sum = ((b[0] + b[I * tile]) + b[2 * I * tile]) + b[3 * I * tile];
             const int64_t row = row0 + rl;
             if (row < p.M) p.y[row * nout + o] = sum + p.obias[o];
@@ -1310,6 +1461,16 @@ extern "C" int rslrl_column_sum_fold(const float* partials, int64_t tiles, int32
 
 extern "C" size_t rslrl_amax_workspace_bytes(void) { return 1024; }
 
+namespace {
+// RSLRL_H3_DEEP = bit mask over ops (1 << RSLRL_LINEAR_*) taking the look-ahead main loop; read per call
+// (A/B measurements in one process)
+int h3_deep(int op) {
+    const char* e = std::getenv("RSLRL_H3_DEEP");
+    const int mask = e ? std::atoi(e) : kH3DeepDefault;
+    return (mask >> op) & 1;
+}
+}  // namespace
+
 // One entry point for every fused linear op in either split arithmetic, with the h3 operand scales
 // (include/rslrl_amd.h rslrl_linear_args_t).
 extern "C" int rslrl_linear_gemm(const rslrl_linear_args_t* a, rslrl_stream_t stream) {
@@ -1333,6 +1494,7 @@ extern "C" int rslrl_linear_gemm(const rslrl_linear_args_t* a, rslrl_stream_t st
     p.a_amax = a->a_amax;
     p.amax_out = a->amax_out;
     p.amax_ws = static_cast<unsigned*>(a->amax_workspace);
+    p.deep = h3_deep(op);
     switch (op) {
         case RSLRL_LINEAR_FWD:
         case RSLRL_LINEAR_FWD_ELU:
