@@ -540,7 +540,7 @@ __device__ __forceinline__ F read_frag(const char* __restrict__ plane, int row, 
 // every XCD per workgroup (+150-200 us per launch measured).  Every thread of the workgroup calls this.
 constexpr int kAmaxGroups = 64;
 #ifndef RSLRL_H3_DEPTH
-#define RSLRL_H3_DEPTH 2
+#define RSLRL_H3_DEPTH 3
 #endif
 constexpr int kH3Depth = RSLRL_H3_DEPTH;  // A look-ahead (chunks) of the unrolled h3 main loop
 constexpr int kH3DeepDefault = (1 << RSLRL_LINEAR_FWD) | (1 << RSLRL_LINEAR_FWD_ELU) | (1 << RSLRL_LINEAR_DGRAD_ELU) |
@@ -635,15 +635,24 @@ __device__ __forceinline__ void h3_deep_loop(const GemmParams& p, int64_t row0, 
     for (int c = 0; c < NCH; ++c) {
         const char* a_lds = lds[c & 1];
         const char* b_lds = lds[c & 1] + PL * planeA;
-        Frag bf[2][PL], af[I][PL];
+        Frag bf[2][PL];
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
             for (int q = 0; q < PL; ++q) bf[j][q] = read_frag<Frag>(b_lds + q * kX6PlaneB, wn * 64 + j * 32 + l32, h);
 #pragma unroll
-        for (int i = 0; i < I; ++i)
+        for (int i = 0; i < I; ++i) {
+            Frag af[PL];
 #pragma unroll
-            for (int q = 0; q < PL; ++q) af[i][q] = read_frag<Frag>(a_lds + q * planeA, wm * (BM / 2) + i * 32 + l32, h);
+            for (int q = 0; q < PL; ++q) af[q] = read_frag<Frag>(a_lds + q * planeA, wm * (BM / 2) + i * 32 + l32, h);
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                if constexpr (EPI == kEpiBiasEluOut)
+                    acc[i][j] = Arith<PL>::mfma(bf[j], af, acc[i][j]);
+                else
+                    acc[i][j] = Arith<PL>::mfma(af, bf[j], acc[i][j]);
+            }
+        }
         if (c + 1 < NCH) {  // buffer (c+1)&1 was last read in chunk c-1; every wave passed the barrier after it
             // pin the use of the prefetched registers here: otherwise the scheduler hoists the scaling
             // multiply right behind the load and the wave waits out the look-ahead right away
@@ -657,15 +666,6 @@ __device__ __forceinline__ void h3_deep_loop(const GemmParams& p, int64_t row0, 
             if (c + 1 + D < NCH) sa_[(c + 1) % D] = load_a<BM, true>(p, row0, (c + 1 + D) * kKC);
             if (c + 2 < NCH) sb = load_b_regs<PL>(bimg, c + 2);
         }
-#pragma unroll
-        for (int i = 0; i < I; ++i)
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                if constexpr (EPI == kEpiBiasEluOut)
-                    acc[i][j] = Arith<PL>::mfma(bf[j], af[i], acc[i][j]);
-                else
-                    acc[i][j] = Arith<PL>::mfma(af[i], bf[j], acc[i][j]);
-            }
         // only LDS writes to retire (lgkmcnt); __syncthreads' release fence would also wait vmcnt(0) and drain
         // the look-ahead every chunk
         if (c + 1 < NCH)
