@@ -144,6 +144,15 @@ size_t rslrl_ppo_loss_workspace_bytes(int64_t B, int32_t A);
 int rslrl_ppo_loss_fwd_bwd(const rslrl_ppo_loss_args_t* args /* host struct */, void* workspace,
                            size_t workspace_bytes, rslrl_stream_t stream);
 
+/* Per-mini-batch tail of PPO.update on device scalars (one launch): when lr is non-NULL, the adaptive-KL rule
+ * of ppo.py:280-284 -- fp32 kl = *kl (stats[4], or the all-reduced mean), kl > kl_hi (= fp32(2 kl*)):
+ * lr = max(lr / 1.5, 1e-5); 0 < kl < kl_lo (= fp32(kl* / 2)): lr = min(lr * 1.5, 1e-2); lr is fp64 (the
+ * reference's Python float), rounded through fp32 when round_fp32 (multi-GPU broadcast, ppo.py:288-290);
+ * *lr32 = fp32(lr) (the optimizer's tensor lr); and when sums is non-NULL, sums[0..2] += (value, surrogate,
+ * entropy) of stats (ppo.py:387-395, fp64).  Replaces the reference's host-side logic and .item() syncs. */
+int rslrl_ppo_update_tail(const float* stats, const float* kl, double* lr, float* lr32, int32_t round_fp32,
+                          float kl_hi, float kl_lo, double* sums, rslrl_stream_t stream);
+
 /* ------------------------------------------------------------------------------------------------
  * Actor/critic MLP hidden layers on fp32 MFMA -- rsl_rl/networks/mlp.py:59-114
  * (nn.Linear + ELU(alpha=1) blocks) and their autograd backward.
@@ -216,8 +225,9 @@ int rslrl_fold_partials(const float* partials, int64_t S, int64_t NK, float* out
                         size_t workspace_bytes, rslrl_stream_t stream);
 
 /* Output-layer backward in one x6 launch (Nred <= 16, % 4 == 0): rslrl_linear_dgrad_elu's outputs plus this
- * layer's weight gradient dW[Nred, K] = dz^T h as per-128-row-tile partials
- * [rslrl_linear_tiles(M)][Nred][K] (rslrl_linear_dgrad_wgrad_partial_bytes), folded by rslrl_fold_partials.
+ * layer's weight gradient dW[Nred, K] = dz^T h and bias gradient db[Nred] = column sums of dz, as
+ * per-128-row-tile partials [rslrl_linear_tiles(M)][Nred * K + Nred] (dW row-major, then db;
+ * rslrl_linear_dgrad_wgrad_partial_bytes), folded by rslrl_fold_partials over Nred * K + Nred columns.
  * The reference runs these as three autograd GEMM/elementwise steps over the same h (mlp.py:106-114). */
 size_t rslrl_linear_dgrad_wgrad_partial_bytes(int64_t M, int32_t Nred, int32_t K);
 int rslrl_linear_dgrad_elu_wgrad(const float* dz, int64_t M, int32_t Nred, int32_t K, const float* h, float* dz_prev,

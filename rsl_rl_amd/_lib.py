@@ -57,6 +57,7 @@ EXPORTED_SYMBOLS = (
     "rslrl_amax_workspace_bytes",
     "rslrl_linear_gemm",
     "rslrl_linear_wgrad_ex",
+    "rslrl_ppo_update_tail",
 )
 
 MAX_GATHER_FIELDS = 16
@@ -266,6 +267,8 @@ def _declare(L):
     L.rslrl_amax_workspace_bytes.argtypes = []
     L.rslrl_linear_gemm.restype = ctypes.c_int
     L.rslrl_linear_gemm.argtypes = [ctypes.POINTER(LinearArgs), P]
+    L.rslrl_ppo_update_tail.restype = ctypes.c_int
+    L.rslrl_ppo_update_tail.argtypes = [P, P, P, P, I32, F, F, P, P]
     L.rslrl_linear_wgrad_ex.restype = ctypes.c_int
     L.rslrl_linear_wgrad_ex.argtypes = [P, P, P, P, I64, I32, I32, I32, P, P, SZ, P]
 

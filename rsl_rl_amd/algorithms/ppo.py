@@ -306,7 +306,11 @@ class PPO:
         # device-resident lr (needs an optimizer that takes a tensor lr: fused / capturable Adam)
         device_lr = adaptive and dev.type == "cuda" and self._optimizer_takes_tensor_lr()
         lr_dev = torch.tensor(self.learning_rate, dtype=torch.float64, device=dev) if device_lr else None
-        stat_idx = torch.tensor([kernels.STATS_VALUE, kernels.STATS_SURROGATE, kernels.STATS_ENTROPY], device=dev)
+        lr32 = None
+        if device_lr:  # the optimizer reads the lr as this fp32 device tensor (written by ppo_update_tail)
+            lr32 = torch.tensor(self.learning_rate, dtype=torch.float32, device=dev)
+            for param_group in self.optimizer.param_groups:
+                param_group["lr"] = lr32
         trainable = self._trainable_params()
 
         generator = self.storage.mini_batch_generator(self.num_mini_batches, self.num_learning_epochs)
@@ -338,12 +342,19 @@ class PPO:
                 use_clipped_value_loss=self.use_clipped_value_loss, compute_kl=adaptive,
                 normalize_advantage=self.normalize_advantage_per_mini_batch, stats=stats_buf,
             )
-            if adaptive:
-                kl_mean = stats[kernels.STATS_KL:kernels.STATS_KL + 1].clone()
-                if device_lr:
-                    lr_dev = self._device_kl_and_lr(kl_mean, lr_dev)
-                else:
-                    self._sync_kl_and_lr(kl_mean)
+            if adaptive and device_lr:
+                # adaptive lr + loss statistics in one launch on device scalars (ppo.py:259-294, :387-395)
+                kl_src = stats[kernels.STATS_KL:kernels.STATS_KL + 1]
+                if self.is_multi_gpu:
+                    kl_src = kl_src.clone()
+                    torch.distributed.all_reduce(kl_src, op=torch.distributed.ReduceOp.SUM)
+                    kl_src /= self.gpu_world_size
+                kernels.ppo_update_tail(stats, kl_src, lr_dev, lr32, self.desired_kl, sums,
+                                        round_fp32=self.is_multi_gpu)
+            else:
+                if adaptive:
+                    self._sync_kl_and_lr(stats[kernels.STATS_KL:kernels.STATS_KL + 1].clone())
+                kernels.ppo_update_tail(stats, None, None, None, 0.0, sums)
 
             # RND loss (ppo.py:352-363)
             if self.rnd:
@@ -375,8 +386,7 @@ class PPO:
             if self.rnd_optimizer:
                 self.rnd_optimizer.step()
 
-            # loss statistics stay on the device (ppo.py:387-395)
-            sums[0:3] += stats.index_select(0, stat_idx).double()
+            # loss statistics stay on the device (ppo.py:387-395): accumulated by ppo_update_tail above
             if self.rnd:
                 sums[3] += rnd_loss.detach().double()
 

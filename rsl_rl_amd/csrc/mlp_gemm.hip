@@ -856,8 +856,20 @@ __global__ __launch_bounds__(kThreads, MINW) void mlp_gemm_x6_kernel(GemmParams 
                 for (int j = 0; j < 2; ++j) red[o * kBN + wn * 64 + j * 32 + l32] = wacc[o][j];
         }
         __syncthreads();
+        // per-tile partial sums of dZ itself (the layer's bias gradient): wave 0, lane (q, c) sums rows
+        // 32 q .. 32 q + 31 of column c in order, the four quarters are added in order
+        const int64_t tile_floats = static_cast<int64_t>(p.K) * p.N + p.K;
+        if (threadIdx.x < 64) {
+            const int c = threadIdx.x & 15, q = threadIdx.x >> 4;
+            float sz = 0.f;
+            for (int r = 32 * q; r < 32 * q + 32; ++r) sz += dzo[r * kMaxWgradRows + c];
+            const float s1 = __shfl(sz, c + 16, 64), s2 = __shfl(sz, c + 32, 64), s3 = __shfl(sz, c + 48, 64);
+            if (q == 0 && c < p.K)
+                p.wpart[static_cast<int64_t>(blockIdx.x) * tile_floats + static_cast<int64_t>(p.K) * p.N + c] =
+                    ((sz + s1) + s2) + s3;
+        }
         if (wm == 1 && h == 0) {
-            float* out = p.wpart + static_cast<int64_t>(blockIdx.x) * p.K * p.N;
+            float* out = p.wpart + static_cast<int64_t>(blockIdx.x) * tile_floats;
 #pragma unroll
             for (int o = 0; o < NR; ++o)
 #pragma unroll
@@ -1421,7 +1433,7 @@ extern "C" int rslrl_linear_dgrad_elu(const float* dz, int64_t M, int32_t Nred, 
 
 extern "C" size_t rslrl_linear_dgrad_wgrad_partial_bytes(int64_t M, int32_t Nred, int32_t K) {
     if (M < 1 || Nred < 1 || K < 1) return 0;
-    return static_cast<size_t>(ceil_div(M, kBM)) * Nred * K * sizeof(float);
+    return static_cast<size_t>(ceil_div(M, kBM)) * (static_cast<size_t>(Nred) * K + Nred) * sizeof(float);
 }
 
 extern "C" int rslrl_linear_dgrad_elu_wgrad(const float* dz, int64_t M, int32_t Nred, int32_t K, const float* h,

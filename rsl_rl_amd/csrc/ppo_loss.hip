@@ -1029,3 +1029,40 @@ extern "C" int rslrl_ppo_loss_fwd_bwd(const rslrl_ppo_loss_args_t* a, void* work
         launch_loss<64>(p, vec, nb, part, ticket, cv, ce, st);
     return launch_status();
 }
+
+// ---- per-mini-batch tail of PPO.update (ppo.py:259-294 adaptive lr, :387-395 loss statistics) ----------
+// One thread: the reference's host logic on device scalars, so the update loop needs no host round trip and
+// no chain of one-element torch launches.
+namespace {
+__global__ void ppo_tail_kernel(const float* __restrict__ stats, const float* __restrict__ kl_src, double* lr,
+                                float* lr32, int round_fp32, float kl_hi, float kl_lo, double* sums) {
+    if (threadIdx.x != 0) return;
+    if (lr) {
+        const float kl = *kl_src;
+        double v = *lr;
+        // ppo.py:280-284 with the reference's operand types: kl (fp32 tensor) against Python floats -> fp32
+        // comparisons; lr stays a Python float (fp64)
+        if (kl > kl_hi) {
+            v = fmax(v / 1.5, 1e-5);
+        } else if (kl < kl_lo && kl > 0.0f) {
+            v = fmin(v * 1.5, 1e-2);
+        }
+        if (round_fp32) v = static_cast<double>(static_cast<float>(v));  // ppo.py:288-290 fp32 broadcast
+        *lr = v;
+        *lr32 = static_cast<float>(v);
+    }
+    if (sums) {  // [value_function, surrogate, entropy] += the mini-batch's means (fp64 host accumulation)
+        sums[0] += static_cast<double>(stats[2]);
+        sums[1] += static_cast<double>(stats[1]);
+        sums[2] += static_cast<double>(stats[3]);
+    }
+}
+}  // namespace
+
+extern "C" int rslrl_ppo_update_tail(const float* stats, const float* kl, double* lr, float* lr32, int32_t round_fp32,
+                                     float kl_hi, float kl_lo, double* sums, rslrl_stream_t stream) {
+    if (!stats || (lr && (!lr32 || !kl))) return RSLRL_E_INVALID_ARGUMENT;
+    hipLaunchKernelGGL(ppo_tail_kernel, dim3(1), dim3(64), 0, reinterpret_cast<hipStream_t>(stream), stats, kl, lr,
+                       lr32, round_fp32, kl_hi, kl_lo, sums);
+    return launch_status();
+}

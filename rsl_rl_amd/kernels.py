@@ -404,3 +404,18 @@ def rollout_record(step, *, obs_pairs, actions, mu, sigma, values, rewards, done
         rc = L.rslrl_rollout_record(ctypes.byref(a), _stream(actions.device))
     _lib.check(rc, "rslrl_rollout_record")
     return keep  # the caller may hold these until the stream has consumed them (torch's allocator is stream-ordered)
+
+
+def ppo_update_tail(stats, kl, lr, lr32, desired_kl, sums, round_fp32=False):
+    """One launch for the per-mini-batch tail of PPO.update (include/rslrl_amd.h rslrl_ppo_update_tail):
+    the adaptive-KL lr rule on the fp64 device lr (when lr is not None; kl: fp32 device scalar) and the loss
+    statistics accumulation sums[0:3] += (value, surrogate, entropy) of stats."""
+    _require_device(stats, kl, lr, lr32, sums)
+    kl_hi = float(desired_kl) * 2.0 if lr is not None else 0.0
+    kl_lo = float(desired_kl) / 2.0 if lr is not None else 0.0
+    rc = _lib.lib().rslrl_ppo_update_tail(
+        stats.data_ptr(), kl.data_ptr() if lr is not None else None, lr.data_ptr() if lr is not None else None,
+        lr32.data_ptr() if lr is not None else None, 1 if round_fp32 else 0, kl_hi, kl_lo,
+        sums.data_ptr() if sums is not None else None, _stream(stats.device))
+    _lib.check(rc, "rslrl_ppo_update_tail")
+

@@ -287,7 +287,7 @@ def linear_dgrad_elu_wgrad(dz, w, h, img, want_amax=False):
     tiles = L.rslrl_linear_tiles(M)
     out = torch.empty(M, K, device=dz.device, dtype=torch.float32)
     part = torch.empty(K, tiles, device=dz.device, dtype=torch.float32)
-    wpart = torch.empty(tiles, N, K, device=dz.device, dtype=torch.float32)
+    wpart = torch.empty(tiles, N * K + N, device=dz.device, dtype=torch.float32)  # per tile: dW [N, K], then db [N]
     amax = torch.empty(1, device=dz.device, dtype=torch.float32) if want_amax else None
     with timer.span(f"linear_dgrad_wgrad[M={M},Nred={N},K={K}]", dz.device, 4 * M * (N + 2 * K), 4 * M * K * N):
         _gemm(_lib.LINEAR_DGRAD_ELU_WGRAD, _lib.ARITH_X6, dz, None, K, img, h=h, c=out, colsum=part, wpart=wpart,
@@ -295,14 +295,16 @@ def linear_dgrad_elu_wgrad(dz, w, h, img, want_amax=False):
     db = torch.empty(K, device=dz.device, dtype=torch.float32)
     rc = L.rslrl_column_sum_fold(part.data_ptr(), tiles, K, db.data_ptr(), _stream(dz))
     _lib.check(rc, "rslrl_column_sum_fold")
-    dw = torch.empty(N, K, device=dz.device, dtype=torch.float32)
-    nbytes = L.rslrl_fold_partials_workspace_bytes(tiles, N * K)
+    dwb = torch.empty(N * K + N, device=dz.device, dtype=torch.float32)
+    nbytes = L.rslrl_fold_partials_workspace_bytes(tiles, N * K + N)
     ws = torch.empty(max(nbytes, 16) // 8, dtype=torch.float64, device=dz.device)
-    rc = L.rslrl_fold_partials(wpart.data_ptr(), tiles, N * K, dw.data_ptr(), ws.data_ptr(), nbytes, _stream(dz))
+    rc = L.rslrl_fold_partials(wpart.data_ptr(), tiles, N * K + N, dwb.data_ptr(), ws.data_ptr(), nbytes,
+                               _stream(dz))
     _lib.check(rc, "rslrl_fold_partials")
+    dw, db_out = dwb[: N * K].view(N, K), dwb[N * K:]
     if want_amax:
-        return out, db, dw, amax
-    return out, db, dw
+        return out, db, dw, db_out, amax
+    return out, db, dw, db_out
 
 
 def linear_wgrad(dz, x, arith=_lib.ARITH_X6, dz_amax=None, x_amax=None):
@@ -430,7 +432,7 @@ class FusedMLPFunction(torch.autograd.Function):
         grads_b = [None] * L
         dz = dy.contiguous()
         dz_amax = None
-        grads_b[L - 1] = dz.sum(0)
+        grads_b[L - 1] = None  # the output layer's bias gradient: column sums of dy
         for l in range(L - 1, -1, -1):
             h_in = hs[l]
             fuse_w = (_FUSE_OUT and ctx.x6 and l == L - 1 and l > 0 and dz.shape[1] <= 16 and h_in.shape[1] <= MAX_WIDTH
@@ -441,10 +443,13 @@ class FusedMLPFunction(torch.autograd.Function):
                 dzp = F.pad(dz, (0, pad)) if pad else dz
                 want = l - 1 > 0 and h3[l - 1]
                 res = linear_dgrad_elu_wgrad(dzp, ws[l], h_in, ctx.dgrad_imgs[l], want_amax=want)
-                dz, grads_b[l - 1], dw = res[:3]
-                dz_amax = res[3] if want else None
+                dz, grads_b[l - 1], dw, db_out = res[:4]
+                dz_amax = res[4] if want else None
                 grads_w[l] = dw[:nred]
+                grads_b[l] = db_out[:nred]  # from the same launch (was a separate reduction of dy)
                 continue
+            if l == L - 1:
+                grads_b[l] = dz.sum(0)
             if ctx.needs_input_grad[1 + 2 * l]:
                 grads_w[l] = _weight_grad(dz, h_in, ctx.x6, h3[l], dz_amax, ctx.amaxes[l])
             if l == 0:

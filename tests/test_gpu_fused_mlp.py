@@ -204,14 +204,15 @@ def test_linear_dgrad_elu_wgrad(M, N, K, cuda_device):
     dz = torch.randn(M, N, device=cuda_device)
     w = torch.randn(N, K, device=cuda_device) / N ** 0.5
     h = torch.nn.functional.elu(torch.randn(M, K, device=cuda_device))
-    out, db, dw = fused_mlp.linear_dgrad_elu_wgrad(dz, w, h, bimage(w, True))
+    out, db, dw, db_out = fused_mlp.linear_dgrad_elu_wgrad(dz, w, h, bimage(w, True))
     d = dz.double().mm(w.double())
     ref = torch.where(h > 0, d, d * (h.double() + 1))
     _close(out, ref.float())
     _close(db, ref.sum(0).float(), 1e-4)
     _close(dw, dz.double().t().mm(h.double()).float(), 2e-5)
-    out2, db2, dw2 = fused_mlp.linear_dgrad_elu_wgrad(dz, w, h, bimage(w, True))
-    assert torch.equal(dw, dw2) and torch.equal(db, db2)  # deterministic
+    _close(db_out, dz.double().sum(0).float(), 1e-5)  # this layer's own bias gradient (column sums of dz)
+    out2, db2, dw2, db_out2 = fused_mlp.linear_dgrad_elu_wgrad(dz, w, h, bimage(w, True))
+    assert torch.equal(dw, dw2) and torch.equal(db, db2) and torch.equal(db_out, db_out2)  # deterministic
 
 
 @pytest.mark.parametrize("S,NK", [(1, 4), (7, 100), (256, 65536), (3072, 3072), (3072, 1024), (129, 20)])

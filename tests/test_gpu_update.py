@@ -62,7 +62,7 @@ def test_update_c1_matches_reference(golden_meta, cuda_device, one_rank_group):
 
     lr_trace = []
     step = alg.optimizer.step
-    alg.optimizer.step = lambda *a, **k: (lr_trace.append(alg.optimizer.param_groups[0]["lr"]), step(*a, **k))[1]
+    alg.optimizer.step = lambda *a, **k: (lr_trace.append(float(alg.optimizer.param_groups[0]["lr"])), step(*a, **k))[1]
     torch.default_generator.set_state(torch.from_numpy(z["gen_state"].copy()))
     loss = alg.update()
     assert lr_trace == m["lr_trace"]
