@@ -13,10 +13,12 @@ import csv
 import glob
 import json
 import os
+import re
 from collections import defaultdict
 
 SHORT = {
     "ppo_loss_kernel": "ppo_loss",
+    "ppo_loss_quad_kernel": "ppo_loss",
     "gae_scan_kernel": "gae_scan",
     "adv_normalize_kernel": "adv_normalize",
     "moments_kernel": "moments",
@@ -29,7 +31,25 @@ SHORT = {
     "__amd_rocclr_copyBuffer": "copyBuffer",
 }
 # kernels launched at several shapes are keyed "<short>@grid=<threads>"
-BY_GRID = {"x6_fwd_elu", "x6_dgrad_elu", "x6_wgrad", "wgrad_fold"}
+BY_GRID = {"x6_fwd_elu", "x6_dgrad_elu", "x6_wgrad", "wgrad_fold", "h3_fwd_elu", "h3_dgrad_elu", "h3_fwd_out",
+           "x6_dgrad_wgrad", "h3_wgrad256", "x6_wgrad64", "x6_fwd_out"}
+
+
+EPI_NAMES = {0: "fwd", 1: "fwd_elu", 2: "dgrad_elu", 3: "dgrad_wgrad", 4: "fwd_out"}
+
+
+def gemm_name(kernel):
+    """mlp_gemm_x6_kernel<EPI, FULL, MINW, NR, PL> / wgrad_x6_kernel<TN, FULL, PL>: arithmetic (PL 2 = h3,
+    3 = x6) and epilogue in the key."""
+    m = re.search(r"mlp_gemm_x6_kernel<(\d+), \w+, \d+, \d+, (\d+)>", kernel)
+    if m:
+        return f"{'h3' if m.group(2) == '2' else 'x6'}_{EPI_NAMES.get(int(m.group(1)), m.group(1))}"
+    m = re.search(r"wgrad_x6_kernel<(\d+), \w+, (\d+)>", kernel)
+    if m:
+        return f"{'h3' if m.group(2) == '2' else 'x6'}_wgrad{m.group(1)}"
+    if "fold_kernel" in kernel:
+        return "wgrad_fold"
+    return None
 
 
 def load(d, counter):
@@ -40,7 +60,7 @@ def load(d, counter):
         for r in csv.DictReader(open(f)):
             if r["Counter_Name"] != counter:
                 continue
-            name = next((v for k, v in SHORT.items() if k in r["Kernel_Name"]), None)
+            name = gemm_name(r["Kernel_Name"]) or next((v for k, v in SHORT.items() if k in r["Kernel_Name"]), None)
             if name:
                 if name in BY_GRID:
                     name = f"{name}@grid={r['Grid_Size']}"
