@@ -233,7 +233,11 @@ def main():
                         "frac": round(ach / peak, 4), "traffic": None,
                         "flops_per_launch": mlp[dm]["flops_per_launch"], "mean_launch_us": mlp[dm]["mean_us"],
                         "arithmetic": arith, "fp32_mfma_peak": FP32_MFMA_PEAK_TFLOPS,
-                        "mlp_ms_per_step": round(sum(e["ms_per_step"] for e in mlp.values()), 3)}
+                        "mlp_ms_per_step": round(sum(e["ms_per_step"] for e in mlp.values()), 3),
+                        # the same launch against the HBM roofline: algorithmic bytes / event time
+                        "hbm": {"achieved": mlp[dm]["achieved_GBps"], "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                                "frac": round(mlp[dm]["achieved_GBps"] / HBM_PEAK_GBPS, 4),
+                                "algorithmic_bytes_per_launch": mlp[dm]["algorithmic_bytes_per_launch"]}}
 
     out = {
         "metric": "PPO env-steps/sec (rollout+GAE+update) at N=65536 envs, 1->8 MI355X",
