@@ -153,6 +153,36 @@ int rslrl_ppo_loss_fwd_bwd(const rslrl_ppo_loss_args_t* args /* host struct */, 
 int rslrl_ppo_update_tail(const float* stats, const float* kl, double* lr, float* lr32, int32_t round_fp32,
                           float kl_hi, float kl_lo, double* sums, rslrl_stream_t stream);
 
+/* Gradient-norm clipping + Adam step over a parameter list (ppo.py:373-374: clip_grad_norm_ then
+ * optimizer.step() of torch.optim.Adam(fused), no weight decay / amsgrad / maximize), two launches:
+ * ||g||_2 over every tensor (fp64, fixed order), coef = min(1, max_grad_norm / (||g|| + 1e-6)) (no clipping
+ * when max_grad_norm <= 0), every step += 1; then per element torch's fused-Adam arithmetic with g * coef.
+ * lr_dev (fp32 device scalar) overrides lr when non-NULL.  offsets are filled by the call.  workspace:
+ * rslrl_adam_workspace_bytes(), zero-filled once (an arrival counter every call leaves zero). */
+#define RSLRL_ADAM_MAX_TENSORS 24
+typedef struct {
+    float* param;
+    const float* grad;
+    float* exp_avg;
+    float* exp_avg_sq;
+    float* step; /* fp32 device scalar (torch's fused-Adam state["step"]) */
+    int64_t numel;
+} rslrl_adam_tensor_t;
+typedef struct {
+    int32_t n;
+    float max_grad_norm;
+    double lr;
+    const float* lr_dev;
+    double beta1;
+    double beta2;
+    double eps;
+    int64_t offsets[RSLRL_ADAM_MAX_TENSORS + 1];
+    rslrl_adam_tensor_t t[RSLRL_ADAM_MAX_TENSORS];
+} rslrl_adam_args_t;
+size_t rslrl_adam_workspace_bytes(void);
+int rslrl_clip_adam_step(const rslrl_adam_args_t* args /* host struct */, void* workspace, size_t workspace_bytes,
+                         rslrl_stream_t stream);
+
 /* ------------------------------------------------------------------------------------------------
  * Actor/critic MLP hidden layers on fp32 MFMA -- rsl_rl/networks/mlp.py:59-114
  * (nn.Linear + ELU(alpha=1) blocks) and their autograd backward.

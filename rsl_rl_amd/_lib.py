@@ -58,6 +58,8 @@ EXPORTED_SYMBOLS = (
     "rslrl_linear_gemm",
     "rslrl_linear_wgrad_ex",
     "rslrl_ppo_update_tail",
+    "rslrl_adam_workspace_bytes",
+    "rslrl_clip_adam_step",
 )
 
 MAX_GATHER_FIELDS = 16
@@ -88,6 +90,22 @@ BIMAGE_LAYOUT_H3 = 2
 
 ARITH_X6, ARITH_H3 = 1, 2
 LINEAR_FWD, LINEAR_FWD_ELU, LINEAR_DGRAD_ELU, LINEAR_DGRAD_ELU_WGRAD, LINEAR_FWD_OUT = 0, 1, 2, 3, 4
+
+
+ADAM_MAX_TENSORS = 24
+
+
+class AdamTensor(ctypes.Structure):
+    _fields_ = [("param", ctypes.c_void_p), ("grad", ctypes.c_void_p), ("exp_avg", ctypes.c_void_p),
+                ("exp_avg_sq", ctypes.c_void_p), ("step", ctypes.c_void_p), ("numel", ctypes.c_int64)]
+
+
+class AdamArgs(ctypes.Structure):
+    """rslrl_adam_args_t (include/rslrl_amd.h)."""
+    _fields_ = [("n", ctypes.c_int32), ("max_grad_norm", ctypes.c_float), ("lr", ctypes.c_double),
+                ("lr_dev", ctypes.c_void_p), ("beta1", ctypes.c_double), ("beta2", ctypes.c_double),
+                ("eps", ctypes.c_double), ("offsets", ctypes.c_int64 * (ADAM_MAX_TENSORS + 1)),
+                ("t", AdamTensor * ADAM_MAX_TENSORS)]
 
 
 class LinearArgs(ctypes.Structure):
@@ -267,6 +285,10 @@ def _declare(L):
     L.rslrl_amax_workspace_bytes.argtypes = []
     L.rslrl_linear_gemm.restype = ctypes.c_int
     L.rslrl_linear_gemm.argtypes = [ctypes.POINTER(LinearArgs), P]
+    L.rslrl_adam_workspace_bytes.restype = SZ
+    L.rslrl_adam_workspace_bytes.argtypes = []
+    L.rslrl_clip_adam_step.restype = ctypes.c_int
+    L.rslrl_clip_adam_step.argtypes = [ctypes.POINTER(AdamArgs), P, SZ, P]
     L.rslrl_ppo_update_tail.restype = ctypes.c_int
     L.rslrl_ppo_update_tail.argtypes = [P, P, P, P, I32, F, F, P, P]
     L.rslrl_linear_wgrad_ex.restype = ctypes.c_int

@@ -121,6 +121,9 @@ class PPO:
         # on a ROCm device Adam runs fused (one kernel per step) and accepts the device-resident lr of update()
         on_gpu = str(device).startswith("cuda")
         self.optimizer = optim.Adam(self.policy.parameters(), lr=learning_rate, fused=True if on_gpu else None)
+        # clip_grad_norm_ + optimizer.step() as two launches (kernels.FusedClipAdam, ppo.py:373-374)
+        self._clip_adam = (kernels.FusedClipAdam(self.optimizer, max_grad_norm)
+                           if on_gpu and kernels.FusedClipAdam.supported(self.optimizer) else None)
         self.storage: RolloutStorage = None  # type: ignore
         self.transition = RolloutStorage.Transition()
 
@@ -381,8 +384,12 @@ class PPO:
             if self.is_multi_gpu:
                 self.reduce_parameters()
 
-            nn.utils.clip_grad_norm_(self.policy.parameters(), self.max_grad_norm)
-            self.optimizer.step()
+            if self._clip_adam is None:
+                nn.utils.clip_grad_norm_(self.policy.parameters(), self.max_grad_norm)
+                self.optimizer.step()
+            else:  # clip + Adam in two launches (ppo.py:373-374)
+                self._clip_adam.max_grad_norm = float(self.max_grad_norm)
+                self._clip_adam.step()
             if self.rnd_optimizer:
                 self.rnd_optimizer.step()
 

@@ -419,3 +419,74 @@ def ppo_update_tail(stats, kl, lr, lr32, desired_kl, sums, round_fp32=False):
         sums.data_ptr() if sums is not None else None, _stream(stats.device))
     _lib.check(rc, "rslrl_ppo_update_tail")
 
+
+class FusedClipAdam:
+    """optimizer.step() for a torch.optim.Adam over ROCm parameters as two launches (include/rslrl_amd.h
+    rslrl_clip_adam_step): gradient-norm clipping at max_grad_norm (ppo.py:373, clip_grad_norm_) folded into
+    torch's fused-Adam arithmetic (ppo.py:374).  The optimizer's state (step / exp_avg / exp_avg_sq, torch's
+    fused layout) and state_dict stay torch's; parameters whose grad is None are skipped, as torch does.
+    Supported: one group of contiguous fp32 device parameters (at most ADAM_MAX_TENSORS), weight_decay 0,
+    no amsgrad / maximize / differentiable; anything else keeps torch's clip_grad_norm_ + step."""
+
+    def __init__(self, optimizer, max_grad_norm):
+        self.opt = optimizer
+        self.max_grad_norm = float(max_grad_norm) if max_grad_norm is not None else 0.0
+        L = _lib.lib()
+        dev = optimizer.param_groups[0]["params"][0].device
+        self.ws = torch.zeros(max(L.rslrl_adam_workspace_bytes() // 4, 1), dtype=torch.int32, device=dev)
+        self.args = _lib.AdamArgs()
+
+    @staticmethod
+    def supported(optimizer) -> bool:
+        if not isinstance(optimizer, torch.optim.Adam) or len(optimizer.param_groups) != 1:
+            return False  # the clip norm spans every gradient: one launch pair over one group
+        if len(optimizer.param_groups[0]["params"]) > _lib.ADAM_MAX_TENSORS:
+            return False
+        for g in optimizer.param_groups:
+            if g["weight_decay"] != 0 or g["amsgrad"] or g["maximize"] or g.get("differentiable", False):
+                return False
+            if not all(p.is_cuda and p.dtype == torch.float32 and p.is_contiguous() for p in g["params"]):
+                return False
+        return True
+
+    def _state(self, p):
+        st = self.opt.state[p]
+        if len(st) == 0:  # torch's lazy init for fused Adam (optim/adam.py _init_group)
+            st["step"] = torch.zeros((), dtype=torch.float32, device=p.device)
+            st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+            st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+        return st
+
+    def step(self, closure=None):
+        if closure is not None:
+            raise RuntimeError("FusedClipAdam.step: closures are not supported")
+        L = _lib.lib()
+        keep = []  # contiguous copies (if any) stay alive until the launch is queued
+        for g in self.opt.param_groups:
+            chunk = [p for p in g["params"] if p.grad is not None]
+            if chunk:
+                a = self.args
+                a.n = len(chunk)
+                a.max_grad_norm = self.max_grad_norm
+                lr = g["lr"]
+                if isinstance(lr, torch.Tensor):
+                    a.lr_dev = lr.data_ptr() if lr.is_cuda and lr.dtype == torch.float32 else None
+                    a.lr = float(lr) if a.lr_dev is None else 0.0
+                else:
+                    a.lr_dev = None
+                    a.lr = float(lr)
+                a.beta1, a.beta2 = float(g["betas"][0]), float(g["betas"][1])
+                a.eps = float(g["eps"])
+                for i, p in enumerate(chunk):
+                    st = self._state(p)
+                    grad = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
+                    keep.append(grad)
+                    t = a.t[i]
+                    t.param, t.grad = p.data_ptr(), grad.data_ptr()
+                    t.exp_avg, t.exp_avg_sq = st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr()
+                    t.step, t.numel = st["step"].data_ptr(), p.numel()
+                rc = L.rslrl_clip_adam_step(ctypes.byref(a), self.ws.data_ptr(), self.ws.numel() * 4,
+                                            _stream(self.ws.device))
+                _lib.check(rc, "rslrl_clip_adam_step")
+        return None
+

@@ -61,8 +61,10 @@ def test_update_c1_matches_reference(golden_meta, cuda_device, one_rank_group):
     torch.testing.assert_close(st.advantages.cpu(), torch.from_numpy(z["storage/advantages"]), rtol=1e-5, atol=1e-5)
 
     lr_trace = []
-    step = alg.optimizer.step
-    alg.optimizer.step = lambda *a, **k: (lr_trace.append(float(alg.optimizer.param_groups[0]["lr"])), step(*a, **k))[1]
+    stepper = alg._clip_adam if alg._clip_adam is not None else alg.optimizer  # fused clip + Adam on a GPU
+    assert alg._clip_adam is not None
+    step = stepper.step
+    stepper.step = lambda *a, **k: (lr_trace.append(float(alg.optimizer.param_groups[0]["lr"])), step(*a, **k))[1]
     torch.default_generator.set_state(torch.from_numpy(z["gen_state"].copy()))
     loss = alg.update()
     assert lr_trace == m["lr_trace"]
