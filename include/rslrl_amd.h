@@ -190,9 +190,10 @@ int rslrl_clip_adam_step(const rslrl_adam_args_t* args /* host struct */, void* 
  *   rslrl_linear_dgrad_elu: dz_prev[M,K] = (dz[M,Nred] weight_t[K,Nred]^T) * ELU'(h[M,K]), where h is the
  *                           ELU output feeding this layer (ELU'(z) = 1 if h > 0 else h + 1), and the
  *                           per-128-row-tile column sums of dz_prev into colsum_partials
- *                           [K, rslrl_linear_tiles(M)] (-> the previous layer's bias gradient);
- *                           weight_t is the layer weight transposed ([K, Nred] row-major).
- *   rslrl_column_sum_fold:  out[N] = sum over tiles of partials[N, tiles] (fixed order).
+ *                           [rslrl_linear_tiles(M), K] (one row per tile; -> the previous layer's bias
+ *                           gradient); weight_t is the layer weight transposed ([K, Nred] row-major).
+ *   rslrl_column_sum_fold:  out[N] = sum over tiles of partials[tiles, N] (fixed order, fp64; two launches).
+ *                           The partials are scratch: the fold overwrites them.
  *   bimage (both calls): NULL -> exact f32 arithmetic (v_mfma_f32_32x32x2_f32, a k-ordered f32 fma
  *                           chain) on weight / weight_t.  Non-NULL -> the "x6" split-bf16 path: the B
  *                           operand comes from an image built by rslrl_linear_prepare_bimage (weight / weight_t
@@ -230,7 +231,7 @@ int rslrl_linear_fwd(const float* x, int64_t M, int32_t K, const float* weight, 
 int rslrl_linear_dgrad_elu(const float* dz, int64_t M, int32_t Nred, const float* weight_t, int32_t K,
                            const float* h, float* dz_prev, float* colsum_partials, const void* bimage,
                            rslrl_stream_t stream);
-int rslrl_column_sum_fold(const float* partials, int64_t tiles, int32_t N, float* out, rslrl_stream_t stream);
+int rslrl_column_sum_fold(float* partials, int64_t tiles, int32_t N, float* out, rslrl_stream_t stream);
 
 /* Last hidden layer and output layer in one x6 launch (the MLP's final Linear, rsl_rl/networks/mlp.py:106-114,
  * 1-32 outputs): h = ELU(x[M,K] W[N,K]^T + bias[N]) -- written to h_out[M,N] unless h_out is NULL (inference:
@@ -277,7 +278,7 @@ int rslrl_linear_wgrad(const float* dz, const float* x, int64_t M, int32_t N, in
  *   op                         A (a, [M, K])  output                      B image (rows = N, depth = K)
  *   RSLRL_LINEAR_FWD[_ELU]     x              c = act(x W^T + bias) [M,N]  W [N, K]
  *   RSLRL_LINEAR_DGRAD_ELU     dz             c = (dz W) * ELU'(h) [M,N]   W^T (transposed image of W [K, N])
- *                                             + colsum_partials [N, rslrl_linear_tiles(M)]
+ *                                             + colsum_partials [rslrl_linear_tiles(M), N]
  *   RSLRL_LINEAR_DGRAD_ELU_WGRAD  (x6 only)   as rslrl_linear_dgrad_elu_wgrad (K = Nred <= 16)
  *   RSLRL_LINEAR_FWD_OUT       x              c = h (nullable), y = h W_out^T + out_bias (rslrl_linear_fwd_out)
  * amax_out (optional, not for FWD_OUT): max |c| over the output, published by the launch's last workgroup;

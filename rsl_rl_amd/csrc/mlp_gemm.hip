@@ -146,15 +146,30 @@ __device__ __forceinline__ void epilogue_tiles_impl(const GemmParams& p, f32x16 
 #pragma unroll
     for (int j = 0; j < J; ++j) colpart[j] = 0.f;
     float hcur[16], hnext[16], hsave[16];
+    // full tiles (N == kBN): wave-uniform base pointers (SGPRs) + 32-bit lane offsets with a compile-time row
+    // stride -> saddr-form loads/stores whose row-in-group steps fold into the immediate.  A 64-bit address per
+    // row (runtime stride) needs 32 VGPRs per tile and spilled ~70 B/lane to scratch around the epilogue.
+    const int wr = full ? __builtin_amdgcn_readfirstlane(static_cast<int>(wrow0)) : 0;  // rows < 2^31 (launch)
+    const int wc = full ? __builtin_amdgcn_readfirstlane(wcol0) : 0;
+    const int64_t ubase = static_cast<int64_t>(wr) * kBN + wc;
+    auto lane_off = [&](int i, int j, int roff) -> uint32_t {
+        return static_cast<uint32_t>((i * 32 + 4 * h + roff) * kBN + j * 32 + l32);
+    };
     auto load_h = [&](int b, float (&dst)[16]) {
         const int i = b / J, j = b % J;
+        if constexpr (full) {
+            const float* hb = p.h + ubase;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) dst[r] = hb[lane_off(i, j, (r & 3) + 8 * (r >> 2))];
+            return;
+        }
         const int col = wcol0 + j * 32 + l32;
         const int64_t rbase = wrow0 + i * 32 + 4 * h;
         const float* hp = p.h + rbase * p.N + col;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int roff = (r & 3) + 8 * (r >> 2);
-            dst[r] = (full || (rbase + roff < p.M && col < p.N)) ? hp[static_cast<int64_t>(roff) * p.N] : 0.f;
+            dst[r] = (rbase + roff < p.M && col < p.N) ? hp[static_cast<int64_t>(roff) * p.N] : 0.f;
         }
     };
     if constexpr (GRAD) load_h(0, hcur);
@@ -170,6 +185,7 @@ __device__ __forceinline__ void epilogue_tiles_impl(const GemmParams& p, f32x16 
         if constexpr (!GRAD) bias = col_ok ? p.bias[col] : 0.f;
         const int64_t rbase = wrow0 + i * 32 + 4 * h;
         float* cp = p.c + rbase * p.N + col;
+        float* cb = p.c + ubase;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int roff = (r & 3) + 8 * (r >> 2);
@@ -188,7 +204,10 @@ __device__ __forceinline__ void epilogue_tiles_impl(const GemmParams& p, f32x16 
                 amx = fmaxf(amx, fabsf(v));
                 // streaming store: the outputs are not re-read by this kernel, and keeping them out of L2
                 // keeps the B image and the A stream resident (-7% kernel time measured)
-                __builtin_nontemporal_store(v, cp + static_cast<int64_t>(roff) * p.N);
+                if constexpr (full)
+                    __builtin_nontemporal_store(v, cb + lane_off(i, j, roff));
+                else
+                    __builtin_nontemporal_store(v, cp + static_cast<int64_t>(roff) * p.N);
             }
         }
         if constexpr (EPI == kEpiEluGradWgrad) {
@@ -271,9 +290,10 @@ __device__ __forceinline__ void epilogue(const GemmParams& p, f32x16 (&acc)[2][2
             if (h == 0) colred[wm * kBN + wn * 64 + j * 32 + l32] = s;
         }
         __syncthreads();
-        // column-major partials [N][tiles]: the fold then reads each column contiguously
+        // tile-major partials [tiles][N]: one contiguous row per workgroup (column-major rows of 4-byte
+        // pieces scattered over the whole buffer cost a read-modify-write of a line each)
         for (int col = threadIdx.x; col < p.N && col < kBN; col += kThreads)
-            p.colsum[static_cast<int64_t>(col) * gridDim.x + blockIdx.x] = colred[col] + colred[kBN + col];
+            p.colsum[static_cast<int64_t>(blockIdx.x) * p.N + col] = colred[col] + colred[kBN + col];
     }
 }
 
@@ -987,9 +1007,8 @@ __global__ __launch_bounds__(kThreads, MINW) void mlp_gemm_x6_kernel(GemmParams 
     }
 #endif
     if constexpr (EPI == kEpiEluGrad || EPI == kEpiEluGradWgrad) {
-        // column sums over the tile's 128 rows -> colsum[col][tile]: lanes l and l + 32 hold the two row
+        // column sums over the tile's 128 rows -> colsum[tile][col]: lanes l and l + 32 hold the two row
         // halves of a column, the two wave rows (wm) are combined in a fixed order through LDS
-        const int64_t tiles = p.ctiles;
         float s[2];
 #pragma unroll
         for (int j = 0; j < 2; ++j) s[j] = colpart[j] + __shfl_xor(colpart[j], 32, 64);
@@ -1000,7 +1019,7 @@ __global__ __launch_bounds__(kThreads, MINW) void mlp_gemm_x6_kernel(GemmParams 
             if (h == 0) colred[wm * kBN + wn * 64 + j * 32 + l32] = s[j];
         __syncthreads();
         for (int col = threadIdx.x; col < p.N && col < kBN; col += kThreads)
-            p.colsum[static_cast<int64_t>(col) * tiles + blockIdx.x] = colred[col] + colred[kBN + col];
+            p.colsum[static_cast<int64_t>(blockIdx.x) * p.N + col] = colred[col] + colred[kBN + col];
     }
     if constexpr (EPI != kEpiBiasEluOut) amax_commit(p, amx);
 }
@@ -1174,7 +1193,7 @@ __global__ __launch_bounds__(kThreads, MINW) void mlp_gemm_x6s_kernel(GemmParams
         }
         __syncthreads();
         for (int col = threadIdx.x; col < p.N && col < kBN; col += kThreads)
-            p.colsum[static_cast<int64_t>(col) * p.ctiles + blockIdx.x] = colred[col] + colred[kBN + col];
+            p.colsum[static_cast<int64_t>(blockIdx.x) * p.N + col] = colred[col] + colred[kBN + col];
     }
 }
 
@@ -1201,16 +1220,40 @@ int x6_shape() {
     return v;
 }
 
-// Bias gradient: out[col] = sum over tiles of part[col][tiles] -- one workgroup per column, lanes stride
-// over the tiles (coalesced), fp64 fold in a fixed order.
-__global__ __launch_bounds__(kBlock) void colsum_fold_kernel(const float* __restrict__ part, int tiles,
-                                                             float* __restrict__ out) {
-    __shared__ double scratch[kBlock / kWave];
-    const float* col = part + static_cast<int64_t>(blockIdx.x) * tiles;
+// Bias gradient: out[col] = sum over tiles of part[tiles][N], in two launches and a fixed order.  Pass 1:
+// workgroup (column group of 64, slice s) sums the slice's tiles (4 phases of 64 columns, fp64, phases
+// folded in order) and leaves the slice sum in the slice's first row (that element was read by the same
+// thread); pass 2 adds the slice sums in order.  The partials are scratch: pass 1 overwrites them.
+constexpr int kFoldCols = 64;
+constexpr int kFoldPhases = kBlock / kFoldCols;
+constexpr int kFoldSlices = 64;
+__global__ __launch_bounds__(kBlock) void colsum_slice_kernel(float* __restrict__ part, int tiles, int n, int per) {
+    __shared__ double scratch[kFoldPhases][kFoldCols];
+    const int c = threadIdx.x % kFoldCols, ph = threadIdx.x / kFoldCols;
+    const int col = blockIdx.x * kFoldCols + c;
+    const int t0 = blockIdx.y * per;
+    const int t1 = t0 + per < tiles ? t0 + per : tiles;
     double s = 0.0;
-    for (int t = threadIdx.x; t < tiles; t += kBlock) s += static_cast<double>(col[t]);
-    s = block_sum(s, scratch);
-    if (threadIdx.x == 0) out[blockIdx.x] = static_cast<float>(s);
+    if (col < n) {
+#pragma unroll 4
+        for (int t = t0 + ph; t < t1; t += kFoldPhases) s += static_cast<double>(part[static_cast<int64_t>(t) * n + col]);
+    }
+    scratch[ph][c] = s;
+    __syncthreads();
+    if (ph == 0 && col < n) {
+        double tot = 0.0;
+        for (int q = 0; q < kFoldPhases; ++q) tot += scratch[q][c];
+        part[static_cast<int64_t>(t0) * n + col] = static_cast<float>(tot);
+    }
+}
+
+__global__ __launch_bounds__(kFoldCols) void colsum_fold_kernel(const float* __restrict__ part, int slices, int n,
+                                                                int per, float* __restrict__ out) {
+    const int col = blockIdx.x * kFoldCols + threadIdx.x;
+    if (col >= n) return;
+    double tot = 0.0;
+    for (int s = 0; s < slices; ++s) tot += static_cast<double>(part[static_cast<int64_t>(s) * per * n + col]);
+    out[col] = static_cast<float>(tot);
 }
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
@@ -1420,11 +1463,16 @@ extern "C" int rslrl_linear_fwd_out(const float* x, int64_t M, int32_t K, const 
     return launch<kEpiBiasEluOut>(p, bimage, reinterpret_cast<hipStream_t>(stream));
 }
 
-extern "C" int rslrl_column_sum_fold(const float* partials, int64_t tiles, int32_t N, float* out,
+extern "C" int rslrl_column_sum_fold(float* partials, int64_t tiles, int32_t N, float* out,
                                      rslrl_stream_t stream) {
     if (tiles < 1 || tiles > INT32_MAX || N < 1 || !partials || !out) return RSLRL_E_INVALID_ARGUMENT;
-    hipLaunchKernelGGL(colsum_fold_kernel, dim3(static_cast<unsigned>(N)), dim3(kBlock), 0,
-                       reinterpret_cast<hipStream_t>(stream), partials, static_cast<int>(tiles), out);
+    const int per = static_cast<int>(ceil_div(tiles, kFoldSlices));
+    const int slices = static_cast<int>(ceil_div(tiles, per));
+    const unsigned cg = static_cast<unsigned>(ceil_div(N, kFoldCols));
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    hipLaunchKernelGGL(colsum_slice_kernel, dim3(cg, static_cast<unsigned>(slices)), dim3(kBlock), 0, st, partials,
+                       static_cast<int>(tiles), N, per);
+    hipLaunchKernelGGL(colsum_fold_kernel, dim3(cg), dim3(kFoldCols), 0, st, partials, slices, N, per, out);
     return launch_status();
 }
 
