@@ -674,7 +674,7 @@ __global__ __launch_bounds__(kThreads, MINW) void mlp_gemm_x6_kernel(GemmParams 
     lds[0] = lds_b0;
     lds[1] = lds_b1;
     const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: SGPR arithmetic
     const int wm = wave >> 2;  // rows wm * BM / 2
     const int wn = wave & 3;   // cols wn * 64
     const int h = lane >> 5;
@@ -917,15 +917,17 @@ __global__ __launch_bounds__(kThreads, MINW) void mlp_gemm_x6_kernel(GemmParams 
                 }
                 if (staged) {
                     __builtin_amdgcn_wave_barrier();  // one wave's LDS accesses execute in order
+                    // wave-uniform tile base + 32-bit lane offsets (one VGPR per store, not a 64-bit address)
+                    const int64_t trow = row0 + wm * (BM / 2) + i * 32;
+                    float* ct = p.c + trow * p.N + (wn * 64 + j * 32);
 #pragma unroll
                     for (int k = 0; k < 4; ++k) {
                         const int sr = 8 * k + (lane >> 3);
                         const int cq = lane & 7;
                         const f32x4 hv = *reinterpret_cast<const f32x4*>(stage + sr * 32 + 4 * (cq ^ ((sr >> 1) & 7)));
-                        const int64_t grow = row0 + wm * (BM / 2) + i * 32 + sr;
                         const int gcol = wn * 64 + j * 32 + 4 * cq;
-                        if (grow < p.M && gcol < p.N) {
-                            f32x4* dst = reinterpret_cast<f32x4*>(p.c + grow * p.N + gcol);
+                        if (trow + sr < p.M && gcol < p.N) {
+                            f32x4* dst = reinterpret_cast<f32x4*>(ct + static_cast<uint32_t>(sr * p.N + 4 * cq));
                             if (p.nt) __builtin_nontemporal_store(hv, dst);
                             else *dst = hv;
                         }

@@ -28,6 +28,7 @@ namespace {
 constexpr int kThreadsW = 512;
 constexpr int kMC = 16;  // rows of m per chunk (one MFMA k step)
 constexpr int kTK = 256;
+constexpr int kWgradDepth = 2;  // chunks of look-ahead in registers (full tiles)
 
 using s16x4 = __attribute__((ext_vector_type(4))) short;
 
@@ -144,6 +145,69 @@ __global__ __launch_bounds__(kThreadsW, 2) void wgrad_x6_kernel(WgradParams p) {
 #pragma unroll
         for (int j = 0; j < J; ++j) acc[i][j] = f32x16{};
 
+    auto compute = [&](const char* a_img) {
+        const char* b_img = a_img + PL * planeA;
+        Frag bf[J][PL];
+#pragma unroll
+        for (int j = 0; j < J; ++j)
+#pragma unroll
+            for (int q = 0; q < PL; ++q) bf[j][q] = read_frag_tr<kTK, Frag>(b_img + q * planeB, wk * (J * 32) + j * 32);
+#pragma unroll
+        for (int i = 0; i < I; ++i) {
+            Frag af[PL];
+#pragma unroll
+            for (int q = 0; q < PL; ++q) af[q] = read_frag_tr<TN, Frag>(a_img + q * planeA, wn * (I * 32) + i * 32);
+#pragma unroll
+            for (int j = 0; j < J; ++j) acc[i][j] = Arith<PL>::mfma(af, bf[j], acc[i][j]);
+        }
+    };
+
+    if constexpr (FULL) {
+        // Look-ahead pipeline: chunk c + 1 is split into LDS at the end of chunk c from registers loaded kWgradDepth
+        // chunks earlier, so kWgradDepth chunks (2 x 32 KiB per workgroup at TN = 256) stay in flight across
+        // the chunk barriers -- a one-chunk look-ahead behind __syncthreads (whose release fence waits
+        // vmcnt(0)) left ~32 KiB per CU in flight, about half of what the HBM latency asks for.
+        constexpr int D = kWgradDepth;
+        float4 ra[D][perA], rb[D][perB];
+        {
+            float4 va[perA], vb[perB];
+            load_tile<TN, true>(p.dz, p.N, m_begin, m_end, p.N, va);
+            load_tile<kTK, true>(p.x, p.K, m_begin, m_end, p.K, vb);
+            store_tile<TN, PL>(va, lds[0], sa);
+            store_tile<kTK, PL>(vb, lds[0] + PL * planeA, sb);
+        }
+        // every look-ahead load is issued, past the end clamped to the last chunk (data unused): with
+        // conditional loads the waitcnt pass cannot count the younger slot's loads and waits vmcnt(0)
+        auto chunk_row = [&](int c) { return m_begin + static_cast<int64_t>(c < nchunks ? c : nchunks - 1) * kMC; };
+#pragma unroll
+        for (int d = 1; d <= D; ++d) {
+            load_tile<TN, true>(p.dz, p.N, chunk_row(d), m_end, p.N, ra[d % D]);
+            load_tile<kTK, true>(p.x, p.K, chunk_row(d), m_end, p.K, rb[d % D]);
+        }
+        __syncthreads();
+        // chunk c (ring position u = c % D) followed by chunk c + 1: no branch between a slot's loads and their
+        // use, so the waitcnt pass counts the younger slot's loads (vmcnt(4 per slot)) instead of draining
+        auto step = [&](auto uc, int c) {
+            constexpr int u = decltype(uc)::value;
+            constexpr int s = (u + 1) % D;
+            compute(lds[u & 1]);
+            __builtin_amdgcn_sched_barrier(0);  // the splits below stay behind this chunk's MFMAs
+            store_tile<TN, PL>(ra[s], lds[(u + 1) & 1], sa);
+            store_tile<kTK, PL>(rb[s], lds[(u + 1) & 1] + PL * planeA, sb);
+            load_tile<TN, true>(p.dz, p.N, chunk_row(c + 1 + D), m_end, p.N, ra[s]);
+            load_tile<kTK, true>(p.x, p.K, chunk_row(c + 1 + D), m_end, p.K, rb[s]);
+            // only the LDS writes must retire before the barrier (not the look-ahead loads)
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        };
+        static_assert(D == 2, "the host guarantees an even chunk count >= 2 for full tiles");
+        int c0 = 0;
+        for (; c0 + D < nchunks; c0 += D) {
+            step(std::integral_constant<int, 0>{}, c0);
+            step(std::integral_constant<int, 1>{}, c0 + 1);
+        }
+        step(std::integral_constant<int, 0>{}, c0);
+        compute(lds[1]);
+    } else {
     float4 va[perA], vb[perB];
     if (nchunks > 0) {
         load_tile<TN, FULL>(p.dz, p.N, m_begin, m_end, p.N, va);
@@ -160,27 +224,14 @@ __global__ __launch_bounds__(kThreadsW, 2) void wgrad_x6_kernel(WgradParams p) {
             load_tile<TN, FULL>(p.dz, p.N, m0, m_end, p.N, va);
             load_tile<kTK, FULL>(p.x, p.K, m0, m_end, p.K, vb);
         }
-        const char* a_img = lds[buf];
-        const char* b_img = lds[buf] + PL * planeA;
-        Frag bf[J][PL];
-#pragma unroll
-        for (int j = 0; j < J; ++j)
-#pragma unroll
-            for (int q = 0; q < PL; ++q) bf[j][q] = read_frag_tr<kTK, Frag>(b_img + q * planeB, wk * (J * 32) + j * 32);
-#pragma unroll
-        for (int i = 0; i < I; ++i) {
-            Frag af[PL];
-#pragma unroll
-            for (int q = 0; q < PL; ++q) af[q] = read_frag_tr<TN, Frag>(a_img + q * planeA, wn * (I * 32) + i * 32);
-#pragma unroll
-            for (int j = 0; j < J; ++j) acc[i][j] = Arith<PL>::mfma(af, bf[j], acc[i][j]);
-        }
+        compute(lds[buf]);
         if (more) {
             store_tile<TN, PL>(va, lds[buf ^ 1], sa);
             store_tile<kTK, PL>(vb, lds[buf ^ 1] + PL * planeA, sb);
         }
         __syncthreads();
     }
+    }  // !FULL
 
     // partial tile -> part[s][n][k]; C/D map: col (k) = lane & 31, row (n) = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
     const int lane = threadIdx.x & 63;
@@ -331,7 +382,8 @@ extern "C" int rslrl_linear_wgrad_ex(const float* dz, const float* dz_amax, cons
     if (workspace_bytes < rslrl_linear_wgrad_workspace_bytes(M, N, K)) return RSLRL_E_WORKSPACE_TOO_SMALL;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     WgradParams p{dz, x, static_cast<float*>(workspace), M, rows_per, N, K, dz_amax, x_amax};
-    bool full = (M % rows_per == 0) && K == kTK;  // and N == TN, checked per branch
+    // full tiles: whole chunks, an even count of them >= 2 (the look-ahead loop), K == kTK (and N == TN, per branch)
+    bool full = (M % rows_per == 0) && K == kTK && (rows_per / kMC) % kWgradDepth == 0;
     const dim3 g(static_cast<unsigned>(S)), b(kThreadsW);
     auto go = [&](auto tn, auto pl) {
         constexpr int TN = decltype(tn)::value, PL = decltype(pl)::value;
