@@ -654,7 +654,8 @@ __device__ __forceinline__ void h3_deep_loop(const GemmParams& p, int64_t row0, 
 
 // 128 rows x 256 columns per workgroup: waves 2 (M) x 4 (N) of 64 x 64 (2 x 2 MFMA tiles); MINW = 4:
 // two workgroups per CU (<= 128 VGPRs), 2: one (the register-hungrier short-K dgrad epilogues).
-// NR: rows of the fused weight gradient (kEpiEluGradWgrad: Nred rounded up to 4; otherwise unused).
+// NR: rows of the fused weight gradient (kEpiEluGradWgrad: Nred rounded up to 4); kEpiBiasEluOut: 1 = VALU output
+// layer (<= 4 outputs), 4 = MFMA output layer (separate code: one register allocation for both spilled).
 // PL: operand planes (3: x6 bf16 on a layout-0 image; 2: h3 fp16 on a layout-2 image, A scaled from *p.a_amax).
 template <int EPI, bool FULL, int MINW, int NR = 4, int PL = 3>
 __global__ __launch_bounds__(kThreads, MINW) void mlp_gemm_x6_kernel(GemmParams p, const uint4* __restrict__ bimg) {
@@ -875,7 +876,7 @@ __global__ __launch_bounds__(kThreads, MINW) void mlp_gemm_x6_kernel(GemmParams 
             return staged ? reinterpret_cast<float*>(lds[1]) + w * 4 * I * tile : reinterpret_cast<float*>(lds[w]);
         };
         const uint4* oimg = p.oimg + wn * (2 * 2 * 3 * 64);
-        const bool valu = p.nout <= 4;  // the critic's value head: VALU dot products beat 32-row MFMA tiles
+        constexpr bool valu = NR == 1;  // the critic's value head: VALU dot products beat 32-row MFMA tiles
 #pragma unroll
         for (int i = 0; i < I; ++i) {
             const int64_t row = row0 + wm * (BM / 2) + i * 32 + l32;
@@ -934,7 +935,7 @@ __global__ __launch_bounds__(kThreads, MINW) void mlp_gemm_x6_kernel(GemmParams 
                     }
                     __builtin_amdgcn_wave_barrier();
                 }
-                if (valu) {
+                if constexpr (valu) {
                     // <= 4 outputs: fp32 FMA chains over the lane's 16 columns (the image's fp32 copy)
                     const float4* wf = reinterpret_cast<const float4*>(p.oimg + kOutImagePlaneUnits) +
                                        2 * ((((wn * 2 + j) * 2) * 2 + h) * 32);
@@ -967,7 +968,7 @@ __global__ __launch_bounds__(kThreads, MINW) void mlp_gemm_x6_kernel(GemmParams 
                 }
             }
             float* rd = red_of(wm) + (wn * I + i) * tile;
-            if (valu) {  // the two lane halves hold different columns of the same row
+            if constexpr (valu) {  // the two lane halves hold different columns of the same row
 #pragma unroll
                 for (int o = 0; o < 4; ++o) {
                     const float t = oval[o] + __shfl_xor(oval[o], 32, 64);
@@ -1334,13 +1335,18 @@ int launch(const GemmParams& p, const void* bimage, hipStream_t st) {
                 }
             }
         } else if constexpr (EPI == kEpiBiasEluOut) {
-            if (out_fwd_occupancy() == 2) {
-                if (fullm) hipLaunchKernelGGL((mlp_gemm_x6_kernel<EPI, true, 2, 4, PL>), g, b, 0, st, p, img);
-                else hipLaunchKernelGGL((mlp_gemm_x6_kernel<EPI, false, 2, 4, PL>), g, b, 0, st, p, img);
-            } else {
-                if (fullm) hipLaunchKernelGGL((mlp_gemm_x6_kernel<EPI, true, 4, 4, PL>), g, b, 0, st, p, img);
-                else hipLaunchKernelGGL((mlp_gemm_x6_kernel<EPI, false, 4, 4, PL>), g, b, 0, st, p, img);
-            }
+            auto go = [&](auto nr) {  // NR 1: VALU output layer (nout <= 4), 4: MFMA output layer
+                constexpr int NR = decltype(nr)::value;
+                if (out_fwd_occupancy() == 2) {
+                    if (fullm) hipLaunchKernelGGL((mlp_gemm_x6_kernel<EPI, true, 2, NR, PL>), g, b, 0, st, p, img);
+                    else hipLaunchKernelGGL((mlp_gemm_x6_kernel<EPI, false, 2, NR, PL>), g, b, 0, st, p, img);
+                } else {
+                    if (fullm) hipLaunchKernelGGL((mlp_gemm_x6_kernel<EPI, true, 4, NR, PL>), g, b, 0, st, p, img);
+                    else hipLaunchKernelGGL((mlp_gemm_x6_kernel<EPI, false, 4, NR, PL>), g, b, 0, st, p, img);
+                }
+            };
+            if (p.nout <= 4) go(std::integral_constant<int, 1>{});
+            else go(std::integral_constant<int, 4>{});
         } else if (short_k) {
             if (fullm) hipLaunchKernelGGL((mlp_gemm_x6_kernel<EPI, true, 2, 4, PL>), g, b, 0, st, p, img);
             else hipLaunchKernelGGL((mlp_gemm_x6_kernel<EPI, false, 2, 4, PL>), g, b, 0, st, p, img);

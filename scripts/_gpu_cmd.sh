@@ -1,4 +1,6 @@
 set -e
-mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1
-timeout -k 10 200 python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-extra > gpurun_out/bench_h3.json 2>gpurun_out/bench_h3.err
+mkdir -p gpurun_out/pmc
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+rm -rf gpurun_out/pmc/*
+timeout -s KILL 120 rocprofv3 --kernel-trace --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE GRBM_COUNT --output-format csv -d gpurun_out/pmc/p1 -o run -- python3 scripts/h3_probe.py > gpurun_out/pmc/p1.json 2>&1
+timeout -s KILL 120 rocprofv3 --kernel-trace --pmc SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VMEM SQ_INST_LEVEL_VMEM SQ_INSTS_VMEM_RD --output-format csv -d gpurun_out/pmc/p2 -o run -- python3 scripts/h3_probe.py > gpurun_out/pmc/p2.json 2>&1
