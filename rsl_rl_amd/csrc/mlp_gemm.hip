@@ -1250,13 +1250,30 @@ __global__ __launch_bounds__(kBlock) void colsum_slice_kernel(float* __restrict_
     }
 }
 
-__global__ __launch_bounds__(kFoldCols) void colsum_fold_kernel(const float* __restrict__ part, int slices, int n,
-                                                                int per, float* __restrict__ out) {
-    const int col = blockIdx.x * kFoldCols + threadIdx.x;
-    if (col >= n) return;
+// pass 2: thread (group g, column c) loads slices g, g + 4, ... (<= 16, all loads issued before the adds) and the
+// four group sums are added in g order
+__global__ __launch_bounds__(kBlock) void colsum_fold_kernel(const float* __restrict__ part, int slices, int n,
+                                                             int per, float* __restrict__ out) {
+    __shared__ double scratch[kFoldPhases][kFoldCols];
+    const int c = threadIdx.x % kFoldCols, g = threadIdx.x / kFoldCols;
+    const int col = blockIdx.x * kFoldCols + c;
+    constexpr int kMaxPer = kFoldSlices / kFoldPhases;
+    float v[kMaxPer];
+#pragma unroll
+    for (int i = 0; i < kMaxPer; ++i) {
+        const int s = g + kFoldPhases * i;
+        v[i] = (col < n && s < slices) ? part[static_cast<int64_t>(s) * per * n + col] : 0.f;
+    }
     double tot = 0.0;
-    for (int s = 0; s < slices; ++s) tot += static_cast<double>(part[static_cast<int64_t>(s) * per * n + col]);
-    out[col] = static_cast<float>(tot);
+#pragma unroll
+    for (int i = 0; i < kMaxPer; ++i) tot += static_cast<double>(v[i]);
+    scratch[g][c] = tot;
+    __syncthreads();
+    if (g == 0 && col < n) {
+        double t = 0.0;
+        for (int q = 0; q < kFoldPhases; ++q) t += scratch[q][c];
+        out[col] = static_cast<float>(t);
+    }
 }
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
@@ -1480,7 +1497,7 @@ extern "C" int rslrl_column_sum_fold(float* partials, int64_t tiles, int32_t N, 
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     hipLaunchKernelGGL(colsum_slice_kernel, dim3(cg, static_cast<unsigned>(slices)), dim3(kBlock), 0, st, partials,
                        static_cast<int>(tiles), N, per);
-    hipLaunchKernelGGL(colsum_fold_kernel, dim3(cg), dim3(kFoldCols), 0, st, partials, slices, N, per, out);
+    hipLaunchKernelGGL(colsum_fold_kernel, dim3(cg), dim3(kBlock), 0, st, partials, slices, N, per, out);
     return launch_status();
 }
 

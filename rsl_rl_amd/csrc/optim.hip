@@ -35,11 +35,17 @@ __global__ __launch_bounds__(kThreadsA) void grad_sq_kernel(rslrl_adam_args_t a,
     const int64_t total = a.offsets[a.n];
     const Span sp = block_span(total);
     double s = 0.0;
-    int ti = 0;
-    for (int64_t e = sp.begin + threadIdx.x; e < sp.end; e += kThreadsA) {
-        while (e >= a.offsets[ti + 1]) ++ti;
-        const float g = a.t[ti].grad[e - a.offsets[ti]];
-        s += static_cast<double>(g) * static_cast<double>(g);
+    // tensors in order, each clipped to the block's span: the tensor index is wave-uniform, so its pointer and
+    // offsets are scalar loads (a per-lane index into the argument block made every element wait on a load
+    // chain)
+    for (int ti = 0; ti < a.n; ++ti) {
+        const int64_t o0 = a.offsets[ti], o1 = a.offsets[ti + 1];
+        const int64_t lo = sp.begin > o0 ? sp.begin : o0, hi = sp.end < o1 ? sp.end : o1;
+        const float* __restrict__ g = a.t[ti].grad - o0;
+        for (int64_t e = lo + threadIdx.x; e < hi; e += kThreadsA) {
+            const float v = g[e];
+            s += static_cast<double>(v) * static_cast<double>(v);
+        }
     }
     // block sum in a fixed order (wave butterflies, then waves in order)
     s = wave_sum(s);
@@ -55,11 +61,21 @@ __global__ __launch_bounds__(kThreadsA) void grad_sq_kernel(rslrl_adam_args_t a,
         last = t == gridDim.x - 1;
     }
     __syncthreads();
-    if (!last || threadIdx.x != 0) return;
+    if (!last) return;
+    // the last block folds the kBlocks partials in a fixed order: one per thread (all loads in flight at
+    // once), wave butterflies, then the waves in order
+    static_assert(kBlocks <= kThreadsA, "one partial per thread");
+    double pv = 0.0;
+    if (threadIdx.x < kBlocks)
+        pv = __longlong_as_double(__hip_atomic_load(reinterpret_cast<unsigned long long*>(part + threadIdx.x),
+                                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    pv = wave_sum(pv);
+    __syncthreads();  // scratch is reused
+    if ((threadIdx.x & (kWave - 1)) == 0) scratch[threadIdx.x / kWave] = pv;
+    __syncthreads();
+    if (threadIdx.x != 0) return;
     double tot = 0.0;
-    for (int b = 0; b < kBlocks; ++b)
-        tot += __longlong_as_double(__hip_atomic_load(reinterpret_cast<unsigned long long*>(part + b), __ATOMIC_RELAXED,
-                                                      __HIP_MEMORY_SCOPE_AGENT));
+    for (int w = 0; w < kThreadsA / kWave; ++w) tot += scratch[w];
     float c = 1.0f;
     if (a.max_grad_norm > 0.0f) {
         const float norm = static_cast<float>(sqrt(tot));
@@ -77,31 +93,30 @@ __global__ __launch_bounds__(kThreadsA) void adam_kernel(rslrl_adam_args_t a, co
     const float c = *coef;
     const double lr = a.lr_dev ? static_cast<double>(*a.lr_dev) : a.lr;
     const double b1 = a.beta1, b2 = a.beta2, eps = a.eps;
-    int ti = -1;
-    float bc1 = 1.f, bc2s = 1.f, step_size = 0.f;
-    for (int64_t e = sp.begin + threadIdx.x; e < sp.end; e += kThreadsA) {
-        int tn = ti < 0 ? 0 : ti;
-        while (e >= a.offsets[tn + 1]) ++tn;
-        if (tn != ti) {
-            ti = tn;
-            const double step = static_cast<double>(*a.t[ti].step);
-            bc1 = static_cast<float>(1.0 - pow(b1, step));
-            bc2s = static_cast<float>(sqrt(1.0 - pow(b2, step)));
-            step_size = static_cast<float>(lr / static_cast<double>(bc1));
+    // tensors in order, clipped to the block's span (wave-uniform tensor index: scalar pointer loads)
+    for (int ti = 0; ti < a.n; ++ti) {
+        const int64_t o0 = a.offsets[ti], o1 = a.offsets[ti + 1];
+        const int64_t lo = sp.begin > o0 ? sp.begin : o0, hi = sp.end < o1 ? sp.end : o1;
+        if (lo >= hi) continue;
+        const rslrl_adam_tensor_t t = a.t[ti];
+        const double step = static_cast<double>(*t.step);
+        const float bc1 = static_cast<float>(1.0 - pow(b1, step));
+        const float bc2s = static_cast<float>(sqrt(1.0 - pow(b2, step)));
+        const float step_size = static_cast<float>(lr / static_cast<double>(bc1));
+        for (int64_t e = lo + threadIdx.x; e < hi; e += kThreadsA) {
+            const int64_t i = e - o0;
+            const float g = t.grad[i] * c;  // the clipped gradient (fp32 multiply, as torch's foreach mul)
+            // torch's build contracts b*m + (1-b)*g into one double fma; the unfused sum rounds differently in
+            // ~0.3% of elements once narrowed to fp32 (measured), so the fma is spelled out here
+            const double gd = static_cast<double>(g);
+            const float m = static_cast<float>(fma(b1, static_cast<double>(t.exp_avg[i]), (1.0 - b1) * gd));
+            const float v = static_cast<float>(fma(b2, static_cast<double>(t.exp_avg_sq[i]), (1.0 - b2) * gd * gd));
+            const float q = sqrtf(v) / bc2s;  // fp32 division, then the double eps add (fused_adam_utils.cuh:77)
+            const float denom = static_cast<float>(static_cast<double>(q) + eps);
+            t.exp_avg[i] = m;
+            t.exp_avg_sq[i] = v;
+            t.param[i] = t.param[i] - step_size * m / denom;
         }
-        const rslrl_adam_tensor_t& t = a.t[ti];
-        const int64_t i = e - a.offsets[ti];
-        const float g = t.grad[i] * c;  // the clipped gradient (fp32 multiply, as torch's foreach mul)
-        // torch's build contracts b*m + (1-b)*g into one double fma; the unfused sum rounds differently in
-        // ~0.3% of elements once narrowed to fp32 (measured), so the fma is spelled out here
-        const double gd = static_cast<double>(g);
-        const float m = static_cast<float>(fma(b1, static_cast<double>(t.exp_avg[i]), (1.0 - b1) * gd));
-        const float v = static_cast<float>(fma(b2, static_cast<double>(t.exp_avg_sq[i]), (1.0 - b2) * gd * gd));
-        const float q = sqrtf(v) / bc2s;  // fp32 division, then the double eps add (fused_adam_utils.cuh:77)
-        const float denom = static_cast<float>(static_cast<double>(q) + eps);
-        t.exp_avg[i] = m;
-        t.exp_avg_sq[i] = v;
-        t.param[i] = t.param[i] - step_size * m / denom;
     }
 }
 
