@@ -316,6 +316,10 @@ typedef struct {
 size_t rslrl_linear_bimage_h3_bytes(int32_t depth);
 size_t rslrl_amax_workspace_bytes(void);
 int rslrl_linear_gemm(const rslrl_linear_args_t* args /* host struct */, rslrl_stream_t stream);
+/* Two RSLRL_LINEAR_FWD[_ELU] problems of the same op, arithmetic, M, K and N in one launch (the rollout's actor
+ * and critic layer l: at M = 65536 one problem fills half of the workgroup slots).  Results are identical to
+ * two rslrl_linear_gemm calls; distinct amax workspaces when both write an amax. */
+int rslrl_linear_gemm_pair(const rslrl_linear_args_t* a0, const rslrl_linear_args_t* a1, rslrl_stream_t stream);
 int rslrl_linear_wgrad_ex(const float* dz, const float* dz_amax, const float* x, const float* x_amax, int64_t M,
                           int32_t N, int32_t K, int32_t arith, float* dw, void* workspace, size_t workspace_bytes,
                           rslrl_stream_t stream);

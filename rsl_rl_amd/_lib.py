@@ -56,6 +56,7 @@ EXPORTED_SYMBOLS = (
     "rslrl_linear_bimage_h3_bytes",
     "rslrl_amax_workspace_bytes",
     "rslrl_linear_gemm",
+    "rslrl_linear_gemm_pair",
     "rslrl_linear_wgrad_ex",
     "rslrl_ppo_update_tail",
     "rslrl_adam_workspace_bytes",
@@ -285,6 +286,8 @@ def _declare(L):
     L.rslrl_amax_workspace_bytes.argtypes = []
     L.rslrl_linear_gemm.restype = ctypes.c_int
     L.rslrl_linear_gemm.argtypes = [ctypes.POINTER(LinearArgs), P]
+    L.rslrl_linear_gemm_pair.restype = ctypes.c_int
+    L.rslrl_linear_gemm_pair.argtypes = [ctypes.POINTER(LinearArgs), ctypes.POINTER(LinearArgs), P]
     L.rslrl_adam_workspace_bytes.restype = SZ
     L.rslrl_adam_workspace_bytes.argtypes = []
     L.rslrl_clip_adam_step.restype = ctypes.c_int

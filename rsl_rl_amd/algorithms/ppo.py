@@ -152,8 +152,14 @@ class PPO:
     def act(self, obs):
         if self.policy.is_recurrent:
             self.transition.hidden_states = self.policy.get_hidden_states()
-        self.transition.actions = self.policy.act(obs).detach()
-        self.transition.values = self.policy.evaluate(obs).detach()
+        pcls = type(self.policy)
+        if isinstance(self.policy, ActorCritic) and pcls.act is ActorCritic.act and pcls.evaluate is ActorCritic.evaluate:
+            # the actor's and critic's hidden layers batched into one launch each (same values and draws)
+            actions, values = self.policy.act_and_evaluate(obs)
+        else:
+            actions, values = self.policy.act(obs), self.policy.evaluate(obs)
+        self.transition.actions = actions.detach()
+        self.transition.values = values.detach()
         self.transition.action_mean = self.policy.action_mean.detach()
         self.transition.action_sigma = self.policy.action_std.detach()
         self.transition.observations = obs

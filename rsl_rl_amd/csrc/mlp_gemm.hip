@@ -657,8 +657,8 @@ __device__ __forceinline__ void h3_deep_loop(const GemmParams& p, int64_t row0, 
 // NR: rows of the fused weight gradient (kEpiEluGradWgrad: Nred rounded up to 4); kEpiBiasEluOut: 1 = VALU output
 // layer (<= 4 outputs), 4 = MFMA output layer (separate code: one register allocation for both spilled).
 // PL: operand planes (3: x6 bf16 on a layout-0 image; 2: h3 fp16 on a layout-2 image, A scaled from *p.a_amax).
-template <int EPI, bool FULL, int MINW, int NR = 4, int PL = 3>
-__global__ __launch_bounds__(kThreads, MINW) void mlp_gemm_x6_kernel(GemmParams p, const uint4* __restrict__ bimg) {
+template <int EPI, bool FULL, int NR, int PL>
+__device__ __forceinline__ void mlp_gemm_x6_body(GemmParams p, const uint4* __restrict__ bimg) {
     static_assert(PL == 3 || EPI != kEpiEluGradWgrad, "the fused output-layer backward is x6 only");
     using Frag = typename Arith<PL>::frag;
     constexpr int BM = kBM;
@@ -1025,6 +1025,25 @@ __global__ __launch_bounds__(kThreads, MINW) void mlp_gemm_x6_kernel(GemmParams 
             p.colsum[static_cast<int64_t>(blockIdx.x) * p.N + col] = colred[col] + colred[kBN + col];
     }
     if constexpr (EPI != kEpiBiasEluOut) amax_commit(p, amx);
+}
+
+template <int EPI, bool FULL, int MINW, int NR = 4, int PL = 3>
+__global__ __launch_bounds__(kThreads, MINW) void mlp_gemm_x6_kernel(GemmParams p, const uint4* __restrict__ bimg) {
+    mlp_gemm_x6_body<EPI, FULL, NR, PL>(p, bimg);
+}
+
+// Two independent problems of one shape in one launch (blockIdx.y picks the problem): the rollout's actor and
+// critic layers, whose 512-tile launches (M = 65536) leave half of the 2-per-CU workgroup slots idle.  Each
+// problem keeps its own amax output and workspace (the protocol counts gridDim.x workgroups per problem).
+struct GemmPair {
+    GemmParams p[2];
+    const uint4* img[2];
+};
+
+template <int EPI, bool FULL, int PL>
+__global__ __launch_bounds__(kThreads, 4) void mlp_gemm_x6_pair_kernel(GemmPair b) {
+    const int y = blockIdx.y;
+    mlp_gemm_x6_body<EPI, FULL, 4, PL>(b.p[y], b.img[y]);
 }
 
 // ---- the same x6 GEMM on v_mfma_f32_16x16x32_bf16 ("paired" x6).  Under load the chip holds a higher
@@ -1579,4 +1598,67 @@ extern "C" int rslrl_linear_gemm(const rslrl_linear_args_t* a, rslrl_stream_t st
         default:
             return RSLRL_E_INVALID_ARGUMENT;
     }
+}
+
+namespace {
+// validated GemmParams of a forward op (rslrl_linear_gemm's checks for RSLRL_LINEAR_FWD[_ELU])
+int fwd_params(const rslrl_linear_args_t* a, GemmParams& p) {
+    const bool h3 = a->arith == RSLRL_ARITH_H3;
+    if (!h3 && a->arith != RSLRL_ARITH_X6) return RSLRL_E_INVALID_ARGUMENT;
+    if (a->M < 0 || a->K < 1 || a->N < 1 || a->N > kBN || (a->K & 3) || a->K > INT32_MAX / 2)
+        return RSLRL_E_INVALID_ARGUMENT;
+    if (!a->a || !a->bimage || (h3 && !a->a_amax) || !a->bias || !a->c) return RSLRL_E_INVALID_ARGUMENT;
+    if (a->amax_out && !a->amax_workspace) return RSLRL_E_INVALID_ARGUMENT;
+    if (!aligned16(a->a) || !aligned16(a->bimage)) return RSLRL_E_MISALIGNED;
+    p = GemmParams{};
+    p.a = a->a;
+    p.M = a->M;
+    p.K = a->K;
+    p.N = a->N;
+    p.a_amax = a->a_amax;
+    p.amax_out = a->amax_out;
+    p.amax_ws = static_cast<unsigned*>(a->amax_workspace);
+    p.deep = h3_deep(a->op);
+    p.bias = a->bias;
+    p.c = a->c;
+    return RSLRL_OK;
+}
+
+template <int EPI, int PL>
+int launch_pair(const GemmPair& b, bool fullm, hipStream_t st) {
+    const int64_t tiles = ceil_div(b.p[0].M, kBM);
+    if (tiles > INT32_MAX) return RSLRL_E_INVALID_ARGUMENT;
+    const dim3 g(static_cast<unsigned>(tiles), 2), blk(kThreads);
+    if (fullm) hipLaunchKernelGGL((mlp_gemm_x6_pair_kernel<EPI, true, PL>), g, blk, 0, st, b);
+    else hipLaunchKernelGGL((mlp_gemm_x6_pair_kernel<EPI, false, PL>), g, blk, 0, st, b);
+    return launch_status();
+}
+}  // namespace
+
+// Two forward problems of one shape (op, arithmetic, M, K, N) in one launch -- e.g. the actor's and the
+// critic's layer l in the rollout.  Each keeps its own operands, bias, output, amax and amax workspace.
+extern "C" int rslrl_linear_gemm_pair(const rslrl_linear_args_t* a0, const rslrl_linear_args_t* a1,
+                                      rslrl_stream_t stream) {
+    if (!a0 || !a1) return RSLRL_E_INVALID_ARGUMENT;
+    const int op = a0->op;
+    if (a1->op != op || (op != RSLRL_LINEAR_FWD && op != RSLRL_LINEAR_FWD_ELU)) return RSLRL_E_UNSUPPORTED;
+    if (a0->arith != a1->arith || a0->M != a1->M || a0->K != a1->K || a0->N != a1->N) return RSLRL_E_INVALID_ARGUMENT;
+    if (a0->amax_out && a1->amax_out && a0->amax_workspace == a1->amax_workspace) return RSLRL_E_INVALID_ARGUMENT;
+    const bool h3 = a0->arith == RSLRL_ARITH_H3;
+    if (!h3 && x6_shape() == 16) {  // the opt-in 16x16x32 x6 forward has no pair kernel: two launches
+        const int rc = rslrl_linear_gemm(a0, stream);
+        return rc ? rc : rslrl_linear_gemm(a1, stream);
+    }
+    GemmPair b{};
+    for (int i = 0; i < 2; ++i) {
+        const int rc = fwd_params(i ? a1 : a0, b.p[i]);
+        if (rc) return rc;
+        b.img[i] = static_cast<const uint4*>((i ? a1 : a0)->bimage);
+    }
+    if (a0->M == 0) return RSLRL_OK;
+    const bool fullm = a0->M % kBM == 0 && a0->K % kKC == 0;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (op == RSLRL_LINEAR_FWD_ELU)
+        return h3 ? launch_pair<kEpiBiasElu, 2>(b, fullm, st) : launch_pair<kEpiBiasElu, 3>(b, fullm, st);
+    return h3 ? launch_pair<kEpiBias, 2>(b, fullm, st) : launch_pair<kEpiBias, 3>(b, fullm, st);
 }

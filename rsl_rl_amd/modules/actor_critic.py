@@ -14,6 +14,7 @@ import torch.nn as nn
 from torch.distributions import Normal
 
 from ..networks import MLP, EmpiricalNormalization
+from ..networks.fused_mlp import fused_mlp_forward_pair
 
 
 class ActorCritic(nn.Module):
@@ -98,17 +99,17 @@ class ActorCritic(nn.Module):
     def entropy(self):
         return self.distribution.entropy().sum(dim=-1)
 
-    def _mean_and_std(self, obs):
-        """(mean [B, A], std) with std either the shared [A] parameter-derived vector or per-row [B, A]."""
+    def _mean_and_std(self, obs, actor_out=None):
+        """(mean [B, A], std) with std either the shared [A] parameter-derived vector or per-row [B, A];
+        actor_out: the actor's output when it was already computed (act_and_evaluate)."""
+        out = self.actor(obs) if actor_out is None else actor_out
         if self.state_dependent_std:
-            mean_and_std = self.actor(obs)
-            mean, std = torch.unbind(mean_and_std, dim=-2)
+            mean, std = torch.unbind(out, dim=-2)
             if self.noise_std_type == "log":
                 std = torch.exp(std)
             return mean, std
-        mean = self.actor(obs)
         std = self.std if self.noise_std_type == "scalar" else torch.exp(self.log_std)
-        return mean, std
+        return out, std
 
     def update_distribution(self, obs):
         mean, std = self._mean_and_std(obs)
@@ -126,12 +127,30 @@ class ActorCritic(nn.Module):
     def act(self, obs, **kwargs):
         obs = self.actor_obs_normalizer(self.get_actor_obs(obs))
         self.update_distribution(obs)
+        return self._sample()
+
+    def _sample(self):
         # = self.distribution.sample(): torch.normal(loc, scale) draws normal_(0, 1) and applies
         # .mul_(scale).add_(loc) -- the same values from the same generator stream -- but first checks
         # scale.min() >= 0 with a device-to-host read that stalls the launch queue every env step
         loc, scale = self.distribution.loc, self.distribution.scale
         with torch.no_grad():
             return torch.empty_like(loc).normal_().mul_(scale).add_(loc)
+
+    def act_and_evaluate(self, obs):
+        """(act(obs), evaluate(obs)) of the rollout step (ppo.py:155-156) with the actor's and the critic's
+        same-shape hidden layers batched into one launch each (networks/fused_mlp.fused_mlp_forward_pair);
+        the same values, distribution and generator draws as the two calls.  Falls back to them when the
+        pair does not qualify."""
+        a_obs = self.actor_obs_normalizer(self.get_actor_obs(obs))
+        c_obs = self.critic_obs_normalizer(self.get_critic_obs(obs))
+        pair = fused_mlp_forward_pair(self.actor, a_obs, self.critic, c_obs) if a_obs.is_cuda else None
+        if pair is None:
+            self.update_distribution(a_obs)
+            return self._sample(), self.critic(c_obs)
+        mean, std = self._mean_and_std(a_obs, actor_out=pair[0])
+        self.distribution = Normal(mean, std.expand_as(mean))
+        return self._sample(), pair[1]
 
     def act_inference(self, obs):
         obs = self.actor_obs_normalizer(self.get_actor_obs(obs))

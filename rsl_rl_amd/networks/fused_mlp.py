@@ -67,13 +67,14 @@ def _split() -> bool:
 _amax_ws: dict = {}
 
 
-def _amax_workspace(device):
-    """Per-device {max bits, ticket} words of the amax reduction (zero once; every launch leaves them zero)."""
-    ws = _amax_ws.get(device)
+def _amax_workspace(device, slot: int = 0):
+    """Per-device {max bits, ticket} words of the amax reduction (zero once; every launch leaves them zero);
+    slot 1: the second problem of a pair launch (rslrl_linear_gemm_pair needs distinct workspaces)."""
+    ws = _amax_ws.get((device, slot))
     if ws is None:
         n = max(_lib.lib().rslrl_amax_workspace_bytes() // 4, 4)
         ws = torch.zeros(n, dtype=torch.int32, device=device)
-        _amax_ws[device] = ws
+        _amax_ws[(device, slot)] = ws
     return ws
 
 
@@ -161,12 +162,16 @@ def bimage(w, transposed: bool):
     return bimages([(w, transposed)])[0]
 
 
-def _gemm(op, arith, a, a_amax, N, img, *, bias=None, h=None, c=None, colsum=None, wpart=None, out_img=None,
-          out_bias=None, y=None, nout=0, amax_out=None):
+def _gemm_args(op, arith, a, a_amax, N, img, *, bias=None, h=None, c=None, colsum=None, wpart=None, out_img=None,
+               out_bias=None, y=None, nout=0, amax_out=None, slot=0):
     M, K = a.shape
-    args = _lib.LinearArgs(op, arith, a.data_ptr(), _ptr(a_amax), M, K, N, img.data_ptr(), _ptr(bias), _ptr(h), _ptr(c),
-                           _ptr(colsum), _ptr(wpart), _ptr(out_img), _ptr(out_bias), _ptr(y), nout, _ptr(amax_out),
-                           _ptr(_amax_workspace(a.device)) if amax_out is not None else None)
+    return _lib.LinearArgs(op, arith, a.data_ptr(), _ptr(a_amax), M, K, N, img.data_ptr(), _ptr(bias), _ptr(h),
+                           _ptr(c), _ptr(colsum), _ptr(wpart), _ptr(out_img), _ptr(out_bias), _ptr(y), nout,
+                           _ptr(amax_out), _ptr(_amax_workspace(a.device, slot)) if amax_out is not None else None)
+
+
+def _gemm(op, arith, a, a_amax, N, img, **kw):
+    args = _gemm_args(op, arith, a, a_amax, N, img, **kw)
     rc = _lib.lib().rslrl_linear_gemm(ctypes.byref(args), _stream(a))
     _lib.check(rc, "rslrl_linear_gemm")
 
@@ -185,6 +190,22 @@ def linear_fwd_ex(x, b, N: int, elu: bool, img, arith, x_amax=None, want_amax=Fa
     with timer.span(f"linear_fwd[M={M},K={K},N={N}]{_tag(arith)}", x.device, 4 * M * (K + N), 2 * M * K * N):
         _gemm(_lib.LINEAR_FWD_ELU if elu else _lib.LINEAR_FWD, arith, x, x_amax, N, img, bias=b, c=y, amax_out=amax)
     return y, amax
+
+
+def linear_fwd_pair(xs, bs, N: int, elu: bool, imgs, arith, x_amaxes, want_amax):
+    """linear_fwd_ex of two problems of one shape in one launch (rslrl_linear_gemm_pair): xs, bs, imgs,
+    x_amaxes, want_amax are pairs; returns ([y0, y1], [amax0, amax1])."""
+    M, K = xs[0].shape
+    ys = [torch.empty(M, N, device=x.device, dtype=torch.float32) for x in xs]
+    amaxes = [torch.empty(1, device=x.device, dtype=torch.float32) if w else None for x, w in zip(xs, want_amax)]
+    op = _lib.LINEAR_FWD_ELU if elu else _lib.LINEAR_FWD
+    args = [_gemm_args(op, arith, xs[i], x_amaxes[i], N, imgs[i], bias=bs[i], c=ys[i], amax_out=amaxes[i], slot=i)
+            for i in range(2)]
+    with timer.span(f"linear_fwd_pair[M={M},K={K},N={N}]{_tag(arith)}", xs[0].device, 8 * M * (K + N),
+                    4 * M * K * N):
+        rc = _lib.lib().rslrl_linear_gemm_pair(ctypes.byref(args[0]), ctypes.byref(args[1]), _stream(xs[0]))
+    _lib.check(rc, "rslrl_linear_gemm_pair")
+    return ys, amaxes
 
 
 def linear_fwd(x, w, b, elu: bool, img=None):
@@ -500,6 +521,60 @@ def fusable_structure(mlp: nn.Sequential) -> bool:
 
 def fusable(mlp: nn.Sequential, x: torch.Tensor) -> bool:
     return x.is_cuda and x.dtype == torch.float32 and x.dim() == 2 and fusable_structure(mlp)
+
+
+def _unflatten(mlp, y):
+    for m in mlp:
+        if isinstance(m, nn.Unflatten):
+            y = m(y)
+    return y
+
+
+def fused_mlp_forward_pair(mlp_a: nn.Sequential, x_a: torch.Tensor, mlp_b: nn.Sequential, x_b: torch.Tensor):
+    """Inference forward of two MLPs (the actor and the critic of the rollout) with their same-shape hidden
+    layers batched into one launch each (rslrl_linear_gemm_pair); identical results to two fused_mlp_forward
+    calls.  Returns (y_a, y_b), or None when the pair does not qualify (gradients wanted, another GEMM mode,
+    different hidden shapes or batch sizes) -- the caller then runs the two forwards."""
+    if not (_split() and getattr(mlp_a, "_fused", True) and getattr(mlp_b, "_fused", True) and fusable(mlp_a, x_a)
+            and fusable(mlp_b, x_b) and x_a.shape[0] == x_b.shape[0]):
+        return None
+    la = [m for m in mlp_a if isinstance(m, nn.Linear)]
+    lb = [m for m in mlp_b if isinstance(m, nn.Linear)]
+    params = [p for m in la + lb for p in (m.weight, m.bias)]
+    if torch.is_grad_enabled() and any(p.requires_grad for p in params + [x_a, x_b]):
+        return None
+    if len(la) != len(lb) or any(a.weight.shape != b.weight.shape for a, b in zip(la[:-1], lb[:-1])):
+        return None
+    ws = ([m.weight for m in la], [m.weight for m in lb])
+    bs = ([m.bias for m in la], [m.bias for m in lb])
+    plans = [_plan(w) for w in ws]
+    h3 = plans[0][1]
+    fuse = [plans[0][2], plans[1][2]]
+    imgs = [_forward_images(ws[i], h3, fuse[i], backward=False) for i in range(2)]
+    nh = len(la) - 1
+    arith = lambda l: _lib.ARITH_H3 if h3[l] else _lib.ARITH_X6  # noqa: E731
+    h = [x_a if x_a.is_contiguous() else x_a.contiguous(), x_b if x_b.is_contiguous() else x_b.contiguous()]
+    amax = [None, None]
+    y = [None, None]
+    for l in range(nh):
+        want = l + 1 < nh and h3[l + 1]
+        last_fused = [fuse[i] and l == nh - 1 for i in range(2)]
+        if not any(last_fused):
+            h, amax = linear_fwd_pair(h, [bs[0][l], bs[1][l]], ws[0][l].shape[0], True, [imgs[0][0][l], imgs[1][0][l]],
+                                      arith(l), amax, [want, want])
+            continue
+        for i in range(2):  # the output layer's fused launches differ per network (output width)
+            if last_fused[i]:
+                h[i], y[i] = linear_fwd_out_ex(h[i], bs[i][l], ws[i][l].shape[0], imgs[i][0][l], arith(l), amax[i],
+                                               bs[i][-1], imgs[i][2], store_h=False)
+            else:
+                h[i], amax[i] = linear_fwd_ex(h[i], bs[i][l], ws[i][l].shape[0], True, imgs[i][0][l], arith(l),
+                                              amax[i], want)
+    out = []
+    for i, mlp in enumerate((mlp_a, mlp_b)):
+        yi = y[i] if y[i] is not None else F.linear(h[i], ws[i][-1], bs[i][-1])
+        out.append(_unflatten(mlp, yi))
+    return out[0], out[1]
 
 
 def fused_mlp_forward(mlp: nn.Sequential, x: torch.Tensor) -> torch.Tensor:

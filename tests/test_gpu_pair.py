@@ -1,0 +1,77 @@
+"""rslrl_linear_gemm_pair (two same-shape forward problems in one launch: the rollout's actor and critic layers)
+against two rslrl_linear_gemm calls -- bit-identical outputs and amaxes -- and ActorCritic.act_and_evaluate
+against act() + evaluate() (ppo.py:155-156) with the same generator state."""
+
+import pytest
+import torch
+
+from rsl_rl_amd import _lib
+from rsl_rl_amd.modules import ActorCritic
+from rsl_rl_amd.networks import fused_mlp
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("M,K,arith", [(65536, 48, "x6"), (65536, 256, "h3"), (1000, 256, "h3"), (777, 48, "x6")])
+def test_pair_matches_two_launches(M, K, arith, cuda_device):
+    dev = cuda_device
+    g = torch.Generator(device=dev).manual_seed(3)
+    N = 256
+    xs = [torch.nn.functional.elu(torch.randn(M, K, device=dev, generator=g)) * s for s in (1.0, 37.0)]
+    ws = [torch.randn(N, K, device=dev, generator=g) / K ** 0.5 for _ in range(2)]
+    bs = [torch.randn(N, device=dev, generator=g) * 0.1 for _ in range(2)]
+    h3 = arith == "h3"
+    layout = _lib.BIMAGE_LAYOUT_H3 if h3 else _lib.BIMAGE_LAYOUT_GEMM
+    imgs = fused_mlp.bimages([(w, False, layout) for w in ws])
+    ar = _lib.ARITH_H3 if h3 else _lib.ARITH_X6
+    x_amax = [x.abs().amax().reshape(1) if h3 else None for x in xs]
+    ref = [fused_mlp.linear_fwd_ex(xs[i], bs[i], N, True, imgs[i], ar, x_amax[i], want_amax=True) for i in range(2)]
+    ys, amaxes = fused_mlp.linear_fwd_pair(xs, bs, N, True, imgs, ar, x_amax, [True, True])
+    torch.cuda.synchronize()
+    for i in range(2):
+        assert torch.equal(ys[i], ref[i][0])
+        assert torch.equal(amaxes[i], ref[i][1])
+        assert float(amaxes[i]) == float(ys[i].abs().max())
+
+
+def test_pair_rejects_mismatched_shapes(cuda_device):
+    x = torch.randn(128, 48, device=cuda_device)
+    w = torch.randn(256, 48, device=cuda_device)
+    b = torch.zeros(256, device=cuda_device)
+    img = fused_mlp.bimages([(w, False)])[0]
+    y = torch.empty(128, 256, device=cuda_device)
+    a0 = fused_mlp._gemm_args(_lib.LINEAR_FWD_ELU, _lib.ARITH_X6, x, None, 256, img, bias=b, c=y)
+    a1 = fused_mlp._gemm_args(_lib.LINEAR_FWD_ELU, _lib.ARITH_X6, x[:64], None, 256, img, bias=b, c=y)
+    import ctypes
+
+    L = _lib.lib()
+    assert L.rslrl_linear_gemm_pair(ctypes.byref(a0), ctypes.byref(a1), None) == -1  # RSLRL_E_INVALID_ARGUMENT
+    a1 = fused_mlp._gemm_args(_lib.LINEAR_DGRAD_ELU, _lib.ARITH_X6, x, None, 256, img, bias=b, c=y)
+    assert L.rslrl_linear_gemm_pair(ctypes.byref(a0), ctypes.byref(a1), None) == -3  # RSLRL_E_UNSUPPORTED
+
+
+@pytest.mark.parametrize("critic_width,state_dependent_std", [(48, False), (48, True), (52, False)])
+def test_act_and_evaluate_matches_two_calls(critic_width, state_dependent_std, cuda_device, monkeypatch):
+    """Same obs width: every hidden layer but the fused output layer goes through the pair launch; another
+    critic width: the pair does not qualify and the two forwards run."""
+    torch.manual_seed(0)
+    obs = {"policy": torch.randn(4096, 48, device=cuda_device),
+           "critic": torch.randn(4096, critic_width, device=cuda_device)}
+    groups = {"policy": ["policy"], "critic": ["critic"]}
+    pol = ActorCritic(obs, groups, 12, actor_hidden_dims=[256, 256, 256], critic_hidden_dims=[256, 256, 256],
+                      actor_obs_normalization=True, critic_obs_normalization=True,
+                      state_dependent_std=state_dependent_std).to(cuda_device)
+    pol.update_normalization(obs)
+    calls = []
+    pair = fused_mlp.linear_fwd_pair
+    monkeypatch.setattr(fused_mlp, "linear_fwd_pair", lambda *a, **k: (calls.append(1), pair(*a, **k))[1])
+    with torch.inference_mode():
+        torch.cuda.manual_seed(5)
+        a_ref = pol.act(obs)
+        mean_ref, std_ref = pol.action_mean.clone(), pol.action_std.clone()
+        v_ref = pol.evaluate(obs)
+        torch.cuda.manual_seed(5)
+        a, v = pol.act_and_evaluate(obs)
+    assert len(calls) == (2 if critic_width == 48 else 0)
+    assert torch.equal(a, a_ref) and torch.equal(v, v_ref)
+    assert torch.equal(pol.action_mean, mean_ref) and torch.equal(pol.action_std, std_ref)
