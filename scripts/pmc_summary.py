@@ -32,7 +32,7 @@ SHORT = {
 }
 # kernels launched at several shapes are keyed "<short>@grid=<threads>"
 BY_GRID = {"x6_fwd_elu", "x6_dgrad_elu", "x6_wgrad", "wgrad_fold", "h3_fwd_elu", "h3_dgrad_elu", "h3_fwd_out",
-           "x6_dgrad_wgrad", "h3_wgrad256", "x6_wgrad64", "x6_fwd_out"}
+           "x6_dgrad_wgrad", "h3_wgrad256", "x6_wgrad64", "x6_fwd_out", "x6_fwd_elu_pair", "h3_fwd_elu_pair"}
 
 
 EPI_NAMES = {0: "fwd", 1: "fwd_elu", 2: "dgrad_elu", 3: "dgrad_wgrad", 4: "fwd_out"}
@@ -44,6 +44,9 @@ def gemm_name(kernel):
     m = re.search(r"mlp_gemm_x6_kernel<(\d+), \w+, \d+, \d+, (\d+)>", kernel)
     if m:
         return f"{'h3' if m.group(2) == '2' else 'x6'}_{EPI_NAMES.get(int(m.group(1)), m.group(1))}"
+    m = re.search(r"mlp_gemm_x6_pair_kernel<(\d+), \w+, (\d+)>", kernel)
+    if m:  # two problems per launch (grid y = 2): bytes per launch cover both
+        return f"{'h3' if m.group(2) == '2' else 'x6'}_{EPI_NAMES.get(int(m.group(1)), m.group(1))}_pair"
     m = re.search(r"wgrad_x6_kernel<(\d+), \w+, (\d+)>", kernel)
     if m:
         return f"{'h3' if m.group(2) == '2' else 'x6'}_wgrad{m.group(1)}"
