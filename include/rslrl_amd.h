@@ -255,7 +255,8 @@ size_t rslrl_fold_partials_workspace_bytes(int64_t S, int64_t NK);
 int rslrl_fold_partials(const float* partials, int64_t S, int64_t NK, float* out, void* workspace,
                         size_t workspace_bytes, rslrl_stream_t stream);
 
-/* Output-layer backward in one x6 launch (Nred <= 16, % 4 == 0): rslrl_linear_dgrad_elu's outputs plus this
+/* Output-layer backward in one launch (Nred <= 16, % 4 == 0; fp32 FMAs on the VALU, W rebuilt exactly from its x6
+ * image -- RSLRL_OUT_BWD=mfma selects the x6 MFMA kernel): rslrl_linear_dgrad_elu's outputs plus this
  * layer's weight gradient dW[Nred, K] = dz^T h and bias gradient db[Nred] = column sums of dz, as
  * per-128-row-tile partials [rslrl_linear_tiles(M)][Nred * K + Nred] (dW row-major, then db;
  * rslrl_linear_dgrad_wgrad_partial_bytes), folded by rslrl_fold_partials over Nred * K + Nred columns.

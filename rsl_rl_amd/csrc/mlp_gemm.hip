@@ -1341,6 +1341,161 @@ int out_fwd_occupancy() {  // tuning knob: RSLRL_OUT_FWD_OCC=2|4 (default 4)
     return v;
 }
 
+// ---- Output-layer backward on the VALU (RSLRL_LINEAR_DGRAD_ELU_WGRAD; x6 image of W^T as input).  With a
+// 4-16 wide reduction this op is a stream over H (read) and dZ_prev (written) with ~24 FMAs per element: MFMA
+// tiles buy nothing here and their epilogue needed 256 registers (one workgroup per CU, hundreds of bytes of
+// scratch per lane).  Per 128-row tile (workgroup of 4 waves, 32 rows each; lane l owns columns 4l..4l+3):
+//   z[c] = sum_o dZ[row][o] W[o][c] (fp32 FMA chain, o ascending; W rebuilt exactly from the image's three
+//   bf16 planes), dZ_prev = z * ELU'(H), column sums of dZ_prev, dW[o][c] += dZ[row][o] H[row][c], and
+//   db_out[o] = sum of dZ[row][o] -- the same per-tile partial layouts as the MFMA kernel (tile-major).
+// dZ rows are wave-uniform (scalar loads); four rows of H are in flight per wave.
+constexpr int kOutBwdThreads = 256;
+
+// CPL columns per lane (4: a wave spans a 256-column row; 2: two waves share a row, so W and the dW
+// accumulators take 2 NR registers each instead of 4 NR -- NR >= 12 needed 178+ registers at CPL 4)
+template <int NR, int CPL>
+__global__ __launch_bounds__(kOutBwdThreads, NR >= 16 ? 3 : 4) void out_bwd_valu_kernel(GemmParams p, const uint4* __restrict__ bimg) {
+    constexpr int WPR = kBN / (kWave * CPL);          // waves per row
+    constexpr int RG = (kOutBwdThreads / kWave) / WPR;  // row groups per workgroup
+    constexpr int RPW = kBM / RG;                      // rows per wave
+    using vec = typename std::conditional<CPL == 4, f32x4, f32x2>::type;
+    __shared__ float red[RG][NR + 1][kBN];  // per-row-group dW rows, then column sums (row NR)
+    __shared__ float dzsum[RG][NR];
+    __shared__ float4 dzt4[kBM][NR / 4];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int rg = wave / WPR;
+    const int c0 = CPL * (lane + kWave * (wave % WPR));
+    const bool col_ok = c0 < p.N;  // N % 4 == 0
+    // W[o][c0 + e] from the image of W^T: chunk 0, row n = c0 + e, k = o; 16-byte half ph holds k = 8 lh + j
+    float w[NR][CPL];
+#pragma unroll
+    for (int e = 0; e < CPL; ++e) {
+        const int n = c0 + e;
+#pragma unroll
+        for (int lh = 0; lh < (NR + 7) / 8; ++lh) {
+            const int ph = lh ^ ((n >> 3) & 1);
+            uint4 q[3];
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl)
+                q[pl] = col_ok ? bimg[(pl * kX6PlaneB + n * kX6RowB + 16 * ph) / 16] : make_uint4(0, 0, 0, 0);
+            const uint32_t* u0 = reinterpret_cast<const uint32_t*>(&q[0]);
+            const uint32_t* u1 = reinterpret_cast<const uint32_t*>(&q[1]);
+            const uint32_t* u2 = reinterpret_cast<const uint32_t*>(&q[2]);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int o = 8 * lh + j;
+                if (o >= NR) break;
+                auto f = [j](const uint32_t* u) {
+                    const uint32_t x = u[j >> 1];
+                    return __uint_as_float((j & 1) ? (x & 0xffff0000u) : (x << 16));
+                };
+                w[o][e] = (f(u0) + f(u1)) + f(u2);  // exact: the planes were split from this fp32 value
+            }
+        }
+    }
+    float wacc[NR][CPL], cs[CPL], dzs[NR];
+#pragma unroll
+    for (int e = 0; e < CPL; ++e) cs[e] = 0.f;
+#pragma unroll
+    for (int o = 0; o < NR; ++o) {
+        dzs[o] = 0.f;
+#pragma unroll
+        for (int e = 0; e < CPL; ++e) wacc[o][e] = 0.f;
+    }
+    float amx = 0.f;
+    // the tile's dZ rows (128 x NR floats) staged once in LDS: a per-row uniform global load is a vector load
+    // the waves would wait on (the compiler cannot prove dZ read-only for the scalar cache)
+    {
+        const int64_t t0 = static_cast<int64_t>(blockIdx.x) * kBM;
+        for (int i = threadIdx.x; i < kBM * NR / 4; i += kOutBwdThreads) {
+            const int r = i / (NR / 4), q = i % (NR / 4);
+            dzt4[r][q] = t0 + r < p.M ? *reinterpret_cast<const float4*>(p.a + (t0 + r) * p.K + 4 * q)
+                                      : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        __syncthreads();
+    }
+    const int64_t row0 = static_cast<int64_t>(blockIdx.x) * kBM + rg * RPW;
+    const int64_t rows = p.M - row0 < RPW ? (p.M - row0 > 0 ? p.M - row0 : 0) : RPW;
+    constexpr int U = 4;  // rows of H in flight per wave
+    for (int r0 = 0; r0 < rows; r0 += U) {
+        vec hv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t row = row0 + (r0 + u < rows ? r0 + u : rows - 1);
+            hv[u] = col_ok ? *reinterpret_cast<const vec*>(p.h + row * p.N + c0) : vec{};
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (r0 + u >= rows) break;  // wave-uniform
+            const int64_t row = row0 + r0 + u;
+            float d[NR];
+#pragma unroll
+            for (int o4 = 0; o4 < NR / 4; ++o4) {  // LDS broadcast (every lane reads the same 16 bytes)
+                const float4 t = dzt4[rg * RPW + r0 + u][o4];
+                d[4 * o4] = t.x;
+                d[4 * o4 + 1] = t.y;
+                d[4 * o4 + 2] = t.z;
+                d[4 * o4 + 3] = t.w;
+            }
+            vec out;
+#pragma unroll
+            for (int e = 0; e < CPL; ++e) {
+                const float hh = hv[u][e];
+                float z = 0.f;
+#pragma unroll
+                for (int o = 0; o < NR; ++o) z = fmaf(d[o], w[o][e], z);
+                const float v = hh > 0.f ? z : z * (hh + 1.f);  // ELU'(x) = 1 if h > 0 else h + 1
+                out[e] = v;
+                cs[e] += v;
+                amx = fmaxf(amx, fabsf(v));
+#pragma unroll
+                for (int o = 0; o < NR; ++o) wacc[o][e] = fmaf(d[o], hh, wacc[o][e]);
+            }
+            if (wave % WPR == 0)
+#pragma unroll
+                for (int o = 0; o < NR; ++o) dzs[o] += d[o];
+            if (col_ok) __builtin_nontemporal_store(out, reinterpret_cast<vec*>(p.c + row * p.N + c0));
+        }
+    }
+    // per-tile partials, the row groups added in order
+#pragma unroll
+    for (int o = 0; o <= NR; ++o)
+#pragma unroll
+        for (int e = 0; e < CPL; ++e) red[rg][o][c0 + e] = o < NR ? wacc[o][e] : cs[e];
+    if (lane == 0 && wave % WPR == 0)
+#pragma unroll
+        for (int o = 0; o < NR; ++o) dzsum[rg][o] = dzs[o];
+    __syncthreads();
+    const int nred = p.K;
+    const int64_t tile_floats = static_cast<int64_t>(nred) * p.N + nred;
+    float* wp = p.wpart + static_cast<int64_t>(blockIdx.x) * tile_floats;
+    for (int idx = threadIdx.x; idx < (NR + 1) * kBN; idx += kOutBwdThreads) {
+        const int o = idx / kBN, c = idx % kBN;
+        if (c >= p.N) continue;
+        float v = red[0][o][c];
+#pragma unroll
+        for (int g = 1; g < RG; ++g) v += red[g][o][c];
+        if (o < nred) wp[static_cast<int64_t>(o) * p.N + c] = v;
+        else if (o == NR) p.colsum[static_cast<int64_t>(blockIdx.x) * p.N + c] = v;
+    }
+    if (threadIdx.x < nred) {
+        float v = dzsum[0][threadIdx.x];
+#pragma unroll
+        for (int g = 1; g < RG; ++g) v += dzsum[g][threadIdx.x];
+        wp[static_cast<int64_t>(nred) * p.N + threadIdx.x] = v;
+    }
+    amax_publish<kOutBwdThreads>(p.amax_out, p.amax_ws, amx);
+}
+
+int out_bwd_mode() {  // tuning knob: RSLRL_OUT_BWD=mfma selects the MFMA kernel (default: VALU)
+    static const int v = [] {
+        const char* e = std::getenv("RSLRL_OUT_BWD");
+        return (e && std::string(e) == "mfma") ? 1 : 0;
+    }();
+    return v;
+}
+
 // bimage == nullptr: exact f32 MFMA main loop on p.bw; otherwise the split main loop on the image (PL = 3: x6
 // bf16 planes, layout-0 image; PL = 2: h3 fp16 planes, layout-2 image, A scaled from *p.a_amax).
 template <int EPI, int PL = 3>
@@ -1357,6 +1512,18 @@ int launch(const GemmParams& p, const void* bimage, hipStream_t st) {
         if constexpr (EPI == kEpiEluGradWgrad) {  // K = Nred in {4, 8, 12, 16}
             if constexpr (PL != 3) {
                 return RSLRL_E_UNSUPPORTED;
+            } else if (out_bwd_mode() == 0) {
+                auto go = [&](auto nr) {
+                    constexpr int NR = decltype(nr)::value;
+                    constexpr int CPL = NR <= 4 ? 4 : 2;
+                    hipLaunchKernelGGL((out_bwd_valu_kernel<NR, CPL>), g, dim3(kOutBwdThreads), 0, st, p, img);
+                };
+                switch (p.K) {
+                    case 4: go(std::integral_constant<int, 4>{}); break;
+                    case 8: go(std::integral_constant<int, 8>{}); break;
+                    case 12: go(std::integral_constant<int, 12>{}); break;
+                    default: go(std::integral_constant<int, 16>{}); break;
+                }
             } else {
                 auto go = [&](auto nr) {
                     constexpr int NR = decltype(nr)::value;
