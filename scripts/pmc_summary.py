@@ -47,6 +47,9 @@ def gemm_name(kernel):
     m = re.search(r"mlp_gemm_x6_pair_kernel<(\d+), \w+, (\d+)>", kernel)
     if m:  # two problems per launch (grid y = 2): bytes per launch cover both
         return f"{'h3' if m.group(2) == '2' else 'x6'}_{EPI_NAMES.get(int(m.group(1)), m.group(1))}_pair"
+    m = re.search(r"out_bwd_valu_kernel<(\d+), (\d+)>", kernel)
+    if m:  # output-layer backward on the VALU, keyed by its reduction width
+        return f"out_bwd_valu_nr{m.group(1)}"
     m = re.search(r"wgrad_x6_kernel<(\d+), \w+, (\d+)>", kernel)
     if m:
         return f"{'h3' if m.group(2) == '2' else 'x6'}_wgrad{m.group(1)}"
