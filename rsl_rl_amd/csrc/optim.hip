@@ -139,8 +139,7 @@ extern "C" int rslrl_clip_adam_step(const rslrl_adam_args_t* args, void* workspa
         a.offsets[i] = off;
         off += t.numel;
     }
-    a.offsets[a.n] = off;
-    if (off == 0) return RSLRL_OK;
+    a.offsets[a.n] = off;  // all-empty tensors still advance the step counters (torch increments them too)
     char* ws = static_cast<char*>(workspace);
     unsigned* ticket = reinterpret_cast<unsigned*>(ws);
     double* part = reinterpret_cast<double*>(ws + 256);

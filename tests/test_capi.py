@@ -72,6 +72,29 @@ def test_linear_abi_rejects_bad_shapes():
     assert L.rslrl_linear_prepare_bimage(16, 16, 16, 0, 8, None) == -4  # misaligned image
 
 
+def test_pair_and_optimizer_abi_validation():
+    L = _lib.lib()
+    a0 = _lib.LinearArgs(_lib.LINEAR_FWD_ELU, _lib.ARITH_X6, 16, None, 128, 48, 256, 16, 16, None, 16)
+    a1 = _lib.LinearArgs(_lib.LINEAR_FWD_ELU, _lib.ARITH_X6, 16, None, 64, 48, 256, 16, 16, None, 16)
+    assert L.rslrl_linear_gemm_pair(ctypes.byref(a0), ctypes.byref(a1), None) == -1  # different M
+    a1.M, a1.op = 128, _lib.LINEAR_DGRAD_ELU
+    assert L.rslrl_linear_gemm_pair(ctypes.byref(a0), ctypes.byref(a1), None) == -3  # not a forward pair
+    a1.op = _lib.LINEAR_FWD_ELU
+    a0.M = a1.M = 0
+    assert L.rslrl_linear_gemm_pair(ctypes.byref(a0), ctypes.byref(a1), None) == 0  # empty batch: no launch
+    assert L.rslrl_linear_gemm_pair(None, ctypes.byref(a1), None) == -1
+    args = _lib.AdamArgs()
+    ws_bytes = L.rslrl_adam_workspace_bytes()
+    assert ws_bytes >= 256 + 128 * 8 + 4
+    args.n = 0
+    assert L.rslrl_clip_adam_step(ctypes.byref(args), 16, ws_bytes, None) == -1  # no tensors
+    args.n = _lib.ADAM_MAX_TENSORS + 1
+    assert L.rslrl_clip_adam_step(ctypes.byref(args), 16, ws_bytes, None) == -1  # too many tensors
+    args.n = 1
+    assert L.rslrl_clip_adam_step(ctypes.byref(args), 16, ws_bytes - 1, None) == -2  # workspace too small
+    assert L.rslrl_clip_adam_step(ctypes.byref(args), 16, ws_bytes, None) == -1  # null tensor pointers
+
+
 def test_randperm_rejects_bad_state():
     L = _lib.lib()
     out = np.empty(10, np.int32)
