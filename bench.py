@@ -3,15 +3,22 @@
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...
 
-Workload (config C3, BASELINE.json configs[2]): per GPU N=65536 synthetic envs, T=24 steps/env, obs 48,
-12 actions, actor/critic MLP 3x256 ELU, fp32, PPO defaults (E=5 epochs x M=4 mini-batches, adaptive
-KL lr).  One "step" = one full OnPolicyRunner iteration: T rollout steps + compute_returns + update.
-With N GPUs every rank owns its own 65536-env shard (weak scaling); gradients are averaged with one
-RCCL all-reduce per mini-batch.  `value` = T * N_envs * world / (max over ranks of the timed seconds).
+Workload.  N=1 (the metric's configuration, C3 = BASELINE.json configs[2]): 65536 synthetic envs, T=24 steps/env,
+obs 48, 12 actions, actor/critic MLP 3x256 ELU, PPO defaults (E=5 epochs x M=4 mini-batches, adaptive KL lr).
+N>1 (C4 = configs[3]): 131072 envs in total, partitioned over the ranks (16384 per GPU at N=8) -- the envs shard,
+every rank owns its slice, its storage and its permutation; gradients (+ the KL) are averaged by ONE RCCL
+all-reduce per mini-batch ("scaling": "strong": the total work is fixed as N grows).  --global-num-envs sets the
+total, --num-envs a fixed per-GPU count instead (weak scaling).  One "step" = one OnPolicyRunner iteration:
+T rollout steps + compute_returns + update.  `value` = T * total envs / (max over ranks of the timed seconds).
 
-Extra fields: `roofline` for the dominant hot-path kernel (algorithmic bytes / live HIP-event duration
-on its stream, against 8 TB/s), `hot_path` (per-kernel times per iteration), and `cpu_baseline` (the
-oracle's CPU PPO iteration on the box's host cores, rank 0, N=1 only, bounded sample).
+The MLP GEMMs run on the x6 split-bf16 kernels (fp32 operands as three bf16 planes, 24 significant bits, six
+products, fp32 accumulation: fp32-faithful); `extra_configs` adds C5 (RND), the exact-fp32 MFMA kernels, the
+reduced-precision h3 mode (labelled as such) and the C4 total on one GPU (the strong-scaling base point).
+
+Extra fields: `roofline` for the dominant hot-path kernel (algorithmic bytes / live HIP-event duration on its
+stream, against 8 TB/s), `hot_path` (per-kernel times per iteration), `roofline_mlp`, and `cpu_baseline` (the
+reference's iteration restated in torch-CPU ops, oracle/torch_cpu_ppo.py, on the box's host cores, rank 0, N=1
+only, bounded samples).
 """
 
 from __future__ import annotations
@@ -36,6 +43,10 @@ X6_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 6  # fp32-equivalent peak of the 6-prod
 H3_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 3  # ... of the 3-product split-fp16 GEMMs (fp16 MFMA = bf16 rate)
 FP32_MFMA_PEAK_TFLOPS = 157.3
 HOT_PATH = ("gae_scan", "adv_normalize", "gather_rows", "ppo_loss", "rollout_record")
+C3_ENVS = 65536  # BASELINE.json configs[2] (N=1 headline)
+with open(os.path.join(ROOT, "BASELINE.json")) as _f:
+    BASELINE_METRIC = json.load(_f)["metric"]
+C4_ENVS = 131072  # BASELINE.json configs[3]: the total partitioned over the ranks
 # per-launch HBM traffic of the hot-path kernels from rocprofv3 FETCH_SIZE / WRITE_SIZE passes over this same
 # bench command (scripts/pmc_summary.py; raw counters next to it).  PMC passes serialise and slow the
 # run, so they are collected separately and the committed summary is reported here.
@@ -73,13 +84,14 @@ def train_cfg(args, rnd=False):
     return cfg
 
 
-def time_runner(args, device, rank, *, rnd=False, steps=3, warmup=1):
+def time_runner(args, device, rank, *, rnd=False, steps=5, warmup=2, num_envs=None):
     """Iterations/s of a fresh runner (for the secondary configurations; world size 1 only)."""
     from rsl_rl_amd.env import SyntheticVecEnv
     from rsl_rl_amd.runners import OnPolicyRunner
 
+    n = num_envs or args.num_envs_local
     torch.manual_seed(1)
-    env = SyntheticVecEnv(args.num_envs, args.num_obs, args.num_actions, device=device, seed=rank)
+    env = SyntheticVecEnv(n, args.num_obs, args.num_actions, device=device, seed=rank)
     with contextlib.redirect_stdout(sys.stderr):
         runner = OnPolicyRunner(env, train_cfg(args, rnd=rnd), log_dir=None, device=device)
         runner.learn(warmup)
@@ -91,52 +103,91 @@ def time_runner(args, device, rank, *, rnd=False, steps=3, warmup=1):
     stats = {k: round(v, 4) for k, v in runner.last_iteration_stats.items() if k != "loss_dict"}
     del runner, env
     torch.cuda.empty_cache()
-    T, N = args.num_steps_per_env, args.num_envs
-    return {"value": round(T * N * steps / el, 1), "unit": "env-steps/s", "steps": steps, "warmup": warmup,
-            "ms_per_step": round(el / steps * 1e3, 3), "phases_last_iter": stats}
+    T = args.num_steps_per_env
+    return {"value": round(T * n * steps / el, 1), "unit": "env-steps/s", "steps": steps, "warmup": warmup,
+            "num_envs": n, "ms_per_step": round(el / steps * 1e3, 3), "phases_last_iter": stats}
+
+
+def _cpu_share():
+    """CPUs this process may use: the affinity mask, capped by a cgroup v2 CPU quota when one is set."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()
+        if quota != "max":
+            n = max(1, min(n, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return n
 
 
 def cpu_baseline(args):
-    from oracle import cpu_ppo
+    """The reference's PPO iteration in torch-CPU ops (oracle/torch_cpu_ppo.py) on every CPU this process may use:
+    a C2-shaped sample (N 4096) and a C3-shaped sample (N 16384, T/obs/act/MLP of C3); value = the latter."""
+    from oracle import torch_cpu_ppo
 
-    threads = min(16, len(os.sched_getaffinity(0)))
-    n = args.cpu_sample_envs
-    rate, secs, parts = cpu_ppo.time_iterations(n, args.num_obs, args.num_actions, T=args.num_steps_per_env,
-                                                iters=1, warmup=1, threads=threads, detail=True)
+    share = _cpu_share()
+    # torch's CPU GEMMs do not always run fastest on every CPU of a throttled share: take the faster of the share
+    # and half of it on a short C2-sized probe (the thread count used is what `cores` reports)
+    probe = {}
+    for th in sorted({share, max(1, share // 2)}, reverse=True):
+        probe[th] = torch_cpu_ppo.time_iterations(4096, args.num_obs, args.num_actions, T=args.num_steps_per_env,
+                                                  iters=1, warmup=1, threads=th)[0]
+    threads = max(probe, key=probe.get)
+    out = {}
+    for name, n in (("C2", 4096), ("C3_sample", args.cpu_sample_envs)):
+        rate, secs, parts = torch_cpu_ppo.time_iterations(n, args.num_obs, args.num_actions,
+                                                          T=args.num_steps_per_env, iters=1, warmup=1,
+                                                          threads=threads)
+        out[name] = {"env_steps_per_s": round(rate, 1), "num_envs": n, "timed_seconds": round(secs, 2),
+                     "update_env_steps_per_s": round(parts["update_env_steps_per_s"], 1),
+                     "hot_path_env_steps_per_s": round(parts["hot_path_env_steps_per_s"], 1),
+                     "phase_seconds": parts["seconds"]}
     model = ""
     try:
         with open("/proc/cpuinfo") as f:
             model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), "")
     except OSError:
         pass
+    big = out["C3_sample"]
     return {
-        "value": round(rate, 1),
+        "value": big["env_steps_per_s"],
         "unit": "env-steps/s",
         "cores": threads,
         "kind": "port",
-        # hot path (GAE + shuffle/gathers + loss) and update phase timed apart as well
-        "hot_path_env_steps_per_s": round(parts["hot_path"], 1),
-        "update_env_steps_per_s": round(parts["update"], 1),
-        "sample": f"1 timed PPO iteration (+1 warmup) of the CPU oracle (oracle/cpu_ppo.py: torch-CPU MLPs + "
-                  f"oracle GAE/randperm/gather/loss) at N={n} envs, T={args.num_steps_per_env}, obs {args.num_obs}, "
-                  f"act {args.num_actions}, 3x256 MLP; {secs:.1f} s timed; {threads} threads; CPU: {model}",
+        "update_env_steps_per_s": big["update_env_steps_per_s"],
+        "hot_path_env_steps_per_s": big["hot_path_env_steps_per_s"],
+        "samples": out,
+        "thread_probe_c2_env_steps_per_s": {str(k): round(v, 1) for k, v in probe.items()},
+        "cpu_share": share,
+        "sample": f"1 timed PPO iteration (+1 warmup) of the reference's algorithm in torch-CPU ops "
+                  f"(oracle/torch_cpu_ppo.py: rollout, compute_returns loop, randperm + per-mini-batch gathers, "
+                  f"Normal log-prob/entropy/KL, clipped losses, autograd, clip_grad_norm_, Adam) at "
+                  f"N={args.cpu_sample_envs} envs with C3's T={args.num_steps_per_env}, obs {args.num_obs}, "
+                  f"act {args.num_actions}, 3x256 MLP (value), and at C2 (N 4096); {threads} threads (the faster of "
+                  f"the {share}-CPU affinity/cgroup share and half of it on a C2 probe); CPU: {model}",
     }
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--num-envs", type=int, default=65536, help="environments per GPU")
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--num-envs", type=int, default=None,
+                    help="environments per GPU (weak scaling); default: --global-num-envs split over the ranks")
+    ap.add_argument("--global-num-envs", type=int, default=None,
+                    help=f"environments in total, partitioned over the ranks (strong scaling); default {C3_ENVS} "
+                         f"on one GPU (C3), {C4_ENVS} over N > 1 GPUs (C4)")
     ap.add_argument("--num-steps-per-env", type=int, default=24)
     ap.add_argument("--num-obs", type=int, default=48)
     ap.add_argument("--num-actions", type=int, default=12)
     ap.add_argument("--hidden", type=int, default=256)
     ap.add_argument("--layers", type=int, default=3)
-    ap.add_argument("--cpu-sample-envs", type=int, default=8192)
+    ap.add_argument("--cpu-sample-envs", type=int, default=16384)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-extra", action="store_true", help="skip the secondary configurations (C5, f32 GEMMs)")
+    ap.add_argument("--no-extra", action="store_true",
+                    help="skip the secondary configurations (C5, f32 / h3 GEMMs, C4 total on one GPU)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -146,13 +197,23 @@ def main():
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 through torch.distributed.run")
     torch.cuda.set_device(local_rank)
     device = f"cuda:{local_rank}"
+    if args.num_envs is not None:
+        if args.global_num_envs is not None:
+            raise SystemExit("--num-envs (per GPU) and --global-num-envs (total) are exclusive")
+        args.num_envs_local, scaling = args.num_envs, "weak"
+        total = args.num_envs * world
+    else:
+        total = args.global_num_envs or (C3_ENVS if world == 1 else C4_ENVS)
+        if total % world:
+            raise SystemExit(f"--global-num-envs {total} does not split evenly over {world} ranks")
+        args.num_envs_local, scaling = total // world, "strong"
 
     from rsl_rl_amd import kernels
     from rsl_rl_amd.env import SyntheticVecEnv
     from rsl_rl_amd.runners import OnPolicyRunner
 
     torch.manual_seed(1)  # policy init; the env stream is seeded per rank
-    env = SyntheticVecEnv(args.num_envs, args.num_obs, args.num_actions, device=device, seed=rank)
+    env = SyntheticVecEnv(args.num_envs_local, args.num_obs, args.num_actions, device=device, seed=rank)
     with contextlib.redirect_stdout(sys.stderr):  # stdout carries only the result line
         runner = OnPolicyRunner(env, train_cfg(args), log_dir=None, device=device)  # inits RCCL when world > 1
 
@@ -184,7 +245,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
 
-    T, N, K = args.num_steps_per_env, args.num_envs, args.steps
+    T, N, K = args.num_steps_per_env, args.num_envs_local, args.steps
     value = T * N * world * K / elapsed
     prof = kernels.timer.summary()
     hot = {}
@@ -216,10 +277,12 @@ def main():
     roofline_mlp = None
     from rsl_rl_amd.networks import fused_mlp
     mode = fused_mlp._mode
-    arith_label = {fused_mlp.GEMM_H3: "h3 split-fp16 MFMA on the hidden layers (x6 split-bf16 on the first and "
-                                      "output layers), fp32-class error (DESIGN.md s5)",
-                   fused_mlp.GEMM_X6: "x6 split-bf16 MFMA, fp32-class error (DESIGN.md s5)",
-                   fused_mlp.GEMM_F32: "fp32 MFMA"}[mode]
+    arith_label = {fused_mlp.GEMM_H3: "h3 (REDUCED precision, opt-in): hidden-layer GEMMs on 2 fp16 planes of "
+                                      "power-of-two scaled operands (22 significant bits, a1*b1 dropped); first "
+                                      "and output layers x6",
+                   fused_mlp.GEMM_X6: "x6: fp32 operands as 3 bf16 planes (24 significant bits), 6 bf16 MFMA "
+                                      "products, fp32 accumulation (fp32-faithful; DESIGN.md s5)",
+                   fused_mlp.GEMM_F32: "fp32 MFMA (exact fp32 fma chain)"}[mode]
     if mlp:
         dm = max(mlp, key=lambda k: mlp[k]["ms_per_step"])
         ach = mlp[dm]["achieved_TFLOPs"]
@@ -240,7 +303,7 @@ def main():
                                 "algorithmic_bytes_per_launch": mlp[dm]["algorithmic_bytes_per_launch"]}}
 
     out = {
-        "metric": "PPO env-steps/sec (rollout+GAE+update) at N=65536 envs, 1->8 MI355X",
+        "metric": BASELINE_METRIC,
         "value": round(value, 1),
         "unit": "env-steps/s",
         "n_gpus": world,
@@ -248,20 +311,21 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / K * 1e3, 3),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": "fp32",
         "gemm_arithmetic": arith_label,
         "data": "synthetic (SyntheticVecEnv: obs/reward ~ N(0,1), dones ~ Bernoulli(0.02); random-init weights)",
         "config": {
-            "workload": f"C3: {N} envs/GPU x T={T}, obs {args.num_obs}, act {args.num_actions}, "
-                        f"actor+critic MLP {args.layers}x{args.hidden} ELU, PPO E=5 M=4 adaptive-KL; "
-                        f"one step = rollout + GAE + update",
+            "workload": (f"{'C3' if world == 1 and total == C3_ENVS else 'C4' if total == C4_ENVS else 'custom'}: "
+                         f"{total} envs ({N} per GPU x {world}) x T={T}, obs {args.num_obs}, act {args.num_actions}, "
+                         f"actor+critic MLP {args.layers}x{args.hidden} ELU, PPO E=5 M=4 adaptive-KL; "
+                         f"one step = rollout + GAE + update"),
             "num_envs_per_gpu": N,
             "global_num_envs": N * world,
             "num_steps_per_env": T,
             "mini_batch_rows": N * T // 4,
-            "parallelism": f"dp{world} (env shards, RCCL grad all-reduce per mini-batch)",
+            "parallelism": f"dp{world} (env shards; one RCCL all-reduce of gradients + KL per mini-batch)",
         },
         "roofline": roofline,
         "roofline_mlp": roofline_mlp,
@@ -278,13 +342,17 @@ def main():
         torch.cuda.empty_cache()
         extra = {"C5_rnd": time_runner(args, device, rank, rnd=True)}
         extra["C5_rnd"]["workload"] = "C3 + RND (predictor/target 48->48->1 ELU, weight 1.0 x step_dt, fused record)"
+        extra["C4_total_1gpu"] = time_runner(args, device, rank, num_envs=C4_ENVS)
+        extra["C4_total_1gpu"]["workload"] = (f"C4's {C4_ENVS} envs on one GPU: the base point of the strong-"
+                                              f"scaling curve that --gpus N partitions")
         prev = fused_mlp.set_gemm_mode(fused_mlp.GEMM_F32)
         extra["C3_fp32_mfma"] = time_runner(args, device, rank)
         extra["C3_fp32_mfma"]["workload"] = "C3 with the exact-fp32 MFMA GEMM kernels (RSLRL_GEMM_MODE=f32)"
-        if prev != fused_mlp.GEMM_X6:
-            fused_mlp.set_gemm_mode(fused_mlp.GEMM_X6)
-            extra["C3_x6"] = time_runner(args, device, rank)
-            extra["C3_x6"]["workload"] = "C3 with every MLP GEMM on x6 split-bf16 (RSLRL_GEMM_MODE=x6)"
+        fused_mlp.set_gemm_mode(fused_mlp.GEMM_H3)
+        extra["C3_h3_reduced_precision"] = time_runner(args, device, rank)
+        extra["C3_h3_reduced_precision"]["workload"] = (
+            "C3 with the hidden-layer GEMMs in h3 (RSLRL_GEMM_MODE=h3): REDUCED precision, 2 fp16 planes = 22-bit "
+            "operands, a1*b1 dropped -- NOT fp32-faithful, reported for comparison only")
         fused_mlp.set_gemm_mode(prev)
         out["extra_configs"] = extra
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -155,14 +155,15 @@ int rslrl_ppo_update_tail(const float* stats, const float* kl, double* lr, float
 
 /* Gradient-norm clipping + Adam step over a parameter list (ppo.py:373-374: clip_grad_norm_ then
  * optimizer.step() of torch.optim.Adam(fused), no weight decay / amsgrad / maximize), two launches:
- * ||g||_2 over every tensor (fp64, fixed order), coef = min(1, max_grad_norm / (||g|| + 1e-6)) (no clipping
- * when max_grad_norm <= 0), every step += 1; then per element torch's fused-Adam arithmetic with g * coef.
+ * ||g||_2 over every tensor (fp64, fixed order), coef = min(1, max_grad_norm / (||g|| + 1e-6)) (NaN stays
+ * NaN like torch.clamp; no clipping when max_grad_norm <= 0), every step += 1; then per element grad = g * coef
+ * (written back, as clip_grad_norm_ leaves .grad) and torch's fused-Adam arithmetic on it.
  * lr_dev (fp32 device scalar) overrides lr when non-NULL.  offsets are filled by the call.  workspace:
  * rslrl_adam_workspace_bytes(), zero-filled once (an arrival counter every call leaves zero). */
 #define RSLRL_ADAM_MAX_TENSORS 24
 typedef struct {
     float* param;
-    const float* grad;
+    float* grad; /* read, then overwritten with the clipped gradient */
     float* exp_avg;
     float* exp_avg_sq;
     float* step; /* fp32 device scalar (torch's fused-Adam state["step"]) */

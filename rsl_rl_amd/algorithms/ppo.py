@@ -5,20 +5,23 @@ intrinsic_rewards, ...) and methods (init_storage, act, process_env_step, comput
 broadcast_parameters, reduce_parameters) keep the reference's signatures and semantics.  The update
 differs in how each mini-batch is evaluated:
 
-* the actor forward yields (mean, sigma) directly (ActorCritic.action_distribution_params) and the
-  critic yields V; one fused kernel (rsl_rl_amd.kernels.ppo_loss_fwd_bwd) computes the KL, the clipped
-  surrogate, the clipped value loss, the entropy and the exact gradients d(loss)/d(mean, sigma, V);
-  `torch.autograd.backward` then pushes those through the two MLPs (PyTorch-ROCm GEMMs);
-* per-parameter gradients are views of one flat buffer, so the multi-GPU average is a single RCCL
-  all-reduce of that buffer with no cat / copy-back (ppo.py:441-469);
-* the KL is the only value read back per mini-batch (it drives the learning-rate rule, which must run
-  before the optimizer step, as in the reference); the loss statistics stay on the device until the
-  end of update().
+* for the standard ActorCritic the update runs without autograd: the actor and critic forwards keep
+  their activations (networks/fused_mlp.train_forward), one fused kernel (kernels.ppo_loss_fwd_bwd)
+  computes the KL, the clipped surrogate, the clipped value loss, the entropy and the exact gradients
+  d(loss)/d(mean, sigma, V), and the MLP backward kernels write every parameter gradient straight into
+  its slot of one contiguous gradient arena (GradArena) -- each parameter's .grad is a view of it;
+* under multi-GPU the arena holds, after the gradients, the mini-batch KL: ONE RCCL all-reduce of that
+  buffer (SUM, then / world size) averages the gradients and the KL together (ppo.py:271-273 and
+  ppo.py:441-469 fused into one collective per mini-batch);
+* the adaptive learning rate, the loss statistics, gradient clipping and the Adam step stay on the device
+  (kernels.ppo_update_tail, kernels.FusedClipAdam): no host synchronisation per mini-batch.
+Any other policy keeps the autograd path (the reference's structure, with the KL appended to the
+gradient concatenation of reduce_parameters).
 
 Multi-GPU LR rule: the reference all-reduces kl_mean, lets rank 0 decide, broadcasts the lr as an fp32
 tensor and reads it back (ppo.py:272-290).  After the all-reduce every rank holds the same kl_mean, so
 each rank applies the same rule locally and rounds the lr through fp32 exactly like the broadcast did:
-same learning rates on every rank, one collective fewer per mini-batch.
+same learning rates on every rank, no broadcast.
 """
 
 from __future__ import annotations
@@ -55,6 +58,42 @@ def adapt_learning_rate_device(lr: torch.Tensor, kl_mean: torch.Tensor, desired_
     down = torch.clamp(lr / 1.5, min=1e-5)
     up = torch.clamp(lr * 1.5, max=1e-2)
     return torch.where(kl > desired_kl * 2.0, down, torch.where((kl < desired_kl / 2.0) & (kl > 0.0), up, lr))
+
+
+class GradArena:
+    """One contiguous fp32 buffer behind every trainable parameter's gradient, in the concatenation order of the
+    reference's reduce_parameters (policy.parameters(), then the RND predictor's; ppo.py:447-450), followed by
+    `extra` scalar slots (the mini-batch KL) that travel in the same all-reduce."""
+
+    def __init__(self, params, extra: int, device):
+        self.params = list(params)
+        self.numel = sum(p.numel() for p in self.params)
+        self.flat = torch.zeros(self.numel + extra, dtype=torch.float32, device=device)
+        self.views, off = [], 0
+        for p in self.params:
+            self.views.append(self.flat[off:off + p.numel()].view_as(p))
+            off += p.numel()
+        self._slot = {id(p): v for p, v in zip(self.params, self.views)}
+        self.extra = self.flat[self.numel:]
+
+    def matches(self, params) -> bool:
+        return len(params) == len(self.params) and all(a is b for a, b in zip(params, self.params))
+
+    def slot(self, p) -> torch.Tensor:
+        return self._slot[id(p)]
+
+    def bind(self):
+        """Make each parameter's .grad its arena view (the optimizers read and write gradients there)."""
+        for p, v in zip(self.params, self.views):
+            if p.grad is None or p.grad.data_ptr() != v.data_ptr():
+                p.grad = v
+
+    def span(self, params) -> torch.Tensor:
+        """The contiguous arena range of consecutive parameters (e.g. the RND predictor's)."""
+        first, last = self.slot(params[0]), self.slot(params[-1])
+        start = first.data_ptr() - self.flat.data_ptr()
+        stop = last.data_ptr() - self.flat.data_ptr() + 4 * last.numel()
+        return self.flat[start // 4: stop // 4]
 
 
 class PPO:
@@ -141,8 +180,8 @@ class PPO:
         self.learning_rate = learning_rate
         self.normalize_advantage_per_mini_batch = normalize_advantage_per_mini_batch
 
-        self._flat_grad = None  # one buffer backing every trainable parameter's .grad (see reduce_parameters)
-        self._flat_views = None
+        self._arena: GradArena | None = None  # gradient arena of the manual update path (see update())
+        self.learning_rate_device = None  # fp64 device scalar of the lr while update() runs
 
     def init_storage(self, training_type, num_envs, num_transitions_per_env, obs, actions_shape):
         self.storage = RolloutStorage(training_type, num_envs, num_transitions_per_env, obs, actions_shape,
@@ -248,32 +287,17 @@ class PPO:
             params += list(self.rnd.predictor.parameters())
         return [p for p in params if p.requires_grad]
 
-    def _bind_flat_grads(self):
-        """Make every trainable parameter's .grad a view of one contiguous fp32 buffer, zeroed.
-
-        Order = policy.parameters() then rnd.parameters(), the concatenation order of ppo.py:447-450."""
+    def grad_arena(self) -> GradArena:
+        """The gradient arena over the trainable parameters (+ one KL slot), created on first use and whenever
+        the parameter list changes."""
         params = self._trainable_params()
-        total = sum(p.numel() for p in params)
-        flat = self._flat_grad
-        if flat is None or flat.numel() != total or flat.device != params[0].device:
-            flat = torch.zeros(total, dtype=torch.float32, device=params[0].device)
-            self._flat_grad = flat
-            self._flat_views = None
-        else:
-            flat.zero_()
-        if self._flat_views is None:
-            views, off = [], 0
-            for p in params:
-                views.append(flat[off:off + p.numel()].view_as(p))
-                off += p.numel()
-            self._flat_views = views
-        for p, v in zip(params, self._flat_views):
-            if p.grad is None or p.grad.data_ptr() != v.data_ptr():
-                p.grad = v
+        if self._arena is None or not self._arena.matches(params) or self._arena.flat.device != params[0].device:
+            self._arena = GradArena(params, extra=1, device=params[0].device)
+        return self._arena
 
     def _sync_kl_and_lr(self, kl_mean: torch.Tensor):
         """KL all-reduce + adaptive lr + fp32 lr rounding under multi-GPU (ppo.py:271-294), host version
-        (one device read-back); update() uses the device-resident _device_kl_and_lr."""
+        (one device read-back); the update keeps the lr on the device instead (kernels.ppo_update_tail)."""
         if self.is_multi_gpu:
             torch.distributed.all_reduce(kl_mean, op=torch.distributed.ReduceOp.SUM)
             kl_mean /= self.gpu_world_size
@@ -285,20 +309,6 @@ class PPO:
             param_group["lr"] = self.learning_rate
         return kl
 
-    def _device_kl_and_lr(self, kl_mean: torch.Tensor, lr: torch.Tensor) -> torch.Tensor:
-        """Same rule as _sync_kl_and_lr with the lr kept on the device: no host synchronisation per
-        mini-batch.  Returns the new fp64 lr; the optimizer reads it as a device tensor (fused Adam)."""
-        if self.is_multi_gpu:
-            torch.distributed.all_reduce(kl_mean, op=torch.distributed.ReduceOp.SUM)
-            kl_mean /= self.gpu_world_size
-        lr = adapt_learning_rate_device(lr, kl_mean, self.desired_kl)
-        if self.is_multi_gpu:  # the reference broadcasts the lr as an fp32 tensor (ppo.py:288-290)
-            lr = lr.float().double()
-        lr32 = lr.float()
-        for param_group in self.optimizer.param_groups:
-            param_group["lr"] = lr32
-        return lr
-
     def update(self):  # noqa: C901
         if self.symmetry:
             raise NotImplementedError(
@@ -307,20 +317,24 @@ class PPO:
             )
         if self.policy.is_recurrent:
             raise NotImplementedError("recurrent policies are outside the MI355X PPO hot-path scope (SURVEY.md §2)")
-        fused_policy = hasattr(self.policy, "action_distribution_params")
         adaptive = self.desired_kl is not None and self.schedule == "adaptive"
         dev = self.storage.values.device
+        if self._clip_adam is not None:
+            self._clip_adam.adopt_loaded_state()  # a checkpoint of a non-fused Adam may have been loaded
         sums = torch.zeros(4, dtype=torch.float64, device=dev)  # value, surrogate, entropy, rnd
         stats_buf = torch.empty(8, dtype=torch.float32, device=dev)
         # device-resident lr (needs an optimizer that takes a tensor lr: fused / capturable Adam)
         device_lr = adaptive and dev.type == "cuda" and self._optimizer_takes_tensor_lr()
         lr_dev = torch.tensor(self.learning_rate, dtype=torch.float64, device=dev) if device_lr else None
+        self.learning_rate_device = lr_dev  # the reference's self.learning_rate during update() (fp64, device)
         lr32 = None
         if device_lr:  # the optimizer reads the lr as this fp32 device tensor (written by ppo_update_tail)
             lr32 = torch.tensor(self.learning_rate, dtype=torch.float32, device=dev)
             for param_group in self.optimizer.param_groups:
                 param_group["lr"] = lr32
-        trainable = self._trainable_params()
+        manual = None  # decided at the first mini-batch (needs the observation batch)
+        arena = None
+        rnd_params = list(self.rnd.predictor.parameters()) if self.rnd else []
 
         generator = self.storage.mini_batch_generator(self.num_mini_batches, self.num_learning_epochs)
         for (
@@ -335,37 +349,51 @@ class PPO:
             hid_states_batch,
             masks_batch,
         ) in generator:
-            # actor / critic forward (PyTorch-ROCm MLPs)
-            if fused_policy:
-                mean, sigma = self.policy.action_distribution_params(obs_batch)
+            if manual is None:
+                manual = (isinstance(self.policy, ActorCritic) and self.policy.manual_update_ok(obs_batch)
+                          and all(p.requires_grad for p in self.policy.parameters()))
+                if manual:
+                    arena = self.grad_arena()
+                    arena.bind()
+            loss_kw = dict(clip_param=self.clip_param, value_loss_coef=self.value_loss_coef,
+                           entropy_coef=self.entropy_coef, use_clipped_value_loss=self.use_clipped_value_loss,
+                           compute_kl=adaptive, normalize_advantage=self.normalize_advantage_per_mini_batch,
+                           stats=stats_buf)
+            if manual:
+                # forward, fused loss and backward without autograd; gradients land in the arena
+                # (ppo.py:246-253 forward, :221-223 + :259-315 loss, :367-368 backward)
+                with torch.no_grad():
+                    mean, sigma, value_batch, tape = self.policy.train_forward(obs_batch)
+                    g_mean, g_sigma = self.policy.train_grad_buffers(mean, sigma)
+                    if g_sigma is None:  # shared std: d sigma reduced by the loss kernel, into the std's slot
+                        g_sigma = (arena.slot(self.policy.std) if self.policy.noise_std_type == "scalar"
+                                   else torch.empty_like(sigma))
+                    stats, g_mean, g_sigma, g_value = kernels.ppo_loss_fwd_bwd(
+                        mean, sigma, value_batch, actions_batch, old_actions_log_prob_batch, advantages_batch,
+                        target_values_batch, returns_batch, old_mu_batch, old_sigma_batch, grad_mu=g_mean,
+                        grad_sigma=g_sigma, **loss_kw)
+                    self.policy.train_backward(tape, g_mean, g_sigma, g_value, sigma, arena.slot)
+                    del tape
             else:
-                self.policy.act(obs_batch, masks=masks_batch, hidden_states=hid_states_batch[0])
-                mean, sigma = self.policy.action_mean, self.policy.action_std
-            value_batch = self.policy.evaluate(obs_batch, masks=masks_batch, hidden_states=hid_states_batch[1])
+                # autograd path for any other policy (ppo.py:246-253, :367-372)
+                if hasattr(self.policy, "action_distribution_params"):
+                    mean, sigma = self.policy.action_distribution_params(obs_batch)
+                else:
+                    self.policy.act(obs_batch, masks=masks_batch, hidden_states=hid_states_batch[0])
+                    mean, sigma = self.policy.action_mean, self.policy.action_std
+                value_batch = self.policy.evaluate(obs_batch, masks=masks_batch, hidden_states=hid_states_batch[1])
+                stats, g_mean, g_sigma, g_value = kernels.ppo_loss_fwd_bwd(
+                    mean, sigma, value_batch, actions_batch, old_actions_log_prob_batch, advantages_batch,
+                    target_values_batch, returns_batch, old_mu_batch, old_sigma_batch, **loss_kw)
+                for p in self.policy.parameters():  # optimizer.zero_grad() (set_to_none)
+                    p.grad = None
+                outs, grads = [mean, value_batch], [g_mean, g_value]
+                if sigma.requires_grad:
+                    outs.append(sigma)
+                    grads.append(g_sigma)
+                torch.autograd.backward(outs, grads)
 
-            # fused loss forward + backward to (mean, sigma, V)  (ppo.py:221-223, :259-315)
-            stats, g_mean, g_sigma, g_value = kernels.ppo_loss_fwd_bwd(
-                mean, sigma, value_batch, actions_batch, old_actions_log_prob_batch, advantages_batch,
-                target_values_batch, returns_batch, old_mu_batch, old_sigma_batch,
-                clip_param=self.clip_param, value_loss_coef=self.value_loss_coef, entropy_coef=self.entropy_coef,
-                use_clipped_value_loss=self.use_clipped_value_loss, compute_kl=adaptive,
-                normalize_advantage=self.normalize_advantage_per_mini_batch, stats=stats_buf,
-            )
-            if adaptive and device_lr:
-                # adaptive lr + loss statistics in one launch on device scalars (ppo.py:259-294, :387-395)
-                kl_src = stats[kernels.STATS_KL:kernels.STATS_KL + 1]
-                if self.is_multi_gpu:
-                    kl_src = kl_src.clone()
-                    torch.distributed.all_reduce(kl_src, op=torch.distributed.ReduceOp.SUM)
-                    kl_src /= self.gpu_world_size
-                kernels.ppo_update_tail(stats, kl_src, lr_dev, lr32, self.desired_kl, sums,
-                                        round_fp32=self.is_multi_gpu)
-            else:
-                if adaptive:
-                    self._sync_kl_and_lr(stats[kernels.STATS_KL:kernels.STATS_KL + 1].clone())
-                kernels.ppo_update_tail(stats, None, None, None, 0.0, sums)
-
-            # RND loss (ppo.py:352-363)
+            # RND loss (ppo.py:352-363, :369-371): autograd into the predictor's gradients
             if self.rnd:
                 with torch.no_grad():
                     rnd_state_batch = self.rnd.get_rnd_state(obs_batch)
@@ -373,27 +401,44 @@ class PPO:
                 predicted_embedding = self.rnd.predictor(rnd_state_batch)
                 target_embedding = self.rnd.target(rnd_state_batch).detach()
                 rnd_loss = nn.functional.mse_loss(predicted_embedding, target_embedding)
-
-            # backward through the MLPs (ppo.py:367-372).  The gradients start as None (the reference's
-            # optimizer.zero_grad() default, set_to_none): autograd then adopts each freshly computed gradient
-            # as .grad instead of launching one accumulate-add per parameter
-            for p in trainable:
-                p.grad = None
-            outs, grads = [mean, value_batch], [g_mean, g_value]
-            if sigma.requires_grad:
-                outs.append(sigma)
-                grads.append(g_sigma)
-            torch.autograd.backward(outs, grads)
-            if self.rnd:
+                if manual:  # zeroed arena range + autograd's in-place accumulation = fresh gradients
+                    arena.span(rnd_params).zero_()
+                else:
+                    for p in rnd_params:
+                        p.grad = None
                 rnd_loss.backward()
 
+            # multi-GPU: gradients (+ the KL) averaged over ranks by one all-reduce (ppo.py:271-273, :376)
+            kl_src = stats[kernels.STATS_KL:kernels.STATS_KL + 1]
             if self.is_multi_gpu:
-                self.reduce_parameters()
+                if manual:
+                    if adaptive:
+                        arena.extra[:1].copy_(kl_src)
+                    self._all_reduce_arena(arena, with_kl=adaptive)
+                    kl_src = arena.extra[:1]
+                else:
+                    kl_src = kl_src.clone() if adaptive else None
+                    self.reduce_parameters(kl_mean=kl_src)
 
+            # adaptive lr + loss statistics (ppo.py:259-294, :387-395)
+            if adaptive and device_lr:
+                kernels.ppo_update_tail(stats, kl_src, lr_dev, lr32, self.desired_kl, sums,
+                                        round_fp32=self.is_multi_gpu)
+            else:
+                if adaptive:  # host rule; the KL is already averaged over ranks
+                    kl = kl_src.item()
+                    self.learning_rate = adapt_learning_rate(self.learning_rate, kl, self.desired_kl)
+                    if self.is_multi_gpu:
+                        self.learning_rate = torch.tensor(self.learning_rate, dtype=torch.float32).item()
+                    for param_group in self.optimizer.param_groups:
+                        param_group["lr"] = self.learning_rate
+                kernels.ppo_update_tail(stats, None, None, None, 0.0, sums)
+
+            # clip + Adam (ppo.py:373-374)
             if self._clip_adam is None:
                 nn.utils.clip_grad_norm_(self.policy.parameters(), self.max_grad_norm)
                 self.optimizer.step()
-            else:  # clip + Adam in two launches (ppo.py:373-374)
+            else:
                 self._clip_adam.max_grad_norm = float(self.max_grad_norm)
                 self._clip_adam.step()
             if self.rnd_optimizer:
@@ -407,6 +452,7 @@ class PPO:
         host = (sums / num_updates).tolist()
         if device_lr:  # back to a Python float, as the reference keeps it (logging, checkpoints)
             self.learning_rate = lr_dev.item()
+            self.learning_rate_device = None
             for param_group in self.optimizer.param_groups:
                 param_group["lr"] = self.learning_rate
         self.storage.clear()
@@ -430,25 +476,37 @@ class PPO:
         if self.rnd:
             self.rnd.predictor.load_state_dict(model_params[1])
 
-    def reduce_parameters(self):
+    def _all_reduce_arena(self, arena: GradArena, with_kl: bool):
+        """The one collective per mini-batch: SUM all-reduce of the arena's gradients (+ its KL slot), then
+        / world size (ppo.py:453-454 for the gradients, :273-274 for the KL)."""
+        buf = arena.flat[:arena.numel + (1 if with_kl else 0)]
+        torch.distributed.all_reduce(buf, op=torch.distributed.ReduceOp.SUM)
+        buf /= self.gpu_world_size
+
+    def reduce_parameters(self, kl_mean: torch.Tensor | None = None):
         """Average gradients across ranks: SUM all-reduce then / world_size (ppo.py:441-469).
 
-        When the gradients are views of the flat buffer (always, inside update()) this is one collective
-        on that buffer; otherwise the reference's cat / all-reduce / copy-back is used."""
+        Gradients that are views of the gradient arena (the manual update path) are reduced in place as one
+        buffer; otherwise the reference's concatenation / all-reduce / copy-back.  kl_mean: an optional fp32
+        1-element tensor appended to the concatenation (averaged in place) so that the KL needs no collective
+        of its own."""
+        arena = self._arena
         params = self._trainable_params()
-        flat = self._flat_grad
-        if flat is not None and self._flat_views is not None and all(
-            p.grad is not None and p.grad.data_ptr() == v.data_ptr() for p, v in zip(params, self._flat_views)
-        ):
-            torch.distributed.all_reduce(flat, op=torch.distributed.ReduceOp.SUM)
-            flat /= self.gpu_world_size
+        if arena is not None and arena.matches(params) and kl_mean is None and all(
+                p.grad is not None and p.grad.data_ptr() == v.data_ptr() for p, v in zip(params, arena.views)):
+            self._all_reduce_arena(arena, with_kl=False)
             return
         grads = [p.grad.view(-1) for p in self.policy.parameters() if p.grad is not None]
         if self.rnd:
             grads += [p.grad.view(-1) for p in self.rnd.parameters() if p.grad is not None]
+        if kl_mean is not None:
+            grads.append(kl_mean.reshape(1).to(grads[0].dtype))
         all_grads = torch.cat(grads)
         torch.distributed.all_reduce(all_grads, op=torch.distributed.ReduceOp.SUM)
         all_grads /= self.gpu_world_size
+        if kl_mean is not None:
+            kl_mean.copy_(all_grads[-1:].reshape(kl_mean.shape))
+            all_grads = all_grads[:-1]
         all_params = self.policy.parameters()
         if self.rnd:
             all_params = chain(all_params, self.rnd.parameters())

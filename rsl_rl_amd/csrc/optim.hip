@@ -7,7 +7,8 @@
 // step += 1 first; bias corrections 1 - beta^step in double, passed on as fp32; the moment updates evaluated
 // as one double fma from fp32 operands and rounded to fp32; step_size = fp32(lr / bc1); denom = fp32(double(sqrtf(v) /
 // bc2_sqrt) + eps) with the division in fp32; param -= step_size * m / denom in fp32.  Clipping: coef = max_norm / (||g||_2 + 1e-6),
-// clamped to <= 1, g = fp32(g * coef) as torch's foreach multiply; the norm is accumulated in fp64 in a fixed
+// clamped to <= 1 (a NaN norm stays NaN), g = fp32(g * coef) as torch's foreach multiply, written back to
+// .grad as clip_grad_norm_ leaves it; the norm is accumulated in fp64 in a fixed
 // order (torch's per-tensor fp32 norms differ from it in the last bit at most).
 #include "common.h"
 
@@ -80,7 +81,8 @@ __global__ __launch_bounds__(kThreadsA) void grad_sq_kernel(rslrl_adam_args_t a,
     if (a.max_grad_norm > 0.0f) {
         const float norm = static_cast<float>(sqrt(tot));
         const float cf = a.max_grad_norm / (norm + 1e-6f);
-        c = cf < 1.0f ? cf : 1.0f;
+        // torch.clamp(clip_coef, max=1.0) propagates a NaN norm (every gradient then becomes NaN, as in torch)
+        c = isnan(cf) ? cf : fminf(cf, 1.0f);
     }
     *coef = c;
     for (int i = 0; i < a.n; ++i) *a.t[i].step += 1.0f;  // torch: _foreach_add_(state_steps, 1) before the update
@@ -106,6 +108,7 @@ __global__ __launch_bounds__(kThreadsA) void adam_kernel(rslrl_adam_args_t a, co
         for (int64_t e = lo + threadIdx.x; e < hi; e += kThreadsA) {
             const int64_t i = e - o0;
             const float g = t.grad[i] * c;  // the clipped gradient (fp32 multiply, as torch's foreach mul)
+            t.grad[i] = g;  // clip_grad_norm_ scales .grad in place: after the step .grad holds the clipped values
             // torch's build contracts b*m + (1-b)*g into one double fma; the unfused sum rounds differently in
             // ~0.3% of elements once narrowed to fp32 (measured), so the fma is spelled out here
             const double gd = static_cast<double>(g);

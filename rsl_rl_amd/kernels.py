@@ -455,7 +455,29 @@ class FusedClipAdam:
             st["step"] = torch.zeros((), dtype=torch.float32, device=p.device)
             st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
             st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+            return st
+        # a state_dict saved by a plain (non-fused) Adam -- e.g. a reference checkpoint -- loads its step as a
+        # CPU tensor (torch keeps non-fused steps on the host); the kernels read and increment it on the device
+        step = st["step"]
+        if not (isinstance(step, torch.Tensor) and step.device == p.device and step.dtype == torch.float32
+                and step.dim() == 0):
+            st["step"] = torch.tensor(float(step), dtype=torch.float32, device=p.device)
+        for k in ("exp_avg", "exp_avg_sq"):
+            v = st[k]
+            if v.device != p.device or v.dtype != p.dtype or not v.is_contiguous():
+                st[k] = v.to(device=p.device, dtype=p.dtype).contiguous()
         return st
+
+    def adopt_loaded_state(self):
+        """After optimizer.load_state_dict of a checkpoint written by a non-fused Adam: the loaded param group
+        carries fused=None and CPU steps.  Re-mark the group fused (torch's fallback step then takes the tensor
+        lr of update()) and move every step to its parameter's device as fp32."""
+        for g in self.opt.param_groups:
+            g["fused"] = True
+            g["foreach"] = None
+            for p in g["params"]:
+                if self.opt.state.get(p):
+                    self._state(p)
 
     def step(self, closure=None):
         if closure is not None:

@@ -14,6 +14,7 @@ import torch.nn as nn
 from torch.distributions import Normal
 
 from ..networks import MLP, EmpiricalNormalization
+from ..networks import fused_mlp
 from ..networks.fused_mlp import fused_mlp_forward_pair
 
 
@@ -123,6 +124,73 @@ class ActorCritic(nn.Module):
         mean, std = self._mean_and_std(obs)
         self.distribution = Normal(mean.detach(), std.detach().expand_as(mean))
         return mean, std
+
+    # ---------------------------------------------------------------- PPO update without autograd
+    def manual_update_ok(self, obs) -> bool:
+        """The PPO update may drive this policy through train_forward / train_backward: an unmodified
+        ActorCritic whose actor and critic are fused Linear+ELU stacks and whose inputs live on a ROCm device."""
+        cls = type(self)
+        if (cls.action_distribution_params is not ActorCritic.action_distribution_params
+                or cls.evaluate is not ActorCritic.evaluate or cls.act is not ActorCritic.act):
+            return False
+        if not (getattr(self.actor, "_fused", False) and getattr(self.critic, "_fused", False)):
+            return False
+        groups = self.obs_groups["policy"] + self.obs_groups["critic"]
+        return all(obs[g].is_cuda and obs[g].dtype == torch.float32 for g in groups)
+
+    @staticmethod
+    def _linears(mlp):
+        lin = [m for m in mlp if isinstance(m, nn.Linear)]
+        return [m.weight for m in lin], [m.bias for m in lin]
+
+    def train_forward(self, obs):
+        """The update's forward (ppo.py:246-253) without an autograd graph: returns (mean [B, A], sigma, value
+        [B, 1], tape) with sigma the shared [A] std (scalar / exp(log_std)) or the per-row [B, A] std of a
+        state-dependent head (strided views of the actor output).  Call under torch.no_grad()."""
+        a_obs = self.actor_obs_normalizer(self.get_actor_obs(obs))
+        c_obs = self.critic_obs_normalizer(self.get_critic_obs(obs))
+        a_obs = a_obs if a_obs.is_contiguous() else a_obs.contiguous()
+        c_obs = c_obs if c_obs.is_contiguous() else c_obs.contiguous()
+        y, tape_a = fused_mlp.train_forward(a_obs, *self._linears(self.actor))
+        A = self.num_actions
+        if self.state_dependent_std:
+            mean, raw = y[:, :A], y[:, A:]  # = unbind(Unflatten([2, A])(y), dim=-2)
+            std = torch.exp(raw) if self.noise_std_type == "log" else raw
+        else:
+            mean = y
+            std = self.std if self.noise_std_type == "scalar" else torch.exp(self.log_std)
+        value, tape_c = fused_mlp.train_forward(c_obs, *self._linears(self.critic))
+        self.distribution = Normal(mean, std.expand_as(mean))  # for logging, as act() leaves it
+        return mean, std, value, (tape_a, tape_c, y.shape)
+
+    def train_grad_buffers(self, mean, std):
+        """(d mean, d sigma) destinations for the fused loss: for a state-dependent head both are the halves of
+        one [B, 2A] buffer, the actor output's gradient; otherwise d mean [B, A] and d sigma [A]."""
+        B, A = mean.shape
+        if self.state_dependent_std:
+            dy = torch.empty(B, 2 * A, device=mean.device, dtype=torch.float32)
+            return dy[:, :A], dy[:, A:]
+        return torch.empty(B, A, device=mean.device, dtype=torch.float32), None
+
+    def train_backward(self, tape, g_mean, g_sigma, g_value, std, slot):
+        """Backward of train_forward given the loss gradients w.r.t. (mean, sigma, value), written into the
+        gradient slots `slot(param)` (a gradient arena).  g_sigma: for the shared std the [A] gradient w.r.t.
+        sigma (for log_std it is chained through exp here); for a state-dependent head the half of the actor-output
+        gradient buffer (train_grad_buffers) the loss kernel wrote."""
+        tape_a, tape_c, y_shape = tape
+        if self.state_dependent_std:
+            dy = torch.as_strided(g_mean, y_shape, (y_shape[1], 1))  # the [B, 2A] buffer behind both halves
+            if self.noise_std_type == "log":  # d raw = d sigma * exp(raw) (ExpBackward: grad * result)
+                g_sigma.mul_(std)
+        else:
+            dy = g_mean
+            if self.noise_std_type == "log":
+                torch.mul(g_sigma, std, out=slot(self.log_std))
+            elif g_sigma.data_ptr() != slot(self.std).data_ptr():
+                slot(self.std).copy_(g_sigma)
+        for mlp, tp, d in ((self.actor, tape_a, dy), (self.critic, tape_c, g_value.reshape(-1, 1))):
+            ws, bs = self._linears(mlp)
+            fused_mlp.train_backward(tp, d, outs=[(slot(w), slot(b)) for w, b in zip(ws, bs)])
 
     def act(self, obs, **kwargs):
         obs = self.actor_obs_normalizer(self.get_actor_obs(obs))

@@ -1,8 +1,11 @@
 """Random Network Distillation intrinsic reward (rsl_rl/modules/rnd.py:14-209).
 
 Same module layout (predictor / target MLPs, optional state and reward normalisers, weight schedules)
-and state_dict keys as the reference; evaluated with PyTorch ops.  Fusing the predictor/target
-forward and the reward add into the rollout-side kernel is the first "next" row of SURVEY.md §8f.
+and state_dict keys as the reference.  During the rollout the predictor/target forward, the
+intrinsic reward and its add to the extrinsic reward run inside the fused record kernel
+(csrc/rollout.hip via PPO.process_env_step) whenever the networks have the one-hidden-layer ELU form
+and reward normalisation is off; the PyTorch forward here serves every other case and the update's
+predictor loss.
 """
 
 from __future__ import annotations
@@ -103,8 +106,9 @@ class RandomNetworkDistillation(nn.Module):
             return self.initial_weight
         if step > final_step:
             return final_value
-        frac = (step - initial_step) / (final_step - initial_step)
-        return self.initial_weight + (final_value - self.initial_weight) * frac
+        # left to right as the reference evaluates it: ((final - init) * (step - i0)) / (f - i0), then + init
+        span = final_value - self.initial_weight
+        return self.initial_weight + span * (step - initial_step) / (final_step - initial_step)
 
 
 def resolve_rnd_config(alg_cfg, obs, obs_groups, env):

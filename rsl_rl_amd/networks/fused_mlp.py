@@ -41,12 +41,23 @@ def _stream(t):
 _FUSE_OUT = os.environ.get("RSLRL_FUSE_OUT", "1") == "1"  # output-layer backward in one launch
 _FUSE_OUT_FWD = os.environ.get("RSLRL_FUSE_OUT_FWD", "1") == "1"  # output-layer forward in the last hidden GEMM
 GEMM_F32 = 0  # v_mfma_f32_32x32x2_f32: exact f32 fma chain
-GEMM_X6 = 1   # fp32 split into 3 bf16 planes, 6 bf16 MFMA products, fp32 accumulation
-GEMM_H3 = 2   # hidden-layer GEMMs on 2 fp16 planes of power-of-two scaled operands, 3 fp16 MFMA products
-#               (include/rslrl_amd.h rslrl_linear_gemm); the first layer (input without a producer max) and
+GEMM_X6 = 1   # fp32 split into 3 bf16 planes (24 significant bits), 6 bf16 MFMA products, fp32 accumulation --
+#               the default: operands carry fp32's full significand, like the reference's fp32 nn.Linear
+GEMM_H3 = 2   # opt-in REDUCED precision: hidden-layer GEMMs on 2 fp16 planes of power-of-two scaled operands
+#               (22 significant bits, the a1*b1 product dropped, values far below a tensor's max in fp16
+#               subnormals), 3 fp16 MFMA products (include/rslrl_amd.h rslrl_linear_gemm); the first layer and
 #               the output layer stay on x6
 _MODE_NAMES = {"f32": GEMM_F32, "x6": GEMM_X6, "h3": GEMM_H3}
-_mode = _MODE_NAMES.get(os.environ.get("RSLRL_GEMM_MODE", "h3"), GEMM_H3)
+
+
+def _mode_from_env() -> int:
+    name = os.environ.get("RSLRL_GEMM_MODE", "x6")
+    if name not in _MODE_NAMES:
+        raise ValueError(f"RSLRL_GEMM_MODE={name!r}: expected one of {sorted(_MODE_NAMES)}")
+    return _MODE_NAMES[name]
+
+
+_mode = _mode_from_env()
 
 
 def set_gemm_mode(mode: int) -> int:
@@ -260,9 +271,9 @@ def _fuse_out_fwd(ws) -> bool:
         and ws[-1].shape[1] % 4 == 0
 
 
-def linear_dgrad_elu(dz, w, h, img=None):
+def linear_dgrad_elu(dz, w, h, img=None, db_out=None):
     """(dz @ w) * ELU'(h) and its column sums; w is the layer weight [N, K] (dz [M, N], h [M, K]); img: B image
-    of w^T (x6 arithmetic) or None (exact f32 MFMA)."""
+    of w^T (x6 arithmetic) or None (exact f32 MFMA).  db_out: optional [K] destination of the column sums."""
     M, N = dz.shape
     K = w.shape[1]
     wt = w.t().contiguous() if img is None else w  # [K, N]: the f32 kernel's B operand rows are the output columns
@@ -274,13 +285,22 @@ def linear_dgrad_elu(dz, w, h, img=None):
         rc = L.rslrl_linear_dgrad_elu(dz.data_ptr(), M, N, wt.data_ptr(), K, h.data_ptr(), out.data_ptr(),
                                       part.data_ptr(), img.data_ptr() if img is not None else None, _stream(dz))
     _lib.check(rc, "rslrl_linear_dgrad_elu")
-    db = torch.empty(K, device=dz.device, dtype=torch.float32)
+    db = _out_or_empty(db_out, (K,), dz.device)
     rc = L.rslrl_column_sum_fold(part.data_ptr(), tiles, K, db.data_ptr(), _stream(dz))
     _lib.check(rc, "rslrl_column_sum_fold")
     return out, db
 
 
-def linear_dgrad_elu_ex(dz, h, img, arith, dz_amax=None, want_amax=False):
+def _out_or_empty(out, shape, device):
+    """A caller-provided destination (contiguous fp32 of `shape`, e.g. a gradient-arena slot) or a new tensor."""
+    if out is None:
+        return torch.empty(shape, device=device, dtype=torch.float32)
+    if tuple(out.shape) != tuple(shape) or not out.is_contiguous() or out.dtype != torch.float32:
+        raise ValueError(f"output slot: expected contiguous fp32 {tuple(shape)}, got {tuple(out.shape)}")
+    return out
+
+
+def linear_dgrad_elu_ex(dz, h, img, arith, dz_amax=None, want_amax=False, db_out=None):
     """((dz W) * ELU'(h), its column sums, max |out| or None) on the split path; img: the B image of W^T in the
     layout of arith (see linear_fwd_ex)."""
     M, N = dz.shape
@@ -293,15 +313,17 @@ def linear_dgrad_elu_ex(dz, h, img, arith, dz_amax=None, want_amax=False):
     with timer.span(f"linear_dgrad[M={M},Nred={N},K={K}]{_tag(arith)}", dz.device, 4 * M * (N + 2 * K),
                     2 * M * K * N):
         _gemm(_lib.LINEAR_DGRAD_ELU, arith, dz, dz_amax, K, img, h=h, c=out, colsum=part, amax_out=amax)
-    db = torch.empty(K, device=dz.device, dtype=torch.float32)
+    db = _out_or_empty(db_out, (K,), dz.device)
     rc = L.rslrl_column_sum_fold(part.data_ptr(), tiles, K, db.data_ptr(), _stream(dz))
     _lib.check(rc, "rslrl_column_sum_fold")
     return out, db, amax
 
 
-def linear_dgrad_elu_wgrad(dz, w, h, img, want_amax=False):
+def linear_dgrad_elu_wgrad(dz, w, h, img, want_amax=False, db_prev_out=None, dwb_out=None):
     """Output-layer backward in one launch (x6; dz [M, Nred <= 16, % 4]): ((dz @ w) * ELU'(h), its column sums,
-    dz^T h).  w is the layer weight [Nred, K] (only its image is read)."""
+    dz^T h).  w is the layer weight [Nred, K] (only its image is read).  db_prev_out: optional [K] destination of
+    the column sums; dwb_out: optional [Nred*K + Nred] destination of dW (row-major) followed by db -- the layout
+    of a Linear's weight and bias adjacent in a gradient arena."""
     M, N = dz.shape
     K = h.shape[1]
     L = _lib.lib()
@@ -313,10 +335,10 @@ def linear_dgrad_elu_wgrad(dz, w, h, img, want_amax=False):
     with timer.span(f"linear_dgrad_wgrad[M={M},Nred={N},K={K}]", dz.device, 4 * M * (N + 2 * K), 4 * M * K * N):
         _gemm(_lib.LINEAR_DGRAD_ELU_WGRAD, _lib.ARITH_X6, dz, None, K, img, h=h, c=out, colsum=part, wpart=wpart,
               amax_out=amax)
-    db = torch.empty(K, device=dz.device, dtype=torch.float32)
+    db = _out_or_empty(db_prev_out, (K,), dz.device)
     rc = L.rslrl_column_sum_fold(part.data_ptr(), tiles, K, db.data_ptr(), _stream(dz))
     _lib.check(rc, "rslrl_column_sum_fold")
-    dwb = torch.empty(N * K + N, device=dz.device, dtype=torch.float32)
+    dwb = _out_or_empty(dwb_out, (N * K + N,), dz.device)
     nbytes = L.rslrl_fold_partials_workspace_bytes(tiles, N * K + N)
     ws = torch.empty(max(nbytes, 16) // 8, dtype=torch.float64, device=dz.device)
     rc = L.rslrl_fold_partials(wpart.data_ptr(), tiles, N * K + N, dwb.data_ptr(), ws.data_ptr(), nbytes,
@@ -328,15 +350,15 @@ def linear_dgrad_elu_wgrad(dz, w, h, img, want_amax=False):
     return out, db, dw, db_out
 
 
-def linear_wgrad(dz, x, arith=_lib.ARITH_X6, dz_amax=None, x_amax=None):
+def linear_wgrad(dz, x, arith=_lib.ARITH_X6, dz_amax=None, x_amax=None, out=None):
     """dz^T x ([N, K]) on the split weight-gradient kernel (x6, or h3 with max |dz|, max |x| as device scalars);
-    dz [M, N], x [M, K], N, K <= 256 and 4-aligned."""
+    dz [M, N], x [M, K], N, K <= 256 and 4-aligned.  out: optional [N, K] destination."""
     M, N = dz.shape
     K = x.shape[1]
     L = _lib.lib()
     nbytes = L.rslrl_linear_wgrad_workspace_bytes(M, N, K)
     ws = torch.empty(nbytes // 4, dtype=torch.float32, device=dz.device)
-    dw = torch.empty(N, K, dtype=torch.float32, device=dz.device)
+    dw = _out_or_empty(out, (N, K), dz.device)
     if arith == _lib.ARITH_H3:
         dz_amax = _amax(dz) if dz_amax is None else dz_amax
         x_amax = _amax(x) if x_amax is None else x_amax
@@ -347,24 +369,31 @@ def linear_wgrad(dz, x, arith=_lib.ARITH_X6, dz_amax=None, x_amax=None):
     return dw
 
 
-def _weight_grad(dz, x, x6: bool, h3=False, dz_amax=None, x_amax=None):
+def _weight_grad(dz, x, x6: bool, h3=False, dz_amax=None, x_amax=None, out=None):
     # the split weight-gradient kernel computes TN x 256 tiles (TN = 32, 64 or 256 rows of its first operand):
     # the square hidden layers run it as dz^T x (h3 when both operands come from h3-layer producers); the first
     # layer (input width <= 64) as (x^T dz)^T on the 64-row tiles (x6); the narrow output layers stay on the
-    # split-K batched GEMM (networks/linear.py) unless their backward is fused (linear_dgrad_elu_wgrad)
+    # split-K batched GEMM (networks/linear.py) unless their backward is fused (linear_dgrad_elu_wgrad).
+    # out: optional [N, K] destination (written directly where the kernel's layout allows, else copied)
+    def deliver(res):
+        if out is None:
+            return res if res.is_contiguous() else res.contiguous()
+        out.copy_(res)
+        return out
+
     if x6 and dz.shape[1] > 64 and x.shape[1] <= 64 and dz.shape[1] <= MAX_WIDTH and dz.shape[1] % 4 == 0:
         pad = (-x.shape[1]) % 4
         xp = F.pad(x, (0, pad)) if pad else x
-        return linear_wgrad(xp, dz)[: x.shape[1]].t().contiguous()
+        return deliver(linear_wgrad(xp, dz)[: x.shape[1]].t())
     if x6 and dz.shape[1] > 32 and x.shape[1] > 64 and dz.shape[1] <= MAX_WIDTH and x.shape[1] <= MAX_WIDTH \
             and x.shape[1] % 4 == 0:
         pad = (-dz.shape[1]) % 4
         if pad:  # the critic's 1-wide output
-            return linear_wgrad(F.pad(dz, (0, pad)), x)[: dz.shape[1]]
+            return deliver(linear_wgrad(F.pad(dz, (0, pad)), x)[: dz.shape[1]])
         if h3:
-            return linear_wgrad(dz, x, _lib.ARITH_H3, dz_amax, x_amax)
-        return linear_wgrad(dz, x)
-    return _splitk_weight_grad(dz, x)
+            return linear_wgrad(dz, x, _lib.ARITH_H3, dz_amax, x_amax, out=out)
+        return linear_wgrad(dz, x, out=out)
+    return deliver(_splitk_weight_grad(dz, x))
 
 
 def _plan(ws):
@@ -415,30 +444,123 @@ def _hidden_forward(x, ws, bs, h3, fuse_out, fwd_imgs, out_img, keep: bool):
     return hs, amaxes, y
 
 
+class MLPTape:
+    """What the backward of one MLP pass needs: the layer inputs (hs[l] = input of linear l), the weights, the
+    transposed B images of the input gradients, the published max |H| of h3 layers and the per-layer plan."""
+
+    __slots__ = ("hs", "ws", "dgrad_imgs", "amaxes", "h3", "x6")
+
+    def __init__(self, hs, ws, dgrad_imgs, amaxes, h3, x6):
+        self.hs, self.ws, self.dgrad_imgs, self.amaxes, self.h3, self.x6 = hs, ws, dgrad_imgs, amaxes, h3, x6
+
+
+def train_forward(x, ws, bs):
+    """y = MLP(x) for hidden ELU(alpha=1) layers (ws/bs: the Linear weights and biases), keeping what the backward
+    needs.  Returns (y, MLPTape)."""
+    split, h3, fuse_out = _plan(ws)
+    nh = len(ws) - 1
+    if split:
+        fwd_imgs, dgrad_imgs, out_img = _forward_images(ws, h3, fuse_out, backward=True)
+        hs, amaxes, y = _hidden_forward(x, ws, bs, h3, fuse_out, fwd_imgs, out_img, keep=True)
+    else:
+        hs, amaxes, h = [x], [None] * (nh + 1), x
+        for l in range(nh):
+            h = linear_fwd(h, ws[l], bs[l], elu=True)
+            hs.append(h)
+        dgrad_imgs, y = [None] * (nh + 1), None
+    if y is None:
+        y = F.linear(hs[-1], ws[-1], bs[-1])
+    return y, MLPTape(hs, list(ws), dgrad_imgs, amaxes, h3, split)
+
+
+def train_backward(tape, dy, need_dx=False, need_w=None, outs=None):
+    """Gradients of one MLP pass: returns (dx or None, [dW_l], [db_l]).  need_w[l]: layer l's weight gradient is
+    wanted (default: all).  outs[l] = (dW destination, db destination) or None: contiguous fp32 tensors the
+    gradients are written into (a gradient arena's slots) instead of new tensors."""
+    hs, ws, h3 = tape.hs, tape.ws, tape.h3
+    L = len(ws)
+    need_w = [True] * L if need_w is None else need_w
+    outs = [None] * L if outs is None else outs
+    w_out = lambda l: outs[l][0] if outs[l] is not None else None  # noqa: E731
+    b_out = lambda l: outs[l][1] if outs[l] is not None else None  # noqa: E731
+    grads_w = [None] * L
+    grads_b = [None] * L
+    dz = dy.contiguous()
+    dz_amax = None
+    dx = None
+    for l in range(L - 1, -1, -1):
+        h_in = hs[l]
+        fuse_w = (_FUSE_OUT and tape.x6 and l == L - 1 and l > 0 and dz.shape[1] <= 16 and h_in.shape[1] <= MAX_WIDTH
+                  and need_w[l])
+        if fuse_w:  # output layer: dgrad + ELU' + bias grad + weight grad over one read of h (one launch)
+            nred = dz.shape[1]
+            K = h_in.shape[1]
+            pad = (-nred) % 4
+            dzp = F.pad(dz, (0, pad)) if pad else dz
+            want = l - 1 > 0 and h3[l - 1]
+            # the kernel's [dW | db] result lands directly in the arena when weight and bias are adjacent there
+            dwb_out = None
+            wo, bo = w_out(l), b_out(l)
+            if not pad and wo is not None and bo is not None and wo.is_contiguous() \
+                    and bo.data_ptr() == wo.data_ptr() + 4 * wo.numel():
+                dwb_out = torch.as_strided(wo, (nred * K + nred,), (1,))
+            res = linear_dgrad_elu_wgrad(dzp, ws[l], h_in, tape.dgrad_imgs[l], want_amax=want,
+                                         db_prev_out=b_out(l - 1), dwb_out=dwb_out)
+            dz, grads_b[l - 1], dw, db_out = res[:4]
+            dz_amax = res[4] if want else None
+            if dwb_out is not None:
+                grads_w[l], grads_b[l] = wo, bo
+            else:
+                grads_w[l], grads_b[l] = dw[:nred], db_out[:nred]
+                if wo is not None:
+                    wo.copy_(grads_w[l])
+                    grads_w[l] = wo
+                if bo is not None:
+                    bo.copy_(grads_b[l])
+                    grads_b[l] = bo
+            continue
+        if l == L - 1:
+            grads_b[l] = dz.sum(0) if b_out(l) is None else torch.sum(dz, 0, out=b_out(l))
+        if need_w[l]:
+            grads_w[l] = _weight_grad(dz, h_in, tape.x6, h3[l], dz_amax, tape.amaxes[l], out=w_out(l))
+        if l == 0:
+            dx = dz.mm(ws[0]) if need_dx else None
+            break
+        # dZ_{l-1} = (dZ_l W_l) * ELU'(H_{l-1}), db_{l-1} = column sums; a reduction width that is not a
+        # multiple of 4 (the critic's 1-wide output) is zero-padded to the next multiple (the x6 image
+        # zero-fills the weight side itself)
+        w = ws[l]
+        img = tape.dgrad_imgs[l]
+        pad = (-dz.shape[1]) % 4
+        if pad:
+            dz = F.pad(dz, (0, pad))
+            if img is None:
+                w = F.pad(w, (0, 0, 0, pad))
+        if h3[l]:
+            want = l - 1 > 0 and h3[l - 1]
+            dz_amax = _amax(dz) if dz_amax is None else dz_amax
+            dz, grads_b[l - 1], dz_amax = linear_dgrad_elu_ex(dz, h_in, img, _lib.ARITH_H3, dz_amax, want,
+                                                              db_out=b_out(l - 1))
+        elif img is not None:
+            want = l - 1 > 0 and h3[l - 1]
+            dz, grads_b[l - 1], dz_amax = linear_dgrad_elu_ex(dz, h_in, img, _lib.ARITH_X6, None, want,
+                                                              db_out=b_out(l - 1))
+        else:
+            dz, grads_b[l - 1] = linear_dgrad_elu(dz, w, h_in, None, db_out=b_out(l - 1))
+            dz_amax = None
+    return dx, grads_w, grads_b
+
+
 class FusedMLPFunction(torch.autograd.Function):
     """y = MLP(x) for hidden ELU(alpha=1) layers; args: (x, W1, b1, ..., WL, bL)."""
 
     @staticmethod
     def forward(ctx, x, *params):
         ws, bs = params[0::2], params[1::2]
-        split, h3, fuse_out = _plan(ws)
-        nh = len(ws) - 1
-        if split:
-            fwd_imgs, dgrad_imgs, out_img = _forward_images(ws, h3, fuse_out, backward=True)
-            hs, amaxes, y = _hidden_forward(x, ws, bs, h3, fuse_out, fwd_imgs, out_img, keep=True)
-        else:
-            hs, amaxes, h = [x], [None] * (nh + 1), x
-            for l in range(nh):
-                h = linear_fwd(h, ws[l], bs[l], elu=True)
-                hs.append(h)
-            dgrad_imgs, y = [None] * (nh + 1), None
-        if y is None:
-            y = F.linear(hs[-1], ws[-1], bs[-1])
-        ctx.dgrad_imgs = dgrad_imgs  # index l: image of W_l^T
-        ctx.amaxes = amaxes
-        ctx.h3 = h3
-        ctx.x6 = split
-        ctx.save_for_backward(*hs, *params)
+        y, tape = train_forward(x, ws, bs)
+        ctx.save_for_backward(*tape.hs, *params)
+        tape.hs, tape.ws = None, None  # re-attached from saved_tensors in backward
+        ctx.tape = tape
         ctx.n_layers = len(ws)
         return y
 
@@ -446,56 +568,10 @@ class FusedMLPFunction(torch.autograd.Function):
     def backward(ctx, dy):
         L = ctx.n_layers
         saved = ctx.saved_tensors
-        hs, params = saved[:L], saved[L:]
-        ws = params[0::2]
-        h3 = ctx.h3
-        grads_w = [None] * L
-        grads_b = [None] * L
-        dz = dy.contiguous()
-        dz_amax = None
-        grads_b[L - 1] = None  # the output layer's bias gradient: column sums of dy
-        for l in range(L - 1, -1, -1):
-            h_in = hs[l]
-            fuse_w = (_FUSE_OUT and ctx.x6 and l == L - 1 and l > 0 and dz.shape[1] <= 16 and h_in.shape[1] <= MAX_WIDTH
-                      and ctx.needs_input_grad[1 + 2 * l])
-            if fuse_w:  # output layer: dgrad + ELU' + bias grad + weight grad over one read of h (one launch)
-                nred = dz.shape[1]
-                pad = (-nred) % 4
-                dzp = F.pad(dz, (0, pad)) if pad else dz
-                want = l - 1 > 0 and h3[l - 1]
-                res = linear_dgrad_elu_wgrad(dzp, ws[l], h_in, ctx.dgrad_imgs[l], want_amax=want)
-                dz, grads_b[l - 1], dw, db_out = res[:4]
-                dz_amax = res[4] if want else None
-                grads_w[l] = dw[:nred]
-                grads_b[l] = db_out[:nred]  # from the same launch (was a separate reduction of dy)
-                continue
-            if l == L - 1:
-                grads_b[l] = dz.sum(0)
-            if ctx.needs_input_grad[1 + 2 * l]:
-                grads_w[l] = _weight_grad(dz, h_in, ctx.x6, h3[l], dz_amax, ctx.amaxes[l])
-            if l == 0:
-                dx = dz.mm(ws[0]) if ctx.needs_input_grad[0] else None
-                break
-            # dZ_{l-1} = (dZ_l W_l) * ELU'(H_{l-1}), db_{l-1} = column sums; a reduction width that is not a
-            # multiple of 4 (the critic's 1-wide output) is zero-padded to the next multiple (the x6 image
-            # zero-fills the weight side itself)
-            w = ws[l]
-            img = ctx.dgrad_imgs[l]
-            pad = (-dz.shape[1]) % 4
-            if pad:
-                dz = F.pad(dz, (0, pad))
-                if img is None:
-                    w = F.pad(w, (0, 0, 0, pad))
-            if h3[l]:
-                want = l - 1 > 0 and h3[l - 1]
-                dz_amax = _amax(dz) if dz_amax is None else dz_amax
-                dz, grads_b[l - 1], dz_amax = linear_dgrad_elu_ex(dz, h_in, img, _lib.ARITH_H3, dz_amax, want)
-            elif img is not None:
-                want = l - 1 > 0 and h3[l - 1]
-                dz, grads_b[l - 1], dz_amax = linear_dgrad_elu_ex(dz, h_in, img, _lib.ARITH_X6, None, want)
-            else:
-                dz, grads_b[l - 1] = linear_dgrad_elu(dz, w, h_in, None)
-                dz_amax = None
+        tape = ctx.tape
+        tape.hs, tape.ws = list(saved[:L]), list(saved[L:][0::2])
+        need_w = [ctx.needs_input_grad[1 + 2 * l] for l in range(L)]
+        dx, grads_w, grads_b = train_backward(tape, dy, need_dx=ctx.needs_input_grad[0], need_w=need_w)
         out = [dx]
         for gw, gb in zip(grads_w, grads_b):
             out += [gw, gb]

@@ -447,6 +447,190 @@ def make_update_c1(PPO, ActorCritic, RolloutStorage):
 
 
 # --------------------------------------------------------------------------------------------------
+# full updates whose storage is regenerated from numpy seeds on the test side (the fixture stores only what
+# the reference's policy produced): multi-rank W = 2 / 4 over gloo (ppo.py:271-294, :428-469) and one update
+# at the real network width (config C2's shape: O48 A12 3x256)
+# --------------------------------------------------------------------------------------------------
+def storage_noise(seed, T, N, O, A):
+    """The policy-independent storage inputs, drawn with numpy's PCG64 (bit-reproducible across machines for
+    a given numpy; tests/test_*update*.py regenerate them): obs, rewards, dones, action noise, last obs."""
+    rng = np.random.default_rng(seed)
+    return {
+        "obs": rng.standard_normal((T, N, O), dtype=np.float32),
+        "rewards": rng.standard_normal((T, N, 1), dtype=np.float32),
+        "dones": (rng.random((T, N, 1)) < 0.05).astype(np.uint8),
+        "noise": rng.standard_normal((T, N, A), dtype=np.float32),
+        "last_obs": rng.standard_normal((N, O), dtype=np.float32),
+    }
+
+
+def _fill_storage_from_noise(st, policy, nz, mu_fp16):
+    """Rollout-consistent storage (as ppo.py:129-140 would record it): mu / sigma / values from the policy for the
+    stored obs, actions = mu + sigma * noise (fp32 mul then add), log-prob of those actions under N(mu, sigma).
+    mu_fp16: the stored mean is rounded to fp16 first (a compact fixture; the first mini-batch's KL then is the
+    small non-zero KL of that rounding).  Returns the arrays the fixture must store."""
+    T, N, O = nz["obs"].shape
+    A = nz["noise"].shape[-1]
+    obs = torch.from_numpy(nz["obs"])
+    st.observations["policy"].copy_(obs)
+    st.rewards.copy_(torch.from_numpy(nz["rewards"]))
+    st.dones.copy_(torch.from_numpy(nz["dones"]))
+    with torch.inference_mode():
+        o = {"policy": obs.reshape(T * N, O)}
+        policy.update_distribution(policy.actor_obs_normalizer(policy.get_actor_obs(o)))
+        mu = policy.action_mean.reshape(T, N, A).clone()
+        sigma = policy.action_std.reshape(T, N, A).clone()
+        if mu_fp16:
+            mu = mu.half().float()
+        actions = mu + sigma * torch.from_numpy(nz["noise"])
+        logp = torch.distributions.Normal(mu, sigma).log_prob(actions).sum(-1, keepdim=True)
+        values = policy.evaluate(o).reshape(T, N, 1).clone()
+    st.values.copy_(values)
+    st.mu.copy_(mu)
+    st.sigma.copy_(sigma)
+    st.actions.copy_(actions)
+    st.actions_log_prob.copy_(logp)
+    st.step = T
+    assert torch.equal(sigma, sigma[:1, :1].expand_as(sigma))
+    return {"mu": mu.half().numpy() if mu_fp16 else f32(mu), "sigma": f32(sigma[0, 0]), "values": f32(values),
+            "actions_log_prob": f32(logp)}
+
+
+def _run_recorded_update(alg, grad_batches=0):
+    """update() recording the lr of every optimizer step and the pre-clip policy gradient (concatenated in
+    parameters() order) of the first `grad_batches` mini-batches."""
+    lr_trace, grads = [], []
+    orig_step = alg.optimizer.step
+    orig_clip = torch.nn.utils.clip_grad_norm_
+
+    def rec_clip(params, *a, **kw):
+        if len(grads) < grad_batches:
+            grads.append(torch.cat([p.grad.reshape(-1) for p in alg.policy.parameters()]).clone())
+        return orig_clip(params, *a, **kw)
+
+    def rec_step(*a, **kw):
+        lr_trace.append(alg.optimizer.param_groups[0]["lr"])
+        return orig_step(*a, **kw)
+
+    alg.optimizer.step = rec_step
+    torch.nn.utils.clip_grad_norm_ = rec_clip
+    try:
+        loss_dict = alg.update()
+    finally:
+        torch.nn.utils.clip_grad_norm_ = orig_clip
+    return loss_dict, lr_trace, grads
+
+
+def _update_case(PPO, ActorCritic, RolloutStorage, *, T, N, O, A, hidden, seed, rank, world, mu_fp16, lr=1e-3,
+                 grad_batches=0, logp_ulp=False):
+    torch.manual_seed(seed + 17 * rank)  # different initial weights per rank; broadcast_parameters syncs them
+    obs0 = {"policy": torch.zeros(N, O)}
+    groups = {"policy": ["policy"], "critic": ["policy"]}
+    pol = ActorCritic(obs0, groups, A, actor_hidden_dims=hidden, critic_hidden_dims=hidden)
+    mcfg = {"global_rank": rank, "local_rank": rank, "world_size": world} if world > 1 else None
+    alg = PPO(pol, num_learning_epochs=5, num_mini_batches=4, device="cpu", multi_gpu_cfg=mcfg, learning_rate=lr)
+    if world > 1:
+        alg.broadcast_parameters()  # on_policy_runner.py:99-101
+    init_state = {k: f32(v) for k, v in pol.state_dict().items()}
+    alg.init_storage("rl", N, T, obs0, [A])
+    nz = storage_noise(seed * 100 + rank, T, N, O, A)
+    stored = _fill_storage_from_noise(alg.storage, pol, nz, mu_fp16)
+    if logp_ulp:  # sensitivity probe: every stored log-prob one ulp up
+        lp = alg.storage.actions_log_prob
+        lp.copy_(torch.nextafter(lp, torch.full_like(lp, float("inf"))))
+    with torch.inference_mode():
+        alg.compute_returns({"policy": torch.from_numpy(nz["last_obs"])})
+    torch.manual_seed(5000 + rank)  # the permutation's generator, per rank
+    gen_state = torch.default_generator.get_state().numpy().copy()
+    loss_dict, lr_trace, grads = _run_recorded_update(alg, grad_batches)
+    arrays = {f"init/{k}": v for k, v in init_state.items()}
+    for j, g in enumerate(grads):  # pre-clip gradients of the first mini-batches (before any trajectory drift)
+        arrays[f"grad_mb{j}"] = f32(g)
+    arrays.update({f"final/{k}": f32(v) for k, v in pol.state_dict().items()})
+    arrays.update({f"storage/{k}": v for k, v in stored.items()})
+    arrays["storage/returns_head"] = f32(alg.storage.returns[:2])  # after compute_returns (un-cleared buffer)
+    arrays["gen_state"] = gen_state
+    arrays["obs_sha256"] = np.frombuffer(hashlib.sha256(nz["obs"].tobytes()).digest(), dtype=np.uint8)
+    meta = {"loss_dict": loss_dict, "lr_trace": lr_trace, "final_lr": alg.learning_rate,
+            "noise_seed": seed * 100 + rank}
+    return arrays, meta
+
+
+MULTIRANK_CASES = [  # name, world, T, N per rank, O, A, hidden, seed, learning rate
+    ("w2", 2, 16, 256, 16, 4, [64, 64], 71, 1e-3),
+    ("w4", 4, 16, 128, 16, 4, [64, 64], 73, 6e-3),  # large steps: the lr-decrease branch is taken as well
+]
+
+
+def _multirank_worker(rank, world, port, ref_path, case, out_dir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.set_num_threads(1)
+    PPO, ActorCritic, RolloutStorage = import_reference(ref_path)
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        name, _, T, N, O, A, hidden, seed, lr = case
+        arrays, meta = _update_case(PPO, ActorCritic, RolloutStorage, T=T, N=N, O=O, A=A, hidden=hidden, seed=seed,
+                                    rank=rank, world=world, mu_fp16=False, lr=lr)
+        np.savez(os.path.join(out_dir, f"r{rank}.npz"), **arrays)
+        with open(os.path.join(out_dir, f"r{rank}.json"), "w") as f:
+            json.dump(meta, f)
+    finally:
+        torch.distributed.destroy_process_group()
+
+
+def make_multirank(ref_path):
+    import socket
+    import tempfile
+
+    import torch.multiprocessing as mp
+
+    meta = {}
+    for case in MULTIRANK_CASES:
+        name, world, T, N, O, A, hidden, seed, lr = case
+        with tempfile.TemporaryDirectory() as d:
+            sock = socket.socket()
+            sock.bind(("127.0.0.1", 0))
+            port = sock.getsockname()[1]
+            sock.close()
+            mp.spawn(_multirank_worker, args=(world, port, ref_path, case, d), nprocs=world, join=True)
+            arrays, ranks = {}, []
+            for r in range(world):
+                z = np.load(os.path.join(d, f"r{r}.npz"))
+                arrays.update({f"r{r}/{k}": z[k] for k in z.files})
+                with open(os.path.join(d, f"r{r}.json")) as f:
+                    ranks.append(json.load(f))
+        np.savez_compressed(os.path.join(HERE, f"update_{name}.npz"), **arrays)
+        meta[name] = {"world": world, "T": T, "N": N, "O": O, "A": A, "hidden": hidden, "M": 4, "E": 5,
+                      "seed": seed, "learning_rate": lr, "ranks": ranks, "mu_fp16": False}
+    return meta
+
+
+def make_update_c2(PPO, ActorCritic, RolloutStorage):
+    """One reference update at config C2's shape: N4096 T24 O48 A12, actor/critic 3x256 ELU, E5 M4 (mini-batch
+    24,576 rows); storage regenerated from numpy seeds on the test side, mean stored as fp16."""
+    T, N, O, A, hidden, seed = 24, 4096, 48, 12, [256, 256, 256], 91
+    arrays, m = _update_case(PPO, ActorCritic, RolloutStorage, T=T, N=N, O=O, A=A, hidden=hidden, seed=seed,
+                             rank=0, world=1, mu_fp16=True, grad_batches=1)
+    np.savez_compressed(os.path.join(HERE, "update_c2.npz"), **arrays)
+    # the reference's own sensitivity: the same update with every stored log-prob one ulp up.  The surrogate's
+    # clip/max branches are discontinuous, so samples at a clip bound flip and the trajectory moves; the test
+    # bounds our deviation by this (per tensor, relative to how far the update moved it)
+    ulp, _ = _update_case(PPO, ActorCritic, RolloutStorage, T=T, N=N, O=O, A=A, hidden=hidden, seed=seed, rank=0,
+                          world=1, mu_fp16=True, logp_ulp=True)
+    sens = {}
+    for k in arrays:
+        if k.startswith("final/"):
+            name = k[6:]
+            moved = np.linalg.norm(arrays[k].astype(np.float64) - arrays["init/" + name].astype(np.float64))
+            sens[name] = float(np.linalg.norm(ulp[k].astype(np.float64) - arrays[k].astype(np.float64)) / moved)
+    m["ulp_sensitivity"] = sens
+    m.update({"T": T, "N": N, "O": O, "A": A, "hidden": hidden, "M": 4, "E": 5, "seed": seed, "mu_fp16": True,
+              "learning_rate": 1e-3})
+    return m
+
+
+# --------------------------------------------------------------------------------------------------
 # rollout side: act + process_env_step + add_transitions + RND (ppo.py:129-169, rollout_storage.py:77-103,
 # rnd.py:113-135) -- the inputs of each step, the transition act() produced, and the storage after T steps
 # --------------------------------------------------------------------------------------------------
@@ -458,6 +642,10 @@ ROLLOUT_CASES = [
      dict(weight=0.5, num_outputs=3, predictor_hidden_dims=[32], target_hidden_dims=[32], state_normalization=True,
           weight_schedule={"mode": "step", "final_step": 2, "final_value": 0.25}), 0.2, "bool", 8),
     ("plain_timeouts", 257, 16, 4, 2, None, 0.5, "float", 9),
+    # linear weight schedule (rnd.py:175-182): weights strictly between the end points on steps 3..5
+    ("rnd_linear_sched", 64, 16, 4, 8,
+     dict(weight=0.3, num_outputs=2, predictor_hidden_dims=[16], target_hidden_dims=[16],
+          weight_schedule={"mode": "linear", "initial_step": 2, "final_step": 6, "final_value": 0.7}), 0.2, "int64", 10),
 ]
 
 
@@ -497,7 +685,7 @@ def make_rollout(PPO, ActorCritic, RolloutStorage):
                 alg.process_env_step({"policy": nobs}, rew, dones, {"time_outs": to})
                 if alg.rnd is not None:
                     arrays[f"step{t}/intrinsic"] = f32(alg.intrinsic_rewards)
-                    arrays[f"step{t}/rnd_weight"] = np.float32(alg.rnd.weight)
+                    arrays[f"step{t}/rnd_weight"] = np.float64(alg.rnd.weight)  # the host-side Python float
                 obs = nobs
         st = alg.storage
         for k in ("rewards", "values", "actions_log_prob", "mu", "sigma", "actions"):
@@ -543,7 +731,8 @@ def make_normalizer(ref_path):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reference", default=os.environ.get("RSL_RL_REFERENCE", "/root/reference"))
-    ap.add_argument("--only", choices=["rollout", "normalizer"], help="regenerate one fixture family, keep the rest")
+    ap.add_argument("--only", choices=["rollout", "normalizer", "multirank", "update_c2"],
+                    help="regenerate one fixture family, keep the rest")
     args = ap.parse_args()
     torch.set_num_threads(4)
     PPO, ActorCritic, RolloutStorage = import_reference(args.reference)
@@ -552,6 +741,10 @@ def main():
             meta = json.load(f)
         if args.only == "rollout":
             meta["rollout"] = make_rollout(PPO, ActorCritic, RolloutStorage)
+        elif args.only == "multirank":
+            meta["multirank"] = make_multirank(args.reference)
+        elif args.only == "update_c2":
+            meta["update_c2"] = make_update_c2(PPO, ActorCritic, RolloutStorage)
         else:
             meta["normalizer"] = make_normalizer(args.reference)
         with open(os.path.join(HERE, "golden.json"), "w") as f:
@@ -569,6 +762,8 @@ def main():
         "update_c1": make_update_c1(PPO, ActorCritic, RolloutStorage),
         "rollout": make_rollout(PPO, ActorCritic, RolloutStorage),
         "normalizer": make_normalizer(args.reference),
+        "multirank": make_multirank(args.reference),
+        "update_c2": make_update_c2(PPO, ActorCritic, RolloutStorage),
     }
     with open(os.path.join(HERE, "golden.json"), "w") as f:
         json.dump(meta, f, indent=1, sort_keys=True)

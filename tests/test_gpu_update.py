@@ -1,12 +1,13 @@
-"""One full PPO.update() on the GPU vs the reference's update captured on CPU (config C1: N512 T16 O16
-A4, 2x64 ELU, E5 M4), and an end-to-end OnPolicyRunner smoke on the synthetic VecEnv.
+"""Full PPO.update() on the GPU vs the reference's update captured on CPU, and an end-to-end OnPolicyRunner
+smoke on the synthetic VecEnv.
 
-The fixture ran the reference with multi_gpu_cfg world_size=1 (so its learning rate went through the
-fp32 broadcast, ppo.py:287-290); the test does the same over a one-rank RCCL ("nccl") group, which also
-exercises the flat-gradient all-reduce path.  Same permutation (torch CPU randperm from the captured
-generator state), same storage, same initial weights; the MLP GEMMs run on hipBLASLt instead of CPU
-BLAS, so parameters are compared with a tolerance (atol 2e-5 after 20 Adam steps at lr <= 2.25e-3)
-while the learning-rate trace (the adaptive-KL decisions) must match exactly.
+C1 (N512 T16 O16 A4, 2x64 ELU, E5 M4): the fixture ran the reference with multi_gpu_cfg world_size=1 (so its
+learning rate went through the fp32 broadcast, ppo.py:287-290); the test does the same over a one-rank RCCL
+("nccl") group, which also exercises the one-collective-per-mini-batch path (gradient arena + KL).  Same
+permutation (torch CPU randperm from the captured generator state), same storage, same initial weights; the
+MLP GEMMs run on our fused MFMA kernels (x6 split-bf16 by default) instead of CPU BLAS, so parameters are
+compared with a tolerance (atol 2e-5 after 20 Adam steps at lr <= 2.25e-3) while the learning-rate trace
+(the adaptive-KL decisions) must match exactly.  C2's shape (3x256, O48, A12) is the second update test.
 """
 
 import os
@@ -130,3 +131,59 @@ def test_runner_with_normalizers_and_rnd(cuda_device, reward_norm):
     assert torch.isfinite(n._mean).all() and (n._std > 0).all()
     assert runner.alg.rnd.state_normalizer.count.item() == 2 * 8 * 1024
     assert torch.isfinite(runner.alg.intrinsic_rewards).all()
+
+
+def test_update_c2_width_matches_reference(golden_meta, cuda_device):
+    """One full update() at config C2's shape (N4096 T24 O48 A12, actor/critic 3x256 ELU, E5 M4; mini-batch 24,576
+    rows) against the reference's update on CPU (make_golden.make_update_c2), once through the default x6
+    split-bf16 GEMMs and once through the exact-fp32 MFMA GEMMs.
+
+    * first mini-batch (no drift yet): every parameter's gradient within 1e-5 of its max |g|;
+    * learning-rate trace (increase, then two decreases) exact; loss means rtol 1e-4;
+    * parameters after the 20 Adam steps, per tensor: ||ours - ref|| <= 2 s + 1e-4 times ||ref - init||, where s is
+      the REFERENCE's own sensitivity (golden.json update_c2.ulp_sensitivity): how far its parameters move, in the
+      same units, when every stored log-prob is raised by one ulp (0.7-2.3 % for the actor, 0 for the critic).
+      The surrogate's clip/max is discontinuous: a sample whose ratio sits within rounding of 1 +- clip_param
+      takes the other branch when its log-prob differs in the last bit (our exp/log vs torch CPU's), which moves
+      the gradient by ~1/sqrt(B) and Adam carries it on.  The GEMM arithmetic is not the residual: the x6 and
+      f32 runs end >100x closer to each other than to the reference (||x6 - f32|| <= 1e-3 ||ref - init||)."""
+    from update_fixtures import build_update, param_errors, run_recorded_update
+    from rsl_rl_amd.networks import fused_mlp
+
+    m = golden_meta["update_c2"]
+    z = np.load(golden_path("update_c2.npz"))
+    finals = {}
+    for mode in ("x6", "f32"):
+        prev = fused_mlp.set_gemm_mode({"x6": fused_mlp.GEMM_X6, "f32": fused_mlp.GEMM_F32}[mode])
+        try:
+            alg, pol = build_update(z, "", m, m, cuda_device)
+            head = torch.from_numpy(z["storage/returns_head"])
+            torch.testing.assert_close(alg.storage.returns[:2].cpu(), head, rtol=1e-5, atol=1e-5)
+            grads = [None]
+            loss, lr_trace = run_recorded_update(alg, grads)
+        finally:
+            fused_mlp.set_gemm_mode(prev)
+        ref_g = torch.from_numpy(z["grad_mb0"]).double()
+        ours_g = grads[0].double()
+        off = 0
+        for name, p in pol.named_parameters():
+            r, o = ref_g[off:off + p.numel()], ours_g[off:off + p.numel()]
+            off += p.numel()
+            err = (o - r).abs().max().item() / r.abs().max().item()
+            assert err <= 1e-5, (mode, name, err)
+        assert lr_trace == m["lr_trace"], mode
+        assert alg.learning_rate == m["final_lr"]
+        for k, v in m["loss_dict"].items():
+            assert abs(loss[k] - v) <= 1e-4 * abs(v) + 1e-6, (mode, k, loss[k], v)
+        errs = param_errors(pol.state_dict(), z, "")
+        print(mode, {k: (f"{a:.2e}", f"{r:.2e}") for k, (a, r) in errs.items()})
+        sens = m["ulp_sensitivity"]
+        for name, (abs_err, rel_moved) in errs.items():
+            assert rel_moved <= 2 * sens[name] + 1e-4, (mode, name, rel_moved, sens[name])
+        finals[mode] = {k: v.detach().cpu().double() for k, v in pol.state_dict().items()}
+    for k in finals["x6"]:
+        ref = torch.from_numpy(z["final/" + k]).double()
+        moved = (ref - torch.from_numpy(z["init/" + k]).double()).norm().item()
+        d = (finals["x6"][k] - finals["f32"][k]).norm().item()
+        print(k, f"||x6 - f32|| / moved = {d / moved:.2e}")
+        assert d <= 1e-3 * moved, (k, d / moved)

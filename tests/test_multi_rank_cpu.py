@@ -1,6 +1,8 @@
 """World-size-2 gloo tests (CPU) of PPO's distributed host logic (ppo.py:271-294, :428-469):
-parameter broadcast, the flat-buffer gradient all-reduce (and the reference's cat/copy-back fallback),
-and the KL all-reduce + adaptive learning-rate rule with the reference's fp32 lr rounding."""
+parameter broadcast, the gradient-arena all-reduce that update() issues once per mini-batch (gradients and
+the KL in one buffer), the reference's cat/copy-back fallback (with the KL appended), and the KL
+all-reduce + adaptive learning-rate rule with the reference's fp32 lr rounding.  The full multi-rank
+update() against the reference's own W=2 / W=4 runs is tests/test_multi_rank_update.py."""
 
 import os
 import socket
@@ -44,18 +46,29 @@ def _worker(rank, port, out_dir):
         ppo.broadcast_parameters()
         res["params"] = {k: v.clone() for k, v in ppo.policy.state_dict().items()}
 
-        # flat-buffer path: rank-specific gradients, averaged by one all-reduce of the flat buffer
-        ppo._bind_flat_grads()
+        # gradient-arena path of update(): every .grad a view of one buffer whose tail holds the KL, averaged
+        # by the one all-reduce update() issues per mini-batch
+        arena = ppo.grad_arena()
+        arena.bind()
         for i, p in enumerate(ppo.policy.parameters()):
             p.grad.copy_(torch.full_like(p, float(rank + 1) * (i + 1)))
+        arena.extra[:1].fill_(0.003 if rank == 0 else 0.001)
+        ppo._all_reduce_arena(arena, with_kl=True)
+        res["arena_grads"] = [p.grad.clone() for p in ppo.policy.parameters()]
+        res["arena_kl"] = arena.extra[0].item()
+        res["arena_is_grad"] = all(p.grad.data_ptr() == v.data_ptr() for p, v in zip(ppo.policy.parameters(),
+                                                                                     arena.views))
+        # reduce_parameters() on arena-backed gradients: the same single collective
         ppo.reduce_parameters()
-        res["flat_grads"] = [p.grad.clone() for p in ppo.policy.parameters()]
+        res["arena_grads2"] = [p.grad.clone() for p in ppo.policy.parameters()]
 
-        # reference fallback path (grads not backed by the flat buffer)
+        # reference cat path (grads not backed by the arena), with the KL appended to the concatenation
         for i, p in enumerate(ppo.policy.parameters()):
             p.grad = torch.full_like(p, float(rank + 1) * (i + 2))
-        ppo.reduce_parameters()
+        kl_t = torch.tensor([0.004 if rank == 0 else 0.002])
+        ppo.reduce_parameters(kl_mean=kl_t)
         res["cat_grads"] = [p.grad.clone() for p in ppo.policy.parameters()]
+        res["cat_kl"] = kl_t.item()
 
         # KL all-reduce + lr rule (kl: rank0 0.003, rank1 0.001 -> mean 0.002 < desired/2 -> lr * 1.5)
         kl = ppo._sync_kl_and_lr(torch.tensor([0.003 if rank == 0 else 0.001]))
@@ -81,11 +94,15 @@ def test_broadcast_parameters(results):
             assert torch.equal(v, ref[k]), k
 
 
-def test_flat_gradient_allreduce(results):
+def test_arena_allreduce(results):
     for r in results:
-        for i, g in enumerate(r["flat_grads"]):
+        assert r["arena_is_grad"]
+        for i, g in enumerate(r["arena_grads"]):
             assert torch.all(g == (1 + 2) * (i + 1) / WORLD)
-    for a, b in zip(results[0]["flat_grads"], results[1]["flat_grads"]):
+        for i, g in enumerate(r["arena_grads2"]):
+            assert torch.all(g == (1 + 2) * (i + 1) / WORLD)  # identical inputs on both ranks: unchanged
+        assert r["arena_kl"] == torch.tensor((0.003 + 0.001) / WORLD, dtype=torch.float32).item()
+    for a, b in zip(results[0]["arena_grads"], results[1]["arena_grads"]):
         assert torch.equal(a, b)
 
 
@@ -93,6 +110,8 @@ def test_reference_cat_path(results):
     for r in results:
         for i, g in enumerate(r["cat_grads"]):
             assert torch.all(g == (1 + 2) * (i + 2) / WORLD)
+        kl = torch.tensor(0.004, dtype=torch.float32) + torch.tensor(0.002, dtype=torch.float32)
+        assert r["cat_kl"] == (kl / WORLD).item()
 
 
 def test_kl_and_learning_rate(results):

@@ -114,7 +114,7 @@ def _rnd_layers(z, prefix, net):
     return [(z[k + ".weight"], z[k + ".bias"]) for k in keys]
 
 
-@pytest.mark.parametrize("case", ["rnd_c5like", "rnd_statenorm_q3", "plain_timeouts"])
+@pytest.mark.parametrize("case", ["rnd_c5like", "rnd_statenorm_q3", "plain_timeouts", "rnd_linear_sched"])
 def test_oracle_rollout_record(case, golden_meta):
     from oracle import ppo_oracle as po
     m = golden_meta["rollout"][case]
