@@ -67,7 +67,7 @@ struct GemmParams {
     const float* a_amax;  // h3: max |A| (device scalar written by A's producer) -> A's power-of-two scale
     float* amax_out;      // optional: max |C| over the stored output (device scalar, for an h3 consumer)
     unsigned* amax_ws;    // with amax_out: {running max bits, arrival ticket}, zero before and after the launch
-    int deep;             // h3, K = 256: the unrolled look-ahead main loop (h3_deep_loop)
+    int deep;             // K = 256: the unrolled look-ahead main loop (h3_deep_loop; x6 and h3)
 };
 
 // global -> registers for one K chunk: A: 128 x 16 floats = 512 float4 (1 per thread); B: 256 x 16 = 1024
@@ -554,6 +554,13 @@ __device__ __forceinline__ F read_frag(const char* __restrict__ plane, int row, 
 #define RSLRL_H3_DEPTH 3
 #endif
 constexpr int kH3Depth = RSLRL_H3_DEPTH;  // A look-ahead (chunks) of the unrolled h3 main loop
+#ifndef RSLRL_X6_DEPTH
+#define RSLRL_X6_DEPTH 1
+#endif
+// the same loop on x6 operands (three planes: more fragment registers).  Measured at M = 393,216 (one process
+// per build, scripts/x6_probe.py): depth 1 / 2 / 3 -> fwd 329 / 352 / 335 us, dgrad 359 / 375 / 375 us against
+// 466-494 us for the generic one-chunk loop; depth 1 is the only one without spills at two workgroups per CU.
+constexpr int kX6Depth = RSLRL_X6_DEPTH;
 constexpr int kH3DeepDefault = (1 << RSLRL_LINEAR_FWD) | (1 << RSLRL_LINEAR_FWD_ELU) | (1 << RSLRL_LINEAR_DGRAD_ELU) |
                                (1 << RSLRL_LINEAR_FWD_OUT);
 __device__ __forceinline__ void amax_commit(const GemmParams& p, float amx) {
@@ -694,9 +701,9 @@ __device__ __forceinline__ void mlp_gemm_x6_body(GemmParams p, const uint4* __re
 
     const float sa = PL == 2 ? h3_scale(*p.a_amax) : 1.f;
     bool deep = false;
-    if constexpr (PL == 2 && FULL) {
+    if constexpr (FULL) {
         if (p.K == 16 * kKC && p.deep) {
-            h3_deep_loop<EPI, BM, PL, 16, kH3Depth, Frag>(p, row0, bimg, lds, acc, sa, wm, wn, l32, h);
+            h3_deep_loop<EPI, BM, PL, 16, PL == 2 ? kH3Depth : kX6Depth, Frag>(p, row0, bimg, lds, acc, sa, wm, wn, l32, h);
             deep = true;
         }
     }
