@@ -172,6 +172,59 @@ __device__ __forceinline__ void epilogue_tiles_impl(const GemmParams& p, f32x16 
             dst[r] = (rbase + roff < p.M && col < p.N) ? hp[static_cast<int64_t>(roff) * p.N] : 0.f;
         }
     };
+    if constexpr (full && EPI != kEpiEluGradWgrad) {
+        // Full tiles: every access through a buffer resource over the wave's rows (wave-uniform base): the
+        // lane part of the offset is one VGPR per column tile, the 8-row group step rides in soffset (an SGPR
+        // constant) and the row within the group in the 12-bit immediate -- no per-store address arithmetic
+        // (the 64-bit vaddr form spent two VALU per store).  The ELU is evaluated branch-free on every lane:
+        // as a guarded call the compiler wrapped each element in an exec-mask branch (3 SALU + a skip each).
+        const uint32_t rbytes = static_cast<uint32_t>(I * 32 * kBN * 4);
+        const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(p.c + ubase, 0, rbytes, 0x00020000);
+        const __amdgpu_buffer_rsrc_t rh =
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(GRAD ? p.h + ubase : p.c), 0, rbytes, 0x00020000);
+        auto voff = [&](int j, int r) { return static_cast<int>(((4 * h + (r & 3)) * kBN + j * 32 + l32) * 4); };
+        auto soff = [&](int i, int r) { return (i * 32 + 8 * (r >> 2)) * kBN * 4; };
+        auto load_hb = [&](int b, float (&dst)[16]) {
+            const int i = b / J, j = b % J;
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                dst[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rh, voff(j, r), soff(i, r), 0));
+        };
+        if constexpr (GRAD) load_hb(0, hcur);
+#pragma unroll
+        for (int b = 0; b < I * J; ++b) {
+            const int i = b / J, j = b % J;
+            if constexpr (GRAD) {
+                if (b + 1 < I * J) load_hb(b + 1, hnext);
+            }
+            float bias = 0.f;
+            if constexpr (!GRAD) bias = p.bias[wcol0 + j * 32 + l32];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                float v = acc[i][j][r];
+                if constexpr (EPI == kEpiBias) {
+                    v = v + bias;
+                } else if constexpr (EPI == kEpiBiasElu) {
+                    v = v + bias;
+                    const float n = elu_neg(fminf(v, 0.f));  // evaluated on every lane: a select, not a branch
+                    v = v > 0.f ? v : n;
+                } else {
+                    const float hv = hcur[r];
+                    const float g = v * (hv + 1.f);
+                    v = hv > 0.f ? v : g;
+                    colpart[j] += v;
+                }
+                amx = fmaxf(amx, fabsf(v));
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), rc, voff(j, r), soff(i, r),
+                                                      2 /* nt */);
+            }
+            if constexpr (GRAD) {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) hcur[r] = hnext[r];
+            }
+        }
+        return;
+    }
     if constexpr (GRAD) load_h(0, hcur);
 #pragma unroll
     for (int b = 0; b < I * J; ++b) {
@@ -597,11 +650,11 @@ __device__ __forceinline__ void store_b_regs(BStage<PL>& b, char* b_lds) {
     }
 }
 
-template <int EPI, int BM, int PL, int NCH, int D, typename Frag>
-__device__ __forceinline__ void h3_deep_loop(const GemmParams& p, int64_t row0, const uint4* __restrict__ bimg,
-                                             char* (&lds)[2], f32x16 (&acc)[BM / 64][2], float sa, int wm,
-                                             int wn, int l32, int h) {
-    constexpr int I = BM / 64;
+// The pipeline alone, for any fragment schedule: compute(a_lds, b_lds) reads one chunk's fragments from the
+// LDS buffer and issues its MFMAs.
+template <int BM, int PL, int NCH, int D, typename Compute>
+__device__ __forceinline__ void deep_pipeline(const GemmParams& p, int64_t row0, const uint4* __restrict__ bimg,
+                                              char* (&lds)[2], float sa, Compute&& compute) {
     constexpr int planeA = BM * kX6RowB;
     AStage<BM> sa_[D];
     BStage<PL> sb;
@@ -617,26 +670,7 @@ __device__ __forceinline__ void h3_deep_loop(const GemmParams& p, int64_t row0, 
     __syncthreads();
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
-        const char* a_lds = lds[c & 1];
-        const char* b_lds = lds[c & 1] + PL * planeA;
-        Frag bf[2][PL];
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int q = 0; q < PL; ++q) bf[j][q] = read_frag<Frag>(b_lds + q * kX6PlaneB, wn * 64 + j * 32 + l32, h);
-#pragma unroll
-        for (int i = 0; i < I; ++i) {
-            Frag af[PL];
-#pragma unroll
-            for (int q = 0; q < PL; ++q) af[q] = read_frag<Frag>(a_lds + q * planeA, wm * (BM / 2) + i * 32 + l32, h);
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                if constexpr (EPI == kEpiBiasEluOut)
-                    acc[i][j] = Arith<PL>::mfma(bf[j], af, acc[i][j]);
-                else
-                    acc[i][j] = Arith<PL>::mfma(af, bf[j], acc[i][j]);
-            }
-        }
+        compute(lds[c & 1], lds[c & 1] + PL * planeA);
         if (c + 1 < NCH) {  // buffer (c+1)&1 was last read in chunk c-1; every wave passed the barrier after it
             // pin the use of the prefetched registers here: otherwise the scheduler hoists the scaling
             // multiply right behind the load and the wave waits out the look-ahead right away
@@ -657,6 +691,34 @@ __device__ __forceinline__ void h3_deep_loop(const GemmParams& p, int64_t row0, 
         else
             __syncthreads();  // the epilogue may reuse the LDS
     }
+}
+
+template <int EPI, int BM, int PL, int NCH, int D, typename Frag>
+__device__ __forceinline__ void h3_deep_loop(const GemmParams& p, int64_t row0, const uint4* __restrict__ bimg,
+                                             char* (&lds)[2], f32x16 (&acc)[BM / 64][2], float sa, int wm,
+                                             int wn, int l32, int h) {
+    constexpr int I = BM / 64;
+    constexpr int planeA = BM * kX6RowB;
+    deep_pipeline<BM, PL, NCH, D>(p, row0, bimg, lds, sa, [&](const char* a_lds, const char* b_lds) {
+        Frag bf[2][PL];
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int q = 0; q < PL; ++q) bf[j][q] = read_frag<Frag>(b_lds + q * kX6PlaneB, wn * 64 + j * 32 + l32, h);
+#pragma unroll
+        for (int i = 0; i < I; ++i) {
+            Frag af[PL];
+#pragma unroll
+            for (int q = 0; q < PL; ++q) af[q] = read_frag<Frag>(a_lds + q * planeA, wm * (BM / 2) + i * 32 + l32, h);
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                if constexpr (EPI == kEpiBiasEluOut)
+                    acc[i][j] = Arith<PL>::mfma(bf[j], af, acc[i][j]);
+                else
+                    acc[i][j] = Arith<PL>::mfma(af, bf[j], acc[i][j]);
+            }
+        }
+    });
 }
 
 // 128 rows x 256 columns per workgroup: waves 2 (M) x 4 (N) of 64 x 64 (2 x 2 MFMA tiles); MINW = 4:
@@ -1160,20 +1222,8 @@ __global__ __launch_bounds__(kThreads, MINW) void mlp_gemm_x6s_kernel(GemmParams
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{};
 
-    const int nchunks = (p.K + kKC - 1) / kKC;
-    load_b_lds<3>(bimg, 0, lds[0] + 3 * planeA);
-    store_a_split<BM, 3>(load_a<BM, FULL>(p, row0, 0), lds[0], 1.f);
-    __syncthreads();
-    for (int c = 0; c < nchunks; ++c) {
-        const int buf = c & 1;
-        const bool more = c + 1 < nchunks;
-        AStage<BM> an;
-        if (more) {
-            load_b_lds<3>(bimg, c + 1, lds[buf ^ 1] + 3 * planeA);
-            an = load_a<BM, FULL>(p, row0, (c + 1) * kKC);
-        }
-        const char* a_lds = lds[buf];
-        const char* b_lds = lds[buf] + 3 * planeA;
+    // one chunk's fragments and MFMAs (a_lds / b_lds: the chunk's A planes and B image in LDS)
+    auto compute = [&](const char* a_lds, const char* b_lds) {
         bf16x8 af[4][2];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -1194,9 +1244,33 @@ __global__ __launch_bounds__(kThreads, MINW) void mlp_gemm_x6s_kernel(GemmParams
                 acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b2, af[i][1], acc[i][j], 0, 0, 0);
             }
         }
+    };
+    bool deep = false;
+    if constexpr (FULL) {
+        if (p.K == 16 * kKC && p.deep) {  // the unrolled look-ahead pipeline (K = 256)
+            char* ldsp[2] = {lds[0], lds[1]};
+            deep_pipeline<BM, 3, 16, kX6Depth>(p, row0, bimg, ldsp, 1.f, compute);
+            deep = true;
+        }
+    }
+    const int nchunks = deep ? 0 : (p.K + kKC - 1) / kKC;
+    if (!deep) {
+    load_b_lds<3>(bimg, 0, lds[0] + 3 * planeA);
+    store_a_split<BM, 3>(load_a<BM, FULL>(p, row0, 0), lds[0], 1.f);
+    __syncthreads();
+    for (int c = 0; c < nchunks; ++c) {
+        const int buf = c & 1;
+        const bool more = c + 1 < nchunks;
+        AStage<BM> an;
+        if (more) {
+            load_b_lds<3>(bimg, c + 1, lds[buf ^ 1] + 3 * planeA);
+            an = load_a<BM, FULL>(p, row0, (c + 1) * kKC);
+        }
+        compute(lds[buf], lds[buf] + 3 * planeA);
         if (more) store_a_split<BM, 3>(an, lds[buf ^ 1], 1.f);
         __syncthreads();
     }
+    }  // !deep
 
     const bool full = (row0 + BM <= p.M) && (p.N == kBN);
     f32x4 colpart[4];
@@ -1241,12 +1315,9 @@ bool x6s_nontemporal() {
 // C3 (bench.py, 3 x 20 iterations each): 16x16x32 13.10 M vs 32x32x16 13.05 M env-steps/s -- on par; the
 // forward kernels gain 2-7 % per launch, the dgrad epilogue does not fit 128 registers on the 16x16 tiling
 // (acc spills in the main loop: 1.2 ms per launch) and stays on 32x32x16.
-int x6_shape() {
-    static const int v = [] {
-        const char* e = std::getenv("RSLRL_X6_SHAPE");
-        return (e && std::atoi(e) == 16) ? 16 : 32;
-    }();
-    return v;
+int x6_shape() {  // read per call (A/B measurements in one process)
+    const char* e = std::getenv("RSLRL_X6_SHAPE");
+    return (e && std::atoi(e) == 16) ? 16 : 32;
 }
 
 // Bias gradient: out[col] = sum over tiles of part[tiles][N], in two launches and a fixed order.  Pass 1:
@@ -1319,7 +1390,11 @@ bool launch_x6s(const GemmParams& p, const uint4* img, bool fullm, dim3 g, hipSt
         if (x6_shape() != 16 || (p.N & 3) || !aligned16(p.c) || !aligned16(p.bias) || p.amax_out)
             return false;  // 16-B epilogue, no amax
         const dim3 b(kThreads);
-        if (x6s_nontemporal()) {
+        const char* mw = std::getenv("RSLRL_X6S_MINW");  // tuning knob, read per call: 2 = one workgroup per CU
+        if (mw && std::atoi(mw) == 2) {
+            if (fullm) hipLaunchKernelGGL((mlp_gemm_x6s_kernel<EPI, true, 2, false>), g, b, 0, st, p, img);
+            else hipLaunchKernelGGL((mlp_gemm_x6s_kernel<EPI, false, 2, false>), g, b, 0, st, p, img);
+        } else if (x6s_nontemporal()) {
             if (fullm) hipLaunchKernelGGL((mlp_gemm_x6s_kernel<EPI, true, 4, true>), g, b, 0, st, p, img);
             else hipLaunchKernelGGL((mlp_gemm_x6s_kernel<EPI, false, 4, true>), g, b, 0, st, p, img);
         } else {

@@ -47,14 +47,23 @@ def main():
         "fwd_out12": lambda: fused_mlp.linear_fwd_out_ex(x, b, 256, im6f, X6, ax, bo, oimg, True),
         "fwd_out1": lambda: fused_mlp.linear_fwd_out_ex(x, b, 256, im6f, X6, ax, bv, vimg, True),
         "dgrad": lambda: fused_mlp.linear_dgrad_elu_ex(dz, x, im6t, X6, adz, True),
+        "fwd_noamax": lambda: fused_mlp.linear_fwd_ex(x, b, 256, True, im6f, X6, ax, False),
+        "fwd16": lambda: fused_mlp.linear_fwd_ex(x, b, 256, True, im6f, X6, ax, False),
+        "fwd16_minw2": lambda: fused_mlp.linear_fwd_ex(x, b, 256, True, im6f, X6, ax, False),
     }
+    knobs = {"fwd16": {"RSLRL_X6_SHAPE": "16"}, "fwd16_minw2": {"RSLRL_X6_SHAPE": "16", "RSLRL_X6S_MINW": "2"}}
     res = {"lib": os.environ.get("RSLRL_AMD_LIB", "default")}
     for name, fn in cases.items():
+        for k, v in knobs.get(name, {}).items():
+            os.environ[k] = v
         r = {}
-        for mask, tag in ((0, "loop1"), (0xff, "deep")):
+        masks = ((0xff, "deep"),) if os.environ.get("PROBE_DEEP_ONLY") else ((0, "loop1"), (0xff, "deep"))
+        for mask, tag in masks:
             os.environ["RSLRL_H3_DEEP"] = str(mask)
             r[tag] = t(fn)
         os.environ.pop("RSLRL_H3_DEEP")
+        for k in knobs.get(name, {}):
+            os.environ.pop(k)
         res[name] = r
     res["wgrad"] = t(lambda: fused_mlp.linear_wgrad(dz, x, X6, adz, ax))
     print(json.dumps(res))
