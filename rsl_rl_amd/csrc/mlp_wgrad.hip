@@ -302,6 +302,48 @@ __global__ __launch_bounds__(kBlock) void fold_kernel(const IN* __restrict__ par
     }
 }
 
+// One-pass fold for wide partials (NK >= 64 * kWideMinBlocks, e.g. the 256 x 256 hidden-layer weight gradient:
+// 256 slices x 65536 values): 64 columns per 256-thread block, the block's threads as 16 column quads x 16 slice
+// phases.  Thread (phase p, quad q) adds slices p, p + 16, ... of its float4 in fp64 with up to 16 loads in
+// flight (the one-quad-per-thread fold_kernel had 8 and one block per CU: 21 us for 67 MB), then the 16
+// phases are added in phase order through LDS.  Deterministic: the order depends on S alone.
+constexpr int kWideMinBlocks = 512;
+__global__ __launch_bounds__(kBlock) void fold_wide_kernel(const float* __restrict__ part, int S, int NK,
+                                                           float* __restrict__ out) {
+    __shared__ double red[16][16][4];
+    const int q = threadIdx.x & 15;
+    const int ph = threadIdx.x >> 4;
+    const int e0 = blockIdx.x * 64 + 4 * q;
+    double a[4] = {0.0, 0.0, 0.0, 0.0};
+    if (e0 < NK) {
+        const float* src = part + e0;
+        for (int s0 = ph; s0 < S; s0 += 16 * 16) {
+            float4 v[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                const int s = s0 + 16 * k;
+                v[k] = s < S ? *reinterpret_cast<const float4*>(src + static_cast<int64_t>(s) * NK)
+                             : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                a[0] += v[k].x; a[1] += v[k].y; a[2] += v[k].z; a[3] += v[k].w;
+            }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) red[ph][q][k] = a[k];
+    __syncthreads();
+    if (ph == 0 && e0 < NK) {
+        double r[4] = {red[0][q][0], red[0][q][1], red[0][q][2], red[0][q][3]};
+        for (int p2 = 1; p2 < 16; ++p2)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) r[k] += red[p2][q][k];
+        *reinterpret_cast<float4*>(out + e0) = make_float4(static_cast<float>(r[0]), static_cast<float>(r[1]),
+                                                          static_cast<float>(r[2]), static_cast<float>(r[3]));
+    }
+}
+
 // Two-stage fold when one pass would leave the chip idle (few columns, many slices -- e.g. the output
 // layer's per-tile partials: 3072 slices x 3072 columns): stage 1 sums groups of kFoldPer slices into fp64
 // [G][NK], stage 2 sums the G groups.  The order is fixed by (S, NK) alone: deterministic.
@@ -347,6 +389,11 @@ extern "C" int rslrl_fold_partials(const float* partials, int64_t S, int64_t NK,
     if (!partials || !out || S < 1 || S > INT32_MAX || NK < 4 || NK > INT32_MAX || (NK & 3)) return RSLRL_E_INVALID_ARGUMENT;
     if ((reinterpret_cast<uintptr_t>(partials) | reinterpret_cast<uintptr_t>(out)) & 15) return RSLRL_E_MISALIGNED;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (ceil_div(NK, 64) >= kWideMinBlocks) {
+        hipLaunchKernelGGL(fold_wide_kernel, dim3(static_cast<unsigned>(ceil_div(NK, 64))), dim3(kBlock), 0, st,
+                           partials, static_cast<int>(S), static_cast<int>(NK), out);
+        return launch_status();
+    }
     const unsigned cols = static_cast<unsigned>(ceil_div(NK, 256));
     const int64_t G = fold_groups(S, NK);
     if (G == 1) {

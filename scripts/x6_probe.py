@@ -1,6 +1,7 @@
-"""Probe: the x6 fused linear kernels at C3 mini-batch shapes (M = 393216), each timed with and without the
-unrolled look-ahead main loop (RSLRL_H3_DEEP bit mask, read per call) in one process.  The look-ahead depth
-is compile-time (RSLRL_X6_DEPTH): run once per library build (RSLRL_AMD_LIB selects the .so)."""
+"""Probe: the x6 fused linear kernels at C3 mini-batch shapes (M = 393216, as the x6 training path calls them: no
+amax), each timed under several per-call knobs in one process (the box-to-box clock spread makes cross-run
+comparisons of a few per cent meaningless).  PROBE_VARIANTS: JSON {tag: {ENV: value}}; default compares the
+look-ahead loop with B staged through LDS against B fragments loaded from global memory (RSLRL_X6_DIRECTB)."""
 
 import json
 import os
@@ -31,8 +32,10 @@ def main():
     M = int(os.environ.get("PROBE_M", 393216))
     torch.manual_seed(0)
     x = F.elu(torch.randn(M, 256, device=dev))
+    x48 = torch.randn(M, 48, device=dev)
     dz = torch.randn(M, 256, device=dev) * 1e-6
     w = torch.randn(256, 256, device=dev) / 16
+    w48 = torch.randn(256, 48, device=dev) / 7
     b = torch.randn(256, device=dev) * 0.1
     wo = torch.randn(12, 256, device=dev) / 16
     bo = torch.randn(12, device=dev)
@@ -40,32 +43,28 @@ def main():
     bv = torch.randn(1, device=dev)
     X6 = _lib.ARITH_X6
     oimg, vimg = fused_mlp.bimages([(wo, False, _lib.BIMAGE_LAYOUT_OUT), (wv, False, _lib.BIMAGE_LAYOUT_OUT)])
-    im6f, im6t = fused_mlp.bimages([(w, False), (w, True)])
-    ax, adz = x.abs().amax().reshape(1), dz.abs().amax().reshape(1)
+    im6f, im6t, im48 = fused_mlp.bimages([(w, False), (w, True), (w48, False)])
     cases = {
-        "fwd": lambda: fused_mlp.linear_fwd_ex(x, b, 256, True, im6f, X6, ax, True),
-        "fwd_out12": lambda: fused_mlp.linear_fwd_out_ex(x, b, 256, im6f, X6, ax, bo, oimg, True),
-        "fwd_out1": lambda: fused_mlp.linear_fwd_out_ex(x, b, 256, im6f, X6, ax, bv, vimg, True),
-        "dgrad": lambda: fused_mlp.linear_dgrad_elu_ex(dz, x, im6t, X6, adz, True),
-        "fwd_noamax": lambda: fused_mlp.linear_fwd_ex(x, b, 256, True, im6f, X6, ax, False),
-        "fwd16": lambda: fused_mlp.linear_fwd_ex(x, b, 256, True, im6f, X6, ax, False),
-        "fwd16_minw2": lambda: fused_mlp.linear_fwd_ex(x, b, 256, True, im6f, X6, ax, False),
+        "fwd48": lambda: fused_mlp.linear_fwd_ex(x48, b, 256, True, im48, X6, None, False),
+        "fwd": lambda: fused_mlp.linear_fwd_ex(x, b, 256, True, im6f, X6, None, False),
+        "fwd_out12": lambda: fused_mlp.linear_fwd_out_ex(x, b, 256, im6f, X6, None, bo, oimg, True),
+        "fwd_out1": lambda: fused_mlp.linear_fwd_out_ex(x, b, 256, im6f, X6, None, bv, vimg, True),
+        "dgrad": lambda: fused_mlp.linear_dgrad_elu_ex(dz, x, im6t, X6, None, False),
+        "wgrad": lambda: fused_mlp.linear_wgrad(dz, x, X6),
     }
-    knobs = {"fwd16": {"RSLRL_X6_SHAPE": "16"}, "fwd16_minw2": {"RSLRL_X6_SHAPE": "16", "RSLRL_X6S_MINW": "2"}}
+    variants = json.loads(os.environ.get("PROBE_VARIANTS", '{"ldsB": {}, "directB": {"RSLRL_X6_DIRECTB": "1"}}'))
     res = {"lib": os.environ.get("RSLRL_AMD_LIB", "default")}
+    rounds = int(os.environ.get("PROBE_ROUNDS", 3))
     for name, fn in cases.items():
-        for k, v in knobs.get(name, {}).items():
-            os.environ[k] = v
-        r = {}
-        masks = ((0xff, "deep"),) if os.environ.get("PROBE_DEEP_ONLY") else ((0, "loop1"), (0xff, "deep"))
-        for mask, tag in masks:
-            os.environ["RSLRL_H3_DEEP"] = str(mask)
-            r[tag] = t(fn)
-        os.environ.pop("RSLRL_H3_DEEP")
-        for k in knobs.get(name, {}):
-            os.environ.pop(k)
-        res[name] = r
-    res["wgrad"] = t(lambda: fused_mlp.linear_wgrad(dz, x, X6, adz, ax))
+        r = {tag: [] for tag in variants}
+        for _ in range(rounds):  # variants interleaved, min over rounds (clock drift)
+            for tag, env in variants.items():
+                for k, v in env.items():
+                    os.environ[k] = v
+                r[tag].append(t(fn))
+                for k in env:
+                    os.environ.pop(k)
+        res[name] = {tag: min(v) for tag, v in r.items()}
     print(json.dumps(res))
 
 
