@@ -185,7 +185,7 @@ int rslrl_clip_adam_step(const rslrl_adam_args_t* args /* host struct */, void* 
                          rslrl_stream_t stream);
 
 /* ------------------------------------------------------------------------------------------------
- * Actor/critic MLP hidden layers on fp32 MFMA -- rsl_rl/networks/mlp.py:59-114
+ * Actor/critic MLP layers on MFMA -- rsl_rl/networks/mlp.py:59-114
  * (nn.Linear + ELU(alpha=1) blocks) and their autograd backward.
  *   rslrl_linear_fwd:       y[M,N] = act(x[M,K] weight[N,K]^T + bias[N]); act 0 = identity, 1 = ELU.
  *   rslrl_linear_dgrad_elu: dz_prev[M,K] = (dz[M,Nred] weight_t[K,Nred]^T) * ELU'(h[M,K]), where h is the
@@ -269,7 +269,8 @@ int rslrl_linear_dgrad_elu_wgrad(const float* dz, int64_t M, int32_t Nred, int32
 int rslrl_linear_wgrad(const float* dz, const float* x, int64_t M, int32_t N, int32_t K, float* dw, void* workspace,
                        size_t workspace_bytes, rslrl_stream_t stream);
 
-/* "h3" arithmetic and the generic entry point of the fused linear ops.
+/* "h3" arithmetic (opt-in, REDUCED precision: 22-bit operands) and the generic entry point of the fused linear
+ * ops.  The default path (networks/fused_mlp.py, RSLRL_GEMM_MODE unset) calls it with arith = X6 only.
  * h3: every fp32 operand x is scaled by a power of two s (max |s x| < 2^15) and split into two fp16 planes
  * x0 + x1 (22 significant bits); three fp16 MFMA products a0b0 + a0b1 + a1b0 accumulate in fp32 and the
  * result is divided by the scales (exact) -- half the MFMA work of x6 at an fp32 GEMM's normwise error
