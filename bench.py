@@ -236,9 +236,17 @@ def main():
     kernels.timer.enabled = False
     # one more iteration with the MLP GEMM launches timed (kept out of the headline timing: ~470 event
     # pairs per iteration would add host overhead to the launch-bound rollout)
+    # (on one stream: the timed iteration overlaps the critic's launches with the actor's on a second stream,
+    # and per-launch event spans of concurrent launches would not add up to the iteration)
     kernels.timer.mlp_enabled = True
+    two = os.environ.get("RSLRL_TWO_STREAMS")
+    os.environ["RSLRL_TWO_STREAMS"] = "0"
     runner.learn(1)
     torch.cuda.synchronize()
+    if two is None:
+        os.environ.pop("RSLRL_TWO_STREAMS")
+    else:
+        os.environ["RSLRL_TWO_STREAMS"] = two
     kernels.timer.mlp_enabled = False
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)

@@ -26,6 +26,8 @@ same learning rates on every rank, no broadcast.
 
 from __future__ import annotations
 
+import os
+
 from itertools import chain
 
 import torch
@@ -363,7 +365,8 @@ class PPO:
                 # forward, fused loss and backward without autograd; gradients land in the arena
                 # (ppo.py:246-253 forward, :221-223 + :259-315 loss, :367-368 backward)
                 with torch.no_grad():
-                    mean, sigma, value_batch, tape = self.policy.train_forward(obs_batch)
+                    side = self._side_stream(dev)
+                    mean, sigma, value_batch, tape = self.policy.train_forward(obs_batch, side_stream=side)
                     g_mean, g_sigma = self.policy.train_grad_buffers(mean, sigma)
                     if g_sigma is None:  # shared std: d sigma reduced by the loss kernel, into the std's slot
                         g_sigma = (arena.slot(self.policy.std) if self.policy.noise_std_type == "scalar"
@@ -372,7 +375,7 @@ class PPO:
                         mean, sigma, value_batch, actions_batch, old_actions_log_prob_batch, advantages_batch,
                         target_values_batch, returns_batch, old_mu_batch, old_sigma_batch, grad_mu=g_mean,
                         grad_sigma=g_sigma, **loss_kw)
-                    self.policy.train_backward(tape, g_mean, g_sigma, g_value, sigma, arena.slot)
+                    self.policy.train_backward(tape, g_mean, g_sigma, g_value, sigma, arena.slot, side_stream=side)
                     del tape
             else:
                 # autograd path for any other policy (ppo.py:246-253, :367-372)
@@ -460,6 +463,17 @@ class PPO:
         if self.rnd:
             loss_dict["rnd"] = host[3]
         return loss_dict
+
+    def _side_stream(self, dev):
+        """A second stream for the critic's MLP launches in the manual update (RSLRL_TWO_STREAMS=0 disables it;
+        read per update)."""
+        if dev.type != "cuda" or os.environ.get("RSLRL_TWO_STREAMS", "1") == "0":
+            return None
+        s = getattr(self, "_side", None)
+        if s is None or s.device != dev:
+            s = torch.cuda.Stream(dev)
+            self._side = s
+        return s
 
     def _optimizer_takes_tensor_lr(self) -> bool:
         d = self.optimizer.defaults

@@ -143,14 +143,24 @@ class ActorCritic(nn.Module):
         lin = [m for m in mlp if isinstance(m, nn.Linear)]
         return [m.weight for m in lin], [m.bias for m in lin]
 
-    def train_forward(self, obs):
+    def train_forward(self, obs, side_stream=None):
         """The update's forward (ppo.py:246-253) without an autograd graph: returns (mean [B, A], sigma, value
         [B, 1], tape) with sigma the shared [A] std (scalar / exp(log_std)) or the per-row [B, A] std of a
-        state-dependent head (strided views of the actor output).  Call under torch.no_grad()."""
+        state-dependent head (strided views of the actor output).  Call under torch.no_grad().
+
+        side_stream: a second stream of the device for the critic's MLP -- the actor's and the critic's launch
+        chains are independent, so each fills the other's launch tails; the current stream waits for it before
+        returning (the results are the same values either way)."""
         a_obs = self.actor_obs_normalizer(self.get_actor_obs(obs))
         c_obs = self.critic_obs_normalizer(self.get_critic_obs(obs))
         a_obs = a_obs if a_obs.is_contiguous() else a_obs.contiguous()
         c_obs = c_obs if c_obs.is_contiguous() else c_obs.contiguous()
+        if side_stream is not None:
+            main = torch.cuda.current_stream(c_obs.device)
+            side_stream.wait_stream(main)
+            c_obs.record_stream(side_stream)  # kept by the critic's tape for its backward on the side stream
+            with torch.cuda.stream(side_stream):
+                value, tape_c = fused_mlp.train_forward(c_obs, *self._linears(self.critic))
         y, tape_a = fused_mlp.train_forward(a_obs, *self._linears(self.actor))
         A = self.num_actions
         if self.state_dependent_std:
@@ -159,7 +169,11 @@ class ActorCritic(nn.Module):
         else:
             mean = y
             std = self.std if self.noise_std_type == "scalar" else torch.exp(self.log_std)
-        value, tape_c = fused_mlp.train_forward(c_obs, *self._linears(self.critic))
+        if side_stream is None:
+            value, tape_c = fused_mlp.train_forward(c_obs, *self._linears(self.critic))
+        else:
+            main.wait_stream(side_stream)
+            value.record_stream(main)  # allocated on the side stream, read by the loss on this one
         self.distribution = Normal(mean, std.expand_as(mean))  # for logging, as act() leaves it
         return mean, std, value, (tape_a, tape_c, y.shape)
 
@@ -172,11 +186,12 @@ class ActorCritic(nn.Module):
             return dy[:, :A], dy[:, A:]
         return torch.empty(B, A, device=mean.device, dtype=torch.float32), None
 
-    def train_backward(self, tape, g_mean, g_sigma, g_value, std, slot):
+    def train_backward(self, tape, g_mean, g_sigma, g_value, std, slot, side_stream=None):
         """Backward of train_forward given the loss gradients w.r.t. (mean, sigma, value), written into the
         gradient slots `slot(param)` (a gradient arena).  g_sigma: for the shared std the [A] gradient w.r.t.
         sigma (for log_std it is chained through exp here); for a state-dependent head the half of the actor-output
-        gradient buffer (train_grad_buffers) the loss kernel wrote."""
+        gradient buffer (train_grad_buffers) the loss kernel wrote.  side_stream: as in train_forward (the
+        critic's backward runs there; the current stream waits for it before returning)."""
         tape_a, tape_c, y_shape = tape
         if self.state_dependent_std:
             dy = torch.as_strided(g_mean, y_shape, (y_shape[1], 1))  # the [B, 2A] buffer behind both halves
@@ -188,9 +203,21 @@ class ActorCritic(nn.Module):
                 torch.mul(g_sigma, std, out=slot(self.log_std))
             elif g_sigma.data_ptr() != slot(self.std).data_ptr():
                 slot(self.std).copy_(g_sigma)
-        for mlp, tp, d in ((self.actor, tape_a, dy), (self.critic, tape_c, g_value.reshape(-1, 1))):
+        def run(mlp, tp, d):
             ws, bs = self._linears(mlp)
             fused_mlp.train_backward(tp, d, outs=[(slot(w), slot(b)) for w, b in zip(ws, bs)])
+
+        if side_stream is None:
+            run(self.actor, tape_a, dy)
+            run(self.critic, tape_c, g_value.reshape(-1, 1))
+            return
+        main = torch.cuda.current_stream(dy.device)
+        side_stream.wait_stream(main)
+        g_value.record_stream(side_stream)  # written by the loss on this stream, read on the side stream
+        with torch.cuda.stream(side_stream):
+            run(self.critic, tape_c, g_value.reshape(-1, 1))
+        run(self.actor, tape_a, dy)
+        main.wait_stream(side_stream)
 
     def act(self, obs, **kwargs):
         obs = self.actor_obs_normalizer(self.get_actor_obs(obs))

@@ -59,6 +59,18 @@ int main() {
                "slot occupancy %.3f (2 workgroups x 256 CUs)\n",
                op, span / 100, ml / tiles / 100, mls[tiles / 10] / 100, mls[9 * tiles / 10] / 100, ep / tiles / 100,
                clk / tiles, busy / (span * 512));
+        // per-workgroup records for offline analysis: start, loop end, end (10 ns ticks from t_min), XCC, CU id
+        char fn[64];
+        snprintf(fn, sizeof(fn), "gpurun_out/tl2_op%d.csv", op);
+        if (FILE* f = fopen(fn, "w")) {
+            fprintf(f, "wg,t0,t1,t2,xcc,hwid\n");
+            for (int64_t i = 0; i < tiles; ++i) {
+                const uint64_t* s = &h[12 * i];
+                fprintf(f, "%ld,%lu,%lu,%lu,%lu,%lu\n", i, s[0] - t_min, s[1] - t_min, s[2] - t_min, s[3] >> 32,
+                        s[3] & 0xffffffffu);
+            }
+            fclose(f);
+        }
     }
     return 0;
 }
