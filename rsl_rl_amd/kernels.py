@@ -188,6 +188,17 @@ def randperm_mt19937(n: int, generator: torch.Generator | None = None, out: torc
     return out[:n]
 
 
+def randperm_mt19937_state(n: int, state: torch.Tensor, out: torch.Tensor) -> None:
+    """randperm_mt19937 on a CPU generator-state blob (torch.Generator.get_state()) instead of a generator:
+    writes the permutation into `out` (contiguous CPU int32, >= n elements) and advances `state` in place to
+    what the generator's state would be afterwards.  Touches no torch state, so it may run on a worker thread
+    (ctypes releases the GIL for the call)."""
+    if out.dtype != torch.int32 or out.device.type != "cpu" or not out.is_contiguous() or out.numel() < n:
+        raise ValueError("randperm_mt19937_state: `out` must be a contiguous CPU int32 tensor with >= n elements")
+    rc = _lib.lib().rslrl_randperm_mt19937(_ptr(state), state.numel(), n, _ptr(out))
+    _lib.check(rc, "rslrl_randperm_mt19937")
+
+
 # ------------------------------------------------------------------------------------------------
 # rollout_storage.py:168-197 -- all mini-batch fields in one launch
 # ------------------------------------------------------------------------------------------------

@@ -83,3 +83,22 @@ def test_permutation_contents_and_tail_drop(cuda_device):
     # epochs reuse the same permutation (rollout_storage.py:165 is outside the epoch loop)
     for i in range(M):
         assert torch.equal(batches[i][0]["policy"], batches[M + i][0]["policy"])
+
+
+def test_prefetched_permutation_matches_plain_draws(cuda_device):
+    """The same sequence of updates with and without interference: every permutation equals torch.randperm on
+    the generator's state at that call, and the generator's state after each update matches."""
+    T, N, M = 4, 50, 2
+    n = (T * N // M) * M
+    st = RolloutStorage("rl", N, T, {"policy": torch.zeros(N, 2)}, [3], cuda_device)
+    st.perm_generator = torch.Generator().manual_seed(21)
+    ref = torch.Generator().manual_seed(21)
+    for k in range(6):
+        if k == 3:  # reseed both between two updates: the prepared permutation is stale and must be dropped
+            st.perm_generator.manual_seed(5)
+            ref.manual_seed(5)
+        for _ in st.mini_batch_generator(M, 1):
+            pass
+        expect = torch.randperm(n, generator=ref)
+        assert torch.equal(st.last_indices.cpu().long(), expect), k
+        assert torch.equal(st.perm_generator.get_state(), ref.get_state()), k
