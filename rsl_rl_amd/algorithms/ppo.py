@@ -26,8 +26,6 @@ same learning rates on every rank, no broadcast.
 
 from __future__ import annotations
 
-import os
-
 from itertools import chain
 
 import torch
@@ -36,6 +34,7 @@ import torch.optim as optim
 
 from .. import kernels
 from ..modules import ActorCritic
+from ..networks import fused_mlp
 from ..modules.rnd import RandomNetworkDistillation
 from ..storage import RolloutStorage
 from ..utils import string_to_callable
@@ -465,15 +464,9 @@ class PPO:
         return loss_dict
 
     def _side_stream(self, dev):
-        """A second stream for the critic's MLP launches in the manual update (RSLRL_TWO_STREAMS=0 disables it;
-        read per update)."""
-        if dev.type != "cuda" or os.environ.get("RSLRL_TWO_STREAMS", "1") == "0":
-            return None
-        s = getattr(self, "_side", None)
-        if s is None or s.device != dev:
-            s = torch.cuda.Stream(dev)
-            self._side = s
-        return s
+        """A second stream for the critic's MLP launches in the manual update (networks/fused_mlp.side_stream;
+        opt-in: RSLRL_TWO_STREAMS=1, read per update)."""
+        return fused_mlp.side_stream(dev)
 
     def _optimizer_takes_tensor_lr(self) -> bool:
         d = self.optimizer.defaults

@@ -606,6 +606,22 @@ def _unflatten(mlp, y):
     return y
 
 
+_side_streams: dict = {}
+
+
+def side_stream(device):
+    """A second stream of `device` for independent launches, or None.  Opt-in (RSLRL_TWO_STREAMS=1, read per call):
+    the critic's launches beside the actor's measured equal to one stream within run-to-run noise (14.74 / 14.56 M
+    vs 14.68 / 14.65 M env-steps/s, alternating 30-iteration benches on one box)."""
+    if device.type != "cuda" or os.environ.get("RSLRL_TWO_STREAMS", "0") != "1":
+        return None
+    s = _side_streams.get(device)
+    if s is None:
+        s = torch.cuda.Stream(device)
+        _side_streams[device] = s
+    return s
+
+
 def fused_mlp_forward_pair(mlp_a: nn.Sequential, x_a: torch.Tensor, mlp_b: nn.Sequential, x_b: torch.Tensor):
     """Inference forward of two MLPs (the actor and the critic of the rollout) with their same-shape hidden
     layers batched into one launch each (rslrl_linear_gemm_pair); identical results to two fused_mlp_forward
@@ -639,13 +655,28 @@ def fused_mlp_forward_pair(mlp_a: nn.Sequential, x_a: torch.Tensor, mlp_b: nn.Se
             h, amax = linear_fwd_pair(h, [bs[0][l], bs[1][l]], ws[0][l].shape[0], True, [imgs[0][0][l], imgs[1][0][l]],
                                       arith(l), amax, [want, want])
             continue
-        for i in range(2):  # the output layer's fused launches differ per network (output width)
-            if last_fused[i]:
-                h[i], y[i] = linear_fwd_out_ex(h[i], bs[i][l], ws[i][l].shape[0], imgs[i][0][l], arith(l), amax[i],
-                                               bs[i][-1], imgs[i][2], store_h=False)
-            else:
-                h[i], amax[i] = linear_fwd_ex(h[i], bs[i][l], ws[i][l].shape[0], True, imgs[i][0][l], arith(l),
-                                              amax[i], want)
+        # the output layer's fused launches differ per network (output width): the second network's runs on a
+        # side stream beside the first's, so the two launches fill each other's tails
+        side = side_stream(h[1].device)
+        main = torch.cuda.current_stream(h[1].device) if side is not None else None
+        for i in range(2):
+            ctx = contextlib.nullcontext()
+            if side is not None and i == 1:
+                side.wait_stream(main)
+                h[1].record_stream(side)
+                ctx = torch.cuda.stream(side)
+            with ctx:
+                if last_fused[i]:
+                    h[i], y[i] = linear_fwd_out_ex(h[i], bs[i][l], ws[i][l].shape[0], imgs[i][0][l], arith(l),
+                                                   amax[i], bs[i][-1], imgs[i][2], store_h=False)
+                else:
+                    h[i], amax[i] = linear_fwd_ex(h[i], bs[i][l], ws[i][l].shape[0], True, imgs[i][0][l], arith(l),
+                                                  amax[i], want)
+        if side is not None:
+            main.wait_stream(side)
+            for t in (h[1], y[1], amax[1]):
+                if t is not None:
+                    t.record_stream(main)
     out = []
     for i, mlp in enumerate((mlp_a, mlp_b)):
         yi = y[i] if y[i] is not None else F.linear(h[i], ws[i][-1], bs[i][-1])

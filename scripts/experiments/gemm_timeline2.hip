@@ -32,10 +32,21 @@ int main() {
     uint64_t* st;
     hipMalloc(&st, tiles * 2 * 6 * 8);
     hipMemcpyToSymbol(HIP_SYMBOL(rslrl::g_stamps), &st, sizeof(st));
-    for (int op : {RSLRL_LINEAR_FWD_ELU, RSLRL_LINEAR_DGRAD_ELU}) {
+    float *wo, *bo, *yo;
+    void* oimg;
+    hipMalloc(&wo, 12 * K * 4); hipMalloc(&bo, 12 * 4); hipMalloc(&yo, M * 12 * 4);
+    fill(wo, 12 * K, 0.06f, 4); hipMemset(bo, 0, 12 * 4);
+    hipMalloc(&oimg, rslrl_linear_out_image_bytes());
+    for (int op : {RSLRL_LINEAR_FWD_ELU, RSLRL_LINEAR_DGRAD_ELU, 100 + 12, 100 + 1}) {
         rslrl_linear_args_t a{};
         a.op = op; a.arith = RSLRL_ARITH_X6; a.a = x; a.M = M; a.K = K; a.N = N; a.bimage = img;
         a.bias = b; a.c = y; a.h = hh; a.colsum_partials = cs;
+        if (op > 100) {  // fused last hidden + output layer with op - 100 outputs
+            const int nout = op - 100;
+            rslrl_bimage_desc_t d{wo, oimg, nout, K, 0, RSLRL_BIMAGE_LAYOUT_OUT};
+            rslrl_linear_prepare_bimages(&d, 1, nullptr);
+            a.op = RSLRL_LINEAR_FWD_OUT; a.out_image = oimg; a.out_bias = bo; a.y = yo; a.nout = nout;
+        }
         for (int i = 0; i < 20; ++i) rslrl_linear_gemm(&a, nullptr);
         hipDeviceSynchronize();
         std::vector<uint64_t> h(tiles * 2 * 6);

@@ -187,3 +187,23 @@ def test_update_c2_width_matches_reference(golden_meta, cuda_device):
         d = (finals["x6"][k] - finals["f32"][k]).norm().item()
         print(k, f"||x6 - f32|| / moved = {d / moved:.2e}")
         assert d <= 1e-3 * moved, (k, d / moved)
+
+
+def test_update_two_streams_bit_identical(golden_meta, cuda_device, monkeypatch):
+    """The opt-in side stream for the critic's MLP launches (RSLRL_TWO_STREAMS=1, update and rollout forward)
+    changes only where the launches run, not what they compute: the C2-shape update ends with bit-identical
+    parameters, learning-rate trace and loss statistics either way."""
+    from update_fixtures import build_update, run_recorded_update
+
+    m = golden_meta["update_c2"]
+    z = np.load(golden_path("update_c2.npz"))
+    res = {}
+    for two in ("0", "1"):
+        monkeypatch.setenv("RSLRL_TWO_STREAMS", two)
+        alg, pol = build_update(z, "", m, m, cuda_device)
+        loss, lr_trace = run_recorded_update(alg)
+        torch.cuda.synchronize()
+        res[two] = (loss, lr_trace, {k: v.detach().cpu().clone() for k, v in pol.state_dict().items()})
+    assert res["0"][0] == res["1"][0] and res["0"][1] == res["1"][1]
+    for k, v in res["0"][2].items():
+        assert torch.equal(v, res["1"][2][k]), k
