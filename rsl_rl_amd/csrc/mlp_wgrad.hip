@@ -53,7 +53,10 @@ __device__ __forceinline__ int swz(int m, int col) {  // byte offset of (m, col)
 }
 
 // stage one operand chunk: rows m0.. m0+15 (global rows < m_end valid), columns < ncols valid
-template <int COLS, bool FULL>
+// MASKC (full tiles whose operand has fewer than COLS columns, e.g. the first layer's 48 inputs on 64-row tiles):
+// columns >= ncols load a clamped in-row address unconditionally and are zeroed by a select, so the load stream
+// keeps no control flow (the look-ahead's waitcnt counting needs that)
+template <int COLS, bool FULL, bool MASKC = false>
 __device__ __forceinline__ void load_tile(const float* __restrict__ src, int ld, int64_t m0, int64_t m_end,
                                           int ncols, float4 (&v)[(kMC * COLS / 4 + kThreadsW - 1) / kThreadsW]) {
     constexpr int units = kMC * COLS / 4;
@@ -64,7 +67,11 @@ __device__ __forceinline__ void load_tile(const float* __restrict__ src, int ld,
         const int m = u / (COLS / 4);
         const int c = 4 * (u % (COLS / 4));
         const int64_t row = m0 + m;
-        if constexpr (FULL) {
+        if constexpr (FULL && MASKC) {
+            const bool ok = c < ncols;
+            const float4 t = *reinterpret_cast<const float4*>(src + row * ld + (ok ? c : 0));
+            v[i] = ((units % kThreadsW == 0 || u < units) && ok) ? t : make_float4(0.f, 0.f, 0.f, 0.f);
+        } else if constexpr (FULL) {
             v[i] = (units % kThreadsW == 0 || u < units)
                        ? *reinterpret_cast<const float4*>(src + row * ld + c) : make_float4(0.f, 0.f, 0.f, 0.f);
         } else {
@@ -116,7 +123,7 @@ __device__ __forceinline__ F read_frag_tr(const char* __restrict__ plane, int cb
 
 // TN = rows of dW per workgroup (256: waves 2 (n) x 4 (k), wave tile 128 x 64; 64: waves 2 x 4, 32 x 64;
 // 32: waves 1 x 8, 32 x 32)
-template <int TN, bool FULL, int PL = 3>
+template <int TN, bool FULL, int PL = 3, bool MASKN = false>
 __global__ __launch_bounds__(kThreadsW, 2) void wgrad_x6_kernel(WgradParams p) {
     using Frag = typename Arith<PL>::frag;
     constexpr int WN = TN == 32 ? 1 : 2;
@@ -171,7 +178,7 @@ __global__ __launch_bounds__(kThreadsW, 2) void wgrad_x6_kernel(WgradParams p) {
         float4 ra[D][perA], rb[D][perB];
         {
             float4 va[perA], vb[perB];
-            load_tile<TN, true>(p.dz, p.N, m_begin, m_end, p.N, va);
+            load_tile<TN, true, MASKN>(p.dz, p.N, m_begin, m_end, p.N, va);
             load_tile<kTK, true>(p.x, p.K, m_begin, m_end, p.K, vb);
             store_tile<TN, PL>(va, lds[0], sa);
             store_tile<kTK, PL>(vb, lds[0] + PL * planeA, sb);
@@ -181,7 +188,7 @@ __global__ __launch_bounds__(kThreadsW, 2) void wgrad_x6_kernel(WgradParams p) {
         auto chunk_row = [&](int c) { return m_begin + static_cast<int64_t>(c < nchunks ? c : nchunks - 1) * kMC; };
 #pragma unroll
         for (int d = 1; d <= D; ++d) {
-            load_tile<TN, true>(p.dz, p.N, chunk_row(d), m_end, p.N, ra[d % D]);
+            load_tile<TN, true, MASKN>(p.dz, p.N, chunk_row(d), m_end, p.N, ra[d % D]);
             load_tile<kTK, true>(p.x, p.K, chunk_row(d), m_end, p.K, rb[d % D]);
         }
         __syncthreads();
@@ -194,7 +201,7 @@ __global__ __launch_bounds__(kThreadsW, 2) void wgrad_x6_kernel(WgradParams p) {
             __builtin_amdgcn_sched_barrier(0);  // the splits below stay behind this chunk's MFMAs
             store_tile<TN, PL>(ra[s], lds[(u + 1) & 1], sa);
             store_tile<kTK, PL>(rb[s], lds[(u + 1) & 1] + PL * planeA, sb);
-            load_tile<TN, true>(p.dz, p.N, chunk_row(c + 1 + D), m_end, p.N, ra[s]);
+            load_tile<TN, true, MASKN>(p.dz, p.N, chunk_row(c + 1 + D), m_end, p.N, ra[s]);
             load_tile<kTK, true>(p.x, p.K, chunk_row(c + 1 + D), m_end, p.K, rb[s]);
             // only the LDS writes must retire before the barrier (not the look-ahead loads)
             asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -435,6 +442,7 @@ extern "C" int rslrl_linear_wgrad_ex(const float* dz, const float* dz_amax, cons
     auto go = [&](auto tn, auto pl) {
         constexpr int TN = decltype(tn)::value, PL = decltype(pl)::value;
         if (full && N == TN) hipLaunchKernelGGL((wgrad_x6_kernel<TN, true, PL>), g, b, 0, st, p);
+        else if (full && N < TN) hipLaunchKernelGGL((wgrad_x6_kernel<TN, true, PL, true>), g, b, 0, st, p);
         else hipLaunchKernelGGL((wgrad_x6_kernel<TN, false, PL>), g, b, 0, st, p);
     };
     using I32 = std::integral_constant<int, 32>;

@@ -51,6 +51,7 @@ def main():
         "fwd_out1": lambda: fused_mlp.linear_fwd_out_ex(x, b, 256, im6f, X6, None, bv, vimg, True),
         "dgrad": lambda: fused_mlp.linear_dgrad_elu_ex(dz, x, im6t, X6, None, False),
         "wgrad": lambda: fused_mlp.linear_wgrad(dz, x, X6),
+        "wgrad48": lambda: fused_mlp.linear_wgrad(x48, dz, X6),
     }
     variants = json.loads(os.environ.get("PROBE_VARIANTS", '{"ldsB": {}, "directB": {"RSLRL_X6_DIRECTB": "1"}}'))
     res = {"lib": os.environ.get("RSLRL_AMD_LIB", "default")}
