@@ -31,7 +31,7 @@ extern "C" {
 
 typedef struct ihipStream_t* rslrl_stream_t; /* == hipStream_t */
 
-#define RSLRL_ABI_VERSION 4
+#define RSLRL_ABI_VERSION 5
 
 enum {
     RSLRL_OK = 0,
@@ -281,7 +281,7 @@ int rslrl_linear_wgrad(const float* dz, const float* x, int64_t M, int32_t N, in
  *   op                         A (a, [M, K])  output                      B image (rows = N, depth = K)
  *   RSLRL_LINEAR_FWD[_ELU]     x              c = act(x W^T + bias) [M,N]  W [N, K]
  *   RSLRL_LINEAR_DGRAD_ELU     dz             c = (dz W) * ELU'(h) [M,N]   W^T (transposed image of W [K, N])
- *                                             + colsum_partials [rslrl_linear_tiles(M), N]
+ *                                             + colsum_partials [rslrl_linear_tiles(M), N] (optional: NULL skips)
  *   RSLRL_LINEAR_DGRAD_ELU_WGRAD  (x6 only)   as rslrl_linear_dgrad_elu_wgrad (K = Nred <= 16)
  *   RSLRL_LINEAR_FWD_OUT       x              c = h (nullable), y = h W_out^T + out_bias (rslrl_linear_fwd_out)
  * amax_out (optional, not for FWD_OUT): max |c| over the output, published by the launch's last workgroup;
@@ -326,6 +326,15 @@ int rslrl_linear_gemm_pair(const rslrl_linear_args_t* a0, const rslrl_linear_arg
 int rslrl_linear_wgrad_ex(const float* dz, const float* dz_amax, const float* x, const float* x_amax, int64_t M,
                           int32_t N, int32_t K, int32_t arith, float* dw, void* workspace, size_t workspace_bytes,
                           rslrl_stream_t stream);
+/* rslrl_linear_wgrad_ex plus the bias gradient of the layer from the same staged rows: bias_side 1 -> the column
+ * sums of dz (N values; N > 64), 2 -> of x (K values; the first layer's (x^T dz)^T form), 0 -> none.  dw_db
+ * receives dw [N, K] followed by the column sums -- a Linear's weight and bias gradients when they are adjacent
+ * (a gradient arena).  Replaces rslrl_linear_dgrad_elu's colsum partials + rslrl_column_sum_fold for that layer
+ * (pass colsum_partials = NULL there).  Workspace: rslrl_linear_wgrad_bias_workspace_bytes. */
+size_t rslrl_linear_wgrad_bias_workspace_bytes(int64_t M, int32_t N, int32_t K, int32_t bias_side);
+int rslrl_linear_wgrad_bias(const float* dz, const float* dz_amax, const float* x, const float* x_amax, int64_t M,
+                            int32_t N, int32_t K, int32_t arith, int32_t bias_side, float* dw_db, void* workspace,
+                            size_t workspace_bytes, rslrl_stream_t stream);
 
 /* ------------------------------------------------------------------------------------------------
  * Rollout-side record: for environment step t, in one launch,

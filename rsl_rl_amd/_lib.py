@@ -19,7 +19,7 @@ import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 # RSLRL_AMD_LIB: an alternative in-tree build of the same library (A/B kernel experiments)
 LIB_PATH = os.environ.get("RSLRL_AMD_LIB") or os.path.join(LIB_DIR, "librslrl_amd.so")
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 # symbols declared in include/rslrl_amd.h (tests/test_capi.py checks the header against this list)
 EXPORTED_SYMBOLS = (
@@ -58,6 +58,8 @@ EXPORTED_SYMBOLS = (
     "rslrl_linear_gemm",
     "rslrl_linear_gemm_pair",
     "rslrl_linear_wgrad_ex",
+    "rslrl_linear_wgrad_bias_workspace_bytes",
+    "rslrl_linear_wgrad_bias",
     "rslrl_ppo_update_tail",
     "rslrl_adam_workspace_bytes",
     "rslrl_clip_adam_step",
@@ -296,6 +298,10 @@ def _declare(L):
     L.rslrl_ppo_update_tail.argtypes = [P, P, P, P, I32, F, F, P, P]
     L.rslrl_linear_wgrad_ex.restype = ctypes.c_int
     L.rslrl_linear_wgrad_ex.argtypes = [P, P, P, P, I64, I32, I32, I32, P, P, SZ, P]
+    L.rslrl_linear_wgrad_bias_workspace_bytes.restype = SZ
+    L.rslrl_linear_wgrad_bias_workspace_bytes.argtypes = [I64, I32, I32, I32]
+    L.rslrl_linear_wgrad_bias.restype = ctypes.c_int
+    L.rslrl_linear_wgrad_bias.argtypes = [P, P, P, P, I64, I32, I32, I32, I32, P, P, SZ, P]
 
 
 def lib():

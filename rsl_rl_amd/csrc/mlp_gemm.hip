@@ -1078,7 +1078,8 @@ __device__ __forceinline__ void mlp_gemm_x6_body(GemmParams p, const uint4* __re
         }
     }
 #endif
-    if constexpr (EPI == kEpiEluGrad || EPI == kEpiEluGradWgrad) {
+    // (colsum == nullptr: the previous layer's bias gradient comes from its weight-gradient kernel instead)
+    if (EPI == kEpiEluGrad || EPI == kEpiEluGradWgrad) if (p.colsum) {
         // column sums over the tile's 128 rows -> colsum[tile][col]: lanes l and l + 32 hold the two row
         // halves of a column, the two wave rows (wm) are combined in a fixed order through LDS
         float s[2];
@@ -1559,7 +1560,7 @@ __global__ __launch_bounds__(kOutBwdThreads, NR >= 16 ? 3 : 4) void out_bwd_valu
 #pragma unroll
         for (int g = 1; g < RG; ++g) v += red[g][o][c];
         if (o < nred) wp[static_cast<int64_t>(o) * p.N + c] = v;
-        else if (o == NR) p.colsum[static_cast<int64_t>(blockIdx.x) * p.N + c] = v;
+        else if (o == NR && p.colsum) p.colsum[static_cast<int64_t>(blockIdx.x) * p.N + c] = v;
     }
     if (threadIdx.x < nred) {
         float v = dzsum[0][threadIdx.x];
@@ -1815,7 +1816,7 @@ extern "C" int rslrl_linear_gemm(const rslrl_linear_args_t* a, rslrl_stream_t st
                 return h3 ? launch<kEpiBiasElu, 2>(p, a->bimage, st) : launch<kEpiBiasElu, 3>(p, a->bimage, st);
             return h3 ? launch<kEpiBias, 2>(p, a->bimage, st) : launch<kEpiBias, 3>(p, a->bimage, st);
         case RSLRL_LINEAR_DGRAD_ELU:
-            if (!a->h || !a->c || !a->colsum_partials) return RSLRL_E_INVALID_ARGUMENT;
+            if (!a->h || !a->c) return RSLRL_E_INVALID_ARGUMENT;  // colsum_partials optional
             p.h = a->h;
             p.c = a->c;
             p.colsum = a->colsum_partials;
@@ -1823,7 +1824,7 @@ extern "C" int rslrl_linear_gemm(const rslrl_linear_args_t* a, rslrl_stream_t st
             return h3 ? launch<kEpiEluGrad, 2>(p, a->bimage, st) : launch<kEpiEluGrad, 3>(p, a->bimage, st);
         case RSLRL_LINEAR_DGRAD_ELU_WGRAD:
             if (h3) return RSLRL_E_UNSUPPORTED;
-            if (a->K > kMaxWgradRows || !a->h || !a->c || !a->colsum_partials || !a->wgrad_partials)
+            if (a->K > kMaxWgradRows || !a->h || !a->c || !a->wgrad_partials)  // colsum_partials optional
                 return RSLRL_E_INVALID_ARGUMENT;
             p.h = a->h;
             p.c = a->c;

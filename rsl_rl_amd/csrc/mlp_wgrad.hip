@@ -123,8 +123,13 @@ __device__ __forceinline__ F read_frag_tr(const char* __restrict__ plane, int cb
 
 // TN = rows of dW per workgroup (256: waves 2 (n) x 4 (k), wave tile 128 x 64; 64: waves 2 x 4, 32 x 64;
 // 32: waves 1 x 8, 32 x 32)
-template <int TN, bool FULL, int PL = 3, bool MASKN = false>
-__global__ __launch_bounds__(kThreadsW, 2) void wgrad_x6_kernel(WgradParams p) {
+// CS: also the column sums of one operand -- the bias gradient of the layer (1: of dz, the TN-row side, TN = 256;
+// 2: of x, the 256-column side) -- accumulated in fp32 from the staged registers (every thread's float4 units
+// share their 4 columns), folded over the 8 threads of a column quad through LDS in a fixed order and written
+// after the tile as the slice's extra partial row: part[s] = [dW (N x K) | colsum (N or K)].
+template <int TN, bool FULL, int PL = 3, bool MASKN = false, int CS = 0>
+__global__ __launch_bounds__(kThreadsW, TN <= 64 ? 4 : 2) void wgrad_x6_kernel(WgradParams p) {  // <= 64: 2 per CU
+    static_assert(CS != 1 || TN == kTK, "column sums of the dz side need 256-row tiles");
     using Frag = typename Arith<PL>::frag;
     constexpr int WN = TN == 32 ? 1 : 2;
     constexpr int WK = 8 / WN;
@@ -151,6 +156,20 @@ __global__ __launch_bounds__(kThreadsW, 2) void wgrad_x6_kernel(WgradParams p) {
     for (int i = 0; i < I; ++i)
 #pragma unroll
         for (int j = 0; j < J; ++j) acc[i][j] = f32x16{};
+    float4 csum = make_float4(0.f, 0.f, 0.f, 0.f);  // CS: this thread's 4 columns
+    // sum the staged chunk of the CS operand (raw values, before any h3 scaling)
+    auto accum_a = [&](const float4 (&v)[perA]) {
+        if constexpr (CS == 1) {
+#pragma unroll
+            for (int i = 0; i < perA; ++i) { csum.x += v[i].x; csum.y += v[i].y; csum.z += v[i].z; csum.w += v[i].w; }
+        }
+    };
+    auto accum_b = [&](const float4 (&v)[perB]) {
+        if constexpr (CS == 2) {
+#pragma unroll
+            for (int i = 0; i < perB; ++i) { csum.x += v[i].x; csum.y += v[i].y; csum.z += v[i].z; csum.w += v[i].w; }
+        }
+    };
 
     auto compute = [&](const char* a_img) {
         const char* b_img = a_img + PL * planeA;
@@ -180,6 +199,8 @@ __global__ __launch_bounds__(kThreadsW, 2) void wgrad_x6_kernel(WgradParams p) {
             float4 va[perA], vb[perB];
             load_tile<TN, true, MASKN>(p.dz, p.N, m_begin, m_end, p.N, va);
             load_tile<kTK, true>(p.x, p.K, m_begin, m_end, p.K, vb);
+            accum_a(va);
+            accum_b(vb);
             store_tile<TN, PL>(va, lds[0], sa);
             store_tile<kTK, PL>(vb, lds[0] + PL * planeA, sb);
         }
@@ -199,6 +220,8 @@ __global__ __launch_bounds__(kThreadsW, 2) void wgrad_x6_kernel(WgradParams p) {
             constexpr int s = (u + 1) % D;
             compute(lds[u & 1]);
             __builtin_amdgcn_sched_barrier(0);  // the splits below stay behind this chunk's MFMAs
+            accum_a(ra[s]);  // chunk c + 1: every real chunk is stored (and summed) exactly once
+            accum_b(rb[s]);
             store_tile<TN, PL>(ra[s], lds[(u + 1) & 1], sa);
             store_tile<kTK, PL>(rb[s], lds[(u + 1) & 1] + PL * planeA, sb);
             load_tile<TN, true, MASKN>(p.dz, p.N, chunk_row(c + 1 + D), m_end, p.N, ra[s]);
@@ -219,6 +242,8 @@ __global__ __launch_bounds__(kThreadsW, 2) void wgrad_x6_kernel(WgradParams p) {
     if (nchunks > 0) {
         load_tile<TN, FULL>(p.dz, p.N, m_begin, m_end, p.N, va);
         load_tile<kTK, FULL>(p.x, p.K, m_begin, m_end, p.K, vb);
+        accum_a(va);
+        accum_b(vb);
         store_tile<TN, PL>(va, lds[0], sa);
         store_tile<kTK, PL>(vb, lds[0] + PL * planeA, sb);
     }
@@ -233,6 +258,8 @@ __global__ __launch_bounds__(kThreadsW, 2) void wgrad_x6_kernel(WgradParams p) {
         }
         compute(lds[buf]);
         if (more) {
+            accum_a(va);
+            accum_b(vb);
             store_tile<TN, PL>(va, lds[buf ^ 1], sa);
             store_tile<kTK, PL>(vb, lds[buf ^ 1] + PL * planeA, sb);
         }
@@ -245,7 +272,32 @@ __global__ __launch_bounds__(kThreadsW, 2) void wgrad_x6_kernel(WgradParams p) {
     const int l32 = lane & 31;
     const int h = lane >> 5;
     const float unscale = PL == 2 ? (1.f / sa) * (1.f / sb) : 1.f;  // exact: powers of two
-    float* out = p.part + static_cast<int64_t>(blockIdx.x) * p.N * p.K;
+    const int E = CS == 1 ? p.N : (CS == 2 ? p.K : 0);
+    float* out = p.part + static_cast<int64_t>(blockIdx.x) * (static_cast<int64_t>(p.N) * p.K + E);
+    if constexpr (CS != 0) {
+        // threads t, t + 64, ..., t + 448 hold columns 4 (t & 63) .. + 3 of different rows: fixed-order fold
+        float* red = reinterpret_cast<float*>(&lds[0][0]);  // [8][256]
+        __syncthreads();  // the last chunk's fragments have been read
+        reinterpret_cast<float4*>(red)[threadIdx.x] = csum;
+        __syncthreads();
+        if (threadIdx.x < 64) {
+            float4 t = reinterpret_cast<const float4*>(red)[threadIdx.x];
+#pragma unroll
+            for (int g = 1; g < 8; ++g) {
+                const float4 v = reinterpret_cast<const float4*>(red)[64 * g + threadIdx.x];
+                t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
+            }
+            const int col = 4 * threadIdx.x;
+            float* dst = out + static_cast<int64_t>(p.N) * p.K;
+            if (col + 3 < E) {
+                *reinterpret_cast<float4*>(dst + col) = t;
+            } else {
+                const float tv[4] = {t.x, t.y, t.z, t.w};
+                for (int e = 0; e < 4; ++e)
+                    if (col + e < E) dst[col + e] = tv[e];
+            }
+        }
+    }
 #pragma unroll
     for (int i = 0; i < I; ++i)
 #pragma unroll
@@ -384,11 +436,22 @@ extern "C" size_t rslrl_fold_partials_workspace_bytes(int64_t S, int64_t NK) {
 }
 
 // workspace: the [S][N][K] partials, then the fold's fp64 group sums
-extern "C" size_t rslrl_linear_wgrad_workspace_bytes(int64_t M, int32_t N, int32_t K) {
-    if (M < 1 || N < 1 || K < 1) return 0;
+namespace rslrl {
+namespace {
+// extra values per partial row for a column-sum side (0 none, 1 dz: N, 2 x: K)
+int64_t colsum_len(int side, int32_t N, int32_t K) { return side == 1 ? N : (side == 2 ? K : 0); }
+}  // namespace
+}  // namespace rslrl
+
+extern "C" size_t rslrl_linear_wgrad_bias_workspace_bytes(int64_t M, int32_t N, int32_t K, int32_t bias_side) {
+    if (M < 1 || N < 1 || K < 1 || bias_side < 0 || bias_side > 2) return 0;
     const int64_t S = ceil_div(M, wgrad_rows_per(M, N));
-    const size_t part = static_cast<size_t>(S) * N * K * sizeof(float);
-    return part + rslrl_fold_partials_workspace_bytes(S, static_cast<int64_t>(N) * K);
+    const int64_t NKE = static_cast<int64_t>(N) * K + colsum_len(bias_side, N, K);
+    return static_cast<size_t>(S) * NKE * sizeof(float) + rslrl_fold_partials_workspace_bytes(S, NKE);
+}
+
+extern "C" size_t rslrl_linear_wgrad_workspace_bytes(int64_t M, int32_t N, int32_t K) {
+    return rslrl_linear_wgrad_bias_workspace_bytes(M, N, K, 0);
 }
 
 extern "C" int rslrl_fold_partials(const float* partials, int64_t S, int64_t NK, float* out, void* workspace,
@@ -421,42 +484,62 @@ extern "C" int rslrl_fold_partials(const float* partials, int64_t S, int64_t NK,
     return launch_status();
 }
 
-extern "C" int rslrl_linear_wgrad_ex(const float* dz, const float* dz_amax, const float* x, const float* x_amax,
-                                     int64_t M, int32_t N, int32_t K, int32_t arith, float* dw, void* workspace,
-                                     size_t workspace_bytes, rslrl_stream_t stream) {
+extern "C" int rslrl_linear_wgrad_bias(const float* dz, const float* dz_amax, const float* x, const float* x_amax,
+                                       int64_t M, int32_t N, int32_t K, int32_t arith, int32_t bias_side, float* dw_db,
+                                       void* workspace, size_t workspace_bytes, rslrl_stream_t stream) {
     if (M < 1 || N < 1 || K < 1 || N > 256 || K > kTK || (N & 3) || (K & 3)) return RSLRL_E_INVALID_ARGUMENT;
-    if (!dz || !x || !dw || !workspace) return RSLRL_E_INVALID_ARGUMENT;
+    if (bias_side < 0 || bias_side > 2 || (bias_side == 1 && N <= 64)) return RSLRL_E_INVALID_ARGUMENT;
+    if (!dz || !x || !dw_db || !workspace) return RSLRL_E_INVALID_ARGUMENT;
     const bool h3 = arith == RSLRL_ARITH_H3;
     if (!h3 && arith != RSLRL_ARITH_X6) return RSLRL_E_INVALID_ARGUMENT;
     if (h3 && (!dz_amax || !x_amax)) return RSLRL_E_INVALID_ARGUMENT;
     if ((reinterpret_cast<uintptr_t>(dz) | reinterpret_cast<uintptr_t>(x)) & 15) return RSLRL_E_MISALIGNED;
     const int64_t rows_per = wgrad_rows_per(M, N);
     const int64_t S = ceil_div(M, rows_per);
-    const size_t part_bytes = static_cast<size_t>(S) * N * K * sizeof(float);  // 16-byte multiple (N, K % 4)
-    if (workspace_bytes < rslrl_linear_wgrad_workspace_bytes(M, N, K)) return RSLRL_E_WORKSPACE_TOO_SMALL;
+    const int64_t NKE = static_cast<int64_t>(N) * K + colsum_len(bias_side, N, K);
+    const size_t part_bytes = static_cast<size_t>(S) * NKE * sizeof(float);  // 16-byte multiple (N, K % 4)
+    if (workspace_bytes < rslrl_linear_wgrad_bias_workspace_bytes(M, N, K, bias_side)) return RSLRL_E_WORKSPACE_TOO_SMALL;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     WgradParams p{dz, x, static_cast<float*>(workspace), M, rows_per, N, K, dz_amax, x_amax};
-    // full tiles: whole chunks, an even count of them >= 2 (the look-ahead loop), K == kTK (and N == TN, per branch)
+    // full tiles: whole chunks, an even count of them >= 2 (the look-ahead loop), K == kTK (and N <= TN, per branch)
     bool full = (M % rows_per == 0) && K == kTK && (rows_per / kMC) % kWgradDepth == 0;
     const dim3 g(static_cast<unsigned>(S)), b(kThreadsW);
-    auto go = [&](auto tn, auto pl) {
-        constexpr int TN = decltype(tn)::value, PL = decltype(pl)::value;
-        if (full && N == TN) hipLaunchKernelGGL((wgrad_x6_kernel<TN, true, PL>), g, b, 0, st, p);
-        else if (full && N < TN) hipLaunchKernelGGL((wgrad_x6_kernel<TN, true, PL, true>), g, b, 0, st, p);
-        else hipLaunchKernelGGL((wgrad_x6_kernel<TN, false, PL>), g, b, 0, st, p);
+    auto go = [&](auto tn, auto pl, auto cs) {
+        constexpr int TN = decltype(tn)::value, PL = decltype(pl)::value, CS = decltype(cs)::value;
+        if constexpr (CS == 1 && TN != kTK) {
+            return;  // excluded above (N > 64 selects 256-row tiles)
+        } else {
+            if (full && N == TN) hipLaunchKernelGGL((wgrad_x6_kernel<TN, true, PL, false, CS>), g, b, 0, st, p);
+            else if (full && N < TN) hipLaunchKernelGGL((wgrad_x6_kernel<TN, true, PL, true, CS>), g, b, 0, st, p);
+            else hipLaunchKernelGGL((wgrad_x6_kernel<TN, false, PL, false, CS>), g, b, 0, st, p);
+        }
+    };
+    auto by_side = [&](auto tn, auto pl) {
+        using C0 = std::integral_constant<int, 0>;
+        using C1 = std::integral_constant<int, 1>;
+        using C2 = std::integral_constant<int, 2>;
+        if (bias_side == 1) go(tn, pl, C1{});
+        else if (bias_side == 2) go(tn, pl, C2{});
+        else go(tn, pl, C0{});
     };
     using I32 = std::integral_constant<int, 32>;
     using I64 = std::integral_constant<int, 64>;
     using I256 = std::integral_constant<int, 256>;
     using P2 = std::integral_constant<int, 2>;
     using P3 = std::integral_constant<int, 3>;
-    if (N <= 32) h3 ? go(I32{}, P2{}) : go(I32{}, P3{});
-    else if (N <= 64) h3 ? go(I64{}, P2{}) : go(I64{}, P3{});
-    else h3 ? go(I256{}, P2{}) : go(I256{}, P3{});
+    if (N <= 32) h3 ? by_side(I32{}, P2{}) : by_side(I32{}, P3{});
+    else if (N <= 64) h3 ? by_side(I64{}, P2{}) : by_side(I64{}, P3{});
+    else h3 ? by_side(I256{}, P2{}) : by_side(I256{}, P3{});
     int rc = launch_status();
     if (rc) return rc;
-    return rslrl_fold_partials(static_cast<const float*>(workspace), S, static_cast<int64_t>(N) * K, dw,
+    return rslrl_fold_partials(static_cast<const float*>(workspace), S, NKE, dw_db,
                                static_cast<char*>(workspace) + part_bytes, workspace_bytes - part_bytes, stream);
+}
+
+extern "C" int rslrl_linear_wgrad_ex(const float* dz, const float* dz_amax, const float* x, const float* x_amax,
+                                     int64_t M, int32_t N, int32_t K, int32_t arith, float* dw, void* workspace,
+                                     size_t workspace_bytes, rslrl_stream_t stream) {
+    return rslrl_linear_wgrad_bias(dz, dz_amax, x, x_amax, M, N, K, arith, 0, dw, workspace, workspace_bytes, stream);
 }
 
 extern "C" int rslrl_linear_wgrad(const float* dz, const float* x, int64_t M, int32_t N, int32_t K, float* dw,

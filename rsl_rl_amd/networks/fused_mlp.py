@@ -300,26 +300,29 @@ def _out_or_empty(out, shape, device):
     return out
 
 
-def linear_dgrad_elu_ex(dz, h, img, arith, dz_amax=None, want_amax=False, db_out=None):
-    """((dz W) * ELU'(h), its column sums, max |out| or None) on the split path; img: the B image of W^T in the
-    layout of arith (see linear_fwd_ex)."""
+def linear_dgrad_elu_ex(dz, h, img, arith, dz_amax=None, want_amax=False, db_out=None, want_db=True):
+    """((dz W) * ELU'(h), its column sums or None, max |out| or None) on the split path; img: the B image of W^T in
+    the layout of arith (see linear_fwd_ex).  want_db=False: no column sums (the previous layer's bias gradient
+    comes from its weight-gradient kernel)."""
     M, N = dz.shape
     K = h.shape[1]
     L = _lib.lib()
     tiles = L.rslrl_linear_tiles(M)
     out = torch.empty(M, K, device=dz.device, dtype=torch.float32)
-    part = torch.empty(K, tiles, device=dz.device, dtype=torch.float32)
+    part = torch.empty(K, tiles, device=dz.device, dtype=torch.float32) if want_db else None
     amax = torch.empty(1, device=dz.device, dtype=torch.float32) if want_amax else None
     with timer.span(f"linear_dgrad[M={M},Nred={N},K={K}]{_tag(arith)}", dz.device, 4 * M * (N + 2 * K),
                     2 * M * K * N):
         _gemm(_lib.LINEAR_DGRAD_ELU, arith, dz, dz_amax, K, img, h=h, c=out, colsum=part, amax_out=amax)
+    if not want_db:
+        return out, None, amax
     db = _out_or_empty(db_out, (K,), dz.device)
     rc = L.rslrl_column_sum_fold(part.data_ptr(), tiles, K, db.data_ptr(), _stream(dz))
     _lib.check(rc, "rslrl_column_sum_fold")
     return out, db, amax
 
 
-def linear_dgrad_elu_wgrad(dz, w, h, img, want_amax=False, db_prev_out=None, dwb_out=None):
+def linear_dgrad_elu_wgrad(dz, w, h, img, want_amax=False, db_prev_out=None, dwb_out=None, want_db_prev=True):
     """Output-layer backward in one launch (x6; dz [M, Nred <= 16, % 4]): ((dz @ w) * ELU'(h), its column sums,
     dz^T h).  w is the layer weight [Nred, K] (only its image is read).  db_prev_out: optional [K] destination of
     the column sums; dwb_out: optional [Nred*K + Nred] destination of dW (row-major) followed by db -- the layout
@@ -329,15 +332,17 @@ def linear_dgrad_elu_wgrad(dz, w, h, img, want_amax=False, db_prev_out=None, dwb
     L = _lib.lib()
     tiles = L.rslrl_linear_tiles(M)
     out = torch.empty(M, K, device=dz.device, dtype=torch.float32)
-    part = torch.empty(K, tiles, device=dz.device, dtype=torch.float32)
+    part = torch.empty(K, tiles, device=dz.device, dtype=torch.float32) if want_db_prev else None
     wpart = torch.empty(tiles, N * K + N, device=dz.device, dtype=torch.float32)  # per tile: dW [N, K], then db [N]
     amax = torch.empty(1, device=dz.device, dtype=torch.float32) if want_amax else None
     with timer.span(f"linear_dgrad_wgrad[M={M},Nred={N},K={K}]", dz.device, 4 * M * (N + 2 * K), 4 * M * K * N):
         _gemm(_lib.LINEAR_DGRAD_ELU_WGRAD, _lib.ARITH_X6, dz, None, K, img, h=h, c=out, colsum=part, wpart=wpart,
               amax_out=amax)
-    db = _out_or_empty(db_prev_out, (K,), dz.device)
-    rc = L.rslrl_column_sum_fold(part.data_ptr(), tiles, K, db.data_ptr(), _stream(dz))
-    _lib.check(rc, "rslrl_column_sum_fold")
+    db = None
+    if want_db_prev:
+        db = _out_or_empty(db_prev_out, (K,), dz.device)
+        rc = L.rslrl_column_sum_fold(part.data_ptr(), tiles, K, db.data_ptr(), _stream(dz))
+        _lib.check(rc, "rslrl_column_sum_fold")
     dwb = _out_or_empty(dwb_out, (N * K + N,), dz.device)
     nbytes = L.rslrl_fold_partials_workspace_bytes(tiles, N * K + N)
     ws = torch.empty(max(nbytes, 16) // 8, dtype=torch.float64, device=dz.device)
@@ -350,50 +355,94 @@ def linear_dgrad_elu_wgrad(dz, w, h, img, want_amax=False, db_prev_out=None, dwb
     return out, db, dw, db_out
 
 
-def linear_wgrad(dz, x, arith=_lib.ARITH_X6, dz_amax=None, x_amax=None, out=None):
+def linear_wgrad(dz, x, arith=_lib.ARITH_X6, dz_amax=None, x_amax=None, out=None, bias_side=0, dwb_out=None):
     """dz^T x ([N, K]) on the split weight-gradient kernel (x6, or h3 with max |dz|, max |x| as device scalars);
-    dz [M, N], x [M, K], N, K <= 256 and 4-aligned.  out: optional [N, K] destination."""
+    dz [M, N], x [M, K], N, K <= 256 and 4-aligned.  out: optional [N, K] destination.
+    bias_side 1 / 2: also the column sums of dz (N values) / of x (K values) from the same kernel -- returns
+    (dw, colsum); dwb_out: optional [N*K + E] destination of both (a Linear's adjacent arena slots)."""
     M, N = dz.shape
     K = x.shape[1]
     L = _lib.lib()
-    nbytes = L.rslrl_linear_wgrad_workspace_bytes(M, N, K)
+    nbytes = L.rslrl_linear_wgrad_bias_workspace_bytes(M, N, K, bias_side)
     ws = torch.empty(nbytes // 4, dtype=torch.float32, device=dz.device)
-    dw = _out_or_empty(out, (N, K), dz.device)
+    E = N if bias_side == 1 else (K if bias_side == 2 else 0)
+    if bias_side:
+        dwb = _out_or_empty(dwb_out, (N * K + E,), dz.device)
+    else:
+        dwb = _out_or_empty(out, (N, K), dz.device)
     if arith == _lib.ARITH_H3:
         dz_amax = _amax(dz) if dz_amax is None else dz_amax
         x_amax = _amax(x) if x_amax is None else x_amax
     with timer.span(f"linear_wgrad[M={M},N={N},K={K}]{_tag(arith)}", dz.device, 4 * M * (N + K), 2 * M * K * N):
-        rc = L.rslrl_linear_wgrad_ex(dz.data_ptr(), _ptr(dz_amax), x.data_ptr(), _ptr(x_amax), M, N, K, arith,
-                                     dw.data_ptr(), ws.data_ptr(), nbytes, _stream(dz))
-    _lib.check(rc, "rslrl_linear_wgrad_ex")
-    return dw
+        rc = L.rslrl_linear_wgrad_bias(dz.data_ptr(), _ptr(dz_amax), x.data_ptr(), _ptr(x_amax), M, N, K, arith,
+                                       bias_side, dwb.data_ptr(), ws.data_ptr(), nbytes, _stream(dz))
+    _lib.check(rc, "rslrl_linear_wgrad_bias")
+    if not bias_side:
+        return dwb
+    return dwb[: N * K].view(N, K), dwb[N * K:]
 
 
-def _weight_grad(dz, x, x6: bool, h3=False, dz_amax=None, x_amax=None, out=None):
+def _weight_grad(dz, x, x6: bool, h3=False, dz_amax=None, x_amax=None, out=None, want_bias=False, db_out=None):
     # the split weight-gradient kernel computes TN x 256 tiles (TN = 32, 64 or 256 rows of its first operand):
     # the square hidden layers run it as dz^T x (h3 when both operands come from h3-layer producers); the first
     # layer (input width <= 64) as (x^T dz)^T on the 64-row tiles (x6); the narrow output layers stay on the
     # split-K batched GEMM (networks/linear.py) unless their backward is fused (linear_dgrad_elu_wgrad).
-    # out: optional [N, K] destination (written directly where the kernel's layout allows, else copied)
+    # out: optional [N, K] destination (written directly where the kernel's layout allows, else copied).
+    # want_bias: also the bias gradient (column sums of dz) from the same kernel where it has one of the two
+    # split forms (bias_from_wgrad) -- returns (dw, db or None); db_out: its optional destination.
     def deliver(res):
         if out is None:
             return res if res.is_contiguous() else res.contiguous()
         out.copy_(res)
         return out
 
-    if x6 and dz.shape[1] > 64 and x.shape[1] <= 64 and dz.shape[1] <= MAX_WIDTH and dz.shape[1] % 4 == 0:
+    def deliver_b(db):
+        if db_out is None:
+            return db
+        db_out.copy_(db)
+        return db_out
+
+    form = _wgrad_form(dz.shape[1], x.shape[1], x6)
+    if form == "first":
         pad = (-x.shape[1]) % 4
         xp = F.pad(x, (0, pad)) if pad else x
-        return deliver(linear_wgrad(xp, dz)[: x.shape[1]].t())
-    if x6 and dz.shape[1] > 32 and x.shape[1] > 64 and dz.shape[1] <= MAX_WIDTH and x.shape[1] <= MAX_WIDTH \
-            and x.shape[1] % 4 == 0:
+        if want_bias:  # (x^T dz)^T: the bias is the column sums of dz, here the kernel's K side
+            dwt, db = linear_wgrad(xp, dz, bias_side=2)
+            return deliver(dwt[: x.shape[1]].t()), deliver_b(db)
+        return deliver(linear_wgrad(xp, dz)[: x.shape[1]].t()), None
+    if form == "square":
         pad = (-dz.shape[1]) % 4
         if pad:  # the critic's 1-wide output
-            return deliver(linear_wgrad(F.pad(dz, (0, pad)), x)[: dz.shape[1]])
-        if h3:
-            return linear_wgrad(dz, x, _lib.ARITH_H3, dz_amax, x_amax, out=out)
-        return linear_wgrad(dz, x, out=out)
-    return deliver(_splitk_weight_grad(dz, x))
+            return deliver(linear_wgrad(F.pad(dz, (0, pad)), x)[: dz.shape[1]]), None
+        arith = _lib.ARITH_H3 if h3 else _lib.ARITH_X6
+        if want_bias and dz.shape[1] > 64:
+            N, K = dz.shape[1], x.shape[1]
+            adjacent = (out is not None and db_out is not None and out.is_contiguous() and db_out.is_contiguous()
+                        and db_out.data_ptr() == out.data_ptr() + 4 * out.numel())
+            dwb_out = torch.as_strided(out, (N * K + N,), (1,)) if adjacent else None
+            dw, db = linear_wgrad(dz, x, arith, dz_amax, x_amax, bias_side=1, dwb_out=dwb_out)
+            if adjacent:
+                return out, db_out
+            return deliver(dw), deliver_b(db)
+        return linear_wgrad(dz, x, arith, dz_amax, x_amax, out=out), None
+    return deliver(_splitk_weight_grad(dz, x)), None
+
+
+def _wgrad_form(n_dz: int, n_x: int, x6: bool):
+    """Which weight-gradient kernel form _weight_grad takes for an output gradient n_dz wide and an input n_x wide:
+    "first" ((x^T dz)^T, input width <= 64), "square" (dz^T x) or None (the split-K fallback)."""
+    if x6 and n_dz > 64 and n_x <= 64 and n_dz <= MAX_WIDTH and n_dz % 4 == 0:
+        return "first"
+    if x6 and n_dz > 32 and n_x > 64 and n_dz <= MAX_WIDTH and n_x <= MAX_WIDTH and n_x % 4 == 0:
+        return "square"
+    return None
+
+
+def _bias_from_wgrad(n_dz: int, n_x: int, x6: bool) -> bool:
+    """A layer whose output gradient is n_dz wide gets its bias gradient from the weight-gradient kernel (the column
+    sums of the dz it stages) instead of from the next layer's input-gradient epilogue + a fold."""
+    form = _wgrad_form(n_dz, n_x, x6)
+    return form == "first" or (form == "square" and n_dz > 64 and n_dz % 4 == 0)
 
 
 def _plan(ws):
@@ -485,6 +534,10 @@ def train_backward(tape, dy, need_dx=False, need_w=None, outs=None):
     b_out = lambda l: outs[l][1] if outs[l] is not None else None  # noqa: E731
     grads_w = [None] * L
     grads_b = [None] * L
+    # hidden layers whose bias gradient comes out of their own weight-gradient kernel (x6 forms): the next layer's
+    # input-gradient epilogue then skips its column sums and their fold
+    bias_wg = [l < L - 1 and need_w[l] and _bias_from_wgrad(ws[l].shape[0], hs[l].shape[1], tape.x6)
+               for l in range(L)]
     dz = dy.contiguous()
     dz_amax = None
     dx = None
@@ -505,7 +558,7 @@ def train_backward(tape, dy, need_dx=False, need_w=None, outs=None):
                     and bo.data_ptr() == wo.data_ptr() + 4 * wo.numel():
                 dwb_out = torch.as_strided(wo, (nred * K + nred,), (1,))
             res = linear_dgrad_elu_wgrad(dzp, ws[l], h_in, tape.dgrad_imgs[l], want_amax=want,
-                                         db_prev_out=b_out(l - 1), dwb_out=dwb_out)
+                                         db_prev_out=b_out(l - 1), dwb_out=dwb_out, want_db_prev=not bias_wg[l - 1])
             dz, grads_b[l - 1], dw, db_out = res[:4]
             dz_amax = res[4] if want else None
             if dwb_out is not None:
@@ -522,7 +575,10 @@ def train_backward(tape, dy, need_dx=False, need_w=None, outs=None):
         if l == L - 1:
             grads_b[l] = dz.sum(0) if b_out(l) is None else torch.sum(dz, 0, out=b_out(l))
         if need_w[l]:
-            grads_w[l] = _weight_grad(dz, h_in, tape.x6, h3[l], dz_amax, tape.amaxes[l], out=w_out(l))
+            grads_w[l], db = _weight_grad(dz, h_in, tape.x6, h3[l], dz_amax, tape.amaxes[l], out=w_out(l),
+                                          want_bias=bias_wg[l], db_out=b_out(l))
+            if bias_wg[l]:
+                grads_b[l] = db
         if l == 0:
             dx = dz.mm(ws[0]) if need_dx else None
             break
@@ -536,18 +592,21 @@ def train_backward(tape, dy, need_dx=False, need_w=None, outs=None):
             dz = F.pad(dz, (0, pad))
             if img is None:
                 w = F.pad(w, (0, 0, 0, pad))
+        want_db = not bias_wg[l - 1]
         if h3[l]:
             want = l - 1 > 0 and h3[l - 1]
             dz_amax = _amax(dz) if dz_amax is None else dz_amax
-            dz, grads_b[l - 1], dz_amax = linear_dgrad_elu_ex(dz, h_in, img, _lib.ARITH_H3, dz_amax, want,
-                                                              db_out=b_out(l - 1))
+            dz, db, dz_amax = linear_dgrad_elu_ex(dz, h_in, img, _lib.ARITH_H3, dz_amax, want,
+                                                  db_out=b_out(l - 1), want_db=want_db)
         elif img is not None:
             want = l - 1 > 0 and h3[l - 1]
-            dz, grads_b[l - 1], dz_amax = linear_dgrad_elu_ex(dz, h_in, img, _lib.ARITH_X6, None, want,
-                                                              db_out=b_out(l - 1))
+            dz, db, dz_amax = linear_dgrad_elu_ex(dz, h_in, img, _lib.ARITH_X6, None, want, db_out=b_out(l - 1),
+                                                  want_db=want_db)
         else:
-            dz, grads_b[l - 1] = linear_dgrad_elu(dz, w, h_in, None, db_out=b_out(l - 1))
+            dz, db = linear_dgrad_elu(dz, w, h_in, None, db_out=b_out(l - 1))
             dz_amax = None
+        if want_db or img is None:
+            grads_b[l - 1] = db
     return dx, grads_w, grads_b
 
 
