@@ -743,6 +743,29 @@ __device__ __forceinline__ void mlp_gemm_x6_body(GemmParams p, const uint4* __re
     char* lds[2];
     lds[0] = lds_b0;
     lds[1] = lds_b1;
+    // kEpiBiasEluOut: the bias and (1 output on the VALU: the value head) the fp32 output weights live in the 4 KiB of buffer 0
+    // that neither the main loop nor the epilogue uses, so the epilogue's dependent chain reads them from LDS
+    // instead of waiting on L2 loads (xs: [256] bias, then [64 (wn, j, s, h)][kXsOut][8] weights)
+    constexpr int kXsOff = PL * planeA + PL * kX6PlaneB;
+    constexpr int kXsOut = 1;  // the value head
+    if constexpr (EPI == kEpiBiasEluOut) {
+        static_assert(kXsOff + 4 * (kBN + 64 * kXsOut * 8) <= bufBytes, "LDS side area");
+        float* xs = reinterpret_cast<float*>(lds_b0 + kXsOff);
+        const int t = threadIdx.x;
+        if (t < kBN / 4)
+            reinterpret_cast<float4*>(xs)[t] =
+                4 * t < p.N ? *reinterpret_cast<const float4*>(p.bias + 4 * t) : make_float4(0.f, 0.f, 0.f, 0.f);
+        if constexpr (NR == 1) {
+            if (p.nout <= kXsOut && t >= 64 && t < 64 + 64 * kXsOut) {
+                const int e = t - 64, combo = e / kXsOut, o = e % kXsOut;
+                const float4* src = reinterpret_cast<const float4*>(p.oimg + kOutImagePlaneUnits) + 2 * (combo * 32 + o);
+                float4* dst = reinterpret_cast<float4*>(xs + kBN) + 2 * e;
+                const bool ok = o < p.nout;
+                dst[0] = ok ? src[0] : make_float4(0.f, 0.f, 0.f, 0.f);
+                dst[1] = ok ? src[1] : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+        }
+    }
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: SGPR arithmetic
     const int wm = wave >> 2;  // rows wm * BM / 2
@@ -960,8 +983,8 @@ __device__ __forceinline__ void mlp_gemm_x6_body(GemmParams p, const uint4* __re
                 for (int g = 0; g < 4; ++g) {
                     const int col = cb + 8 * g;
                     const bool col_ok = col < p.N;  // N % 4 == 0
-                    const float4 b4 = col_ok ? *reinterpret_cast<const float4*>(p.bias + col)
-                                             : make_float4(0.f, 0.f, 0.f, 0.f);
+                    // (zero past N in the LDS copy)
+                    const float4 b4 = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(lds[0] + kXsOff) + col);
                     float t[4] = {acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
                     if constexpr (PL == 2) {  // h3: C = acc / (s_a t_n), exact
                         const float4 f4 = *reinterpret_cast<const float4*>(
@@ -977,7 +1000,10 @@ __device__ __forceinline__ void mlp_gemm_x6_body(GemmParams p, const uint4* __re
                     t[2] += b4.z;
                     t[3] += b4.w;
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) v[4 * g + e] = t[e] > 0.f ? t[e] : elu_neg(t[e]);
+                    for (int e = 0; e < 4; ++e) {  // branch-free (see the full-tile epilogue)
+                        const float n = elu_neg(fminf(t[e], 0.f));
+                        v[4 * g + e] = t[e] > 0.f ? t[e] : n;
+                    }
                     const f32x4 hv = {v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]};
                     if (staged) {
                         *reinterpret_cast<f32x4*>(stage + l32 * 32 + 4 * ((2 * g + h) ^ ((l32 >> 1) & 7))) = hv;
@@ -1005,15 +1031,19 @@ __device__ __forceinline__ void mlp_gemm_x6_body(GemmParams p, const uint4* __re
                     __builtin_amdgcn_wave_barrier();
                 }
                 if constexpr (valu) {
-                    // <= 4 outputs: fp32 FMA chains over the lane's 16 columns (the image's fp32 copy)
+                    // <= 4 outputs: fp32 FMA chains over the lane's 16 columns (the image's fp32 copy; for 1
+                    // output the copy in LDS, kXsOut entries per (wn, j, s, h))
+                    const bool in_lds = p.nout <= kXsOut;
                     const float4* wf = reinterpret_cast<const float4*>(p.oimg + kOutImagePlaneUnits) +
                                        2 * ((((wn * 2 + j) * 2) * 2 + h) * 32);
+                    const float4* wl = reinterpret_cast<const float4*>(reinterpret_cast<const float*>(lds[0] + kXsOff) +
+                                                                       kBN) + 2 * ((((wn * 2 + j) * 2) * 2 + h) * kXsOut);
 #pragma unroll
                     for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
                         for (int o = 0; o < 4; ++o) {
                             if (o >= p.nout) break;
-                            const float4* q = wf + 2 * (s2 * 64 + o);
+                            const float4* q = in_lds ? wl + 2 * (s2 * 2 * kXsOut + o) : wf + 2 * (s2 * 64 + o);
                             const float4 w0 = q[0], w1 = q[1];
                             const float w[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
 #pragma unroll
