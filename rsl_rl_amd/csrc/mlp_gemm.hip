@@ -745,18 +745,20 @@ __device__ __forceinline__ void mlp_gemm_x6_body(GemmParams p, const uint4* __re
     lds[1] = lds_b1;
     // kEpiBiasEluOut: the bias and (1 output on the VALU: the value head) the fp32 output weights live in the 4 KiB of buffer 0
     // that neither the main loop nor the epilogue uses, so the epilogue's dependent chain reads them from LDS
-    // instead of waiting on L2 loads (xs: [256] bias, then [64 (wn, j, s, h)][kXsOut][8] weights)
-    constexpr int kXsOff = PL * planeA + PL * kX6PlaneB;
+    // instead of waiting on L2 loads (xs: [256] bias, then [32 (wn, j, s, h)][kXsOut][8] weights)
+    // past the main loop's operands and past the epilogue's H stage / reduction tiles (8 waves x 4 KiB)
+    constexpr int kXsOff = PL * planeA + PL * kX6PlaneB > 8 * 4096 ? PL * planeA + PL * kX6PlaneB : 8 * 4096;
     constexpr int kXsOut = 1;  // the value head
     if constexpr (EPI == kEpiBiasEluOut) {
-        static_assert(kXsOff + 4 * (kBN + 64 * kXsOut * 8) <= bufBytes, "LDS side area");
+        static_assert(kXsOff + 4 * (kBN + kOutImageThreads / 32 * kXsOut * 8) <= bufBytes, "LDS side area");
         float* xs = reinterpret_cast<float*>(lds_b0 + kXsOff);
         const int t = threadIdx.x;
         if (t < kBN / 4)
             reinterpret_cast<float4*>(xs)[t] =
                 4 * t < p.N ? *reinterpret_cast<const float4*>(p.bias + 4 * t) : make_float4(0.f, 0.f, 0.f, 0.f);
         if constexpr (NR == 1) {
-            if (p.nout <= kXsOut && t >= 64 && t < 64 + 64 * kXsOut) {
+            // the fp32 section holds kOutImageThreads / 32 = 32 (wn, j, s, h) combinations x 32 outputs
+            if (p.nout <= kXsOut && t >= 64 && t < 64 + kOutImageThreads / 32 * kXsOut) {
                 const int e = t - 64, combo = e / kXsOut, o = e % kXsOut;
                 const float4* src = reinterpret_cast<const float4*>(p.oimg + kOutImagePlaneUnits) + 2 * (combo * 32 + o);
                 float4* dst = reinterpret_cast<float4*>(xs + kBN) + 2 * e;
