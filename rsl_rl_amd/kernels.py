@@ -495,6 +495,7 @@ class FusedClipAdam:
             raise RuntimeError("FusedClipAdam.step: closures are not supported")
         L = _lib.lib()
         keep = []  # contiguous copies (if any) stay alive until the launch is queued
+        back = []  # (grad, copy): the kernel writes the clipped gradient into the copy; .grad gets it back
         for g in self.opt.param_groups:
             chunk = [p for p in g["params"] if p.grad is not None]
             if chunk:
@@ -514,6 +515,8 @@ class FusedClipAdam:
                     st = self._state(p)
                     grad = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
                     keep.append(grad)
+                    if grad is not p.grad:
+                        back.append((p.grad, grad))
                     t = a.t[i]
                     t.param, t.grad = p.data_ptr(), grad.data_ptr()
                     t.exp_avg, t.exp_avg_sq = st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr()
@@ -521,5 +524,7 @@ class FusedClipAdam:
                 rc = L.rslrl_clip_adam_step(ctypes.byref(a), self.ws.data_ptr(), self.ws.numel() * 4,
                                             _stream(self.ws.device))
                 _lib.check(rc, "rslrl_clip_adam_step")
+        for g, c in back:
+            g.copy_(c)
         return None
 

@@ -1,32 +1,62 @@
-"""Host-side profile of one training iteration at C3 (torch.profiler, CPU activities only): which Python/ATen calls
-the launch thread spends its time in during the rollout and the update.  Diagnostic, not part of the bench.
+"""Host-side cost of the rollout at C3: cProfile of the launch thread over one iteration's 24 env steps (after
+warm-up), and the host issue time per step next to the GPU time per step.  Diagnostic, not part of the bench.
 
     python scripts/rollout_host_profile.py > gpurun_out/host_profile.txt
 """
+import cProfile
+import io
 import os
+import pstats
 import sys
+import time
+import types
 
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import bench  # noqa: E402
 from rsl_rl_amd.env import SyntheticVecEnv  # noqa: E402
+from rsl_rl_amd.networks import fused_mlp  # noqa: E402
 from rsl_rl_amd.runners import OnPolicyRunner  # noqa: E402
 
 
 def main():
     dev = torch.device("cuda:0")
-    import types
     args = types.SimpleNamespace(num_steps_per_env=24, num_obs=48, num_actions=12, hidden=256, layers=3)
     torch.manual_seed(1)
     env = SyntheticVecEnv(65536, args.num_obs, args.num_actions, device=dev)
     runner = OnPolicyRunner(env, bench.train_cfg(args), log_dir=None, device=dev)
     runner.learn(3)
     torch.cuda.synchronize()
-    with torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CPU]) as prof:
-        runner.learn(1)
-        torch.cuda.synchronize()
-    print(prof.key_averages().table(sort_by="self_cpu_time_total", row_limit=40))
+    alg = runner.alg
+    obs = env.get_observations().to(dev)
+
+    def rollout(n):
+        nonlocal obs
+        with torch.inference_mode(), fused_mlp.frozen_weights():
+            for _ in range(n):
+                actions = alg.act(obs)
+                obs, rewards, dones, extras = env.step(actions)
+                alg.process_env_step(obs, rewards, dones, extras)
+        alg.storage.clear()
+
+    # host issue time vs GPU time per step
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    rollout(24)
+    t1 = time.perf_counter()
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    print(f"host issue {1e6 * (t1 - t0) / 24:.1f} us/step, until GPU done {1e6 * (t2 - t0) / 24:.1f} us/step")
+    torch.cuda.synchronize()
+    pr = cProfile.Profile()
+    pr.enable()
+    rollout(24)
+    pr.disable()
+    torch.cuda.synchronize()
+    s = io.StringIO()
+    pstats.Stats(pr, stream=s).sort_stats("tottime").print_stats(35)
+    print(s.getvalue())
 
 
 if __name__ == "__main__":

@@ -4,6 +4,8 @@ torch.optim.Adam(fused=True).step() (ppo.py:373-374) on the same parameters and 
 moments bit-identical; with clipping active the norm is accumulated in another order (fp64 here, per-tensor
 fp32 norms in torch), so parameters agree to 1e-6 relative."""
 
+import io
+
 import pytest
 import torch
 
@@ -53,3 +55,96 @@ def test_unsupported_optimizers_fall_back():
     p = [torch.nn.Parameter(torch.zeros(3))]
     assert not kernels.FusedClipAdam.supported(torch.optim.SGD(p, lr=0.1))
     assert not kernels.FusedClipAdam.supported(torch.optim.Adam(p, lr=0.1, weight_decay=0.1))
+
+
+@pytest.mark.parametrize("max_norm", [1.0, 1e9])
+def test_nan_gradient_poisons_every_parameter(max_norm, cuda_device):
+    """clip_grad_norm_ with a NaN total norm: torch.clamp(coef, max=1) keeps the NaN, every gradient is scaled
+    by it and Adam turns every parameter NaN -- the fused step must fail the same way, not only where the
+    gradient was NaN."""
+    ours = _make(cuda_device, 2)
+    ref = [torch.nn.Parameter(p.detach().clone()) for p in ours]
+    opt_o = torch.optim.Adam(ours, lr=1e-3, fused=True)
+    opt_r = torch.optim.Adam(ref, lr=1e-3, fused=True)
+    fused = kernels.FusedClipAdam(opt_o, max_norm)
+    for po, pr in zip(ours, ref):
+        gr = torch.randn(po.shape, device=cuda_device)
+        po.grad, pr.grad = gr.clone(), gr.clone()
+    ours[2].grad[3, 5] = float("nan")
+    ref[2].grad[3, 5] = float("nan")
+    fused.step()
+    torch.nn.utils.clip_grad_norm_(ref, max_norm)
+    opt_r.step()
+    torch.cuda.synchronize()
+    for po, pr in zip(ours, ref):
+        assert torch.isnan(pr.data).all()
+        assert torch.isnan(po.data).all()
+        assert torch.isnan(po.grad).all()  # .grad holds the clipped (NaN-scaled) gradient, as after clip_grad_norm_
+
+
+def test_clipped_gradient_written_back(cuda_device):
+    """After the step .grad holds the clipped gradient (clip_grad_norm_ scales in place), also for a
+    non-contiguous .grad (the kernel works on a contiguous copy, copied back)."""
+    ours = _make(cuda_device, 3)
+    ref = [torch.nn.Parameter(p.detach().clone()) for p in ours]
+    opt_o = torch.optim.Adam(ours, lr=1e-3, fused=True)
+    fused = kernels.FusedClipAdam(opt_o, 0.5)
+    for po, pr in zip(ours, ref):
+        gr = torch.randn(po.shape, device=cuda_device) * 2.0
+        if gr.dim() == 2:  # a transposed (non-contiguous) view with the same values
+            po.grad = gr.t().contiguous().t()
+            assert not po.grad.is_contiguous()
+        else:
+            po.grad = gr.clone()
+        pr.grad = gr.clone()
+    fused.step()
+    torch.nn.utils.clip_grad_norm_(ref, 0.5)
+    torch.cuda.synchronize()
+    for po, pr in zip(ours, ref):
+        torch.testing.assert_close(po.grad, pr.grad, rtol=1e-6, atol=1e-8)
+
+
+def test_resume_from_non_fused_adam_state(cuda_device):
+    """A checkpoint written by a plain (non-fused) torch Adam -- what a reference run saves -- loads with
+    fused=None in its param group and CPU step tensors (torch keeps non-fused steps on the host).  PPO.update()
+    calls adopt_loaded_state(); the fused step must then continue the same Adam trajectory as the plain Adam
+    that wrote the checkpoint (steps on the device, moments continued), without touching host memory."""
+    ours = _make(cuda_device, 4)
+    ref = [torch.nn.Parameter(p.detach().clone()) for p in ours]
+    plain = torch.optim.Adam(ref, lr=1e-3, foreach=False)
+    g = torch.Generator(device=cuda_device).manual_seed(5)
+    grads = [[torch.randn(p.shape, device=cuda_device, generator=g) for p in ours] for _ in range(5)]
+    for it in range(3):
+        for pr, gr in zip(ref, grads[it]):
+            pr.grad = gr.clone()
+        torch.nn.utils.clip_grad_norm_(ref, 1.0)
+        plain.step()
+    buf = io.BytesIO()  # a checkpoint round trip (load_state_dict alone would share the moment tensors)
+    torch.save(plain.state_dict(), buf)
+    buf.seek(0)
+    sd = torch.load(buf, weights_only=True)
+    with torch.no_grad():
+        for po, pr in zip(ours, ref):
+            po.copy_(pr)
+    opt_o = torch.optim.Adam(ours, lr=1e-3, fused=True)
+    opt_o.load_state_dict(sd)
+    assert opt_o.param_groups[0]["fused"] is None  # what the advisor saw: the checkpoint's flag wins
+    assert opt_o.state[ours[0]]["step"].device.type == "cpu"
+    fused = kernels.FusedClipAdam(opt_o, 1.0)
+    fused.adopt_loaded_state()
+    assert opt_o.param_groups[0]["fused"] is True
+    for po in ours:
+        st = opt_o.state[po]
+        assert st["step"].device == po.device and st["step"].dtype == torch.float32 and float(st["step"]) == 3.0
+    for it in range(3, 5):
+        for po, pr, gr in zip(ours, ref, grads[it]):
+            po.grad, pr.grad = gr.clone(), gr.clone()
+        fused.step()
+        torch.nn.utils.clip_grad_norm_(ref, 1.0)
+        plain.step()
+    torch.cuda.synchronize()
+    for po, pr in zip(ours, ref):
+        assert float(opt_o.state[po]["step"]) == 5.0
+        # plain (for-loop) Adam vs torch's fused arithmetic: fp32 rounding apart
+        torch.testing.assert_close(po.data, pr.data, rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(opt_o.state[po]["exp_avg_sq"], plain.state[pr]["exp_avg_sq"], rtol=1e-5, atol=1e-9)

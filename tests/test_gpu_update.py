@@ -207,3 +207,41 @@ def test_update_two_streams_bit_identical(golden_meta, cuda_device, monkeypatch)
     assert res["0"][0] == res["1"][0] and res["0"][1] == res["1"][1]
     for k, v in res["0"][2].items():
         assert torch.equal(v, res["1"][2][k]), k
+
+
+def test_runner_resumes_non_fused_adam_checkpoint(cuda_device, tmp_path):
+    """A checkpoint whose optimizer state was written by a plain (non-fused) torch Adam -- as a reference run
+    saves it: param group fused=None, step tensors on the CPU -- loads through OnPolicyRunner.load and the next
+    learn() iteration runs the fused clip+Adam step on it (steps moved to the device, the trajectory continued)."""
+    torch.manual_seed(0)
+    cfg = {
+        "num_steps_per_env": 16, "save_interval": 10**9, "obs_groups": {"policy": ["policy"]},
+        "policy": {"class_name": "ActorCritic", "actor_hidden_dims": [64, 64], "critic_hidden_dims": [64, 64],
+                   "activation": "elu", "init_noise_std": 1.0},
+        "algorithm": {"class_name": "PPO", "num_learning_epochs": 2, "num_mini_batches": 2},
+    }
+    runner = OnPolicyRunner(SyntheticVecEnv(512, 16, 4, device=cuda_device, seed=0), cfg, log_dir=None,
+                            device=str(cuda_device))
+    params = [p.detach().clone().requires_grad_(True) for p in runner.alg.policy.parameters()]
+    plain = torch.optim.Adam(params, lr=1e-3, foreach=False)
+    for p in params:
+        p.grad = torch.randn_like(p) * 0.1
+    plain.step()
+    plain.step()
+    sd = plain.state_dict()
+    assert sd["param_groups"][0]["fused"] is None
+    with torch.no_grad():
+        pol_sd = {k: v.clone() for k, v in runner.alg.policy.state_dict().items()}
+    torch.save({"model_state_dict": pol_sd, "optimizer_state_dict": sd, "iter": 7, "infos": None},
+               str(tmp_path / "ref.pt"))
+    runner.load(str(tmp_path / "ref.pt"))
+    assert runner.alg._clip_adam is not None
+    runner.learn(1)
+    s = runner.last_iteration_stats
+    assert all(np.isfinite(v) for v in s["loss_dict"].values())
+    opt = runner.alg.optimizer
+    assert opt.param_groups[0]["fused"] is True
+    for p in runner.alg.policy.parameters():
+        st = opt.state[p]
+        assert st["step"].device == p.device and float(st["step"]) == 2 + 2 * 2  # + E * M fused steps
+        assert torch.isfinite(p).all()
