@@ -31,7 +31,7 @@ extern "C" {
 
 typedef struct ihipStream_t* rslrl_stream_t; /* == hipStream_t */
 
-#define RSLRL_ABI_VERSION 5
+#define RSLRL_ABI_VERSION 6
 
 enum {
     RSLRL_OK = 0,
@@ -89,6 +89,31 @@ typedef struct {
 
 int rslrl_gather_rows(const rslrl_gather_field_t* fields /* host array */, int32_t num_fields,
                       const int32_t* indices, int64_t num_rows, rslrl_stream_t stream);
+
+/* ------------------------------------------------------------------------------------------------
+ * Transition records -- the same mini-batch assembly (rollout_storage.py:168-197) over a storage whose
+ * gathered fields live side by side in one fp32 record per env-step ([T*N, record_floats], record_floats
+ * % 4 == 0, records 16-byte aligned; RolloutStorage's record layout).  A random row then costs the record's
+ * whole 128-byte lines instead of one line per field, and the scalar fields no line each.
+ *
+ * rslrl_gather_records: for each field f, dst_f[r] = records[indices[r]][offset_f : offset_f + width_f]
+ *   (dst_f contiguous [num_rows, width_f]); the record's first max(offset_f + width_f) floats (<= 256)
+ *   are read once per row.  indices: device int32 [num_rows], each in [0, number of records).
+ * rslrl_record_scatter_columns: records[i][offset + j] = columns[j][i] for i < n, j < num_columns (<= 4);
+ *   puts the [T, N] scalar fields (values, log-prob, returns, advantages) into their record slots.
+ * ----------------------------------------------------------------------------------------------*/
+#define RSLRL_MAX_RECORD_FLOATS 256
+typedef struct {
+    int64_t offset; /* floats from the record start */
+    int64_t width;  /* floats */
+    float* dst;     /* device, [num_rows, width] */
+} rslrl_record_field_t;
+
+int rslrl_gather_records(const float* records, int64_t record_floats, const rslrl_record_field_t* fields /* host */,
+                         int32_t num_fields, const int32_t* indices, int64_t num_rows, rslrl_stream_t stream);
+int rslrl_record_scatter_columns(float* records, int64_t record_floats, int64_t offset,
+                                 const float* const* columns /* host array of device pointers */,
+                                 int32_t num_columns, int64_t n, rslrl_stream_t stream);
 
 /* ------------------------------------------------------------------------------------------------
  * Fused PPO loss forward + backward for one mini-batch -- rsl_rl/algorithms/ppo.py:221-223
@@ -343,6 +368,10 @@ int rslrl_linear_wgrad_bias(const float* dz, const float* dz_amax, const float* 
  *   reward = (rewards + extra_reward + r_int) + gamma * (values * time_outs)   (ppo.py:147-164)
  * and writes storage row t: obs groups, actions, reward, uint8(dones), values, logp, mu, sigma
  * (rollout_storage.py:77-103).  out_* point at row t of each [T, N, d] buffer (contiguous [N, d]).
+ * record_floats > 0: the copied fields (obs groups, actions, mu, sigma) live in transition records
+ * (rslrl_gather_records) starting at out_records: each destination is a field of record 0 (in that order,
+ * not overlapping) with row stride record_floats; record_floats, A and every obs width must be multiples
+ * of 4 with 16-byte aligned pointers.  The launch writes the records whole: units outside the fields get 0.
  * RND nets: Linear(in -> hidden) + ELU + Linear(hidden -> out), in, hidden <= 64, out <= 8, packed per
  * net as [W1 (hidden x in) | b1 | W2 (out x hidden) | b2]; optional state normalisation
  * (s - mean) / (std + eps).  dones / time_outs dtype: RSLRL_DTYPE_*; time_outs may be NULL.
@@ -394,6 +423,8 @@ typedef struct {
     float* out_logp;
     float* out_mu;
     float* out_sigma;
+    int64_t record_floats; /* 0: contiguous destinations; > 0: record row stride (floats) */
+    float* out_records;    /* record mode: the first record of step t ([N, record_floats], 16-byte aligned) */
 } rslrl_rollout_args_t;
 int rslrl_rollout_record(const rslrl_rollout_args_t* args /* host struct */, rslrl_stream_t stream);
 

@@ -19,7 +19,7 @@ import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 # RSLRL_AMD_LIB: an alternative in-tree build of the same library (A/B kernel experiments)
 LIB_PATH = os.environ.get("RSLRL_AMD_LIB") or os.path.join(LIB_DIR, "librslrl_amd.so")
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 # symbols declared in include/rslrl_amd.h (tests/test_capi.py checks the header against this list)
 EXPORTED_SYMBOLS = (
@@ -31,6 +31,8 @@ EXPORTED_SYMBOLS = (
     "rslrl_normalize_advantages",
     "rslrl_randperm_mt19937",
     "rslrl_gather_rows",
+    "rslrl_gather_records",
+    "rslrl_record_scatter_columns",
     "rslrl_ppo_loss_workspace_bytes",
     "rslrl_ppo_loss_fwd_bwd",
     "rslrl_linear_tiles",
@@ -66,6 +68,7 @@ EXPORTED_SYMBOLS = (
 )
 
 MAX_GATHER_FIELDS = 16
+MAX_RECORD_FLOATS = 256
 PPO_LOSS_MAX_ACTIONS = 64
 
 
@@ -79,6 +82,11 @@ class RslrlError(RuntimeError):
 
 class GatherField(ctypes.Structure):
     _fields_ = [("src", ctypes.c_void_p), ("dst", ctypes.c_void_p), ("row_bytes", ctypes.c_int64)]
+
+
+class RecordField(ctypes.Structure):
+    """rslrl_record_field_t (include/rslrl_amd.h)."""
+    _fields_ = [("offset", ctypes.c_int64), ("width", ctypes.c_int64), ("dst", ctypes.c_void_p)]
 
 
 class BImageDesc(ctypes.Structure):
@@ -181,6 +189,8 @@ class RolloutArgs(ctypes.Structure):
         ("out_logp", ctypes.c_void_p),
         ("out_mu", ctypes.c_void_p),
         ("out_sigma", ctypes.c_void_p),
+        ("record_floats", ctypes.c_int64),
+        ("out_records", ctypes.c_void_p),
     ]
 
 
@@ -238,6 +248,10 @@ def _declare(L):
     L.rslrl_randperm_mt19937.argtypes = [P, SZ, I64, P]
     L.rslrl_gather_rows.restype = ctypes.c_int
     L.rslrl_gather_rows.argtypes = [ctypes.POINTER(GatherField), I32, P, I64, P]
+    L.rslrl_gather_records.restype = ctypes.c_int
+    L.rslrl_gather_records.argtypes = [P, I64, ctypes.POINTER(RecordField), I32, P, I64, P]
+    L.rslrl_record_scatter_columns.restype = ctypes.c_int
+    L.rslrl_record_scatter_columns.argtypes = [P, I64, I64, ctypes.POINTER(ctypes.c_void_p), I32, I64, P]
     L.rslrl_ppo_loss_workspace_bytes.restype = SZ
     L.rslrl_ppo_loss_workspace_bytes.argtypes = [I64, I32]
     L.rslrl_ppo_loss_fwd_bwd.restype = ctypes.c_int

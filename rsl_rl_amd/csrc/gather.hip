@@ -7,6 +7,8 @@
 // contiguous run (16-byte units when the row size and pointers allow it, 4-byte units otherwise) and
 // the destination is written fully coalesced.
 
+#include <algorithm>
+
 #include "common.h"
 
 namespace rslrl {
@@ -90,5 +92,158 @@ extern "C" int rslrl_gather_rows(const rslrl_gather_field_t* fields, int32_t num
     if (nb > INT32_MAX) return RSLRL_E_INVALID_ARGUMENT;
     hipLaunchKernelGGL(gather_rows_kernel, dim3(static_cast<unsigned>(nb)), dim3(kBlock), 0,
                        reinterpret_cast<hipStream_t>(stream), p, indices, num_rows);
+    return launch_status();
+}
+
+// ------------------------------------------------------------------------------------------------
+// Transition records: the gathered fields of an env-step side by side in one record (RolloutStorage's
+// record layout), so a random row costs the record's own 128-byte lines (3 for the 352 used bytes of a
+// 384-byte C3 record) instead of >= one line per field.  A 256-thread block owns kRecTile (or
+// kRecTile / 2 for records over 128 floats) destination rows: it reads each source record's used prefix in
+// 16-byte units into an LDS tile (rows padded by one unit against bank conflicts), then writes every field
+// as one contiguous [rows, width] block -- both sides coalesced.
+// ------------------------------------------------------------------------------------------------
+namespace rslrl {
+namespace {
+
+constexpr int kRecTile = 64;
+constexpr int kRecLdsUnits = kRecTile * 33;  // 64 rows x (32 + 1) or 32 rows x (64 + 1) units of 16 bytes
+
+struct RecField {
+    int32_t offset;  // floats
+    int32_t width;   // floats
+    int32_t vec16;
+    float* dst;
+};
+
+struct RecParams {
+    RecField f[RSLRL_MAX_GATHER_FIELDS];
+    int32_t nf;
+    int32_t units;  // 16-byte units read per record
+    int32_t tile;   // rows per block
+    int32_t r4;     // record stride in 16-byte units
+};
+
+__global__ __launch_bounds__(kBlock) void gather_records_kernel(RecParams p, const float4* __restrict__ rec,
+                                                                const int32_t* __restrict__ indices, int64_t num_rows) {
+    __shared__ float4 tile[kRecLdsUnits];
+    __shared__ int32_t ridx[kRecTile];
+    const int64_t row0 = static_cast<int64_t>(blockIdx.x) * p.tile;
+    const int nrows = static_cast<int>(min<int64_t>(p.tile, num_rows - row0));
+    for (int r = threadIdx.x; r < nrows; r += kBlock) ridx[r] = indices[row0 + r];
+    __syncthreads();
+    const unsigned U = static_cast<unsigned>(p.units);
+    const int s4 = p.units + 1;
+    const unsigned total = static_cast<unsigned>(nrows) * U;
+    // four independent 16-byte loads in flight per thread before their LDS stores
+    for (unsigned k0 = threadIdx.x; k0 < total; k0 += 4 * kBlock) {
+        float4 v[4];
+        unsigned slot[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const unsigned k = k0 + j * kBlock;
+            const unsigned kk = k < total ? k : total - 1;
+            const unsigned r = kk / U, u = kk - r * U;
+            slot[j] = r * s4 + u;
+            v[j] = rec[static_cast<int64_t>(ridx[r]) * p.r4 + u];
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (k0 + j * kBlock < total) tile[slot[j]] = v[j];
+    }
+    __syncthreads();
+    const float* tf = reinterpret_cast<const float*>(tile);
+    for (int f = 0; f < p.nf; ++f) {
+        const RecField g = p.f[f];
+        if (g.vec16) {
+            const unsigned w4 = static_cast<unsigned>(g.width >> 2), o4 = static_cast<unsigned>(g.offset >> 2);
+            float4* d = reinterpret_cast<float4*>(g.dst) + row0 * w4;
+            const unsigned n = static_cast<unsigned>(nrows) * w4;
+            for (unsigned k = threadIdx.x; k < n; k += kBlock) {
+                const unsigned r = k / w4, c = k - r * w4;
+                d[k] = tile[r * s4 + o4 + c];
+            }
+        } else {
+            const unsigned w = static_cast<unsigned>(g.width);
+            float* d = g.dst + row0 * w;
+            const unsigned n = static_cast<unsigned>(nrows) * w;
+            for (unsigned k = threadIdx.x; k < n; k += kBlock) {
+                const unsigned r = k / w, c = k - r * w;
+                d[k] = tf[(r * s4) * 4 + g.offset + c];
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void record_scatter_kernel(float* __restrict__ rec, int64_t R, int64_t offset,
+                                                                const float* c0, const float* c1, const float* c2,
+                                                                const float* c3, int nc, int vec, int64_t n) {
+    const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
+    for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < n; i += stride) {
+        float* d = rec + i * R + offset;
+        if (vec) {
+            *reinterpret_cast<float4*>(d) = make_float4(c0[i], c1[i], c2[i], c3[i]);
+        } else {
+            d[0] = c0[i];
+            if (nc > 1) d[1] = c1[i];
+            if (nc > 2) d[2] = c2[i];
+            if (nc > 3) d[3] = c3[i];
+        }
+    }
+}
+
+}  // namespace
+}  // namespace rslrl
+
+extern "C" int rslrl_gather_records(const float* records, int64_t record_floats, const rslrl_record_field_t* fields,
+                                    int32_t num_fields, const int32_t* indices, int64_t num_rows,
+                                    rslrl_stream_t stream) {
+    if (num_fields < 0 || num_fields > RSLRL_MAX_GATHER_FIELDS || num_rows < 0) return RSLRL_E_INVALID_ARGUMENT;
+    if (num_rows == 0 || num_fields == 0) return RSLRL_OK;
+    if (!records || !fields || !indices || record_floats <= 0 || (record_floats & 3)) return RSLRL_E_INVALID_ARGUMENT;
+    if (reinterpret_cast<uintptr_t>(records) & 15) return RSLRL_E_MISALIGNED;
+    RecParams p{};
+    p.nf = num_fields;
+    int64_t used = 0;
+    for (int i = 0; i < num_fields; ++i) {
+        const rslrl_record_field_t& f = fields[i];
+        if (!f.dst || f.width < 1 || f.offset < 0 || f.offset + f.width > record_floats) return RSLRL_E_INVALID_ARGUMENT;
+        used = std::max<int64_t>(used, f.offset + f.width);
+        const bool v16 = (f.width % 4 == 0) && (f.offset % 4 == 0) && ((reinterpret_cast<uintptr_t>(f.dst) & 15) == 0);
+        p.f[i] = RecField{static_cast<int32_t>(f.offset), static_cast<int32_t>(f.width), v16 ? 1 : 0, f.dst};
+    }
+    if (used > RSLRL_MAX_RECORD_FLOATS) return RSLRL_E_UNSUPPORTED;
+    p.units = static_cast<int32_t>((used + 3) / 4);
+    p.tile = p.units <= 32 ? kRecTile : kRecTile / 2;
+    if (static_cast<int64_t>(p.tile) * (p.units + 1) > kRecLdsUnits) return RSLRL_E_UNSUPPORTED;
+    if (record_floats / 4 > INT32_MAX) return RSLRL_E_INVALID_ARGUMENT;
+    p.r4 = static_cast<int32_t>(record_floats / 4);
+    const int64_t nb = ceil_div(num_rows, p.tile);
+    if (nb > INT32_MAX) return RSLRL_E_INVALID_ARGUMENT;
+    hipLaunchKernelGGL(gather_records_kernel, dim3(static_cast<unsigned>(nb)), dim3(kBlock), 0,
+                       reinterpret_cast<hipStream_t>(stream), p, reinterpret_cast<const float4*>(records), indices,
+                       num_rows);
+    return launch_status();
+}
+
+extern "C" int rslrl_record_scatter_columns(float* records, int64_t record_floats, int64_t offset,
+                                            const float* const* columns, int32_t num_columns, int64_t n,
+                                            rslrl_stream_t stream) {
+    if (n < 0 || num_columns < 0 || num_columns > 4 || record_floats <= 0 || offset < 0 ||
+        offset + num_columns > record_floats)
+        return RSLRL_E_INVALID_ARGUMENT;
+    if (n == 0 || num_columns == 0) return RSLRL_OK;
+    if (!records || !columns) return RSLRL_E_INVALID_ARGUMENT;
+    const float* c[4] = {nullptr, nullptr, nullptr, nullptr};
+    for (int j = 0; j < num_columns; ++j) {
+        if (!columns[j]) return RSLRL_E_INVALID_ARGUMENT;
+        c[j] = columns[j];
+    }
+    const int vec = num_columns == 4 && (record_floats % 4 == 0) && (offset % 4 == 0) &&
+                    ((reinterpret_cast<uintptr_t>(records) & 15) == 0);
+    const int64_t nb = std::min<int64_t>(ceil_div(n, kBlock), 4096);
+    hipLaunchKernelGGL(record_scatter_kernel, dim3(static_cast<unsigned>(nb)), dim3(kBlock), 0,
+                       reinterpret_cast<hipStream_t>(stream), records, record_floats, offset, c[0], c[1], c[2], c[3],
+                       num_columns, vec, n);
     return launch_status();
 }

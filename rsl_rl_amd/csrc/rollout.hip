@@ -67,9 +67,70 @@ __device__ __forceinline__ void rnd_forward(const float* __restrict__ w, int in,
         if (q < Q) y[q] = __fadd_rn(y[q], b2[q]);
 }
 
-__global__ __launch_bounds__(kBlock) void rollout_record_kernel(rslrl_rollout_args_t a, int copy_blocks) {
+// Record-mode copy segments (obs groups, actions, mu, sigma) in 16-byte units of a destination record
+constexpr int kMaxSeg = RSLRL_ROLLOUT_MAX_OBS + 3;
+constexpr int kRecRows = 64;  // records per copy block
+struct RecSegs {
+    const float4* src[kMaxSeg];
+    float4* dst0;                // record row 0 of step t (record start, 16-byte aligned)
+    int32_t start[kMaxSeg];      // first unit of each segment inside the record
+    int32_t end[kMaxSeg];        // one past its last unit
+    int32_t src_units[kMaxSeg];  // source row stride in units (0: one row shared by all envs)
+    int32_t nseg;
+    int32_t r4;  // record stride in units: every unit of a record is written (zeros past the segments), so
+                 // the copy leaves whole 64-byte sectors and no partial-line write-backs
+    float rcp_r4;
+};
+
+__global__ __launch_bounds__(kBlock) void rollout_record_kernel(rslrl_rollout_args_t a, int copy_blocks, RecSegs rs) {
     extern __shared__ float lds_w[];  // RND target then predictor weights
     const int64_t N = a.N;
+    if (static_cast<int>(blockIdx.x) < copy_blocks && a.record_floats > 0) {
+        // ---- record mode: block b writes records [64 b, 64 b + 64) unit by unit (contiguous stores); the unit ->
+        // segment map and the segment table live in LDS
+        __shared__ int8_t useg[RSLRL_MAX_RECORD_FLOATS / 4];
+        __shared__ const float4* ssrc[kMaxSeg];
+        __shared__ int32_t sstart[kMaxSeg], ssu[kMaxSeg];
+#pragma unroll
+        for (int q = 0; q < kMaxSeg; ++q)
+            if (static_cast<int>(threadIdx.x) == q) {
+                ssrc[q] = rs.src[q];
+                sstart[q] = rs.start[q];
+                ssu[q] = rs.src_units[q];
+            }
+        for (int u = threadIdx.x; u < rs.r4; u += kBlock) {
+            int sg = -1;
+#pragma unroll
+            for (int q = 0; q < kMaxSeg; ++q)
+                if (q < rs.nseg && u >= rs.start[q] && u < rs.end[q]) sg = q;
+            useg[u] = static_cast<int8_t>(sg);
+        }
+        __syncthreads();
+        const int64_t n0 = static_cast<int64_t>(blockIdx.x) * kRecRows;
+        const int rows = static_cast<int>(min<int64_t>(kRecRows, N - n0));
+        const int total = rows * rs.r4;  // <= 64 * 64: exact float division below
+        float4* dst = rs.dst0 + n0 * rs.r4;
+        // every load of a pass is issued before its stores (a store between two loads would order them)
+        constexpr int kPass = 8;
+        for (int k0 = threadIdx.x; k0 < total; k0 += kPass * kBlock) {
+            float4 v[kPass];
+#pragma unroll
+            for (int j = 0; j < kPass; ++j) {
+                const int k = k0 + j * kBlock;
+                v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (k < total) {
+                    const int r = static_cast<int>((static_cast<float>(k) + 0.5f) * rs.rcp_r4);
+                    const int u = k - r * rs.r4;
+                    const int sg = useg[u];
+                    if (sg >= 0) v[j] = ssrc[sg][(n0 + r) * ssu[sg] + (u - sstart[sg])];
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < kPass; ++j)
+                if (k0 + j * kBlock < total) dst[k0 + j * kBlock] = v[j];
+        }
+        return;
+    }
     if (static_cast<int>(blockIdx.x) < copy_blocks) {
         // ---- slab copies: obs groups [N, d], actions / mu [N, A], sigma expanded [N, A]
         const int64_t tid = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
@@ -189,7 +250,34 @@ extern "C" int rslrl_rollout_record(const rslrl_rollout_args_t* args, rslrl_stre
         if ((reinterpret_cast<uintptr_t>(a.obs[g].src) | reinterpret_cast<uintptr_t>(a.obs[g].dst)) & 15)
             return RSLRL_E_MISALIGNED;
     }
-    if ((a.A & 3) == 0 && ((reinterpret_cast<uintptr_t>(a.actions) | reinterpret_cast<uintptr_t>(a.mu) |
+    RecSegs rs{};
+    if (a.record_floats > 0) {
+        if ((a.record_floats & 3) || (a.A & 3) || a.record_floats > RSLRL_MAX_RECORD_FLOATS) return RSLRL_E_INVALID_ARGUMENT;
+        // the destinations must be fields of the record at out_records, in order and not overlapping
+        const float* base = a.out_records;
+        if (!base || (reinterpret_cast<uintptr_t>(base) & 15)) return RSLRL_E_INVALID_ARGUMENT;
+        int32_t units = 0;
+        bool ok = true;
+        auto add = [&](const float* src, const float* dst, int64_t floats, bool shared) {
+            const int64_t off = dst - base;
+            if (off < 0 || (off & 3) || off / 4 < units || off + floats > a.record_floats) ok = false;
+            rs.src[rs.nseg] = reinterpret_cast<const float4*>(src);
+            rs.start[rs.nseg] = static_cast<int32_t>(off / 4);
+            rs.end[rs.nseg] = static_cast<int32_t>((off + floats) / 4);
+            rs.src_units[rs.nseg] = shared ? 0 : static_cast<int32_t>(floats / 4);
+            units = rs.end[rs.nseg];
+            ++rs.nseg;
+        };
+        for (int g = 0; g < a.n_obs; ++g) add(a.obs[g].src, a.obs[g].dst, a.obs[g].row_floats, false);
+        add(a.actions, a.out_actions, a.A, false);
+        add(a.mu, a.out_mu, a.A, false);
+        add(a.sigma, a.out_sigma, a.A, a.sigma_mode == 0);
+        if (!ok) return RSLRL_E_INVALID_ARGUMENT;
+        rs.dst0 = reinterpret_cast<float4*>(a.out_records);
+        rs.r4 = static_cast<int32_t>(a.record_floats / 4);
+        rs.rcp_r4 = 1.0f / static_cast<float>(rs.r4);
+    }
+    if (((a.A & 3) == 0 || a.record_floats > 0) && ((reinterpret_cast<uintptr_t>(a.actions) | reinterpret_cast<uintptr_t>(a.mu) |
                             reinterpret_cast<uintptr_t>(a.sigma) | reinterpret_cast<uintptr_t>(a.out_actions) |
                             reinterpret_cast<uintptr_t>(a.out_mu) | reinterpret_cast<uintptr_t>(a.out_sigma)) & 15))
         return RSLRL_E_MISALIGNED;
@@ -204,10 +292,13 @@ extern "C" int rslrl_rollout_record(const rslrl_rollout_args_t* args, rslrl_stre
     }
     int64_t copy_elems = a.N * a.A;
     for (int g = 0; g < a.n_obs; ++g) copy_elems += a.N * a.obs[g].row_floats;
-    const int copy_blocks = static_cast<int>(std::min<int64_t>(1024, std::max<int64_t>(1, ceil_div(copy_elems / 4, kBlock * 4))));
+    const int64_t cb = a.record_floats > 0 ? ceil_div(a.N, kRecRows)
+                                           : std::min<int64_t>(1024, std::max<int64_t>(1, ceil_div(copy_elems / 4, kBlock * 4)));
+    if (cb > INT32_MAX / 2) return RSLRL_E_INVALID_ARGUMENT;
+    const int copy_blocks = static_cast<int>(cb);
     const int64_t row_blocks = ceil_div(a.N, kBlock);
     if (row_blocks + copy_blocks > INT32_MAX) return RSLRL_E_INVALID_ARGUMENT;
     hipLaunchKernelGGL(rollout_record_kernel, dim3(static_cast<unsigned>(copy_blocks + row_blocks)), dim3(kBlock), lds,
-                       reinterpret_cast<hipStream_t>(stream), a, copy_blocks);
+                       reinterpret_cast<hipStream_t>(stream), a, copy_blocks, rs);
     return launch_status();
 }

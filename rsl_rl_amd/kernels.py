@@ -19,6 +19,8 @@ __all__ = [
     "normalize_advantages_",
     "randperm_mt19937",
     "gather_rows",
+    "gather_records",
+    "record_scatter_columns",
     "ppo_loss_fwd_bwd",
     "PPOLossFunction",
     "rollout_record",
@@ -228,6 +230,52 @@ def gather_rows(pairs, indices: torch.Tensor):
     _lib.check(rc, "rslrl_gather_rows")
 
 
+def gather_records(records: torch.Tensor, fields, indices: torch.Tensor):
+    """Mini-batch gather over transition records (include/rslrl_amd.h rslrl_gather_records).
+
+    records: [..., R] contiguous fp32 (one record of R floats per env-step, R % 4 == 0); fields: list of
+    (offset, width, dst [count, width] contiguous fp32); dst[r] = records.view(-1, R)[indices[r], offset:offset+width].
+    """
+    if len(fields) > _lib.MAX_GATHER_FIELDS:
+        raise ValueError(f"gather_records: at most {_lib.MAX_GATHER_FIELDS} fields per launch")
+    _require_device(records, indices, *[f[2] for f in fields])
+    if records.dtype != torch.float32 or not records.is_contiguous():
+        raise ValueError("gather_records: records must be contiguous fp32")
+    if indices.dtype != torch.int32 or not indices.is_contiguous():
+        raise ValueError("gather_records: indices must be contiguous int32")
+    R = records.shape[-1]
+    count = indices.numel()
+    arr = (_lib.RecordField * max(len(fields), 1))()
+    used, moved = 0, 0
+    for i, (off, width, dst) in enumerate(fields):
+        if dst.dtype != torch.float32 or not dst.is_contiguous() or dst.numel() != count * width:
+            raise ValueError("gather_records: dst must be contiguous fp32 [count, width]")
+        arr[i] = _lib.RecordField(int(off), int(width), dst.data_ptr())
+        used = max(used, off + width)
+        moved += 8 * width * count
+    dev = indices.device
+    with timer.span("gather_rows", dev, moved + 4 * count):
+        rc = _lib.lib().rslrl_gather_records(_ptr(records), R, arr, len(fields), _ptr(indices), count,
+                                             ctypes.c_void_p(_stream(dev)))
+    _lib.check(rc, "rslrl_gather_records")
+
+
+def record_scatter_columns(records: torch.Tensor, offset: int, columns):
+    """records.view(-1, R)[:, offset + j] = columns[j].view(-1) for up to 4 contiguous fp32 columns."""
+    _require_device(records, *columns)
+    if records.dtype != torch.float32 or not records.is_contiguous():
+        raise ValueError("record_scatter_columns: records must be contiguous fp32")
+    R = records.shape[-1]
+    n = records.numel() // R
+    if len(columns) > 4 or any(c.dtype != torch.float32 or not c.is_contiguous() or c.numel() != n for c in columns):
+        raise ValueError("record_scatter_columns: up to 4 contiguous fp32 columns of one value per record")
+    ptrs = (ctypes.c_void_p * 4)(*[c.data_ptr() for c in columns])
+    with timer.span("record_scatter", records.device, 8 * len(columns) * n):
+        rc = _lib.lib().rslrl_record_scatter_columns(_ptr(records), R, int(offset), ptrs, len(columns), n,
+                                                     ctypes.c_void_p(_stream(records.device)))
+    _lib.check(rc, "rslrl_record_scatter_columns")
+
+
 # ------------------------------------------------------------------------------------------------
 # ppo.py:221-315 + backward of :368
 # ------------------------------------------------------------------------------------------------
@@ -352,10 +400,11 @@ def pack_rnd_net(mlp) -> torch.Tensor:
 
 def rollout_record(step, *, obs_pairs, actions, mu, sigma, values, rewards, dones, time_outs, gamma,
                    out_actions, out_rewards, out_dones, out_values, out_logp, out_mu, out_sigma,
-                   extra_reward=None, rnd=None, intrinsic_out=None):
+                   extra_reward=None, rnd=None, intrinsic_out=None, out_records=None):
     """One launch for the transition of env step `step` (ppo.py:142-169 + rollout_storage.py:77-103).
 
-    obs_pairs: [(src [N, d], dst [N, d]), ...] observation groups to store.  rnd: None or a dict with
+    obs_pairs: [(src [N, d], dst [N, d]), ...] observation groups to store.  out_records [N, R]: the obs, actions,
+    mu and sigma destinations are fields of these transition records (written whole, zeros elsewhere).  rnd: None or a dict with
     keys obs [N, in], target / predictor (packed, pack_rnd_net), hidden, out, weight, and optionally
     state_mean / state_std / state_eps.  Returns nothing; all outputs are written in place."""
     _require_device(actions, mu, values, rewards)
@@ -407,6 +456,10 @@ def rollout_record(step, *, obs_pairs, actions, mu, sigma, values, rewards, done
     a.out_actions, a.out_rewards, a.out_dones = out_actions.data_ptr(), out_rewards.data_ptr(), out_dones.data_ptr()
     a.out_values, a.out_logp = out_values.data_ptr(), out_logp.data_ptr()
     a.out_mu, a.out_sigma = out_mu.data_ptr(), out_sigma.data_ptr()
+    if out_records is not None:
+        if out_records.dim() != 2 or out_records.shape[0] != N or not out_records.is_contiguous():
+            raise ValueError("rollout_record: out_records must be contiguous [N, R]")
+        a.record_floats, a.out_records = out_records.shape[1], out_records.data_ptr()
     # algorithmic bytes per env (SURVEY §8d style): obs groups in+out, actions/mu in+out, sigma out (+in if
     # per row), values/rewards/dones/time-outs in, reward/value/log-prob/done out
     obs_b = sum(8 * src.shape[-1] for src, _ in obs_pairs)

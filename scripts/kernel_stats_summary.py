@@ -23,7 +23,8 @@ FAMILIES = [
     ("ppo_loss", r"ppo_loss_kernel"),
     ("gae_scan", r"gae_scan_kernel"),
     ("adv_normalize", r"adv_normalize_kernel|moments_kernel"),
-    ("gather_rows", r"gather_rows_kernel"),
+    ("gather_rows", r"gather_rows_kernel|gather_records_kernel"),
+    ("record_scatter", r"record_scatter_kernel"),
     ("hipBLASLt GEMM", r"^Cijk_"),
     ("torch reduce", r"reduce_kernel"),
     ("torch multi_tensor (optimizer/clip)", r"multi_tensor_apply"),

@@ -23,6 +23,8 @@ SHORT = {
     "adv_normalize_kernel": "adv_normalize",
     "moments_kernel": "moments",
     "gather_rows_kernel": "gather_rows",
+    "gather_records_kernel": "gather_rows",
+    "record_scatter_kernel": "record_scatter",
     "rollout_record_kernel": "rollout_record",
     "mlp_gemm_x6_kernel<1": "x6_fwd_elu",
     "mlp_gemm_x6_kernel<2": "x6_dgrad_elu",

@@ -102,3 +102,76 @@ def test_prefetched_permutation_matches_plain_draws(cuda_device):
         expect = torch.randperm(n, generator=ref)
         assert torch.equal(st.last_indices.cpu().long(), expect), k
         assert torch.equal(st.perm_generator.get_state(), ref.get_state()), k
+
+
+@pytest.mark.parametrize("R,fields", [
+    (96, [(0, 48), (48, 12), (84, 1), (85, 1), (86, 1), (87, 1), (60, 12), (72, 12)]),  # C3's record
+    (32, [(0, 3), (3, 5), (8, 4), (13, 1)]),  # odd widths / offsets: 4-byte path
+    (160, [(0, 132), (132, 4), (136, 1), (140, 8)]),  # > 128 used floats: 32-row tiles
+    (256, [(0, 256)]),  # the maximum
+])
+def test_gather_records_vs_oracle(R, fields, cuda_device):
+    rng = np.random.default_rng(R)
+    rows, count = 3000, 2777  # a ragged last tile
+    src = rng.standard_normal((rows, R), dtype=np.float32)
+    idx = rng.integers(0, rows, count).astype(np.int32)
+    rec = torch.from_numpy(src).to(cuda_device)
+    outs = [(o, w, torch.empty(count, w, device=cuda_device)) for o, w in fields]
+    kernels.gather_records(rec, outs, torch.from_numpy(idx).to(cuda_device))
+    for o, w, d in outs:
+        ref = O.gather_rows(np.ascontiguousarray(src[:, o:o + w]), idx.astype(np.int64))
+        assert np.array_equal(d.cpu().numpy(), ref), (o, w)
+
+
+@pytest.mark.parametrize("ncols,offset", [(4, 84), (3, 5), (1, 31)])
+def test_record_scatter_columns(ncols, offset, cuda_device):
+    rng = np.random.default_rng(ncols)
+    T, N, R = 5, 1031, 96 if offset > 31 else 32
+    base = rng.standard_normal((T, N, R), dtype=np.float32)
+    rec = torch.from_numpy(base).to(cuda_device)
+    cols = [torch.from_numpy(rng.standard_normal((T, N, 1), dtype=np.float32)).to(cuda_device) for _ in range(ncols)]
+    kernels.record_scatter_columns(rec, offset, cols)
+    ref = base.copy()
+    for j, c in enumerate(cols):
+        ref[:, :, offset + j] = c.cpu().numpy()[:, :, 0]
+    assert np.array_equal(rec.cpu().numpy(), ref)
+
+
+def _fill_storage(st, rng, T, N, groups, A):
+    for k, d in groups.items():
+        st.observations[k].copy_(torch.from_numpy(rng.standard_normal((T, N, d), dtype=np.float32)))
+    for k in ("actions", "values", "returns", "actions_log_prob", "advantages", "mu", "sigma"):
+        shape = (T, N, A) if k in ("actions", "mu", "sigma") else (T, N, 1)
+        getattr(st, k).copy_(torch.from_numpy(rng.standard_normal(shape, dtype=np.float32)))
+
+
+def test_record_storage_minibatches_bit_exact(cuda_device, monkeypatch):
+    """The record layout (two observation groups, A = 8) yields exactly the reference's
+    field.flatten(0, 1)[indices[mb]] for every field, like the one-buffer-per-field layout."""
+    T, N, A, M, E = 6, 333, 8, 3, 2
+    groups = {"policy": 20, "critic": 12}
+    obs0 = {k: torch.zeros(N, d) for k, d in groups.items()}
+    st = RolloutStorage("rl", N, T, obs0, [A], cuda_device)
+    assert st.records is not None and st.records.shape[-1] == 64  # 20 + 12 + 24 + 4 = 60 -> 64
+    monkeypatch.setenv("RSLRL_RECORD_LAYOUT", "0")
+    soa = RolloutStorage("rl", N, T, obs0, [A], cuda_device)
+    assert soa.records is None
+    _fill_storage(st, np.random.default_rng(3), T, N, groups, A)
+    _fill_storage(soa, np.random.default_rng(3), T, N, groups, A)
+    st.perm_generator = torch.Generator().manual_seed(4)
+    soa.perm_generator = torch.Generator().manual_seed(4)
+    got = list(st.mini_batch_generator(M, E))
+    ref = list(soa.mini_batch_generator(M, E))
+    idx = st.last_indices.cpu().long()
+    mb = (T * N) // M
+    flat = {k: getattr(soa, k).flatten(0, 1).cpu() for k in ("actions", "values", "advantages", "returns",
+                                                           "actions_log_prob", "mu", "sigma")}
+    names = ["actions", "values", "advantages", "returns", "actions_log_prob", "mu", "sigma"]
+    for j, (g, r) in enumerate(zip(got, ref)):
+        sel = idx[(j % M) * mb:(j % M + 1) * mb]
+        for k in groups:
+            assert torch.equal(g[0][k].cpu(), r[0][k].cpu())
+            assert torch.equal(g[0][k].cpu(), soa.observations[k].flatten(0, 1).cpu()[sel])
+        for nm, a, b in zip(names, g[1:8], r[1:8]):
+            assert torch.equal(a.cpu(), b.cpu()), (j, nm)
+            assert torch.equal(a.cpu(), flat[nm][sel]), (j, nm)

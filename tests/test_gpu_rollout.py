@@ -36,12 +36,17 @@ def _build(m, z, dev):
     return alg
 
 
+@pytest.mark.parametrize("layout", ["records", "fields"])
 @pytest.mark.parametrize("case", ["rnd_c5like", "rnd_statenorm_q3", "plain_timeouts", "rnd_linear_sched"])
-def test_rollout_record_matches_reference(case, golden_meta, cuda_device):
+def test_rollout_record_matches_reference(case, layout, golden_meta, cuda_device, monkeypatch):
+    """Both storage layouts: transition records (the default here: every width a multiple of 4) and one
+    buffer per field (RSLRL_RECORD_LAYOUT=0)."""
+    monkeypatch.setenv("RSLRL_RECORD_LAYOUT", "1" if layout == "records" else "0")
     m = golden_meta["rollout"][case]
     z = np.load(golden_path(f"rollout_{case}.npz"))
     dev = cuda_device
     alg = _build(m, z, dev)
+    assert (alg.storage.records is not None) == (layout == "records")
     g = lambda k: torch.from_numpy(z[k]).to(dev)  # noqa: E731
     ddtype = {"int64": torch.int64, "bool": torch.bool, "float": torch.float32}[m["dones_dtype"]]
     for t in range(m["T"]):
@@ -124,3 +129,32 @@ def test_act_sampling_equals_torch_normal(cuda_device):
     torch.cuda.set_rng_state(state)
     ref = pol.distribution.sample()
     assert torch.equal(ours, ref)
+
+
+@pytest.mark.parametrize("per_row", [False, True])
+def test_rollout_record_kernel_record_mode(per_row, cuda_device):
+    """Record mode: obs groups, actions, mu and sigma land in their record fields (row stride R), the rest of
+    each record is zero-filled (whole records: no partial-line writes); the scalar outputs as in the plain mode."""
+    torch.manual_seed(6)
+    dev = cuda_device
+    N, O1, O2, A, R = 777, 8, 20, 12, 96
+    rec = torch.full((N, R), 7.0, device=dev)
+    offs = {"o1": 0, "o2": 8, "actions": 28, "mu": 40, "sigma": 52}
+    obs1, obs2 = torch.randn(N, O1, device=dev), torch.randn(N, O2, device=dev)
+    actions, mu = torch.randn(N, A, device=dev), torch.randn(N, A, device=dev)
+    sigma = (0.5 + torch.rand(N, A, device=dev)) if per_row else (0.5 + torch.rand(A, device=dev))
+    values, rewards = torch.randn(N, 1, device=dev), torch.randn(N, device=dev)
+    dones = torch.rand(N, device=dev) < 0.3
+    r, v, lp = torch.empty(N, 1, device=dev), torch.empty(N, 1, device=dev), torch.empty(N, 1, device=dev)
+    d = torch.empty(N, 1, dtype=torch.uint8, device=dev)
+    f = lambda k, w: rec[:, offs[k]:offs[k] + w]  # noqa: E731
+    kernels.rollout_record(0, obs_pairs=[(obs1, f("o1", O1)), (obs2, f("o2", O2))], actions=actions, mu=mu,
+                           sigma=sigma, values=values, rewards=rewards, dones=dones, time_outs=None, gamma=0.97,
+                           out_actions=f("actions", A), out_rewards=r, out_dones=d, out_values=v, out_logp=lp,
+                           out_mu=f("mu", A), out_sigma=f("sigma", A), out_records=rec)
+    torch.cuda.synchronize()
+    assert torch.equal(f("o1", O1), obs1) and torch.equal(f("o2", O2), obs2)
+    assert torch.equal(f("actions", A), actions) and torch.equal(f("mu", A), mu)
+    assert torch.equal(f("sigma", A), sigma.expand(N, A))
+    assert (rec[:, 64:] == 0).all()  # past the fields: the record is written whole
+    assert torch.equal(v, values) and torch.equal(d[:, 0], dones.to(torch.uint8))
