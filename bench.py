@@ -42,7 +42,7 @@ BF16_MFMA_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA at 2.4 GHz (MI355X_MICROARCH.m
 X6_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 6  # fp32-equivalent peak of the 6-product split-bf16 GEMMs
 H3_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 3  # ... of the 3-product split-fp16 GEMMs (fp16 MFMA = bf16 rate)
 FP32_MFMA_PEAK_TFLOPS = 157.3
-HOT_PATH = ("gae_scan", "adv_normalize", "record_scatter", "gather_rows", "ppo_loss", "rollout_record")
+HOT_PATH = ("gae_scan", "adv_normalize", "record_fill_slot", "gather_rows", "ppo_loss", "rollout_record")
 C3_ENVS = 65536  # BASELINE.json configs[2] (N=1 headline)
 with open(os.path.join(ROOT, "BASELINE.json")) as _f:
     BASELINE_METRIC = json.load(_f)["metric"]

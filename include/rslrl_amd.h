@@ -99,8 +99,11 @@ int rslrl_gather_rows(const rslrl_gather_field_t* fields /* host array */, int32
  * rslrl_gather_records: for each field f, dst_f[r] = records[indices[r]][offset_f : offset_f + width_f]
  *   (dst_f contiguous [num_rows, width_f]); the record's first max(offset_f + width_f) floats (<= 256)
  *   are read once per row.  indices: device int32 [num_rows], each in [0, number of records).
- * rslrl_record_scatter_columns: records[i][offset + j] = columns[j][i] for i < n, j < num_columns (<= 4);
- *   puts the [T, N] scalar fields (values, log-prob, returns, advantages) into their record slots.
+ * rslrl_record_fill_slot: records[i][offset : offset + slot_floats] = row_src[i][0 : row_width] (contiguous
+ *   [n, row_width]), then columns[j][i] for j < num_columns (<= 4), then zeros -- the slot written whole.
+ *   RolloutStorage's slot is {value, log-prob, return, advantage, 0, 0, 0, 0}, a 32-byte piece of its own
+ *   filled once per update (written whole: no partial-piece writes).
+ *   offset, slot_floats % 4 == 0, slot_floats <= 64.
  * ----------------------------------------------------------------------------------------------*/
 #define RSLRL_MAX_RECORD_FLOATS 256
 typedef struct {
@@ -111,9 +114,10 @@ typedef struct {
 
 int rslrl_gather_records(const float* records, int64_t record_floats, const rslrl_record_field_t* fields /* host */,
                          int32_t num_fields, const int32_t* indices, int64_t num_rows, rslrl_stream_t stream);
-int rslrl_record_scatter_columns(float* records, int64_t record_floats, int64_t offset,
-                                 const float* const* columns /* host array of device pointers */,
-                                 int32_t num_columns, int64_t n, rslrl_stream_t stream);
+int rslrl_record_fill_slot(float* records, int64_t record_floats, int64_t offset, int32_t slot_floats,
+                           const float* row_src, int32_t row_width,
+                           const float* const* columns /* host array of device pointers */, int32_t num_columns,
+                           int64_t n, rslrl_stream_t stream);
 
 /* ------------------------------------------------------------------------------------------------
  * Fused PPO loss forward + backward for one mini-batch -- rsl_rl/algorithms/ppo.py:221-223
@@ -371,7 +375,8 @@ int rslrl_linear_wgrad_bias(const float* dz, const float* dz_amax, const float* 
  * record_floats > 0: the copied fields (obs groups, actions, mu, sigma) live in transition records
  * (rslrl_gather_records) starting at out_records: each destination is a field of record 0 (in that order,
  * not overlapping) with row stride record_floats; record_floats, A and every obs width must be multiples
- * of 4 with 16-byte aligned pointers.  The launch writes the records whole: units outside the fields get 0.
+ * of 4 with 16-byte aligned pointers.  The launch writes the records whole: units outside the fields get 0
+ * (no partial-line writes).
  * RND nets: Linear(in -> hidden) + ELU + Linear(hidden -> out), in, hidden <= 64, out <= 8, packed per
  * net as [W1 (hidden x in) | b1 | W2 (out x hidden) | b2]; optional state normalisation
  * (s - mean) / (std + eps).  dones / time_outs dtype: RSLRL_DTYPE_*; time_outs may be NULL.

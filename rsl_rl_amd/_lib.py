@@ -32,7 +32,7 @@ EXPORTED_SYMBOLS = (
     "rslrl_randperm_mt19937",
     "rslrl_gather_rows",
     "rslrl_gather_records",
-    "rslrl_record_scatter_columns",
+    "rslrl_record_fill_slot",
     "rslrl_ppo_loss_workspace_bytes",
     "rslrl_ppo_loss_fwd_bwd",
     "rslrl_linear_tiles",
@@ -250,8 +250,8 @@ def _declare(L):
     L.rslrl_gather_rows.argtypes = [ctypes.POINTER(GatherField), I32, P, I64, P]
     L.rslrl_gather_records.restype = ctypes.c_int
     L.rslrl_gather_records.argtypes = [P, I64, ctypes.POINTER(RecordField), I32, P, I64, P]
-    L.rslrl_record_scatter_columns.restype = ctypes.c_int
-    L.rslrl_record_scatter_columns.argtypes = [P, I64, I64, ctypes.POINTER(ctypes.c_void_p), I32, I64, P]
+    L.rslrl_record_fill_slot.restype = ctypes.c_int
+    L.rslrl_record_fill_slot.argtypes = [P, I64, I64, I32, P, I32, ctypes.POINTER(ctypes.c_void_p), I32, I64, P]
     L.rslrl_ppo_loss_workspace_bytes.restype = SZ
     L.rslrl_ppo_loss_workspace_bytes.argtypes = [I64, I32]
     L.rslrl_ppo_loss_fwd_bwd.restype = ctypes.c_int

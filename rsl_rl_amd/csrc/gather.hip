@@ -175,20 +175,28 @@ __global__ __launch_bounds__(kBlock) void gather_records_kernel(RecParams p, con
     }
 }
 
-__global__ __launch_bounds__(kBlock) void record_scatter_kernel(float* __restrict__ rec, int64_t R, int64_t offset,
-                                                                const float* c0, const float* c1, const float* c2,
-                                                                const float* c3, int nc, int vec, int64_t n) {
-    const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
-    for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < n; i += stride) {
-        float* d = rec + i * R + offset;
-        if (vec) {
-            *reinterpret_cast<float4*>(d) = make_float4(c0[i], c1[i], c2[i], c3[i]);
-        } else {
-            d[0] = c0[i];
-            if (nc > 1) d[1] = c1[i];
-            if (nc > 2) d[2] = c2[i];
-            if (nc > 3) d[3] = c3[i];
+// One thread per 16-byte unit of a slot: consecutive lanes cover a slot's units in order, so each slot
+// leaves the store as whole 64-byte pieces (partial ones are read-modify-writes at the HBM).
+__global__ __launch_bounds__(kBlock) void record_fill_slot_kernel(float* __restrict__ rec, int64_t R, int64_t offset,
+                                                                  int su, const float* __restrict__ row, int rw,
+                                                                  const float* c0, const float* c1, const float* c2,
+                                                                  const float* c3, int nc, uint32_t total) {
+    const uint32_t stride = gridDim.x * kBlock;
+    for (uint32_t k = blockIdx.x * kBlock + threadIdx.x; k < total; k += stride) {
+        const uint32_t i = k / static_cast<uint32_t>(su);
+        const int u = static_cast<int>(k - i * su);
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int f = 4 * u + e;
+            const int c = f - rw;
+            v[e] = f < rw ? row[static_cast<int64_t>(i) * rw + f]
+                          : c == 0 && nc > 0 ? c0[i]
+                          : c == 1 && nc > 1 ? c1[i]
+                          : c == 2 && nc > 2 ? c2[i]
+                          : c == 3 && nc > 3 ? c3[i] : 0.f;
         }
+        *reinterpret_cast<float4*>(rec + static_cast<int64_t>(i) * R + offset + 4 * u) = make_float4(v[0], v[1], v[2], v[3]);
     }
 }
 
@@ -226,24 +234,27 @@ extern "C" int rslrl_gather_records(const float* records, int64_t record_floats,
     return launch_status();
 }
 
-extern "C" int rslrl_record_scatter_columns(float* records, int64_t record_floats, int64_t offset,
-                                            const float* const* columns, int32_t num_columns, int64_t n,
-                                            rslrl_stream_t stream) {
-    if (n < 0 || num_columns < 0 || num_columns > 4 || record_floats <= 0 || offset < 0 ||
-        offset + num_columns > record_floats)
+extern "C" int rslrl_record_fill_slot(float* records, int64_t record_floats, int64_t offset, int32_t slot_floats,
+                                      const float* row_src, int32_t row_width, const float* const* columns,
+                                      int32_t num_columns, int64_t n, rslrl_stream_t stream) {
+    if (n < 0 || record_floats <= 0 || (record_floats & 3) || offset < 0 || (offset & 3) || slot_floats <= 0 ||
+        (slot_floats & 3) || slot_floats > 64 || offset + slot_floats > record_floats || row_width < 0 ||
+        num_columns < 0 || num_columns > 4 || row_width + num_columns > slot_floats)
         return RSLRL_E_INVALID_ARGUMENT;
-    if (n == 0 || num_columns == 0) return RSLRL_OK;
-    if (!records || !columns) return RSLRL_E_INVALID_ARGUMENT;
+    if (n == 0) return RSLRL_OK;
+    if (!records || (row_width > 0 && !row_src) || (num_columns > 0 && !columns)) return RSLRL_E_INVALID_ARGUMENT;
+    if (reinterpret_cast<uintptr_t>(records) & 15) return RSLRL_E_MISALIGNED;
     const float* c[4] = {nullptr, nullptr, nullptr, nullptr};
     for (int j = 0; j < num_columns; ++j) {
         if (!columns[j]) return RSLRL_E_INVALID_ARGUMENT;
         c[j] = columns[j];
     }
-    const int vec = num_columns == 4 && (record_floats % 4 == 0) && (offset % 4 == 0) &&
-                    ((reinterpret_cast<uintptr_t>(records) & 15) == 0);
-    const int64_t nb = std::min<int64_t>(ceil_div(n, kBlock), 4096);
-    hipLaunchKernelGGL(record_scatter_kernel, dim3(static_cast<unsigned>(nb)), dim3(kBlock), 0,
-                       reinterpret_cast<hipStream_t>(stream), records, record_floats, offset, c[0], c[1], c[2], c[3],
-                       num_columns, vec, n);
+    const int su = slot_floats / 4;
+    if (n * su > UINT32_MAX / 2) return RSLRL_E_INVALID_ARGUMENT;
+    const uint32_t total = static_cast<uint32_t>(n * su);
+    const int64_t nb = std::min<int64_t>(ceil_div(total, kBlock), 8192);
+    hipLaunchKernelGGL(record_fill_slot_kernel, dim3(static_cast<unsigned>(nb)), dim3(kBlock), 0,
+                       reinterpret_cast<hipStream_t>(stream), records, record_floats, offset, su, row_src, row_width,
+                       c[0], c[1], c[2], c[3], num_columns, total);
     return launch_status();
 }

@@ -20,7 +20,7 @@ __all__ = [
     "randperm_mt19937",
     "gather_rows",
     "gather_records",
-    "record_scatter_columns",
+    "record_fill_slot",
     "ppo_loss_fwd_bwd",
     "PPOLossFunction",
     "rollout_record",
@@ -260,20 +260,26 @@ def gather_records(records: torch.Tensor, fields, indices: torch.Tensor):
     _lib.check(rc, "rslrl_gather_records")
 
 
-def record_scatter_columns(records: torch.Tensor, offset: int, columns):
-    """records.view(-1, R)[:, offset + j] = columns[j].view(-1) for up to 4 contiguous fp32 columns."""
-    _require_device(records, *columns)
+def record_fill_slot(records: torch.Tensor, offset: int, slot_floats: int, row=None, columns=()):
+    """records.view(-1, R)[:, offset:offset + slot_floats] = [row | columns... | zeros] per record
+    (include/rslrl_amd.h rslrl_record_fill_slot): row [.., w] and up to 4 columns [..] contiguous fp32, one
+    entry per record."""
+    _require_device(records, row, *columns)
     if records.dtype != torch.float32 or not records.is_contiguous():
-        raise ValueError("record_scatter_columns: records must be contiguous fp32")
+        raise ValueError("record_fill_slot: records must be contiguous fp32")
     R = records.shape[-1]
     n = records.numel() // R
-    if len(columns) > 4 or any(c.dtype != torch.float32 or not c.is_contiguous() or c.numel() != n for c in columns):
-        raise ValueError("record_scatter_columns: up to 4 contiguous fp32 columns of one value per record")
+    rw = 0 if row is None else row.shape[-1]
+    for t in ([row] if row is not None else []) + list(columns):
+        if t.dtype != torch.float32 or not t.is_contiguous():
+            raise ValueError("record_fill_slot: row and columns must be contiguous fp32")
+    if (row is not None and row.numel() != n * rw) or any(c.numel() != n for c in columns) or len(columns) > 4:
+        raise ValueError("record_fill_slot: one row / value per record, at most 4 columns")
     ptrs = (ctypes.c_void_p * 4)(*[c.data_ptr() for c in columns])
-    with timer.span("record_scatter", records.device, 8 * len(columns) * n):
-        rc = _lib.lib().rslrl_record_scatter_columns(_ptr(records), R, int(offset), ptrs, len(columns), n,
-                                                     ctypes.c_void_p(_stream(records.device)))
-    _lib.check(rc, "rslrl_record_scatter_columns")
+    with timer.span("record_fill_slot", records.device, (4 * rw + 4 * len(columns) + 4 * slot_floats) * n):
+        rc = _lib.lib().rslrl_record_fill_slot(_ptr(records), R, int(offset), int(slot_floats), _ptr(row), rw, ptrs,
+                                               len(columns), n, ctypes.c_void_p(_stream(records.device)))
+    _lib.check(rc, "rslrl_record_fill_slot")
 
 
 # ------------------------------------------------------------------------------------------------

@@ -20,13 +20,13 @@ CPU randperm algorithm on `perm_generator` (default: torch's process-wide CPU ge
 reproducible under torch.manual_seed and bit-exact with the reference run on CPU.
 
 Transition records (ROCm storages of feed-forward RL with 4-multiple widths): the gathered fields of an
-env-step -- observation groups, actions, mu, sigma, and copies of value, log-prob, return and advantage --
-sit side by side in one fp32 record padded to whole 128-byte lines ([T, N, R]; 96 floats at C3).
-`observations[k]`, `actions`, `mu` and `sigma` are strided views of it (same shapes and values as the
-reference's buffers); the [T, N, 1] scalar fields stay contiguous for GAE and are copied into their record
-slots once per update.  A randomly drawn row then reads its record's own lines (1.09x the used bytes at
-C3) instead of at least one line per field (2.2x with one buffer per field).  RSLRL_RECORD_LAYOUT=0 keeps
-one buffer per field.
+env-step sit side by side in one fp32 record padded to whole 128-byte lines ([T, N, R]; 96 floats at C3):
+observation groups, actions, mu and sigma (written by the rollout; `observations[k]`, `actions`, `mu`,
+`sigma` are strided views of the records, same shapes and values as the reference's buffers), then a
+32-byte slot {value, log-prob, return, advantage, 0, 0, 0, 0} filled once per update from the contiguous
+[T, N, 1] scalar buffers (GAE wants those contiguous).  A randomly drawn row then reads its record's own
+lines (1.09x the used bytes at C3) instead of at least one line per field (2.2x with one buffer per field).
+RSLRL_RECORD_LAYOUT=0 keeps one buffer per field.
 
 The host draw (1.57M elements at C3: ~4.7 ms, with the GPU idle behind it) is computed ahead: right after a
 draw, a worker thread draws the NEXT permutation from a copy of the generator state.  The next
@@ -132,14 +132,20 @@ class RolloutStorage:
         A = actions_shape[0]
         if A % 4 or len(widths) > 4:
             return None
-        widths += [("actions", A), ("mu", A), ("sigma", A), ("scalars", 4)]
+        widths += [("actions", A), ("mu", A), ("sigma", A)]
         offs, used = {}, 0
         for name, w in widths:
             offs[name] = used
             used += w
+        # the per-update slot {value, log-prob, return, advantage, 0, 0, 0, 0}: a 32-byte piece of its own
+        # (measured on MI355X: writing it whole costs no more than the 16 bytes alone; a 64-byte slot that also
+        # carries sigma, copied per update from a buffer of its own, cost more in the rollout than it saved)
+        offs["slot"] = -(-used // 8) * 8
+        offs["slot_floats"] = 8
+        used = offs["slot"] + 4
         if used > 256:
             return None
-        return -(-used // 32) * 32, offs
+        return -(-(offs["slot"] + 8) // 32) * 32, offs
 
     # ------------------------------------------------------------------ filling (rollout_storage.py:77-125)
     def add_transitions(self, transition: Transition):
@@ -317,11 +323,11 @@ class RolloutStorage:
         p = self._packed_buffers(rows)
         if self.records is not None:
             R, offs = self.record_layout
-            o = offs["scalars"]
-            # the scalar fields' final values into their record slots, then one gather of whole records
-            kernels.record_scatter_columns(self.records, o, [self.values, self.actions_log_prob, self.returns,
-                                                             self.advantages])
             A = self.actions_shape[0]
+            o = offs["slot"]
+            # the scalar fields' final values into each record's slot, then one gather of whole records
+            kernels.record_fill_slot(self.records, o, offs["slot_floats"],
+                                     columns=[self.values, self.actions_log_prob, self.returns, self.advantages])
             fields = [(offs["obs/" + k], v.shape[-1], p["obs"][k]) for k, v in self.observations.items()]
             fields += [(offs["actions"], A, p["actions"]), (o, 1, p["values"]), (o + 1, 1, p["actions_log_prob"]),
                        (o + 2, 1, p["returns"]), (o + 3, 1, p["advantages"]), (offs["mu"], A, p["mu"]),

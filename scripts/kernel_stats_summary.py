@@ -24,7 +24,7 @@ FAMILIES = [
     ("gae_scan", r"gae_scan_kernel"),
     ("adv_normalize", r"adv_normalize_kernel|moments_kernel"),
     ("gather_rows", r"gather_rows_kernel|gather_records_kernel"),
-    ("record_scatter", r"record_scatter_kernel"),
+    ("record_fill_slot", r"record_fill_slot_kernel"),
     ("hipBLASLt GEMM", r"^Cijk_"),
     ("torch reduce", r"reduce_kernel"),
     ("torch multi_tensor (optimizer/clip)", r"multi_tensor_apply"),

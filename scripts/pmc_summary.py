@@ -24,7 +24,7 @@ SHORT = {
     "moments_kernel": "moments",
     "gather_rows_kernel": "gather_rows",
     "gather_records_kernel": "gather_rows",
-    "record_scatter_kernel": "record_scatter",
+    "record_fill_slot_kernel": "record_fill_slot",
     "rollout_record_kernel": "rollout_record",
     "mlp_gemm_x6_kernel<1": "x6_fwd_elu",
     "mlp_gemm_x6_kernel<2": "x6_dgrad_elu",

@@ -123,17 +123,21 @@ def test_gather_records_vs_oracle(R, fields, cuda_device):
         assert np.array_equal(d.cpu().numpy(), ref), (o, w)
 
 
-@pytest.mark.parametrize("ncols,offset", [(4, 84), (3, 5), (1, 31)])
-def test_record_scatter_columns(ncols, offset, cuda_device):
-    rng = np.random.default_rng(ncols)
-    T, N, R = 5, 1031, 96 if offset > 31 else 32
+@pytest.mark.parametrize("offset,slot,rw,ncols", [(80, 16, 12, 4), (48, 16, 8, 4), (4, 8, 0, 3), (0, 64, 60, 4)])
+def test_record_fill_slot(offset, slot, rw, ncols, cuda_device):
+    rng = np.random.default_rng(offset + rw)
+    T, N, R = 5, 1031, 96 if offset + slot > 64 else 64
     base = rng.standard_normal((T, N, R), dtype=np.float32)
     rec = torch.from_numpy(base).to(cuda_device)
+    row = torch.from_numpy(rng.standard_normal((T, N, rw), dtype=np.float32)).to(cuda_device) if rw else None
     cols = [torch.from_numpy(rng.standard_normal((T, N, 1), dtype=np.float32)).to(cuda_device) for _ in range(ncols)]
-    kernels.record_scatter_columns(rec, offset, cols)
+    kernels.record_fill_slot(rec, offset, slot, row=row, columns=cols)
     ref = base.copy()
+    ref[:, :, offset:offset + slot] = 0
+    if rw:
+        ref[:, :, offset:offset + rw] = row.cpu().numpy()
     for j, c in enumerate(cols):
-        ref[:, :, offset + j] = c.cpu().numpy()[:, :, 0]
+        ref[:, :, offset + rw + j] = c.cpu().numpy()[:, :, 0]
     assert np.array_equal(rec.cpu().numpy(), ref)
 
 
@@ -152,7 +156,7 @@ def test_record_storage_minibatches_bit_exact(cuda_device, monkeypatch):
     groups = {"policy": 20, "critic": 12}
     obs0 = {k: torch.zeros(N, d) for k, d in groups.items()}
     st = RolloutStorage("rl", N, T, obs0, [A], cuda_device)
-    assert st.records is not None and st.records.shape[-1] == 64  # 20 + 12 + 24 + 4 = 60 -> 64
+    assert st.records is not None and st.records.shape[-1] == 64  # 20 + 12 + 24, the 8-float slot at 56 -> 64
     monkeypatch.setenv("RSLRL_RECORD_LAYOUT", "0")
     soa = RolloutStorage("rl", N, T, obs0, [A], cuda_device)
     assert soa.records is None
