@@ -366,7 +366,8 @@ __global__ __launch_bounds__(kBlock) void fold_kernel(const IN* __restrict__ par
 // phases.  Thread (phase p, quad q) adds slices p, p + 16, ... of its float4 in fp64 with up to 16 loads in
 // flight (the one-quad-per-thread fold_kernel had 8 and one block per CU: 21 us for 67 MB), then the 16
 // phases are added in phase order through LDS.  Deterministic: the order depends on S alone.
-constexpr int kWideMinBlocks = 512;
+constexpr int kWideMinBlocks = 128;  // the first layer's 48 x 256 (+ bias) partials (193 blocks): 14.4 us in
+                                     // two fold_kernel stages; one pass keeps 64 KiB per CU in flight
 __global__ __launch_bounds__(kBlock) void fold_wide_kernel(const float* __restrict__ part, int S, int NK,
                                                            float* __restrict__ out) {
     __shared__ double red[16][16][4];

@@ -15,7 +15,9 @@
 namespace rslrl {
 namespace {
 
-constexpr int kBlocks = 128;  // fixed partition of the concatenated elements (deterministic order)
+constexpr int kBlocks = 512;  // fixed partition of the concatenated elements (deterministic order); 512 blocks
+                              // keep ~2 elements per thread at C3's 290k parameters (128: ~9 dependent
+                              // iterations per thread, 19-20 us per launch)
 constexpr int kThreadsA = 256;
 
 struct Span {
@@ -63,17 +65,32 @@ __global__ __launch_bounds__(kThreadsA) void grad_sq_kernel(rslrl_adam_args_t a,
     }
     __syncthreads();
     if (!last) return;
-    // the last block folds the kBlocks partials in a fixed order: one per thread (all loads in flight at
-    // once), wave butterflies, then the waves in order
-    static_assert(kBlocks <= kThreadsA, "one partial per thread");
-    double pv = 0.0;
-    if (threadIdx.x < kBlocks)
-        pv = __longlong_as_double(__hip_atomic_load(reinterpret_cast<unsigned long long*>(part + threadIdx.x),
-                                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    // the last block folds the kBlocks partials in a fixed order: kBlocks / kThreadsA per thread (all loads in
+    // flight at once, added in index order), wave butterflies, then the waves in order
+    static_assert(kBlocks % kThreadsA == 0, "whole partials per thread");
+    constexpr int kPer = kBlocks / kThreadsA;
+    double pl[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k)
+        pl[k] = __longlong_as_double(__hip_atomic_load(
+            reinterpret_cast<unsigned long long*>(part + threadIdx.x + k * kThreadsA), __ATOMIC_RELAXED,
+            __HIP_MEMORY_SCOPE_AGENT));
+    double pv = pl[0];
+#pragma unroll
+    for (int k = 1; k < kPer; ++k) pv += pl[k];
     pv = wave_sum(pv);
     __syncthreads();  // scratch is reused
     if ((threadIdx.x & (kWave - 1)) == 0) scratch[threadIdx.x / kWave] = pv;
     __syncthreads();
+    // torch: _foreach_add_(state_steps, 1) before the update -- one lane per tensor, all in flight at once (a
+    // loop on one lane waited out ~14 dependent load/store round trips)
+    {
+        float* sp = nullptr;
+#pragma unroll
+        for (int i = 0; i < RSLRL_ADAM_MAX_TENSORS; ++i)
+            if (static_cast<int>(threadIdx.x) == i) sp = a.t[i].step;
+        if (static_cast<int>(threadIdx.x) < a.n) *sp += 1.0f;
+    }
     if (threadIdx.x != 0) return;
     double tot = 0.0;
     for (int w = 0; w < kThreadsA / kWave; ++w) tot += scratch[w];
@@ -85,7 +102,6 @@ __global__ __launch_bounds__(kThreadsA) void grad_sq_kernel(rslrl_adam_args_t a,
         c = isnan(cf) ? cf : fminf(cf, 1.0f);
     }
     *coef = c;
-    for (int i = 0; i < a.n; ++i) *a.t[i].step += 1.0f;  // torch: _foreach_add_(state_steps, 1) before the update
     __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
