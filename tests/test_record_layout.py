@@ -1,0 +1,48 @@
+"""Host logic of the transition-record layout (RolloutStorage._record_layout): which storages get
+records and where each field sits.  CPU only (the layout is decided before any device buffer exists)."""
+
+import pytest
+import torch
+
+from rsl_rl_amd.storage.rollout_storage import RolloutStorage
+
+layout = RolloutStorage._record_layout
+
+
+def test_c3_record():
+    R, offs = layout("rl", {"policy": torch.zeros(4, 48)}, [12], "cuda")
+    assert R == 96  # 384 bytes: three 128-byte lines
+    assert offs == {"obs/policy": 0, "actions": 48, "mu": 60, "sigma": 72, "slot": 88, "slot_floats": 8}
+
+
+def test_fields_in_order_and_slot_is_a_32_byte_piece():
+    R, offs = layout("rl", {"policy": torch.zeros(4, 20), "critic": torch.zeros(4, 12)}, [8], "cuda:0")
+    assert [offs[k] for k in ("obs/policy", "obs/critic", "actions", "mu", "sigma")] == [0, 20, 32, 40, 48]
+    assert offs["slot"] % 8 == 0 and offs["slot"] >= 56 and offs["slot"] + 8 <= R and R % 32 == 0
+
+
+@pytest.mark.parametrize("kw", [
+    dict(training_type="distillation"),
+    dict(device="cpu"),
+    dict(obs={"policy": torch.zeros(4, 6)}),  # width not a multiple of 4
+    dict(actions=[3]),
+    dict(actions=[2, 2]),
+    dict(obs={f"g{i}": torch.zeros(4, 8) for i in range(5)}),  # more groups than the record launch copies
+    dict(obs={"policy": torch.zeros(4, 256)}),  # more than 256 floats
+    dict(obs={"policy": torch.zeros(4, 3, 4)}),
+])
+def test_storages_without_records(kw):
+    args = dict(training_type="rl", obs={"policy": torch.zeros(4, 48)}, actions=[12], device="cuda")
+    args.update(kw)
+    assert layout(args["training_type"], args["obs"], args["actions"], args["device"]) is None
+
+
+def test_env_switch(monkeypatch):
+    monkeypatch.setenv("RSLRL_RECORD_LAYOUT", "0")
+    assert layout("rl", {"policy": torch.zeros(4, 48)}, [12], "cuda") is None
+
+
+def test_cpu_storage_keeps_contiguous_fields():
+    st = RolloutStorage("rl", 8, 3, {"policy": torch.zeros(8, 16)}, [4], "cpu")
+    assert st.records is None
+    assert st.observations["policy"].is_contiguous() and st.actions.is_contiguous() and st.sigma.is_contiguous()
