@@ -43,6 +43,7 @@ constexpr int kThreads = 512;
 // kEpiBiasEluOut: kEpiBiasElu for the last hidden layer that also applies the (<= 32 wide) output layer to
 // the activation tile while it is in registers (x6 path only; the main loop computes C^T tiles)
 enum Epilogue { kEpiBias = 0, kEpiBiasElu = 1, kEpiEluGrad = 2, kEpiEluGradWgrad = 3, kEpiBiasEluOut = 4 };
+constexpr int kH0StageBytes = 4096;  // kEpiEluGrad: one wave's first H block staged in LDS (stage_h_block0)
 constexpr int kMaxWgradRows = 16;
 constexpr int kMaxOutWidth = 32;     // kEpiBiasEluOut
 constexpr int kStagedOutWidth = 20;  // kEpiBiasEluOut: widths whose reduction tiles fit beside the h stage
@@ -190,7 +191,19 @@ __device__ __forceinline__ void epilogue_tiles_impl(const GemmParams& p, f32x16 
             for (int r = 0; r < 16; ++r)
                 dst[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rh, voff(j, r), soff(i, r), 0));
         };
-        if constexpr (GRAD) load_hb(0, hcur);
+        if constexpr (EPI == kEpiEluGrad) {
+            if (dzo) {  // block 0 was staged in LDS during the last main-loop chunk (row-major 32 x 32)
+                // this wave's own DMA must have landed: the barrier after the main loop does not wait for loads
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                const float* hs = dzo + (threadIdx.x >> 6) * (kH0StageBytes / 4);
+#pragma unroll
+                for (int r = 0; r < 16; ++r) hcur[r] = hs[(4 * h + (r & 3) + 8 * (r >> 2)) * 32 + l32];
+            } else {
+                load_hb(0, hcur);
+            }
+        } else if constexpr (GRAD) {
+            load_hb(0, hcur);
+        }
 #pragma unroll
         for (int b = 0; b < I * J; ++b) {
             const int i = b / J, j = b % J;
@@ -298,12 +311,13 @@ __device__ __forceinline__ void epilogue_tiles_impl(const GemmParams& p, f32x16 
 // full (wave-uniform): every row and column of the tile exists.  The two paths are separate code: a
 // runtime `full ||` test per element puts a branch around every store, and the compiler then waits
 // vmcnt(0) before each store (64 serialised stores per wave: the epilogue ran 3x longer).
+// h0 (kEpiEluGrad, full tiles): the LDS copy of each wave's first H block (stage_h_block0), or nullptr
 template <int EPI, int I, int J>
 __device__ __forceinline__ void epilogue_tiles(const GemmParams& p, f32x16 (&acc)[I][J], int64_t wrow0, int wcol0,
-                                               bool full, float (&colpart)[J], float& amx) {
+                                               bool full, float (&colpart)[J], float& amx, const float* h0 = nullptr) {
     f32x2 wacc[1];  // unused (no weight-gradient accumulation)
     if (full)
-        epilogue_tiles_impl<EPI, I, J, true, 1>(p, acc, wrow0, wcol0, colpart, nullptr, 0, wacc, amx);
+        epilogue_tiles_impl<EPI, I, J, true, 1>(p, acc, wrow0, wcol0, colpart, h0, 0, wacc, amx);
     else
         epilogue_tiles_impl<EPI, I, J, false, 1>(p, acc, wrow0, wcol0, colpart, nullptr, 0, wacc, amx);
 }
@@ -652,9 +666,15 @@ __device__ __forceinline__ void store_b_regs(BStage<PL>& b, char* b_lds) {
 
 // The pipeline alone, for any fragment schedule: compute(a_lds, b_lds) reads one chunk's fragments from the
 // LDS buffer and issues its MFMAs.
-template <int BM, int PL, int NCH, int D, typename Compute>
+struct NoHook {
+    __device__ void operator()(char*) const {}
+};
+
+// last_hook(free_buffer): called before the last chunk's compute with the LDS buffer no chunk reads any more
+// (a compile-time object: a DMA into it does not make the compiler wait for it before the other buffer's reads)
+template <int BM, int PL, int NCH, int D, typename Compute, typename Hook = NoHook>
 __device__ __forceinline__ void deep_pipeline(const GemmParams& p, int64_t row0, const uint4* __restrict__ bimg,
-                                              char* (&lds)[2], float sa, Compute&& compute) {
+                                              char* (&lds)[2], float sa, Compute&& compute, Hook&& last_hook = Hook{}) {
     constexpr int planeA = BM * kX6RowB;
     AStage<BM> sa_[D];
     BStage<PL> sb;
@@ -670,6 +690,7 @@ __device__ __forceinline__ void deep_pipeline(const GemmParams& p, int64_t row0,
     __syncthreads();
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
+        if (c + 1 == NCH) last_hook(lds[(c + 1) & 1]);
         compute(lds[c & 1], lds[c & 1] + PL * planeA);
         if (c + 1 < NCH) {  // buffer (c+1)&1 was last read in chunk c-1; every wave passed the barrier after it
             // pin the use of the prefetched registers here: otherwise the scheduler hoists the scaling
@@ -693,12 +714,32 @@ __device__ __forceinline__ void deep_pipeline(const GemmParams& p, int64_t row0,
     }
 }
 
+// Input-gradient epilogue: H block (i = 0, j = 0) of each wave (32 x 32 fp32, row-major, kH0StageBytes at wave *
+// kH0StageBytes) DMA'd into the free LDS buffer during the last chunk, so the epilogue's first ELU' does not wait
+// out an HBM load (the later blocks are prefetched one ahead in registers).  Full tiles only (the caller checks).
+__device__ __forceinline__ void stage_h_block0(const GemmParams& p, int64_t row0, int wm, int wn, char* buf) {
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const float* hb = p.h + (row0 + wm * 64) * kBN + wn * 64;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int r = 8 * k + (lane >> 3), c4 = lane & 7;
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(hb + r * kBN + 4 * c4),
+                                         (__attribute__((address_space(3))) void*)(buf + wave * kH0StageBytes + k * 1024),
+                                         16, 0, 0);
+    }
+}
+
 template <int EPI, int BM, int PL, int NCH, int D, typename Frag>
 __device__ __forceinline__ void h3_deep_loop(const GemmParams& p, int64_t row0, const uint4* __restrict__ bimg,
                                              char* (&lds)[2], f32x16 (&acc)[BM / 64][2], float sa, int wm,
-                                             int wn, int l32, int h) {
+                                             int wn, int l32, int h, bool stage_h0 = false) {
     constexpr int I = BM / 64;
     constexpr int planeA = BM * kX6RowB;
+    auto hook = [&](char* free_buf) {
+        if constexpr (EPI == kEpiEluGrad && PL == 3)
+            if (stage_h0) stage_h_block0(p, row0, wm, wn, free_buf);
+    };
     deep_pipeline<BM, PL, NCH, D>(p, row0, bimg, lds, sa, [&](const char* a_lds, const char* b_lds) {
         Frag bf[2][PL];
 #pragma unroll
@@ -718,7 +759,7 @@ __device__ __forceinline__ void h3_deep_loop(const GemmParams& p, int64_t row0, 
                     acc[i][j] = Arith<PL>::mfma(af, bf[j], acc[i][j]);
             }
         }
-    });
+    }, hook);
 }
 
 // 128 rows x 256 columns per workgroup: waves 2 (M) x 4 (N) of 64 x 64 (2 x 2 MFMA tiles); MINW = 4:
@@ -788,9 +829,16 @@ __device__ __forceinline__ void mlp_gemm_x6_body(GemmParams p, const uint4* __re
 
     const float sa = PL == 2 ? h3_scale(*p.a_amax) : 1.f;
     bool deep = false;
+    // x6 input gradient on a full tile: each wave's first H block goes to the free LDS buffer during the last
+    // chunk (stage_h_block0); lds[0] is that buffer for the 16-chunk loop (the last chunk reads lds[1])
+    // (the same condition as the deep loop below: FULL, K = 256, p.deep -- the DMA is issued from that loop)
+    const bool stage_h0 = FULL && EPI == kEpiEluGrad && PL == 3 && (row0 + BM <= p.M) && p.N == kBN &&
+                          p.K == 16 * kKC && p.deep && p.h != nullptr;
+    static_assert(EPI != kEpiEluGrad || PL != 3 || 8 * kH0StageBytes <= bufBytes, "H block stage");
     if constexpr (FULL) {
         if (p.K == 16 * kKC && p.deep) {
-            h3_deep_loop<EPI, BM, PL, 16, PL == 2 ? kH3Depth : kX6Depth, Frag>(p, row0, bimg, lds, acc, sa, wm, wn, l32, h);
+            h3_deep_loop<EPI, BM, PL, 16, PL == 2 ? kH3Depth : kX6Depth, Frag>(p, row0, bimg, lds, acc, sa, wm, wn, l32, h,
+                                                                            stage_h0);
             deep = true;
         }
     }
@@ -1094,7 +1142,8 @@ __device__ __forceinline__ void mlp_gemm_x6_body(GemmParams p, const uint4* __re
             if (row < p.M) p.y[row * nout + o] = sum + p.obias[o];
         }
     } else {
-        epilogue_tiles<EPI, I, 2>(p, acc, row0 + wm * (BM / 2), wn * 64, full, colpart, amx);
+        epilogue_tiles<EPI, I, 2>(p, acc, row0 + wm * (BM / 2), wn * 64, full, colpart, amx,
+                                  stage_h0 && full ? reinterpret_cast<const float*>(lds[0]) : nullptr);
     }
 #ifdef RSLRL_STAMPS
     {
