@@ -688,6 +688,7 @@ __device__ __forceinline__ void deep_pipeline(const GemmParams& p, int64_t row0,
         if (d < NCH) sa_[d % D] = load_a<BM, true>(p, row0, d * kKC);
     if (NCH > 1) sb = load_b_regs<PL>(bimg, 1);
     __syncthreads();
+    constexpr bool kHook = !std::is_same_v<std::decay_t<Hook>, NoHook>;
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
         if (c + 1 == NCH) last_hook(lds[(c + 1) & 1]);
@@ -707,10 +708,13 @@ __device__ __forceinline__ void deep_pipeline(const GemmParams& p, int64_t row0,
         }
         // only LDS writes to retire (lgkmcnt); __syncthreads' release fence would also wait vmcnt(0) and drain
         // the look-ahead every chunk
-        if (c + 1 < NCH)
+        if (c + 1 < NCH) {
             asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        else
+        } else {
+            // a hook's LDS DMA may be read by other waves after the barrier, which does not wait for loads
+            if constexpr (kHook) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();  // the epilogue may reuse the LDS
+        }
     }
 }
 
@@ -737,6 +741,7 @@ __device__ __forceinline__ void h3_deep_loop(const GemmParams& p, int64_t row0, 
     constexpr int I = BM / 64;
     constexpr int planeA = BM * kX6RowB;
     auto hook = [&](char* free_buf) {
+        // (the forward's biases staged the same way measured 2-4 % slower: kept as L2 loads)
         if constexpr (EPI == kEpiEluGrad && PL == 3)
             if (stage_h0) stage_h_block0(p, row0, wm, wn, free_buf);
     };
@@ -767,7 +772,7 @@ __device__ __forceinline__ void h3_deep_loop(const GemmParams& p, int64_t row0, 
 // NR: rows of the fused weight gradient (kEpiEluGradWgrad: Nred rounded up to 4); kEpiBiasEluOut: 1 = VALU output
 // layer (<= 4 outputs), 4 = MFMA output layer (separate code: one register allocation for both spilled).
 // PL: operand planes (3: x6 bf16 on a layout-0 image; 2: h3 fp16 on a layout-2 image, A scaled from *p.a_amax).
-template <int EPI, bool FULL, int NR, int PL>
+template <int EPI, bool FULL, int NR, int PL, bool STAGE = true>
 __device__ __forceinline__ void mlp_gemm_x6_body(GemmParams p, const uint4* __restrict__ bimg) {
     static_assert(PL == 3 || EPI != kEpiEluGradWgrad, "the fused output-layer backward is x6 only");
     using Frag = typename Arith<PL>::frag;
@@ -832,8 +837,9 @@ __device__ __forceinline__ void mlp_gemm_x6_body(GemmParams p, const uint4* __re
     // x6 input gradient on a full tile: each wave's first H block goes to the free LDS buffer during the last
     // chunk (stage_h_block0); lds[0] is that buffer for the 16-chunk loop (the last chunk reads lds[1])
     // (the same condition as the deep loop below: FULL, K = 256, p.deep -- the DMA is issued from that loop)
-    const bool stage_h0 = FULL && EPI == kEpiEluGrad && PL == 3 && (row0 + BM <= p.M) && p.N == kBN &&
-                          p.K == 16 * kKC && p.deep && p.h != nullptr;
+    // STAGE = false (the pair kernel): a spill at its register budget cost more than the staged loads save
+    const bool stage_h0 = STAGE && FULL && EPI == kEpiEluGrad && PL == 3 && p.h != nullptr && (row0 + BM <= p.M) &&
+                          p.N == kBN && p.K == 16 * kKC && p.deep;
     static_assert(EPI != kEpiEluGrad || PL != 3 || 8 * kH0StageBytes <= bufBytes, "H block stage");
     if constexpr (FULL) {
         if (p.K == 16 * kKC && p.deep) {
@@ -1194,7 +1200,7 @@ struct GemmPair {
 template <int EPI, bool FULL, int PL>
 __global__ __launch_bounds__(kThreads, 4) void mlp_gemm_x6_pair_kernel(GemmPair b) {
     const int y = blockIdx.y;
-    mlp_gemm_x6_body<EPI, FULL, 4, PL>(b.p[y], b.img[y]);
+    mlp_gemm_x6_body<EPI, FULL, 4, PL, false>(b.p[y], b.img[y]);
 }
 
 // ---- the same x6 GEMM on v_mfma_f32_16x16x32_bf16 ("paired" x6).  Under load the chip holds a higher
