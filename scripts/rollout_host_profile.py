@@ -24,7 +24,7 @@ def main():
     dev = torch.device("cuda:0")
     args = types.SimpleNamespace(num_steps_per_env=24, num_obs=48, num_actions=12, hidden=256, layers=3)
     torch.manual_seed(1)
-    env = SyntheticVecEnv(65536, args.num_obs, args.num_actions, device=dev)
+    env = SyntheticVecEnv(int(os.environ.get("HP_ENVS", 65536)), args.num_obs, args.num_actions, device=dev)
     runner = OnPolicyRunner(env, bench.train_cfg(args), log_dir=None, device=dev)
     runner.learn(3)
     torch.cuda.synchronize()
@@ -48,6 +48,19 @@ def main():
     torch.cuda.synchronize()
     t2 = time.perf_counter()
     print(f"host issue {1e6 * (t1 - t0) / 24:.1f} us/step, until GPU done {1e6 * (t2 - t0) / 24:.1f} us/step")
+    # the policy half alone (act + process_env_step on a fixed env output): host issue per step
+    with torch.inference_mode(), fused_mlp.frozen_weights():
+        o2, r2, d2, e2 = env.step(alg.act(obs))
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    with torch.inference_mode(), fused_mlp.frozen_weights():
+        for _ in range(24):
+            alg.act(obs)
+            alg.process_env_step(o2, r2, d2, e2)
+    t1 = time.perf_counter()
+    alg.storage.clear()
+    torch.cuda.synchronize()
+    print(f"policy half host issue {1e6 * (t1 - t0) / 24:.1f} us/step")
     torch.cuda.synchronize()
     pr = cProfile.Profile()
     pr.enable()
@@ -56,6 +69,7 @@ def main():
     torch.cuda.synchronize()
     s = io.StringIO()
     pstats.Stats(pr, stream=s).sort_stats("tottime").print_stats(35)
+    pstats.Stats(pr, stream=s).sort_stats("cumulative").print_stats(30)
     print(s.getvalue())
 
 
