@@ -163,6 +163,8 @@ typedef struct {
     int64_t grad_sigma_stride;
     float* grad_values;
     float* stats;
+    int64_t grad_values_stride; /* elements between rows of grad_values (0 or 1: contiguous [B]); e.g. 4 writes
+                                   column 0 of a zero-padded [B, 4] buffer, the value head's padded gradient */
 } rslrl_ppo_loss_args_t;
 
 #define RSLRL_PPO_LOSS_MAX_ACTIONS 64

@@ -223,6 +223,7 @@ class PPOLossArgs(ctypes.Structure):
         ("grad_sigma_stride", ctypes.c_int64),
         ("grad_values", ctypes.c_void_p),
         ("stats", ctypes.c_void_p),
+        ("grad_values_stride", ctypes.c_int64),
     ]
 
 

@@ -58,6 +58,7 @@ struct LossParams {
     float* grad_sigma;
     int64_t grad_sigma_stride;
     float* grad_values;
+    int64_t gv_stride;  // grad_values row stride (elements)
     const float* adv_stats;  // [2] = (mean, std) when normalize_adv
     float* stats;
 };
@@ -238,7 +239,7 @@ __global__ __launch_bounds__(kBlock) void ppo_loss_kernel(LossParams p, double* 
             vterm = e * e;
             dV = -2.0f * p.g_value * e;
         }
-        p.grad_values[i] = dV;
+        p.grad_values[i * p.gv_stride] = dV;
 
         // d/dmu = g_logp (x - mu) / sigma^2;  d/dsigma = g_logp ((x - mu)^2 / sigma^3 - 1 / sigma) + g_ent / sigma
         float gmu[MAXA], gsg[MAXA];
@@ -537,7 +538,8 @@ __global__ __launch_bounds__(kBlock, quad_waves(APL, SHARED, KL)) void ppo_loss_
     const rsrc_t r_v = make_rsrc(p.values, B32 * 4u);
     const rsrc_t r_tv = make_rsrc(p.target_values, B32 * 4u);
     const rsrc_t r_ret = make_rsrc(p.returns, B32 * 4u);
-    const rsrc_t r_gv = make_rsrc(p.grad_values, B32 * 4u);
+    const rsrc_t r_gv = make_rsrc(p.grad_values, static_cast<uint32_t>(((p.B - 1) * p.gv_stride + 1) * 4));
+    const uint32_t gv_row = static_cast<uint32_t>(p.gv_stride) * 4u;
     const uint32_t mu_row = static_cast<uint32_t>(p.mu_stride) * 4u;
     const uint32_t gmu_row = static_cast<uint32_t>(p.grad_mu_stride) * 4u;
     const uint32_t sg_row = static_cast<uint32_t>(p.sigma_stride) * 4u;
@@ -666,7 +668,7 @@ __global__ __launch_bounds__(kBlock, quad_waves(APL, SHARED, KL)) void ppo_loss_
             vterm = e * e;
             dV = -2.0f * p.g_value * e;
         }
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, dV), r_gv, is * 4u, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, dV), r_gv, is * gv_row, 0, 0);
         if (vs) {
             acc_surr += fmaxf(surr, surr_c);
             acc_value += vterm;
@@ -985,6 +987,7 @@ extern "C" int rslrl_ppo_loss_fwd_bwd(const rslrl_ppo_loss_args_t* a, void* work
     p.grad_sigma = a->grad_sigma;
     p.grad_sigma_stride = a->grad_sigma_stride;
     p.grad_values = a->grad_values;
+    p.gv_stride = a->grad_values_stride > 1 ? a->grad_values_stride : 1;
     p.adv_stats = a->stats + 5;
     p.stats = a->stats;
 
@@ -1005,7 +1008,7 @@ extern "C" int rslrl_ppo_loss_fwd_bwd(const rslrl_ppo_loss_args_t* a, void* work
     const float cv = a->value_loss_coef, ce = a->entropy_coef;
     const int64_t max_row = std::max({a->mu_stride, a->grad_mu_stride, a->sigma_mode == 1 ? a->sigma_stride : 0,
                                       a->sigma_mode == 1 ? a->grad_sigma_stride : 0, static_cast<int64_t>(A)});
-    const bool fits32 = a->B * max_row * 4 < (int64_t{1} << 31);  // 32-bit buffer offsets
+    const bool fits32 = a->B * std::max(max_row, p.gv_stride) * 4 < (int64_t{1} << 31);  // 32-bit buffer offsets
     if (vec && fits32 && A % 4 == 0 && A <= 16 && use_quad(a->sigma_mode)) {
         switch (A / 4) {
             case 1: launch_quad<1>(p, nbq, part, ticket, cv, ce, st); break;

@@ -315,6 +315,13 @@ def ppo_loss_fwd_bwd(mu, sigma, values, actions, old_logp, advantages, target_va
     for t in (v_d, old_logp, advantages, target_values, returns):
         if t.numel() != B or not t.is_contiguous():
             raise ValueError("ppo_loss: [B] operands must be contiguous with B elements")
+    gv_stride = 1
+    if grad_values is not None:  # [B] / [B, 1] contiguous, or a [B, 1] column of a wider buffer
+        if grad_values.numel() != B or (grad_values.dim() == 2 and grad_values.shape[1] != 1) or grad_values.dim() > 2:
+            raise ValueError("ppo_loss: grad_values must hold B values ([B] or [B, 1])")
+        gv_stride = grad_values.stride(0) if grad_values.dim() == 2 else (1 if grad_values.is_contiguous() else 0)
+        if gv_stride < 1:
+            raise ValueError("ppo_loss: grad_values rows must be evenly spaced")
     for t in (actions, old_mu, old_sigma):
         if tuple(t.shape) != (B, A) or not t.is_contiguous():
             raise ValueError("ppo_loss: actions/old_mu/old_sigma must be contiguous [B, A]")
@@ -344,6 +351,7 @@ def ppo_loss_fwd_bwd(mu, sigma, values, actions, old_logp, advantages, target_va
     args.grad_sigma = grad_sigma.data_ptr()
     args.grad_sigma_stride = _row_stride(grad_sigma, A) if sigma_mode == 1 else 0
     args.grad_values = grad_values.data_ptr()
+    args.grad_values_stride = gv_stride
     args.stats = stats.data_ptr()
     L = _lib.lib()
     ws = _ws.get(dev, "ppo_loss", L.rslrl_ppo_loss_workspace_bytes(B, A))

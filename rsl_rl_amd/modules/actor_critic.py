@@ -186,12 +186,13 @@ class ActorCritic(nn.Module):
             return dy[:, :A], dy[:, A:]
         return torch.empty(B, A, device=mean.device, dtype=torch.float32), None
 
-    def train_backward(self, tape, g_mean, g_sigma, g_value, std, slot, side_stream=None):
+    def train_backward(self, tape, g_mean, g_sigma, g_value, std, slot, side_stream=None, g_value_padded=None):
         """Backward of train_forward given the loss gradients w.r.t. (mean, sigma, value), written into the
         gradient slots `slot(param)` (a gradient arena).  g_sigma: for the shared std the [A] gradient w.r.t.
         sigma (for log_std it is chained through exp here); for a state-dependent head the half of the actor-output
         gradient buffer (train_grad_buffers) the loss kernel wrote.  side_stream: as in train_forward (the
-        critic's backward runs there; the current stream waits for it before returning)."""
+        critic's backward runs there; the current stream waits for it before returning).  g_value_padded: a zero-padded
+        [B, 4] buffer whose column 0 is g_value (the loss kernel wrote it there), or None."""
         tape_a, tape_c, y_shape = tape
         if self.state_dependent_std:
             dy = torch.as_strided(g_mean, y_shape, (y_shape[1], 1))  # the [B, 2A] buffer behind both halves
@@ -203,19 +204,19 @@ class ActorCritic(nn.Module):
                 torch.mul(g_sigma, std, out=slot(self.log_std))
             elif g_sigma.data_ptr() != slot(self.std).data_ptr():
                 slot(self.std).copy_(g_sigma)
-        def run(mlp, tp, d):
+        def run(mlp, tp, d, d_pad=None):
             ws, bs = self._linears(mlp)
-            fused_mlp.train_backward(tp, d, outs=[(slot(w), slot(b)) for w, b in zip(ws, bs)])
+            fused_mlp.train_backward(tp, d, outs=[(slot(w), slot(b)) for w, b in zip(ws, bs)], dy_padded=d_pad)
 
         if side_stream is None:
             run(self.actor, tape_a, dy)
-            run(self.critic, tape_c, g_value.reshape(-1, 1))
+            run(self.critic, tape_c, g_value.reshape(-1, 1), g_value_padded)
             return
         main = torch.cuda.current_stream(dy.device)
         side_stream.wait_stream(main)
         g_value.record_stream(side_stream)  # written by the loss on this stream, read on the side stream
         with torch.cuda.stream(side_stream):
-            run(self.critic, tape_c, g_value.reshape(-1, 1))
+            run(self.critic, tape_c, g_value.reshape(-1, 1), g_value_padded)
         run(self.actor, tape_a, dy)
         main.wait_stream(side_stream)
 

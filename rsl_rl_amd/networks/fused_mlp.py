@@ -522,10 +522,12 @@ def train_forward(x, ws, bs):
     return y, MLPTape(hs, list(ws), dgrad_imgs, amaxes, h3, split)
 
 
-def train_backward(tape, dy, need_dx=False, need_w=None, outs=None):
+def train_backward(tape, dy, need_dx=False, need_w=None, outs=None, dy_padded=None):
     """Gradients of one MLP pass: returns (dx or None, [dW_l], [db_l]).  need_w[l]: layer l's weight gradient is
     wanted (default: all).  outs[l] = (dW destination, db destination) or None: contiguous fp32 tensors the
-    gradients are written into (a gradient arena's slots) instead of new tensors."""
+    gradients are written into (a gradient arena's slots) instead of new tensors.  dy_padded: optional contiguous
+    [B, 4k] tensor whose first columns are dy and the rest zero (the fused output-layer backward's operand; dy
+    may then be a strided view of it) -- saves the pad copy of a narrow head such as the value head."""
     hs, ws, h3 = tape.hs, tape.ws, tape.h3
     L = len(ws)
     need_w = [True] * L if need_w is None else need_w
@@ -538,18 +540,26 @@ def train_backward(tape, dy, need_dx=False, need_w=None, outs=None):
     # input-gradient epilogue then skips its column sums and their fold
     bias_wg = [l < L - 1 and need_w[l] and _bias_from_wgrad(ws[l].shape[0], hs[l].shape[1], tape.x6)
                for l in range(L)]
-    dz = dy.contiguous()
+    if dy_padded is not None and not (dy_padded.is_contiguous() and dy_padded.shape[0] == dy.shape[0]
+                                      and dy_padded.shape[1] == dy.shape[1] + (-dy.shape[1]) % 4):
+        raise ValueError("train_backward: dy_padded must be contiguous [B, round_up(dy width, 4)]")
+    dz = dy if dy_padded is not None else dy.contiguous()
     dz_amax = None
     dx = None
     for l in range(L - 1, -1, -1):
         h_in = hs[l]
         fuse_w = (_FUSE_OUT and tape.x6 and l == L - 1 and l > 0 and dz.shape[1] <= 16 and h_in.shape[1] <= MAX_WIDTH
                   and need_w[l])
+        if dy_padded is not None and l == L - 1 and not fuse_w:
+            dz = dz.contiguous()
         if fuse_w:  # output layer: dgrad + ELU' + bias grad + weight grad over one read of h (one launch)
             nred = dz.shape[1]
             K = h_in.shape[1]
             pad = (-nred) % 4
-            dzp = F.pad(dz, (0, pad)) if pad else dz
+            if dy_padded is not None:
+                dzp = dy_padded
+            else:
+                dzp = F.pad(dz, (0, pad)) if pad else dz
             want = l - 1 > 0 and h3[l - 1]
             # the kernel's [dW | db] result lands directly in the arena when weight and bias are adjacent there
             dwb_out = None
@@ -565,12 +575,16 @@ def train_backward(tape, dy, need_dx=False, need_w=None, outs=None):
                 grads_w[l], grads_b[l] = wo, bo
             else:
                 grads_w[l], grads_b[l] = dw[:nred], db_out[:nred]
-                if wo is not None:
-                    wo.copy_(grads_w[l])
-                    grads_w[l] = wo
-                if bo is not None:
-                    bo.copy_(grads_b[l])
-                    grads_b[l] = bo
+                if wo is not None and bo is not None:  # one multi-tensor copy launch for both
+                    torch._foreach_copy_([wo, bo], [grads_w[l], grads_b[l]])
+                    grads_w[l], grads_b[l] = wo, bo
+                else:
+                    if wo is not None:
+                        wo.copy_(grads_w[l])
+                        grads_w[l] = wo
+                    if bo is not None:
+                        bo.copy_(grads_b[l])
+                        grads_b[l] = bo
             continue
         if l == L - 1:
             grads_b[l] = dz.sum(0) if b_out(l) is None else torch.sum(dz, 0, out=b_out(l))

@@ -154,3 +154,24 @@ def test_autograd_function_matches_torch(cuda_device):
     assert abs(loss.item() - ref.item()) <= 1e-5 * abs(ref.item())
     for a, b in zip(g_ours, [mu.grad, std.grad, V.grad]):
         assert (a - b).abs().max().item() <= 1e-5 * b.abs().max().item() + 1e-9
+
+
+@pytest.mark.parametrize("kernel", ["quad", "lane"])
+def test_value_gradient_into_padded_column(kernel, cuda_device, monkeypatch):
+    """grad_values as column 0 of a zero-padded [B, 4] buffer (row stride 4, the value head's padded operand):
+    the same bits as the contiguous [B] output, and the other columns stay zero."""
+    monkeypatch.setenv("RSLRL_LOSS_KERNEL", kernel)
+    torch.manual_seed(3)
+    B, A = 5000, 12
+    d = cuda_device
+    mu, x, omu = (torch.randn(B, A, device=d) for _ in range(3))
+    osig = 0.5 + torch.rand(B, A, device=d)
+    sigma = 0.5 + torch.rand(A, device=d)
+    V, old_logp, adv, tv, R = (torch.randn(B, 1, device=d) for _ in range(5))
+    args = (mu, sigma, V, x, old_logp, adv, tv, R, omu, osig)
+    _, _, _, gv = kernels.ppo_loss_fwd_bwd(*args)
+    pad = torch.zeros(B, 4, device=d)
+    _, _, _, gv2 = kernels.ppo_loss_fwd_bwd(*args, grad_values=pad[:, :1])
+    torch.cuda.synchronize()
+    assert gv2.data_ptr() == pad.data_ptr()
+    assert torch.equal(pad[:, 0], gv.reshape(-1)) and (pad[:, 1:] == 0).all()
