@@ -772,7 +772,9 @@ __device__ __forceinline__ void h3_deep_loop(const GemmParams& p, int64_t row0, 
 // NR: rows of the fused weight gradient (kEpiEluGradWgrad: Nred rounded up to 4); kEpiBiasEluOut: 1 = VALU output
 // layer (<= 4 outputs), 4 = MFMA output layer (separate code: one register allocation for both spilled).
 // PL: operand planes (3: x6 bf16 on a layout-0 image; 2: h3 fp16 on a layout-2 image, A scaled from *p.a_amax).
-template <int EPI, bool FULL, int NR, int PL, bool STAGE = true>
+// KCH = 3: a kernel for K = 48 only (the first layer), whose look-ahead loop is its only main loop (one body with
+// both loop instances ran the K = 256 forward ~2 % slower)
+template <int EPI, bool FULL, int NR, int PL, bool STAGE = true, int KCH = 0>
 __device__ __forceinline__ void mlp_gemm_x6_body(GemmParams p, const uint4* __restrict__ bimg) {
     static_assert(PL == 3 || EPI != kEpiEluGradWgrad, "the fused output-layer backward is x6 only");
     using Frag = typename Arith<PL>::frag;
@@ -841,7 +843,12 @@ __device__ __forceinline__ void mlp_gemm_x6_body(GemmParams p, const uint4* __re
     const bool stage_h0 = STAGE && FULL && EPI == kEpiEluGrad && PL == 3 && p.h != nullptr && (row0 + BM <= p.M) &&
                           p.N == kBN && p.K == 16 * kKC && p.deep;
     static_assert(EPI != kEpiEluGrad || PL != 3 || 8 * kH0StageBytes <= bufBytes, "H block stage");
-    if constexpr (FULL) {
+    if constexpr (FULL && KCH == 3) {
+        // the first layer (K = 48: three chunks) on the look-ahead loop: the generic loop's per-chunk __syncthreads
+        // drains every load, which a three-chunk tile pays in full (the host launches KCH = 3 for K = 48 only)
+        h3_deep_loop<EPI, BM, PL, 3, 1, Frag>(p, row0, bimg, lds, acc, sa, wm, wn, l32, h);
+        deep = true;
+    } else if constexpr (FULL) {
         if (p.K == 16 * kKC && p.deep) {
             h3_deep_loop<EPI, BM, PL, 16, PL == 2 ? kH3Depth : kX6Depth, Frag>(p, row0, bimg, lds, acc, sa, wm, wn, l32, h,
                                                                             stage_h0);
@@ -1184,9 +1191,15 @@ __device__ __forceinline__ void mlp_gemm_x6_body(GemmParams p, const uint4* __re
     if constexpr (EPI != kEpiBiasEluOut) amax_commit(p, amx);
 }
 
-template <int EPI, bool FULL, int MINW, int NR = 4, int PL = 3>
+template <int EPI, bool FULL, int MINW, int NR = 4, int PL = 3, int KCH = 0>
 __global__ __launch_bounds__(kThreads, MINW) void mlp_gemm_x6_kernel(GemmParams p, const uint4* __restrict__ bimg) {
-    mlp_gemm_x6_body<EPI, FULL, NR, PL>(p, bimg);
+    mlp_gemm_x6_body<EPI, FULL, NR, PL, true, KCH>(p, bimg);
+}
+
+// the K = 48 kernel applies to full tiles of a forward on x6 operands with the deep loop enabled
+template <int EPI>
+bool k48_deep(const GemmParams& p, bool fullm, int pl) {
+    return (EPI == kEpiBias || EPI == kEpiBiasElu) && pl == 3 && fullm && p.K == 3 * kKC && p.deep;
 }
 
 // Two independent problems of one shape in one launch (blockIdx.y picks the problem): the rollout's actor and
@@ -1197,10 +1210,10 @@ struct GemmPair {
     const uint4* img[2];
 };
 
-template <int EPI, bool FULL, int PL>
+template <int EPI, bool FULL, int PL, int KCH = 0>
 __global__ __launch_bounds__(kThreads, 4) void mlp_gemm_x6_pair_kernel(GemmPair b) {
     const int y = blockIdx.y;
-    mlp_gemm_x6_body<EPI, FULL, 4, PL, false>(b.p[y], b.img[y]);
+    mlp_gemm_x6_body<EPI, FULL, 4, PL, false, KCH>(b.p[y], b.img[y]);
 }
 
 // ---- the same x6 GEMM on v_mfma_f32_16x16x32_bf16 ("paired" x6).  Under load the chip holds a higher
@@ -1723,6 +1736,9 @@ int launch(const GemmParams& p, const void* bimage, hipStream_t st) {
         } else if (short_k) {
             if (fullm) hipLaunchKernelGGL((mlp_gemm_x6_kernel<EPI, true, 2, 4, PL>), g, b, 0, st, p, img);
             else hipLaunchKernelGGL((mlp_gemm_x6_kernel<EPI, false, 2, 4, PL>), g, b, 0, st, p, img);
+        } else if (k48_deep<EPI>(p, fullm, PL)) {
+            if constexpr (PL == 3 && (EPI == kEpiBias || EPI == kEpiBiasElu))
+                hipLaunchKernelGGL((mlp_gemm_x6_kernel<EPI, true, 4, 4, PL, 3>), g, b, 0, st, p, img);
         } else if (PL != 3 || !launch_x6s<EPI>(p, img, fullm, g, st)) {
             if (fullm) hipLaunchKernelGGL((mlp_gemm_x6_kernel<EPI, true, 4, 4, PL>), g, b, 0, st, p, img);
             else hipLaunchKernelGGL((mlp_gemm_x6_kernel<EPI, false, 4, 4, PL>), g, b, 0, st, p, img);
@@ -1966,6 +1982,12 @@ int launch_pair(const GemmPair& b, bool fullm, hipStream_t st) {
     const int64_t tiles = ceil_div(b.p[0].M, kBM);
     if (tiles > INT32_MAX) return RSLRL_E_INVALID_ARGUMENT;
     const dim3 g(static_cast<unsigned>(tiles), 2), blk(kThreads);
+    if constexpr (PL == 3 && (EPI == kEpiBias || EPI == kEpiBiasElu)) {
+        if (k48_deep<EPI>(b.p[0], fullm, PL)) {  // both problems share the shape and the op
+            hipLaunchKernelGGL((mlp_gemm_x6_pair_kernel<EPI, true, PL, 3>), g, blk, 0, st, b);
+            return launch_status();
+        }
+    }
     if (fullm) hipLaunchKernelGGL((mlp_gemm_x6_pair_kernel<EPI, true, PL>), g, blk, 0, st, b);
     else hipLaunchKernelGGL((mlp_gemm_x6_pair_kernel<EPI, false, PL>), g, blk, 0, st, b);
     return launch_status();
