@@ -668,6 +668,7 @@ __global__ __launch_bounds__(kBlock, quad_waves(APL, SHARED, KL)) void ppo_loss_
             vterm = e * e;
             dV = -2.0f * p.g_value * e;
         }
+        // (stride 4: whole {dV, 0, 0, 0} rows measured slower than the 4-byte writes: 34.4 vs 32.2 us at C3)
         __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, dV), r_gv, is * gv_row, 0, 0);
         if (vs) {
             acc_surr += fmaxf(surr, surr_c);

@@ -158,8 +158,8 @@ def test_autograd_function_matches_torch(cuda_device):
 
 @pytest.mark.parametrize("kernel", ["quad", "lane"])
 def test_value_gradient_into_padded_column(kernel, cuda_device, monkeypatch):
-    """grad_values as column 0 of a zero-padded [B, 4] buffer (row stride 4, the value head's padded operand):
-    the same bits as the contiguous [B] output, and the other columns stay zero."""
+    """grad_values as column 0 of a [B, 4] buffer (row stride 4, the value head's padded operand): the same bits
+    as the contiguous [B] output; the other columns are left as they were."""
     monkeypatch.setenv("RSLRL_LOSS_KERNEL", kernel)
     torch.manual_seed(3)
     B, A = 5000, 12
@@ -170,8 +170,8 @@ def test_value_gradient_into_padded_column(kernel, cuda_device, monkeypatch):
     V, old_logp, adv, tv, R = (torch.randn(B, 1, device=d) for _ in range(5))
     args = (mu, sigma, V, x, old_logp, adv, tv, R, omu, osig)
     _, _, _, gv = kernels.ppo_loss_fwd_bwd(*args)
-    pad = torch.zeros(B, 4, device=d)
+    pad = torch.full((B, 4), 7.0, device=d)
     _, _, _, gv2 = kernels.ppo_loss_fwd_bwd(*args, grad_values=pad[:, :1])
     torch.cuda.synchronize()
     assert gv2.data_ptr() == pad.data_ptr()
-    assert torch.equal(pad[:, 0], gv.reshape(-1)) and (pad[:, 1:] == 0).all()
+    assert torch.equal(pad[:, 0], gv.reshape(-1)) and (pad[:, 1:] == 7.0).all()
