@@ -182,7 +182,11 @@ class PPO:
         self.normalize_advantage_per_mini_batch = normalize_advantage_per_mini_batch
 
         self._arena: GradArena | None = None  # gradient arena of the manual update path (see update())
-        self.learning_rate_device = None  # fp64 device scalar of the lr while update() runs
+        # while update() runs: the fp64 device scalar that holds the reference's self.learning_rate (decided on the
+        # device per mini-batch, read back once at the end); None otherwise.  Read by anything that wants the lr a
+        # given optimizer step uses without a host sync point per mini-batch (tests/update_fixtures.py records the
+        # lr trace through it)
+        self.learning_rate_device = None
 
     def init_storage(self, training_type, num_envs, num_transitions_per_env, obs, actions_shape):
         self.storage = RolloutStorage(training_type, num_envs, num_transitions_per_env, obs, actions_shape,
@@ -347,7 +351,9 @@ class PPO:
                 param_group["lr"] = lr32
         manual = None  # decided at the first mini-batch (needs the observation batch)
         arena = None
-        rnd_params = list(self.rnd.predictor.parameters()) if self.rnd else []
+        # the predictor's trainable parameters: the same filter as _trainable_params, so that they are exactly the
+        # arena's RND span
+        rnd_params = [p for p in self.rnd.predictor.parameters() if p.requires_grad] if self.rnd else []
 
         generator = self.storage.mini_batch_generator(self.num_mini_batches, self.num_learning_epochs)
         for (
@@ -420,7 +426,8 @@ class PPO:
                 target_embedding = self.rnd.target(rnd_state_batch).detach()
                 rnd_loss = nn.functional.mse_loss(predicted_embedding, target_embedding)
                 if manual:  # zeroed arena range + autograd's in-place accumulation = fresh gradients
-                    arena.span(rnd_params).zero_()
+                    if rnd_params:
+                        arena.span(rnd_params).zero_()
                 else:
                     for p in rnd_params:
                         p.grad = None

@@ -708,10 +708,11 @@ def fused_mlp_forward_pair(mlp_a: nn.Sequential, x_a: torch.Tensor, mlp_b: nn.Se
     memo_key = (id(mlp_a), id(mlp_b), _mode) if _frozen_depth and not torch.is_grad_enabled() else None
     memo = _pair_memo.get(memo_key) if memo_key is not None else None
     if memo is not None and memo[0]() is mlp_a and memo[1]() is mlp_b:
-        if not (x_a.is_cuda and x_b.is_cuda and x_a.dtype == torch.float32 and x_b.dtype == torch.float32
-                and x_a.dim() == 2 and x_b.dim() == 2 and x_a.shape[0] == x_b.shape[0]):
-            return None
         ws, bs, h3, fuse, imgs, nh = memo[2]
+        if not (x_a.is_cuda and x_b.is_cuda and x_a.dtype == torch.float32 and x_b.dtype == torch.float32
+                and x_a.dim() == 2 and x_b.dim() == 2 and x_a.shape[0] == x_b.shape[0]
+                and x_a.shape[1] == ws[0][0].shape[1] and x_b.shape[1] == ws[1][0].shape[1]):
+            return None
     else:
         if not (_split() and getattr(mlp_a, "_fused", True) and getattr(mlp_b, "_fused", True) and fusable(mlp_a, x_a)
                 and fusable(mlp_b, x_b) and x_a.shape[0] == x_b.shape[0]):

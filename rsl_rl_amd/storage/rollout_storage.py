@@ -288,9 +288,15 @@ class RolloutStorage:
         after = before.clone()
         slot = self._perm_slot ^ 1
         buf = self._staging(slot, n)
-        worker = threading.Thread(target=kernels.randperm_mt19937_state, args=(n, after, buf), daemon=True)
+        done = []  # appended to only when the draw returned normally
+
+        def draw():
+            kernels.randperm_mt19937_state(n, after, buf)
+            done.append(True)
+
+        worker = threading.Thread(target=draw, daemon=True)
         worker.start()
-        self._prefetch = (n, before, after, slot, worker)
+        self._prefetch = (n, before, after, slot, worker, done)
 
     def draw_permutation(self, n: int) -> torch.Tensor:
         """Device int32 permutation of range(n) with torch CPU randperm semantics on perm_generator.
@@ -300,10 +306,12 @@ class RolloutStorage:
         """
         pf, self._prefetch = self._prefetch, None
         if pf is not None:
-            pn, before, after, slot, worker = pf
+            pn, before, after, slot, worker, done = pf
             worker.join()
             gen = self._gen()
-            if pn == n and torch.equal(gen.get_state(), before):
+            # the drawn-ahead permutation is used only if its draw succeeded (the state advanced) and the generator
+            # still holds the state it was drawn from; otherwise draw synchronously below
+            if done and pn == n and not torch.equal(after, before) and torch.equal(gen.get_state(), before):
                 gen.set_state(after)
                 return self._upload(self._perm_bufs[slot][:n], slot)
         slot = self._perm_slot ^ 1

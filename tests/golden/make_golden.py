@@ -498,8 +498,9 @@ def _fill_storage_from_noise(st, policy, nz, mu_fp16):
 
 def _run_recorded_update(alg, grad_batches=0):
     """update() recording the lr of every optimizer step and the pre-clip policy gradient (concatenated in
-    parameters() order) of the first `grad_batches` mini-batches."""
-    lr_trace, grads = [], []
+    parameters() order) of the first `grad_batches` mini-batches (with RND: also the RND predictor's gradient,
+    after reduce_parameters, as rnd_optimizer.step sees it)."""
+    lr_trace, grads, rnd_grads = [], [], []
     orig_step = alg.optimizer.step
     orig_clip = torch.nn.utils.clip_grad_norm_
 
@@ -513,40 +514,88 @@ def _run_recorded_update(alg, grad_batches=0):
         return orig_step(*a, **kw)
 
     alg.optimizer.step = rec_step
+    if alg.rnd_optimizer is not None:
+        orig_rnd_step = alg.rnd_optimizer.step
+
+        def rec_rnd_step(*a, **kw):
+            if len(rnd_grads) < grad_batches:
+                rnd_grads.append(torch.cat([p.grad.reshape(-1) for p in alg.rnd.predictor.parameters()]).clone())
+            return orig_rnd_step(*a, **kw)
+
+        alg.rnd_optimizer.step = rec_rnd_step
     torch.nn.utils.clip_grad_norm_ = rec_clip
     try:
         loss_dict = alg.update()
     finally:
         torch.nn.utils.clip_grad_norm_ = orig_clip
-    return loss_dict, lr_trace, grads
+    return loss_dict, lr_trace, grads, rnd_grads
 
 
 def _update_case(PPO, ActorCritic, RolloutStorage, *, T, N, O, A, hidden, seed, rank, world, mu_fp16, lr=1e-3,
-                 grad_batches=0, logp_ulp=False):
+                 grad_batches=0, logp_ulp=False, rnd_cfg=None, policy_kw=None):
+    """One reference update() on rank `rank` of `world` (world > 1: inside an initialised gloo group).
+    rnd_cfg: the PPO rnd_cfg (num_states / obs_groups filled in here, rnd.py:185-209); with state_normalization the
+    RND state normaliser is first fed two batches of numpy-seeded states, as the rollout's update_normalization
+    would (ppo.py:145-146)."""
     torch.manual_seed(seed + 17 * rank)  # different initial weights per rank; broadcast_parameters syncs them
     obs0 = {"policy": torch.zeros(N, O)}
     groups = {"policy": ["policy"], "critic": ["policy"]}
-    pol = ActorCritic(obs0, groups, A, actor_hidden_dims=hidden, critic_hidden_dims=hidden)
+    if rnd_cfg is not None:
+        groups["rnd_state"] = ["policy"]
+    pol = ActorCritic(obs0, groups, A, actor_hidden_dims=hidden, critic_hidden_dims=hidden, **(policy_kw or {}))
     mcfg = {"global_rank": rank, "local_rank": rank, "world_size": world} if world > 1 else None
-    alg = PPO(pol, num_learning_epochs=5, num_mini_batches=4, device="cpu", multi_gpu_cfg=mcfg, learning_rate=lr)
+    rcfg = None if rnd_cfg is None else dict(rnd_cfg, num_states=O, obs_groups=groups)
+    alg = PPO(pol, num_learning_epochs=5, num_mini_batches=4, device="cpu", multi_gpu_cfg=mcfg, learning_rate=lr,
+              rnd_cfg=rcfg)
     if world > 1:
         alg.broadcast_parameters()  # on_policy_runner.py:99-101
     init_state = {k: f32(v) for k, v in pol.state_dict().items()}
+    if isinstance(logp_ulp, str) and logp_ulp.startswith("par"):  # sensitivity probe: every initial policy
+        # parameter one ulp up or down at random (as a GEMM's last-bit rounding moves every forward value)
+        g = torch.Generator().manual_seed(int(logp_ulp[3:]) * 1000 + 7)
+        with torch.no_grad():
+            for p in pol.parameters():
+                up = torch.nextafter(p, torch.full_like(p, float("inf")))
+                down = torch.nextafter(p, torch.full_like(p, float("-inf")))
+                p.copy_(torch.where(torch.rand(p.shape, generator=g) < 0.5, up, down))
+    rnd_init = {}
+    if alg.rnd is not None:
+        if alg.rnd.state_normalization:
+            nrng = np.random.default_rng(seed * 100 + rank + 50)
+            for _ in range(2):
+                x = nrng.standard_normal((N, O), dtype=np.float32) * 1.5 + 0.25
+                alg.rnd.update_normalization({"policy": torch.from_numpy(x)})
+        rnd_init = {k: (v.numpy().copy() if v.dtype == torch.int64 else f32(v))
+                    for k, v in alg.rnd.state_dict().items()}
     alg.init_storage("rl", N, T, obs0, [A])
     nz = storage_noise(seed * 100 + rank, T, N, O, A)
     stored = _fill_storage_from_noise(alg.storage, pol, nz, mu_fp16)
-    if logp_ulp:  # sensitivity probe: every stored log-prob one ulp up
+    if logp_ulp and not (isinstance(logp_ulp, str) and logp_ulp.startswith("par")):  # sensitivity probe: the stored log-probs one ulp off (True / "up": every one up; "down": every
+        # one down; "rand<k>": up or down at random per sample, seeded by k and the rank)
         lp = alg.storage.actions_log_prob
-        lp.copy_(torch.nextafter(lp, torch.full_like(lp, float("inf"))))
+        up = torch.nextafter(lp, torch.full_like(lp, float("inf")))
+        down = torch.nextafter(lp, torch.full_like(lp, float("-inf")))
+        if logp_ulp is True or logp_ulp == "up":
+            lp.copy_(up)
+        elif logp_ulp == "down":
+            lp.copy_(down)
+        else:
+            g = torch.Generator().manual_seed(int(logp_ulp[4:]) * 1000 + rank)
+            lp.copy_(torch.where(torch.rand(lp.shape, generator=g) < 0.5, up, down))
     with torch.inference_mode():
         alg.compute_returns({"policy": torch.from_numpy(nz["last_obs"])})
     torch.manual_seed(5000 + rank)  # the permutation's generator, per rank
     gen_state = torch.default_generator.get_state().numpy().copy()
-    loss_dict, lr_trace, grads = _run_recorded_update(alg, grad_batches)
+    loss_dict, lr_trace, grads, rnd_grads = _run_recorded_update(alg, grad_batches)
     arrays = {f"init/{k}": v for k, v in init_state.items()}
     for j, g in enumerate(grads):  # pre-clip gradients of the first mini-batches (before any trajectory drift)
         arrays[f"grad_mb{j}"] = f32(g)
+    for j, g in enumerate(rnd_grads):
+        arrays[f"rnd_grad_mb{j}"] = f32(g)
     arrays.update({f"final/{k}": f32(v) for k, v in pol.state_dict().items()})
+    if alg.rnd is not None:
+        arrays.update({f"rnd_init/{k}": v for k, v in rnd_init.items()})
+        arrays.update({f"rnd_final/{k}": f32(v) for k, v in alg.rnd.predictor.state_dict().items()})
     arrays.update({f"storage/{k}": v for k, v in stored.items()})
     arrays["storage/returns_head"] = f32(alg.storage.returns[:2])  # after compute_returns (un-cleared buffer)
     arrays["gen_state"] = gen_state
@@ -556,22 +605,56 @@ def _update_case(PPO, ActorCritic, RolloutStorage, *, T, N, O, A, hidden, seed, 
     return arrays, meta
 
 
-MULTIRANK_CASES = [  # name, world, T, N per rank, O, A, hidden, seed, learning rate
+C5_RND = dict(weight=1.0 * 0.02, num_outputs=1, predictor_hidden_dims=[-1], target_hidden_dims=[-1],
+              learning_rate=1e-3)  # config C5: weight 1.0 x step_dt 0.02, 48->48->1
+MULTIRANK_CASES = [  # name, world, T, N per rank, O, A, hidden, seed, learning rate[, options]
     ("w2", 2, 16, 256, 16, 4, [64, 64], 71, 1e-3),
     ("w4", 4, 16, 128, 16, 4, [64, 64], 73, 6e-3),  # large steps: the lr-decrease branch is taken as well
+    # round 3: eight ranks at C1's shape, and two ranks at C4's per-rank network (3x256, O48, A12)
+    ("w8", 8, 16, 64, 16, 4, [64, 64], 79, 1e-3, {"sensitivity": True}),
+    ("w2_c4net", 2, 24, 1024, 48, 12, [256, 256, 256], 83, 1e-3,
+     {"mu_fp16": True, "sensitivity": True, "shared_params": True, "grad_batches": 1}),
+]
+# PPO.update() with RND (ppo.py:352-372, :383-384, :447-450): the predictor trained every mini-batch
+RND_UPDATE_CASES = [
+    ("rnd_c5_w1", 1, 24, 1024, 48, 12, [256, 256, 256], 89, 1e-3,
+     {"mu_fp16": True, "sensitivity": True, "grad_batches": 1, "rnd": C5_RND}),
+    ("rnd_c5_w2", 2, 24, 512, 48, 12, [256, 256, 256], 97, 1e-3,
+     {"mu_fp16": True, "sensitivity": True, "shared_params": True, "grad_batches": 1, "rnd": C5_RND}),
+    ("rnd_statenorm_w1", 1, 16, 256, 16, 4, [64, 64], 101, 1e-3,
+     {"sensitivity": True, "grad_batches": 1,
+      "rnd": dict(weight=0.5, num_outputs=3, predictor_hidden_dims=[32], target_hidden_dims=[32],
+                  state_normalization=True, learning_rate=2e-3)}),
 ]
 
 
-def _multirank_worker(rank, world, port, ref_path, case, out_dir):
+# the std parameterisations through a whole update at a shape the fused MLP path takes (O a multiple of 4):
+# state-dependent std (actor_critic.py:63-86, :119-128) with scalar and log std, and a log_std parameter
+STD_UPDATE_CASES = [
+    ("sdstd_scalar", 1, 8, 256, 16, 4, [64, 64], 103, 1e-3,
+     {"grad_batches": 1, "policy_kw": {"state_dependent_std": True}}),
+    ("sdstd_log", 1, 8, 256, 16, 4, [64, 64], 107, 1e-3,
+     {"grad_batches": 1, "policy_kw": {"state_dependent_std": True, "noise_std_type": "log"}}),
+    ("logstd", 1, 8, 256, 16, 4, [64, 64], 109, 1e-3, {"grad_batches": 1, "policy_kw": {"noise_std_type": "log"}}),
+]
+
+
+def _case_kw(case, logp_ulp=False):
+    name, world, T, N, O, A, hidden, seed, lr = case[:9]
+    opt = case[9] if len(case) > 9 else {}
+    return dict(T=T, N=N, O=O, A=A, hidden=hidden, seed=seed, world=world, mu_fp16=opt.get("mu_fp16", False),
+                lr=lr, grad_batches=opt.get("grad_batches", 0), logp_ulp=logp_ulp,
+                rnd_cfg=dict(opt["rnd"]) if opt.get("rnd") else None, policy_kw=opt.get("policy_kw"))
+
+
+def _multirank_worker(rank, world, port, ref_path, case, out_dir, logp_ulp):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     torch.set_num_threads(1)
     PPO, ActorCritic, RolloutStorage = import_reference(ref_path)
     torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        name, _, T, N, O, A, hidden, seed, lr = case
-        arrays, meta = _update_case(PPO, ActorCritic, RolloutStorage, T=T, N=N, O=O, A=A, hidden=hidden, seed=seed,
-                                    rank=rank, world=world, mu_fp16=False, lr=lr)
+        arrays, meta = _update_case(PPO, ActorCritic, RolloutStorage, rank=rank, **_case_kw(case, logp_ulp))
         np.savez(os.path.join(out_dir, f"r{rank}.npz"), **arrays)
         with open(os.path.join(out_dir, f"r{rank}.json"), "w") as f:
             json.dump(meta, f)
@@ -579,31 +662,95 @@ def _multirank_worker(rank, world, port, ref_path, case, out_dir):
         torch.distributed.destroy_process_group()
 
 
-def make_multirank(ref_path):
+def _run_update_case(ref_path, case, logp_ulp=False):
+    """All ranks of one case: ({f"r{rank}/...": array}, [per-rank meta])."""
     import socket
     import tempfile
 
     import torch.multiprocessing as mp
 
+    world = case[1]
+    if world == 1:
+        PPO, ActorCritic, RolloutStorage = import_reference(ref_path)
+        a, m = _update_case(PPO, ActorCritic, RolloutStorage, rank=0, **_case_kw(case, logp_ulp))
+        return {f"r0/{k}": v for k, v in a.items()}, [m]
+    with tempfile.TemporaryDirectory() as d:
+        sock = socket.socket()
+        sock.bind(("127.0.0.1", 0))
+        port = sock.getsockname()[1]
+        sock.close()
+        mp.spawn(_multirank_worker, args=(world, port, ref_path, case, d, logp_ulp), nprocs=world, join=True)
+        arrays, ranks = {}, []
+        for r in range(world):
+            z = np.load(os.path.join(d, f"r{r}.npz"))
+            arrays.update({f"r{r}/{k}": z[k] for k in z.files})
+            with open(os.path.join(d, f"r{r}.json")) as f:
+                ranks.append(json.load(f))
+    return arrays, ranks
+
+
+def _make_update_family(ref_path, cases):
+    """Reference update() captures of `cases`: tests/golden/update_<name>.npz + their golden.json entries.
+
+    options: mu_fp16 (stored mean rounded to fp16: a compact fixture), grad_batches (pre-clip gradients of the first
+    mini-batches), sensitivity (the reference's own parameter movement when every stored log-prob is one ulp up,
+    per tensor relative to how far the update moved it -- the bound the tests use at widths where the surrogate's
+    clip discontinuity makes last-bit log-prob differences visible, see make_update_c2), shared_params (initial and
+    final parameters and the recorded (all-reduced) gradients stored for rank 0 only: every rank holds the same ones
+    after broadcast_parameters / reduce_parameters; asserted here), rnd (rnd_cfg of the PPO)."""
     meta = {}
-    for case in MULTIRANK_CASES:
-        name, world, T, N, O, A, hidden, seed, lr = case
-        with tempfile.TemporaryDirectory() as d:
-            sock = socket.socket()
-            sock.bind(("127.0.0.1", 0))
-            port = sock.getsockname()[1]
-            sock.close()
-            mp.spawn(_multirank_worker, args=(world, port, ref_path, case, d), nprocs=world, join=True)
-            arrays, ranks = {}, []
-            for r in range(world):
-                z = np.load(os.path.join(d, f"r{r}.npz"))
-                arrays.update({f"r{r}/{k}": z[k] for k in z.files})
-                with open(os.path.join(d, f"r{r}.json")) as f:
-                    ranks.append(json.load(f))
+    for case in cases:
+        name, world, T, N, O, A, hidden, seed, lr = case[:9]
+        opt = case[9] if len(case) > 9 else {}
+        arrays, ranks = _run_update_case(ref_path, case)
+        if opt.get("shared_params"):
+            for r in range(1, world):
+                for k in [k for k in arrays if k.startswith(f"r{r}/") and (
+                        k.split("/")[1] in ("init", "final", "rnd_final")
+                        or k.split("/")[1].startswith(("grad_mb", "rnd_grad_mb")))]:
+                    assert np.array_equal(arrays[k], arrays["r0/" + k.split("/", 1)[1]]), k
+                    del arrays[k]
+        m = {"world": world, "T": T, "N": N, "O": O, "A": A, "hidden": hidden, "M": 4, "E": 5, "seed": seed,
+             "learning_rate": lr, "ranks": ranks, "mu_fp16": opt.get("mu_fp16", False),
+             "shared_params": bool(opt.get("shared_params")), "rnd_cfg": opt.get("rnd"),
+             "policy_kw": opt.get("policy_kw") or {}}
+        if opt.get("sensitivity"):
+            # the envelope over several one-ulp probes of the reference itself: the stored log-probs all up, all
+            # down, up/down at random, and the initial policy parameters up/down at random (two patterns; as a
+            # GEMM's last-bit rounding moves every forward value).  One probe may happen to flip no sample at a clip
+            # bound where another last-bit pattern flips one (each flipped sample moves a mini-batch gradient by
+            # ~1/sqrt(B), and Adam carries it on)
+            sens = {}
+            probes = ("up", "down", "rand0", "par0", "par1")
+            for probe in probes:
+                ulp, _ = _run_update_case(ref_path, case, logp_ulp=probe)
+                for pre, init_pre in (("r0/final/", "r0/init/"), ("r0/rnd_final/", None)):
+                    for k in [k for k in arrays if k.startswith(pre)]:
+                        pname = k[len(pre):]
+                        init = (arrays[init_pre + pname] if init_pre else
+                                arrays["r0/rnd_init/predictor." + pname])
+                        moved = np.linalg.norm(arrays[k].astype(np.float64) - init.astype(np.float64))
+                        d = np.linalg.norm(ulp[k].astype(np.float64) - arrays[k].astype(np.float64))
+                        key = ("rnd/" if init_pre is None else "") + pname
+                        sens[key] = max(sens.get(key, 0.0), float(d / moved) if moved else float(d))
+            m["ulp_sensitivity"] = sens
+            m["ulp_probes"] = list(probes)
         np.savez_compressed(os.path.join(HERE, f"update_{name}.npz"), **arrays)
-        meta[name] = {"world": world, "T": T, "N": N, "O": O, "A": A, "hidden": hidden, "M": 4, "E": 5,
-                      "seed": seed, "learning_rate": lr, "ranks": ranks, "mu_fp16": False}
+        meta[name] = m
+        print("update case", name, "lr", ranks[0]["lr_trace"][:4], "...", ranks[0]["final_lr"], flush=True)
     return meta
+
+
+def make_multirank(ref_path, names=None):
+    return _make_update_family(ref_path, [c for c in MULTIRANK_CASES if names is None or c[0] in names])
+
+
+def make_update_rnd(ref_path):
+    return _make_update_family(ref_path, RND_UPDATE_CASES)
+
+
+def make_update_std(ref_path):
+    return _make_update_family(ref_path, STD_UPDATE_CASES)
 
 
 def make_update_c2(PPO, ActorCritic, RolloutStorage):
@@ -731,8 +878,10 @@ def make_normalizer(ref_path):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reference", default=os.environ.get("RSL_RL_REFERENCE", "/root/reference"))
-    ap.add_argument("--only", choices=["rollout", "normalizer", "multirank", "update_c2"],
+    ap.add_argument("--only", choices=["rollout", "normalizer", "multirank", "update_c2", "update_rnd",
+                                           "update_std"],
                     help="regenerate one fixture family, keep the rest")
+    ap.add_argument("--cases", default=None, help="with --only multirank: comma-separated case names to (re)generate")
     args = ap.parse_args()
     torch.set_num_threads(4)
     PPO, ActorCritic, RolloutStorage = import_reference(args.reference)
@@ -742,7 +891,12 @@ def main():
         if args.only == "rollout":
             meta["rollout"] = make_rollout(PPO, ActorCritic, RolloutStorage)
         elif args.only == "multirank":
-            meta["multirank"] = make_multirank(args.reference)
+            names = args.cases.split(",") if args.cases else None
+            meta["multirank"] = dict(meta.get("multirank", {}), **make_multirank(args.reference, names))
+        elif args.only == "update_rnd":
+            meta["update_rnd"] = make_update_rnd(args.reference)
+        elif args.only == "update_std":
+            meta["update_std"] = make_update_std(args.reference)
         elif args.only == "update_c2":
             meta["update_c2"] = make_update_c2(PPO, ActorCritic, RolloutStorage)
         else:
@@ -764,6 +918,8 @@ def main():
         "normalizer": make_normalizer(args.reference),
         "multirank": make_multirank(args.reference),
         "update_c2": make_update_c2(PPO, ActorCritic, RolloutStorage),
+        "update_rnd": make_update_rnd(args.reference),
+        "update_std": make_update_std(args.reference),
     }
     with open(os.path.join(HERE, "golden.json"), "w") as f:
         json.dump(meta, f, indent=1, sort_keys=True)
