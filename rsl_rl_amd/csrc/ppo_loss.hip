@@ -61,6 +61,7 @@ struct LossParams {
     int64_t gv_stride;  // grad_values row stride (elements)
     const float* adv_stats;  // [2] = (mean, std) when normalize_adv
     float* stats;
+    int32_t kl_fast;  // shared-sigma KL on per-action constants (quad kernel); 0: full expression everywhere
 };
 
 template <int MAXA, bool VEC>
@@ -495,6 +496,14 @@ __global__ __launch_bounds__(kBlock, quad_waves(APL, SHARED, KL)) void ppo_loss_
     const int a0 = q * APL;
 
     float c_s[APL], c_ls[APL], c_inv_den[APL], c_inv_s[APL], c_inv_s3[APL];
+    // KL with a shared sigma (ppo.py:262-268): the rollout stored one sigma per action for every sample (the
+    // same std parameter), so log(sigma / old_sigma + 1e-5) is a per-action constant -- evaluated once here
+    // from sample 0's old sigma and used for every element whose old sigma has exactly those bits (any other
+    // element takes the full expression) -- and the division by the per-action constant D = 2 sigma^2 is
+    // done as q0 = n * RN(1/D), q = fma(fma(-q0, D, n), RN(1/D), q0): the correctly rounded quotient
+    // (Markstein's theorem; tested against true division in oracle/kl_division_check.c) for n and D in the
+    // normal range, which the per-element test below keeps it to.  Same bits as __fdiv_rn, ~30 fewer VALU.
+    float c_os[APL], c_t1[APL], c_D[APL], c_rD[APL];
     float ent_shared = 0.0f;
     if constexpr (SHARED) {
 #pragma unroll
@@ -506,6 +515,15 @@ __global__ __launch_bounds__(kBlock, quad_waves(APL, SHARED, KL)) void ppo_loss_
             c_inv_den[k] = 1.0f / __fmul_rn(2.0f, __fmul_rn(s, s));
             c_inv_s[k] = inv_s;
             c_inv_s3[k] = inv_s * inv_s * inv_s;
+            if constexpr (KL) {
+                const float os0 = p.B > 0 ? p.old_sigma[a0 + k] : 1.0f;
+                const float D = __fmul_rn(2.0f, __fmul_rn(s, s));
+                const bool d_ok = D >= 0x1p-60f && D <= 0x1p60f;  // else: every element takes the full path
+                c_os[k] = (d_ok && p.kl_fast) ? os0 : __builtin_nanf("");  // NaN never compares equal
+                c_t1[k] = logf(__fadd_rn(__fdiv_rn(s, os0), 1.0e-5f));
+                c_D[k] = D;
+                c_rD[k] = __fdiv_rn(1.0f, D);
+            }
         }
 #pragma unroll
         for (int a = 0; a < A; ++a) ent_shared = __fadd_rn(ent_shared, __fadd_rn(kEntC, logf(p.sigma[a])));
@@ -592,7 +610,8 @@ __global__ __launch_bounds__(kBlock, quad_waves(APL, SHARED, KL)) void ppo_loss_
         const auto& osg = cur.osg;
         const auto& sr = cur.sr;
 
-        float d[4][APL], lp[4];
+        float d[4][APL], lp[4], klp[4];
+        bool kl_slow = false;  // some element of this lane needs the full KL expression
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const bool vq = base + 16 * j + s16 < B32;
@@ -616,17 +635,48 @@ __global__ __launch_bounds__(kBlock, quad_waves(APL, SHARED, KL)) void ppo_loss_
                 if constexpr (KL) {
                     const float os = osg[j][k];
                     const float dm = __fsub_rn(omu[j][k], mu[j][k]);
-                    const float t1 = logf(__fadd_rn(__fdiv_rn(s, os), 1.0e-5f));
-                    const float t2 = __fdiv_rn(__fadd_rn(__fmul_rn(os, os), __fmul_rn(dm, dm)),
-                                               __fmul_rn(2.0f, __fmul_rn(s, s)));
+                    const float n = __fadd_rn(__fmul_rn(os, os), __fmul_rn(dm, dm));
+                    float t1, t2;
+                    if constexpr (SHARED) {
+                        t1 = c_t1[k];
+                        const float q0 = __fmul_rn(n, c_rD[k]);
+                        t2 = __builtin_fmaf(__builtin_fmaf(-q0, c_D[k], n), c_rD[k], q0);
+                        kl_slow |= !(os == c_os[k] && n >= 0x1p-60f && n <= 0x1p60f);
+                    } else {
+                        t1 = logf(__fadd_rn(__fdiv_rn(s, os), 1.0e-5f));
+                        t2 = __fdiv_rn(n, __fmul_rn(2.0f, __fmul_rn(s, s)));
+                    }
                     klpart = __fadd_rn(klpart, __fsub_rn(__fadd_rn(t1, t2), 0.5f));
                 }
             }
+            klp[j] = klpart;
             if (vq) {
-                acc_kl += klpart;
                 if constexpr (!SHARED) acc_ent += entpart;
             }
             lp[j] = quad_sum(lpart);
+        }
+        if constexpr (KL) {
+            if constexpr (SHARED) {
+                if (kl_slow) {  // the reference's exact expression for every element of this lane (rare)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        float klpart = 0.0f;
+#pragma unroll
+                        for (int k = 0; k < APL; ++k) {
+                            const float s = c_s[k], os = osg[j][k];
+                            const float dm = __fsub_rn(omu[j][k], mu[j][k]);
+                            const float t1 = logf(__fadd_rn(__fdiv_rn(s, os), 1.0e-5f));
+                            const float t2 = __fdiv_rn(__fadd_rn(__fmul_rn(os, os), __fmul_rn(dm, dm)),
+                                                       __fmul_rn(2.0f, __fmul_rn(s, s)));
+                            klpart = __fadd_rn(klpart, __fsub_rn(__fadd_rn(t1, t2), 0.5f));
+                        }
+                        klp[j] = klpart;
+                    }
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (base + 16 * j + s16 < B32) acc_kl += klp[j];
         }
 
         // ---- sample layout: lane l <- log-prob of sample base + l (quad l & 15 of round l >> 4)
@@ -991,6 +1041,10 @@ extern "C" int rslrl_ppo_loss_fwd_bwd(const rslrl_ppo_loss_args_t* a, void* work
     p.gv_stride = a->grad_values_stride > 1 ? a->grad_values_stride : 1;
     p.adv_stats = a->stats + 5;
     p.stats = a->stats;
+    {  // RSLRL_KL_FAST=0 disables the per-action-constant KL (read per call: the tests compare both bitwise)
+        const char* e = std::getenv("RSLRL_KL_FAST");
+        p.kl_fast = (e && e[0] == '0') ? 0 : 1;
+    }
 
     if (p.normalize_adv) {
         const int mb = static_cast<int>(std::min<int64_t>(ceil_div(a->B, kBlock), kMomentBlocks));

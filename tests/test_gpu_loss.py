@@ -175,3 +175,40 @@ def test_value_gradient_into_padded_column(kernel, cuda_device, monkeypatch):
     torch.cuda.synchronize()
     assert gv2.data_ptr() == pad.data_ptr()
     assert torch.equal(pad[:, 0], gv.reshape(-1)) and (pad[:, 1:] == 7.0).all()
+
+
+@pytest.mark.parametrize("B,perturb", [(393216, 0), (393216, 37), (4099, 5), (64, 64)])
+def test_shared_sigma_kl_fast_path_bit_exact(B, perturb, cuda_device, monkeypatch):
+    """The quad kernel's shared-sigma KL (per-action log term, division by the constant 2 sigma^2 through the
+    correctly rounded reciprocal + fma correction) gives the same bits as the reference's full expression
+    (RSLRL_KL_FAST=0), with old sigmas as a rollout stores them (one value per action) plus `perturb` rows whose
+    old sigma or mean differs (those elements take the full expression in the fast kernel too); and the KL
+    matches the oracle."""
+    monkeypatch.setenv("RSLRL_LOSS_KERNEL", "quad")
+    A = 12
+    rng = np.random.default_rng(B + perturb)
+    mu = rng.standard_normal((B, A), dtype=np.float32)
+    sig_vec = rng.uniform(0.3, 1.5, A).astype(np.float32)
+    old_vec = (sig_vec * rng.uniform(0.9, 1.1, A)).astype(np.float32)
+    osig = np.broadcast_to(old_vec, (B, A)).copy()
+    omu = (mu + 0.05 * rng.standard_normal((B, A))).astype(np.float32)
+    rows = rng.choice(B, size=perturb, replace=False) if perturb else np.zeros(0, np.int64)
+    osig[rows[: perturb // 2]] *= np.float32(1.25)
+    omu[rows[perturb // 2:]] = np.float32(3e19)  # (old mu - mu)^2 beyond the fast path's range
+    x = rng.standard_normal((B, A), dtype=np.float32)
+    old_logp = rng.standard_normal(B).astype(np.float32) - 10.0
+    adv, tv, V, R = (rng.standard_normal(B, dtype=np.float32) for _ in range(4))
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(cuda_device)  # noqa: E731
+    args = (t(mu), t(sig_vec), t(V), t(x), t(old_logp), t(adv), t(tv), t(R), t(omu), t(osig))
+    out = {}
+    for fast in ("1", "0"):
+        monkeypatch.setenv("RSLRL_KL_FAST", fast)
+        stats, gmu, gsig, gv = kernels.ppo_loss_fwd_bwd(*args)
+        torch.cuda.synchronize()
+        out[fast] = (stats.cpu().clone(), gmu.cpu().clone(), gsig.cpu().clone(), gv.cpu().clone())
+    for a, b in zip(out["1"], out["0"]):
+        assert torch.equal(a, b)
+    if perturb == 0:
+        ref = O.ppo_loss(mu, np.broadcast_to(sig_vec, (B, A)), V, x, old_logp, adv, tv, R, omu, osig)
+        kl = float(out["1"][0][kernels.STATS_KL])
+        assert abs(kl - ref["kl_mean"]) <= RTOL * abs(ref["kl_mean"]) + 1e-7
