@@ -31,7 +31,7 @@ extern "C" {
 
 typedef struct ihipStream_t* rslrl_stream_t; /* == hipStream_t */
 
-#define RSLRL_ABI_VERSION 6
+#define RSLRL_ABI_VERSION 7
 
 enum {
     RSLRL_OK = 0,
@@ -454,6 +454,51 @@ int rslrl_normalizer_apply(const float* x, int64_t N, int32_t D, int64_t row_str
 int rslrl_reward_normalize(const float* rewards, int64_t N, float gamma, float* disc_avg, int32_t first, float* mean,
                            float* var, float* std, int64_t* count, int64_t until, int32_t training, float* out,
                            void* workspace, size_t workspace_bytes, rslrl_stream_t stream);
+
+/* ------------------------------------------------------------------------------------------------
+ * RND predictor loss + backward of one mini-batch (the update leg), replacing
+ * rsl_rl/algorithms/ppo.py:352-363 (state extraction + normalisation, predictor / detached target forward,
+ * MSE) and :369-372 (rnd_loss.backward() into the predictor's .grad) -- rsl_rl/modules/rnd.py:85-95 networks.
+ *   state [B, in] rows (row stride state_stride); optional (s - mean) / (std + eps) (normalization.py:40-42);
+ *   predictor / target: Linear(in -> hidden) + ELU + Linear(hidden -> out) given as four tensors each
+ *   (w1 [hidden, in], b1 [hidden], w2 [out, hidden], b2 [out]); in, hidden <= 64, out <= 8.
+ *   target_w1 != NULL: the target forward runs here and, when target_embedding != NULL, its [B, out] values are
+ *   stored there; target_w1 == NULL: target_embedding is read instead (the target is constant within update()).
+ *   grad: the predictor's gradient, packed [dW1 | db1 | dW2 | db2] (the order of predictor.parameters() -- a
+ *   contiguous span of the gradient arena), overwritten with d(mse)/d(params); per-workgroup fp32 partials are
+ *   folded in fp64 in a fixed order (deterministic).  loss_sum (fp64, optional) += (double)(float)mse, the
+ *   reference's rnd_loss.item() accumulation (ppo.py:391-392); loss (fp32, optional) = mse.
+ *   Workspace: rslrl_rnd_update_workspace_bytes.
+ * ----------------------------------------------------------------------------------------------*/
+#define RSLRL_RND_MAX_IN 64
+#define RSLRL_RND_MAX_HIDDEN 64
+#define RSLRL_RND_MAX_OUT 8
+typedef struct {
+    int64_t B;
+    int32_t in;
+    int32_t hidden;
+    int32_t out;
+    float state_eps;
+    const float* state;
+    int64_t state_stride;
+    const float* state_mean; /* NULL: no state normalisation */
+    const float* state_std;
+    const float* pred_w1;
+    const float* pred_b1;
+    const float* pred_w2;
+    const float* pred_b2;
+    const float* target_w1; /* NULL: read target_embedding */
+    const float* target_b1;
+    const float* target_w2;
+    const float* target_b2;
+    float* target_embedding; /* [B, out] */
+    float* grad;             /* [hidden*in + hidden + out*hidden + out] */
+    double* loss_sum;        /* optional */
+    float* loss;             /* optional */
+} rslrl_rnd_update_args_t;
+size_t rslrl_rnd_update_workspace_bytes(int64_t B, int32_t in, int32_t hidden, int32_t out);
+int rslrl_rnd_update(const rslrl_rnd_update_args_t* args /* host struct */, void* workspace, size_t workspace_bytes,
+                     rslrl_stream_t stream);
 
 #ifdef __cplusplus
 }

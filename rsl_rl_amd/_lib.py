@@ -19,7 +19,7 @@ import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 # RSLRL_AMD_LIB: an alternative in-tree build of the same library (A/B kernel experiments)
 LIB_PATH = os.environ.get("RSLRL_AMD_LIB") or os.path.join(LIB_DIR, "librslrl_amd.so")
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 # symbols declared in include/rslrl_amd.h (tests/test_capi.py checks the header against this list)
 EXPORTED_SYMBOLS = (
@@ -65,6 +65,8 @@ EXPORTED_SYMBOLS = (
     "rslrl_ppo_update_tail",
     "rslrl_adam_workspace_bytes",
     "rslrl_clip_adam_step",
+    "rslrl_rnd_update_workspace_bytes",
+    "rslrl_rnd_update",
 )
 
 MAX_GATHER_FIELDS = 16
@@ -227,6 +229,35 @@ class PPOLossArgs(ctypes.Structure):
     ]
 
 
+class RndUpdateArgs(ctypes.Structure):
+    """include/rslrl_amd.h rslrl_rnd_update_args_t"""
+    _fields_ = [
+        ("B", ctypes.c_int64),
+        ("in_", ctypes.c_int32),
+        ("hidden", ctypes.c_int32),
+        ("out", ctypes.c_int32),
+        ("state_eps", ctypes.c_float),
+        ("state", ctypes.c_void_p),
+        ("state_stride", ctypes.c_int64),
+        ("state_mean", ctypes.c_void_p),
+        ("state_std", ctypes.c_void_p),
+        ("pred_w1", ctypes.c_void_p),
+        ("pred_b1", ctypes.c_void_p),
+        ("pred_w2", ctypes.c_void_p),
+        ("pred_b2", ctypes.c_void_p),
+        ("target_w1", ctypes.c_void_p),
+        ("target_b1", ctypes.c_void_p),
+        ("target_w2", ctypes.c_void_p),
+        ("target_b2", ctypes.c_void_p),
+        ("target_embedding", ctypes.c_void_p),
+        ("grad", ctypes.c_void_p),
+        ("loss_sum", ctypes.c_void_p),
+        ("loss", ctypes.c_void_p),
+    ]
+
+
+RND_MAX_IN, RND_MAX_HIDDEN, RND_MAX_OUT = 64, 64, 8
+
 _lib = None
 _lock = threading.Lock()
 
@@ -317,6 +348,10 @@ def _declare(L):
     L.rslrl_linear_wgrad_bias_workspace_bytes.argtypes = [I64, I32, I32, I32]
     L.rslrl_linear_wgrad_bias.restype = ctypes.c_int
     L.rslrl_linear_wgrad_bias.argtypes = [P, P, P, P, I64, I32, I32, I32, I32, P, P, SZ, P]
+    L.rslrl_rnd_update_workspace_bytes.restype = SZ
+    L.rslrl_rnd_update_workspace_bytes.argtypes = [I64, I32, I32, I32]
+    L.rslrl_rnd_update.restype = ctypes.c_int
+    L.rslrl_rnd_update.argtypes = [ctypes.POINTER(RndUpdateArgs), P, SZ, P]
 
 
 def lib():

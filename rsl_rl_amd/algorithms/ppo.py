@@ -164,6 +164,11 @@ class PPO:
         # clip_grad_norm_ + optimizer.step() as two launches (kernels.FusedClipAdam, ppo.py:373-374)
         self._clip_adam = (kernels.FusedClipAdam(self.optimizer, max_grad_norm)
                            if on_gpu and kernels.FusedClipAdam.supported(self.optimizer) else None)
+        # the RND predictor's optimizer.step() (unclipped, ppo.py:383-384) as one fused launch pair, used when the
+        # update runs the RND step on the fused kernels (_rnd_update_plan)
+        self._rnd_adam = (kernels.FusedClipAdam(self.rnd_optimizer, 0.0)
+                          if on_gpu and self.rnd_optimizer is not None
+                          and kernels.FusedClipAdam.supported(self.rnd_optimizer) else None)
         self.storage: RolloutStorage = None  # type: ignore
         self.transition = RolloutStorage.Transition()
 
@@ -354,6 +359,8 @@ class PPO:
         # the predictor's trainable parameters: the same filter as _trainable_params, so that they are exactly the
         # arena's RND span
         rnd_params = [p for p in self.rnd.predictor.parameters() if p.requires_grad] if self.rnd else []
+        rnd_fused = None  # decided at the first mini-batch (needs the observation batch and the arena)
+        target_cache = {}  # RND target embedding per mini-batch slice of this update's gathered storage
 
         generator = self.storage.mini_batch_generator(self.num_mini_batches, self.num_learning_epochs)
         for (
@@ -417,8 +424,15 @@ class PPO:
                     grads.append(g_sigma)
                 torch.autograd.backward(outs, grads)
 
-            # RND loss (ppo.py:352-363, :369-371): autograd into the predictor's gradients
-            if self.rnd:
+            # RND loss (ppo.py:352-363, :369-371)
+            if self.rnd and rnd_fused is None:
+                rnd_fused = self._rnd_update_plan(obs_batch, rnd_params, arena if manual else None)
+            if self.rnd and rnd_fused:
+                # one launch pair: predictor forward, detached target (computed in the first epoch, then read from
+                # the per-update cache -- its weights and inputs do not change within update()), MSE, backward
+                # straight into the predictor's arena span; the loss statistic accumulates into sums[3]
+                self._rnd_update_fused(obs_batch, arena.span(rnd_params), sums, target_cache)
+            elif self.rnd:
                 with torch.no_grad():
                     rnd_state_batch = self.rnd.get_rnd_state(obs_batch)
                     rnd_state_batch = self.rnd.state_normalizer(rnd_state_batch)
@@ -467,10 +481,13 @@ class PPO:
                 self._clip_adam.max_grad_norm = float(self.max_grad_norm)
                 self._clip_adam.step()
             if self.rnd_optimizer:
-                self.rnd_optimizer.step()
+                if rnd_fused and self._rnd_adam is not None:
+                    self._rnd_adam.step()  # the reference's unclipped Adam on the predictor (ppo.py:383-384)
+                else:
+                    self.rnd_optimizer.step()
 
             # loss statistics stay on the device (ppo.py:387-395): accumulated by ppo_update_tail above
-            if self.rnd:
+            if self.rnd and not rnd_fused:
                 sums[3] += rnd_loss.detach().double()
 
         num_updates = self.num_learning_epochs * self.num_mini_batches
@@ -485,6 +502,59 @@ class PPO:
         if self.rnd:
             loss_dict["rnd"] = host[3]
         return loss_dict
+
+    def _rnd_update_plan(self, obs_batch, rnd_params, arena) -> bool:
+        """Whether the RND predictor's step runs on the fused kernels (kernels.rnd_update): the manual update's
+        gradient arena, Linear-ELU-Linear networks of the kernel's sizes, all four predictor parameters trainable
+        (their arena span is then [W1 | b1 | W2 | b2]), an identity or empirical state normaliser, fp32 GPU
+        observations, our RolloutStorage (its mini-batches are fixed slices of one gathered buffer per update,
+        which the target cache relies on)."""
+        from ..networks.normalization import EmpiricalNormalization
+        rnd = self.rnd
+        if arena is None or not isinstance(self.storage, RolloutStorage):
+            return False
+        pred, targ = kernels.rnd_linears(rnd.predictor), kernels.rnd_linears(rnd.target)
+        if pred is None or targ is None:
+            return False
+        if [(m.in_features, m.out_features) for m in pred] != [(m.in_features, m.out_features) for m in targ]:
+            return False
+        if len(rnd_params) != 4 or any(a is not b for a, b in zip(rnd_params, [pred[0].weight, pred[0].bias,
+                                                                                pred[1].weight, pred[1].bias])):
+            return False
+        sn = rnd.state_normalizer
+        if not isinstance(sn, (nn.Identity, EmpiricalNormalization)):
+            return False
+        state = self._rnd_state(obs_batch)
+        if state is None or not state.is_cuda or state.dtype != torch.float32 or state.shape[1] != pred[0].in_features:
+            return False
+        if self._rnd_adam is not None:
+            self._rnd_adam.adopt_loaded_state()
+        return True
+
+    def _rnd_state(self, obs_batch):
+        """The RND state of a mini-batch (rnd.py get_rnd_state) without a copy when it is one observation group."""
+        groups = self.rnd.obs_groups["rnd_state"]
+        if len(groups) == 1:
+            s = obs_batch[groups[0]]
+            return s if s.dim() == 2 and s.stride(1) == 1 else None
+        return self.rnd.get_rnd_state(obs_batch)
+
+    def _rnd_update_fused(self, obs_batch, grad_span, sums, target_cache):
+        rnd = self.rnd
+        state = self._rnd_state(obs_batch)
+        B = state.shape[0]
+        pred, targ = kernels.rnd_linears(rnd.predictor), kernels.rnd_linears(rnd.target)
+        key = (state.data_ptr(), B, state.stride(0))
+        temb = target_cache.get(key)
+        compute_target = temb is None
+        if compute_target:
+            temb = torch.empty(B, targ[1].out_features, dtype=torch.float32, device=state.device)
+            target_cache[key] = temb
+        kw = {}
+        if rnd.state_normalization:
+            sn = rnd.state_normalizer
+            kw = dict(state_mean=sn._mean.reshape(-1), state_std=sn._std.reshape(-1), state_eps=sn.eps)
+        kernels.rnd_update(state, pred, targ if compute_target else None, temb, grad_span, loss_sum=sums[3:4], **kw)
 
     def _side_stream(self, dev):
         """A second stream for the critic's MLP launches in the manual update (networks/fused_mlp.side_stream;

@@ -16,6 +16,7 @@
 #include <algorithm>
 
 #include "common.h"
+#include "rnd_mlp.h"
 
 namespace rslrl {
 namespace {
@@ -25,13 +26,6 @@ constexpr int kMaxRndHidden = 64;
 constexpr int kMaxRndOut = 8;
 constexpr int kMaxA = 64;
 
-struct RndNet {  // packed layout of rslrl_rollout_args_t::rnd_target / rnd_predictor
-    const float* w1;  // [H, in]
-    const float* b1;  // [H]
-    const float* w2;  // [Q, H]
-    const float* b2;  // [Q]
-};
-
 __device__ __forceinline__ float load_flag(const void* p, int dtype, int64_t i) {
     switch (dtype) {
         case RSLRL_DTYPE_U8: return static_cast<float>(static_cast<const uint8_t*>(p)[i]);
@@ -39,32 +33,6 @@ __device__ __forceinline__ float load_flag(const void* p, int dtype, int64_t i) 
         case RSLRL_DTYPE_I64: return static_cast<float>(static_cast<const int64_t*>(p)[i]);
         default: return static_cast<const float*>(p)[i];
     }
-}
-
-// RND MLP forward for one state row held in registers: in -> H (ELU) -> Q, weights in LDS
-__device__ __forceinline__ void rnd_forward(const float* __restrict__ w, int in, int H, int Q, const float (&x)[kMaxRndIn],
-                                            float (&y)[kMaxRndOut]) {
-    const float* w1 = w;
-    const float* b1 = w1 + H * in;
-    const float* w2 = b1 + H;
-    const float* b2 = w2 + Q * H;
-#pragma unroll
-    for (int q = 0; q < kMaxRndOut; ++q) y[q] = 0.f;
-    for (int hh = 0; hh < H; ++hh) {
-        float z = 0.f;
-        const float* wr = w1 + hh * in;
-#pragma unroll
-        for (int i = 0; i < kMaxRndIn; ++i)
-            if (i < in) z = fmaf(wr[i], x[i], z);
-        z = __fadd_rn(z, b1[hh]);
-        const float a = z > 0.f ? z : expm1f(z);  // ELU, alpha 1 (torch: expm1)
-#pragma unroll
-        for (int q = 0; q < kMaxRndOut; ++q)
-            if (q < Q) y[q] = fmaf(w2[q * H + hh], a, y[q]);
-    }
-#pragma unroll
-    for (int q = 0; q < kMaxRndOut; ++q)
-        if (q < Q) y[q] = __fadd_rn(y[q], b2[q]);
 }
 
 // Record-mode copy segments (obs groups, actions, mu, sigma) in 16-byte units of a destination record
@@ -82,8 +50,16 @@ struct RecSegs {
     float rcp_r4;
 };
 
+// RND networks of the per-env part: 0 none, 1 config C5's 48 -> 48 -> 1 (exact widths), 2 any size the ABI admits
+template <int RNDK>
+struct RndShape {
+    static constexpr int INP = RNDK == 1 ? 48 : 64, HP = RNDK == 1 ? 48 : 64, Q = RNDK == 1 ? 1 : kMaxRndOut;
+    static constexpr bool EXACT = RNDK == 1;
+};
+
+template <int RNDK>
 __global__ __launch_bounds__(kBlock) void rollout_record_kernel(rslrl_rollout_args_t a, int copy_blocks, RecSegs rs) {
-    extern __shared__ float lds_w[];  // RND target then predictor weights
+    extern __shared__ __attribute__((aligned(16))) float lds_w[];  // RND target then predictor images (rnd_mlp.h)
     const int64_t N = a.N;
     if (static_cast<int>(blockIdx.x) < copy_blocks && a.record_floats > 0) {
         // ---- record mode: block b writes records [64 b, 64 b + 64) unit by unit (contiguous stores); the unit ->
@@ -167,13 +143,16 @@ __global__ __launch_bounds__(kBlock) void rollout_record_kernel(rslrl_rollout_ar
     }
 
     // ---- per-env work
-    const bool rnd = a.rnd_target != nullptr;
-    if (rnd) {
-        const int nw = a.rnd_hidden * a.rnd_in + a.rnd_hidden + a.rnd_out * a.rnd_hidden + a.rnd_out;
-        for (int i = threadIdx.x; i < nw; i += kBlock) {
-            lds_w[i] = a.rnd_target[i];
-            lds_w[nw + i] = a.rnd_predictor[i];
-        }
+    using RS = RndShape<RNDK>;
+    const int nw = rnd_net_floats(RS::INP, RS::HP, RNDK == 1 ? 1 : a.rnd_out);
+    if constexpr (RNDK != 0) {
+        const int Q = RNDK == 1 ? 1 : a.rnd_out;
+        // the packed nets [W1 | b1 | W2 | b2] (rslrl_rollout_args_t) into their LDS images
+        const int in = a.rnd_in, H = a.rnd_hidden;
+        rnd_stage_net_t(lds_w, a.rnd_target, a.rnd_target + H * in, a.rnd_target + H * in + H,
+                      a.rnd_target + H * in + H + Q * H, in, H, Q, RS::INP, RS::HP);
+        rnd_stage_net_t(lds_w + nw, a.rnd_predictor, a.rnd_predictor + H * in, a.rnd_predictor + H * in + H,
+                      a.rnd_predictor + H * in + H + Q * H, in, H, Q, RS::INP, RS::HP);
         __syncthreads();
     }
     const int64_t n = static_cast<int64_t>(blockIdx.x - copy_blocks) * kBlock + threadIdx.x;
@@ -197,24 +176,37 @@ __global__ __launch_bounds__(kBlock) void rollout_record_kernel(rslrl_rollout_ar
 
     float reward = a.rewards[n];
     if (a.extra_reward) reward = __fadd_rn(reward, a.extra_reward[n]);
-    if (rnd) {
-        float x[kMaxRndIn];
+    if constexpr (RNDK != 0) {
+        const int in = RS::EXACT ? RS::INP : a.rnd_in;
+        const int Q = RNDK == 1 ? 1 : a.rnd_out;
+        float x[RS::INP];
         const float* sx = a.rnd_obs + n * a.rnd_obs_stride;
 #pragma unroll
-        for (int i = 0; i < kMaxRndIn; ++i) {
-            float v = i < a.rnd_in ? sx[i] : 0.f;
-            if (a.rnd_state_mean && i < a.rnd_in)  // (x - mean) / (std + eps), normalization.py forward
+        for (int i = 0; i < RS::INP; ++i) {
+            float v = i < in ? sx[i] : 0.f;
+            if (a.rnd_state_mean && i < in)  // (x - mean) / (std + eps), normalization.py forward
                 v = __fdiv_rn(__fsub_rn(v, a.rnd_state_mean[i]), __fadd_rn(a.rnd_state_std[i], a.rnd_state_eps));
             x[i] = v;
         }
-        const int nw = a.rnd_hidden * a.rnd_in + a.rnd_hidden + a.rnd_out * a.rnd_hidden + a.rnd_out;
-        float yt[kMaxRndOut], yp[kMaxRndOut];
-        rnd_forward(lds_w, a.rnd_in, a.rnd_hidden, a.rnd_out, x, yt);
-        rnd_forward(lds_w + nw, a.rnd_in, a.rnd_hidden, a.rnd_out, x, yp);
+        float yt[RS::Q], yp[RS::Q];
+        {
+            float h[RS::HP];
+            rnd_hidden_t<RS::INP, RS::HP, RS::EXACT>(lds_w, in, x, h);
+#pragma unroll
+            for (int k = 0; k < RS::HP; ++k) h[k] = rnd_elu(h[k]);
+            rnd_output<RS::INP, RS::HP, RS::Q>(lds_w, Q, h, yt);
+        }
+        {
+            float h[RS::HP];
+            rnd_hidden_t<RS::INP, RS::HP, RS::EXACT>(lds_w + nw, in, x, h);
+#pragma unroll
+            for (int k = 0; k < RS::HP; ++k) h[k] = rnd_elu(h[k]);
+            rnd_output<RS::INP, RS::HP, RS::Q>(lds_w + nw, Q, h, yp);
+        }
         float ss = 0.f;
 #pragma unroll
-        for (int q = 0; q < kMaxRndOut; ++q)
-            if (q < a.rnd_out) {
+        for (int q = 0; q < RS::Q; ++q)
+            if (q < Q) {
                 const float d = __fsub_rn(yt[q], yp[q]);
                 ss = __fadd_rn(ss, __fmul_rn(d, d));
             }
@@ -287,9 +279,10 @@ extern "C" int rslrl_rollout_record(const rslrl_rollout_args_t* args, rslrl_stre
             a.rnd_hidden > kMaxRndHidden || a.rnd_out < 1 || a.rnd_out > kMaxRndOut)
             return RSLRL_E_UNSUPPORTED;
         if ((a.rnd_state_mean == nullptr) != (a.rnd_state_std == nullptr)) return RSLRL_E_INVALID_ARGUMENT;
-        const int nw = a.rnd_hidden * a.rnd_in + a.rnd_hidden + a.rnd_out * a.rnd_hidden + a.rnd_out;
-        lds = 2 * static_cast<size_t>(nw) * sizeof(float);
     }
+    const bool c5 = a.rnd_target && a.rnd_in == 48 && a.rnd_hidden == 48 && a.rnd_out == 1;
+    if (a.rnd_target)
+        lds = 2 * sizeof(float) * static_cast<size_t>(c5 ? rnd_net_floats(48, 48, 1) : rnd_net_floats(64, 64, a.rnd_out));
     int64_t copy_elems = a.N * a.A;
     for (int g = 0; g < a.n_obs; ++g) copy_elems += a.N * a.obs[g].row_floats;
     const int64_t cb = a.record_floats > 0 ? ceil_div(a.N, kRecRows)
@@ -298,7 +291,13 @@ extern "C" int rslrl_rollout_record(const rslrl_rollout_args_t* args, rslrl_stre
     const int copy_blocks = static_cast<int>(cb);
     const int64_t row_blocks = ceil_div(a.N, kBlock);
     if (row_blocks + copy_blocks > INT32_MAX) return RSLRL_E_INVALID_ARGUMENT;
-    hipLaunchKernelGGL(rollout_record_kernel, dim3(static_cast<unsigned>(copy_blocks + row_blocks)), dim3(kBlock), lds,
-                       reinterpret_cast<hipStream_t>(stream), a, copy_blocks, rs);
+    const dim3 grid(static_cast<unsigned>(copy_blocks + row_blocks));
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (!a.rnd_target)
+        hipLaunchKernelGGL(rollout_record_kernel<0>, grid, dim3(kBlock), 0, st, a, copy_blocks, rs);
+    else if (c5)
+        hipLaunchKernelGGL(rollout_record_kernel<1>, grid, dim3(kBlock), lds, st, a, copy_blocks, rs);
+    else
+        hipLaunchKernelGGL(rollout_record_kernel<2>, grid, dim3(kBlock), lds, st, a, copy_blocks, rs);
     return launch_status();
 }

@@ -147,18 +147,15 @@ def compute_returns(values, rewards, dones, last_values, gamma, lam, normalize_a
     dev = values.device
     nbytes = L.rslrl_compute_returns_workspace_bytes(T, N)
     ws = _ws.get(dev, "gae", nbytes)
-    # with the timer on, scan and normaliser go through two entry points so that each recorded span
-    # covers one pass (bench.py only; the fused entry point launches the same two kernels)
-    split = timer.enabled and normalize_advantage
-    with timer.span("gae_scan", dev, 17 * T * N + 4 * N):
+    # one span over the production entry point (scan + fused normalisation): algorithmic bytes of both passes
+    moved = 17 * T * N + 4 * N + (8 * T * N if normalize_advantage else 0)
+    with timer.span("compute_returns", dev, moved):
         rc = L.rslrl_compute_returns(
             _ptr(values), _ptr(rewards), _ptr(dones), _ptr(last_values), ctypes.c_float(gamma), ctypes.c_float(lam),
-            T, N, 0 if split else int(bool(normalize_advantage)), _ptr(returns), _ptr(advantages), _ptr(ws),
+            T, N, int(bool(normalize_advantage)), _ptr(returns), _ptr(advantages), _ptr(ws),
             ws.numel(), ctypes.c_void_p(_stream(dev)),
         )
     _lib.check(rc, "rslrl_compute_returns")
-    if split:
-        normalize_advantages_(advantages.view(-1))
 
 
 def normalize_advantages_(adv: torch.Tensor, eps: float = 1e-8) -> torch.Tensor:
@@ -601,3 +598,68 @@ class FusedClipAdam:
             g.copy_(c)
         return None
 
+
+
+# --------------------------------------------------------------------------------------------------
+# ppo.py:352-363 + :369-372 -- RND predictor loss and gradient of one mini-batch
+# --------------------------------------------------------------------------------------------------
+def rnd_linears(mlp):
+    """(Linear, Linear) of a Linear-ELU(alpha 1)-Linear MLP whose sizes the fused RND kernels take, else None."""
+    mods = list(mlp)
+    lin = [m for m in mods if isinstance(m, torch.nn.Linear)]
+    if (len(mods) != 3 or len(lin) != 2 or not isinstance(mods[1], torch.nn.ELU) or mods[1].alpha != 1.0
+            or lin[0].in_features > _lib.RND_MAX_IN or lin[0].out_features > _lib.RND_MAX_HIDDEN
+            or lin[1].out_features > _lib.RND_MAX_OUT or lin[1].in_features != lin[0].out_features):
+        return None
+    if any(not (t.is_contiguous() and t.dtype == torch.float32) for m in lin for t in (m.weight, m.bias)):
+        return None
+    return lin[0], lin[1]
+
+
+def rnd_update(state, predictor, target, target_embedding, grad, loss_sum=None, loss=None, state_mean=None,
+               state_std=None, state_eps=0.0):
+    """One launch pair for the RND predictor's training step of a mini-batch (include/rslrl_amd.h rslrl_rnd_update).
+
+    state [B, in] fp32 (unit column stride); predictor / target: (Linear, Linear) of rnd_linears; target None:
+    target_embedding [B, out] holds the (detached) target values already, else they are computed and, when
+    target_embedding is given, stored there.  grad: contiguous fp32 of the predictor's parameter count, packed
+    [dW1 | db1 | dW2 | db2] -- overwritten.  loss_sum (fp64 [1], optional) += the fp32 mse; loss (fp32 [1]) = mse."""
+    l1, l2 = predictor
+    B, n_in = state.shape
+    H, Q = l1.out_features, l2.out_features
+    _require_device(state, grad, target_embedding, loss_sum, loss, state_mean, state_std)
+    if state.dtype != torch.float32 or state.stride(1) != 1:
+        raise ValueError("rnd_update: state must be fp32 with unit column stride")
+    if n_in != l1.in_features:
+        raise ValueError(f"rnd_update: state has {n_in} columns, the predictor takes {l1.in_features}")
+    P = H * n_in + H + Q * H + Q
+    if grad.dtype != torch.float32 or not grad.is_contiguous() or grad.numel() != P:
+        raise ValueError("rnd_update: grad must be a contiguous fp32 buffer of the predictor's parameter count")
+    if target_embedding is not None and (target_embedding.dtype != torch.float32 or not target_embedding.is_contiguous()
+                                         or target_embedding.numel() != B * Q):
+        raise ValueError("rnd_update: target_embedding must be contiguous fp32 [B, out]")
+    a = _lib.RndUpdateArgs()
+    a.B, a.in_, a.hidden, a.out = B, n_in, H, Q
+    a.state, a.state_stride = state.data_ptr(), state.stride(0)
+    if state_mean is not None:
+        a.state_mean, a.state_std, a.state_eps = state_mean.data_ptr(), state_std.data_ptr(), float(state_eps)
+    a.pred_w1, a.pred_b1 = l1.weight.data_ptr(), l1.bias.data_ptr()
+    a.pred_w2, a.pred_b2 = l2.weight.data_ptr(), l2.bias.data_ptr()
+    if target is not None:
+        t1, t2 = target
+        if (t1.in_features, t1.out_features, t2.out_features) != (n_in, H, Q):
+            raise ValueError("rnd_update: predictor and target must have the same shapes")
+        a.target_w1, a.target_b1 = t1.weight.data_ptr(), t1.bias.data_ptr()
+        a.target_w2, a.target_b2 = t2.weight.data_ptr(), t2.bias.data_ptr()
+    elif target_embedding is None:
+        raise ValueError("rnd_update: without the target network the target embedding must be given")
+    a.target_embedding = target_embedding.data_ptr() if target_embedding is not None else None
+    a.grad = grad.data_ptr()
+    a.loss_sum = loss_sum.data_ptr() if loss_sum is not None else None
+    a.loss = loss.data_ptr() if loss is not None else None
+    L = _lib.lib()
+    dev = state.device
+    ws = _ws.get(dev, "rnd", L.rslrl_rnd_update_workspace_bytes(B, n_in, H, Q))
+    with timer.span("rnd_update", dev, 4 * (n_in + Q) * B, 2 * B * (3 if target is not None else 2) * (H * n_in + Q * H)):
+        rc = L.rslrl_rnd_update(ctypes.byref(a), _ptr(ws), ws.numel(), ctypes.c_void_p(_stream(dev)))
+    _lib.check(rc, "rslrl_rnd_update")
