@@ -42,7 +42,7 @@ BF16_MFMA_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA at 2.4 GHz (MI355X_MICROARCH.m
 X6_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 6  # fp32-equivalent peak of the 6-product split-bf16 GEMMs
 H3_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 3  # ... of the 3-product split-fp16 GEMMs (fp16 MFMA = bf16 rate)
 FP32_MFMA_PEAK_TFLOPS = 157.3
-HOT_PATH = ("gae_scan", "adv_normalize", "record_fill_slot", "gather_rows", "ppo_loss", "rollout_record")
+HOT_PATH = ("compute_returns", "record_fill_slot", "gather_rows", "ppo_loss", "rollout_record", "rnd_update")
 C3_ENVS = 65536  # BASELINE.json configs[2] (N=1 headline)
 with open(os.path.join(ROOT, "BASELINE.json")) as _f:
     BASELINE_METRIC = json.load(_f)["metric"]
@@ -123,7 +123,10 @@ def _cpu_share():
 
 def cpu_baseline(args):
     """The reference's PPO iteration in torch-CPU ops (oracle/torch_cpu_ppo.py) on every CPU this process may use:
-    a C2-shaped sample (N 4096) and a C3-shaped sample (N 16384, T/obs/act/MLP of C3); value = the latter."""
+    a bounded sample of the C3 iteration at its full size (N 65536: the whole rollout and compute_returns, then
+    `--cpu-mini-batches` of the 20 update mini-batches, the update extrapolated from them) = value, and one whole
+    C2 iteration (N 4096) for reference.  scripts/ref_cpu_timing.py times the reference's own iteration next to this
+    port on the build host (the port runs ~1.2x faster than the reference there: the baseline is not understated)."""
     from oracle import torch_cpu_ppo
 
     share = _cpu_share()
@@ -132,40 +135,43 @@ def cpu_baseline(args):
     probe = {}
     for th in sorted({share, max(1, share // 2)}, reverse=True):
         probe[th] = torch_cpu_ppo.time_iterations(4096, args.num_obs, args.num_actions, T=args.num_steps_per_env,
-                                                  iters=1, warmup=1, threads=th)[0]
+                                                  iters=1, warmup=0, threads=th)[0]
     threads = max(probe, key=probe.get)
     out = {}
-    for name, n in (("C2", 4096), ("C3_sample", args.cpu_sample_envs)):
-        rate, secs, parts = torch_cpu_ppo.time_iterations(n, args.num_obs, args.num_actions,
-                                                          T=args.num_steps_per_env, iters=1, warmup=1,
-                                                          threads=threads)
-        out[name] = {"env_steps_per_s": round(rate, 1), "num_envs": n, "timed_seconds": round(secs, 2),
-                     "update_env_steps_per_s": round(parts["update_env_steps_per_s"], 1),
-                     "hot_path_env_steps_per_s": round(parts["hot_path_env_steps_per_s"], 1),
-                     "phase_seconds": parts["seconds"]}
+    rate, secs, parts = torch_cpu_ppo.time_iterations(4096, args.num_obs, args.num_actions, T=args.num_steps_per_env,
+                                                      iters=1, warmup=1, threads=threads)
+    out["C2"] = {"env_steps_per_s": round(rate, 1), "num_envs": 4096, "timed_seconds": round(secs, 2),
+                 "update_env_steps_per_s": round(parts["update_env_steps_per_s"], 1), "phase_seconds": parts["seconds"]}
+    n = args.num_envs_local
+    rate, secs, parts = torch_cpu_ppo.time_full_size_sample(n, args.num_obs, args.num_actions,
+                                                            T=args.num_steps_per_env,
+                                                            mini_batches=args.cpu_mini_batches, threads=threads)
+    out["C3_full_size_sample"] = {"env_steps_per_s": round(rate, 1), "num_envs": n, "timed_seconds": round(secs, 2),
+                                  "update_env_steps_per_s": round(parts["update_env_steps_per_s"], 1),
+                                  "phase_seconds": parts["seconds"]}
     model = ""
     try:
         with open("/proc/cpuinfo") as f:
             model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), "")
     except OSError:
         pass
-    big = out["C3_sample"]
+    big = out["C3_full_size_sample"]
     return {
         "value": big["env_steps_per_s"],
         "unit": "env-steps/s",
         "cores": threads,
         "kind": "port",
         "update_env_steps_per_s": big["update_env_steps_per_s"],
-        "hot_path_env_steps_per_s": big["hot_path_env_steps_per_s"],
         "samples": out,
         "thread_probe_c2_env_steps_per_s": {str(k): round(v, 1) for k, v in probe.items()},
         "cpu_share": share,
-        "sample": f"1 timed PPO iteration (+1 warmup) of the reference's algorithm in torch-CPU ops "
-                  f"(oracle/torch_cpu_ppo.py: rollout, compute_returns loop, randperm + per-mini-batch gathers, "
-                  f"Normal log-prob/entropy/KL, clipped losses, autograd, clip_grad_norm_, Adam) at "
-                  f"N={args.cpu_sample_envs} envs with C3's T={args.num_steps_per_env}, obs {args.num_obs}, "
-                  f"act {args.num_actions}, 3x256 MLP (value), and at C2 (N 4096); {threads} threads (the faster of "
-                  f"the {share}-CPU affinity/cgroup share and half of it on a C2 probe); CPU: {model}",
+        "sample": f"the reference's algorithm in torch-CPU ops (oracle/torch_cpu_ppo.py: rollout, compute_returns loop, "
+                  f"randperm + per-mini-batch gathers, Normal log-prob/entropy/KL, clipped losses, autograd, "
+                  f"clip_grad_norm_, Adam) at the bench workload's full size N={n}, T={args.num_steps_per_env}, obs "
+                  f"{args.num_obs}, act {args.num_actions}, 3x256 MLP: the whole rollout + compute_returns timed, then "
+                  f"{args.cpu_mini_batches} of the 20 update mini-batches, the update extrapolated as first + 19 x "
+                  f"mean(rest) (value); plus one whole C2 iteration (N 4096); {threads} threads (the faster of the "
+                  f"{share}-CPU affinity/cgroup share and half of it on a C2 probe); CPU: {model}",
     }
 
 
@@ -184,7 +190,8 @@ def main():
     ap.add_argument("--num-actions", type=int, default=12)
     ap.add_argument("--hidden", type=int, default=256)
     ap.add_argument("--layers", type=int, default=3)
-    ap.add_argument("--cpu-sample-envs", type=int, default=16384)
+    ap.add_argument("--cpu-mini-batches", type=int, default=3,
+                    help="update mini-batches the CPU baseline times at full size (the rest are extrapolated)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true",
                     help="skip the secondary configurations (C5, f32 / h3 GEMMs, C4 total on one GPU)")

@@ -109,11 +109,17 @@ class TorchCpuPPO:
                 idx = indices[i * mb:(i + 1) * mb]
                 yield {k: v[idx] for k, v in flat.items()}
 
-    def update(self):
+    def update(self, max_mini_batches=None):
+        """One update; with max_mini_batches only that many of the E*M mini-batches run (a bounded sample; the
+        wall time of each, generator gather included, is in self.timing["mini_batch_seconds"])."""
         sums = [0.0, 0.0, 0.0]
         hot = 0.0
         gen = self._batches()
+        mb_times = []
         while True:
+            if max_mini_batches is not None and len(mb_times) >= max_mini_batches:
+                break
+            t_mb = time.perf_counter()
             t0 = time.perf_counter()
             b = next(gen, None)
             hot += time.perf_counter() - t0
@@ -153,8 +159,10 @@ class TorchCpuPPO:
             sums[0] += value_loss.item()
             sums[1] += surrogate_loss.item()
             sums[2] += entropy.mean().item()
+            mb_times.append(time.perf_counter() - t_mb)
         n = self.E * self.M
         self.timing["hot_loss_and_batches"] = hot
+        self.timing["mini_batch_seconds"] = mb_times
         return {"value_function": sums[0] / n, "surrogate": sums[1] / n, "entropy": sums[2] / n}
 
     def iteration(self):
@@ -187,4 +195,35 @@ def time_iterations(N, O=48, A=12, T=24, iters=1, warmup=1, threads=None):
         "update_env_steps_per_s": steps / (agg["returns"] + agg["update"]),
         "hot_path_env_steps_per_s": steps / hot,
         "seconds": {k: round(v, 3) for k, v in agg.items()},
+    }
+
+
+def time_full_size_sample(N, O=48, A=12, T=24, mini_batches=3, threads=None):
+    """A bounded sample of one iteration at the full size N (no shrinking of the workload): the whole rollout and
+    compute_returns are timed, then the first `mini_batches` of the E*M mini-batches of the update (each with its
+    generator gathers; the first one also draws the permutation); the update time is extrapolated as
+    first + (E*M - 1) * mean(the others).  Returns (env-steps/s end to end, seconds of CPU work timed, details)."""
+    if threads:
+        torch.set_num_threads(threads)
+    ppo = TorchCpuPPO(N, O, A, T=T)
+    with torch.inference_mode():  # first-touch / thread-pool warm-up on one small forward, outside the timing
+        ppo.actor(torch.randn(1024, O))
+    t0 = time.perf_counter()
+    ppo.rollout()
+    t1 = time.perf_counter()
+    ppo.compute_returns()
+    t2 = time.perf_counter()
+    ppo.update(max_mini_batches=mini_batches)
+    t3 = time.perf_counter()
+    mbs = ppo.timing["mini_batch_seconds"]
+    n_mb = ppo.E * ppo.M
+    rest = sum(mbs[1:]) / max(1, len(mbs) - 1) if len(mbs) > 1 else mbs[0]
+    update_est = mbs[0] + (n_mb - 1) * rest
+    steps = N * T
+    total_est = (t1 - t0) + (t2 - t1) + update_est
+    return steps / total_est, t3 - t0, {
+        "update_env_steps_per_s": steps / ((t2 - t1) + update_est),
+        "seconds": {"rollout": round(t1 - t0, 3), "returns": round(t2 - t1, 3),
+                    "mini_batches_timed": [round(x, 3) for x in mbs], "update_extrapolated": round(update_est, 3),
+                    "iteration_extrapolated": round(total_est, 3)},
     }

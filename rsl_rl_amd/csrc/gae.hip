@@ -115,7 +115,35 @@ __global__ __launch_bounds__(kBlock) void moments_kernel(const float* __restrict
     if (threadIdx.x == 0) partials[blockIdx.x] = make_double2(s, ss);
 }
 
-// Mean and unbiased std (torch.Tensor.std default, correction = 1) from the partials, in a fixed order.
+// fp64 mean of the vector from the partials' sums (.x), folded in a fixed order (every block gets the same bits).
+__device__ __forceinline__ double fold_mean(const double2* __restrict__ partials, int np, int64_t n) {
+    __shared__ double scratch[kBlock / kWave];
+    double s = 0.0;
+    for (int i = threadIdx.x; i < np; i += kBlock) s += partials[i].x;
+    s = block_sum(s, scratch);
+    return s / static_cast<double>(n);
+}
+
+// Second pass of the two-pass variance: block b (of the np blocks that wrote the sums) replaces partials[b].y with
+// sum over its grid-stride slice of (a - mean)^2 in fp64 (the first pass's sum of squares is not used: no
+// cancellation between sum(a^2) and n mean^2).
+__global__ __launch_bounds__(kBlock) void centered_sq_kernel(const float* __restrict__ x, int64_t n,
+                                                             double2* __restrict__ partials) {
+    __shared__ double scratch[kBlock / kWave];
+    const double mean = fold_mean(partials, gridDim.x, n);
+    double ss = 0.0;
+    const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
+    for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < n; i += stride) {
+        const double d = static_cast<double>(x[i]) - mean;
+        ss += d * d;
+    }
+    ss = block_sum(ss, scratch);
+    __syncthreads();  // every wave of this block has read partials[*].x (fold_mean) before .y is replaced
+    if (threadIdx.x == 0) partials[blockIdx.x].y = ss;
+}
+
+// Mean and unbiased std (torch.Tensor.std default, correction = 1) from the partials (.x sums, .y centred sums of
+// squares from centered_sq_kernel), in a fixed order.
 __device__ __forceinline__ void fold_moments(const double2* __restrict__ partials, int np, int64_t n,
                                              float* mean_out, float* std_out) {
     __shared__ double scratch[2][kBlock / kWave];
@@ -128,8 +156,7 @@ __device__ __forceinline__ void fold_moments(const double2* __restrict__ partial
     s = block_sum(s, scratch[0]);
     ss = block_sum(ss, scratch[1]);
     const double mean = s / static_cast<double>(n);
-    double var = (ss - s * mean) / static_cast<double>(n - 1);
-    if (var < 0.0) var = 0.0;  // rounding guard for constant inputs (true variance is 0)
+    const double var = n > 1 ? ss / static_cast<double>(n - 1) : __builtin_nan("");  // torch: NaN std for one element
     *mean_out = static_cast<float>(mean);
     *std_out = static_cast<float>(sqrt(var));
 }
@@ -219,6 +246,9 @@ extern "C" int rslrl_compute_returns(const float* values, const float* rewards, 
     int rc = launch_status();
     if (rc != RSLRL_OK || !normalize_advantage) return rc;
     const int64_t n = T * N;
+    hipLaunchKernelGGL(centered_sq_kernel, dim3(nb), dim3(kBlock), 0, st, advantages, n, part);
+    rc = launch_status();
+    if (rc != RSLRL_OK) return rc;
     hipLaunchKernelGGL(adv_normalize_kernel, dim3(elementwise_blocks(n)), dim3(kBlock), 0, st, advantages, n, part,
                        nb, 1e-8f);
     return launch_status();
@@ -236,6 +266,9 @@ extern "C" int rslrl_normalize_advantages(float* advantages, int64_t n, float ep
     const int nb = static_cast<int>(std::min<int64_t>(ceil_div(n, kBlock), kMaxPartials));
     hipLaunchKernelGGL(moments_kernel, dim3(nb), dim3(kBlock), 0, st, advantages, n, part);
     int rc = launch_status();
+    if (rc != RSLRL_OK) return rc;
+    hipLaunchKernelGGL(centered_sq_kernel, dim3(nb), dim3(kBlock), 0, st, advantages, n, part);
+    rc = launch_status();
     if (rc != RSLRL_OK) return rc;
     hipLaunchKernelGGL(adv_normalize_kernel, dim3(elementwise_blocks(n)), dim3(kBlock), 0, st, advantages, n, part,
                        nb, eps);

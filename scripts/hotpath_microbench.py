@@ -86,7 +86,10 @@ def main():
             sig = (0.5 + torch.rand(A if mode == "loss" else (B, A), device=dev, generator=g)).contiguous()
             x = torch.randn(B, A, device=dev, generator=g)
             omu = torch.randn(B, A, device=dev, generator=g)
-            osig = 0.5 + torch.rand(B, A, device=dev, generator=g)
+            # as a rollout stores it: one old sigma per action for every sample with a shared std (the training
+            # step's case), per row otherwise
+            osig = ((0.5 + torch.rand(A, device=dev, generator=g)).expand(B, A).contiguous() if mode == "loss"
+                    else 0.5 + torch.rand(B, A, device=dev, generator=g))
             sc = [torch.randn(B, 1, device=dev, generator=g) for _ in range(5)]
             sets.append((mu, sig, sc[0], x, sc[1], sc[2], sc[3], sc[4], omu, osig))
         outs = [(torch.empty(B, A, device=dev), torch.empty(sets[0][1].shape, device=dev),
