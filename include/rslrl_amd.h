@@ -500,6 +500,17 @@ size_t rslrl_rnd_update_workspace_bytes(int64_t B, int32_t in, int32_t hidden, i
 int rslrl_rnd_update(const rslrl_rnd_update_args_t* args /* host struct */, void* workspace, size_t workspace_bytes,
                      rslrl_stream_t stream);
 
+/* ------------------------------------------------------------------------------------------------
+ * Benchmark environment (SURVEY.md §8d synthetic VecEnv; not a reference interface): one env step for N envs in
+ * one launch -- obs [N, num_obs] ~ N(0,1) (num_obs % 4 == 0, 16-byte aligned), rewards [N] ~ N(0,1), then with
+ * u ~ U[0,1): episode_length += 1, over = episode_length >= max_episode_length, dones (int64) = over or
+ * u < done_prob, time_outs (fp32) = over or u < done_prob * timeout_prob, episode_length = 0 where done.
+ * Counter-based (philox4x32-10 keyed by seed, counter by step and env): deterministic for (seed, step).
+ * ----------------------------------------------------------------------------------------------*/
+int rslrl_synthetic_env_step(float* obs, int32_t num_obs, float* rewards, int64_t* dones, float* time_outs,
+                             int64_t* episode_length, int64_t N, uint64_t seed, uint32_t step, float done_prob,
+                             float timeout_prob, int64_t max_episode_length, rslrl_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -67,6 +67,7 @@ EXPORTED_SYMBOLS = (
     "rslrl_clip_adam_step",
     "rslrl_rnd_update_workspace_bytes",
     "rslrl_rnd_update",
+    "rslrl_synthetic_env_step",
 )
 
 MAX_GATHER_FIELDS = 16
@@ -352,6 +353,8 @@ def _declare(L):
     L.rslrl_rnd_update_workspace_bytes.argtypes = [I64, I32, I32, I32]
     L.rslrl_rnd_update.restype = ctypes.c_int
     L.rslrl_rnd_update.argtypes = [ctypes.POINTER(RndUpdateArgs), P, SZ, P]
+    L.rslrl_synthetic_env_step.restype = ctypes.c_int
+    L.rslrl_synthetic_env_step.argtypes = [P, I32, P, P, P, P, I64, ctypes.c_uint64, ctypes.c_uint32, F, F, I64, P]
 
 
 def lib():

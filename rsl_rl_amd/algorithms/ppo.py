@@ -35,6 +35,7 @@ import torch.optim as optim
 from .. import kernels
 from ..modules import ActorCritic
 from ..networks import fused_mlp
+from ..modules.act_graph import RolloutActGraph
 from ..modules.rnd import RandomNetworkDistillation
 from ..storage import RolloutStorage
 from ..utils import string_to_callable
@@ -169,6 +170,7 @@ class PPO:
         self._rnd_adam = (kernels.FusedClipAdam(self.rnd_optimizer, 0.0)
                           if on_gpu and self.rnd_optimizer is not None
                           and kernels.FusedClipAdam.supported(self.rnd_optimizer) else None)
+        self._act_graph = RolloutActGraph(self.policy) if on_gpu and isinstance(self.policy, ActorCritic) else None
         self.storage: RolloutStorage = None  # type: ignore
         self.transition = RolloutStorage.Transition()
 
@@ -203,8 +205,12 @@ class PPO:
             self.transition.hidden_states = self.policy.get_hidden_states()
         pcls = type(self.policy)
         if isinstance(self.policy, ActorCritic) and pcls.act is ActorCritic.act and pcls.evaluate is ActorCritic.evaluate:
-            # the actor's and critic's hidden layers batched into one launch each (same values and draws)
-            actions, values = self.policy.act_and_evaluate(obs)
+            # the actor's and critic's hidden layers batched into one launch each (same values and draws), replayed
+            # as one captured HIP graph per configuration (modules/act_graph.py)
+            res = None
+            if self._act_graph is not None and RolloutActGraph.enabled():
+                res = self._act_graph(obs)
+            actions, values = res if res is not None else self.policy.act_and_evaluate(obs)
         else:
             actions, values = self.policy.act(obs), self.policy.evaluate(obs)
         self.transition.actions = actions.detach()

@@ -32,6 +32,12 @@ class SyntheticVecEnv(VecEnv):
         self.gen = torch.Generator(device=self.device)
         self.gen.manual_seed(seed)
         self._obs = self._draw_obs()
+        # on a ROCm device one step is one launch (rslrl_synthetic_env_step: the same distributions and done /
+        # time-out / episode-length rules from a counter-based generator keyed by `seed`); CPU tensors and
+        # privileged observation groups keep the torch implementation below
+        self._fused = self.device.type == "cuda" and num_privileged_obs == 0 and num_obs % 4 == 0
+        self._seed = int(seed)
+        self._step_count = 0
 
     @property
     def unwrapped(self):
@@ -48,6 +54,8 @@ class SyntheticVecEnv(VecEnv):
         return self._obs
 
     def step(self, actions: torch.Tensor):
+        if self._fused:
+            return self._step_fused()
         n = self.num_envs
         self._obs = self._draw_obs()
         rewards = torch.randn(n, generator=self.gen, device=self.device)
@@ -63,4 +71,22 @@ class SyntheticVecEnv(VecEnv):
         time_outs = torch.where(over, torch.ones_like(time_outs), time_outs)
         self.episode_length_buf = torch.where(dones > 0, torch.zeros_like(self.episode_length_buf),
                                               self.episode_length_buf)
+        return self._obs, rewards, dones, {"time_outs": time_outs}
+
+    def _step_fused(self):
+        from .. import _lib
+        from ..kernels import _stream
+
+        n, dev = self.num_envs, self.device
+        obs = torch.empty(n, self.num_obs, device=dev)
+        rewards = torch.empty(n, device=dev)
+        dones = torch.empty(n, dtype=torch.long, device=dev)
+        time_outs = torch.empty(n, device=dev)
+        self._step_count += 1
+        rc = _lib.lib().rslrl_synthetic_env_step(
+            obs.data_ptr(), self.num_obs, rewards.data_ptr(), dones.data_ptr(), time_outs.data_ptr(),
+            self.episode_length_buf.data_ptr(), n, self._seed, self._step_count & 0xFFFFFFFF, float(self.done_prob),
+            float(self.timeout_prob), int(self.max_episode_length), _stream(dev))
+        _lib.check(rc, "rslrl_synthetic_env_step")
+        self._obs = TensorDict({"policy": obs}, batch_size=[n], device=dev)
         return self._obs, rewards, dones, {"time_outs": time_outs}

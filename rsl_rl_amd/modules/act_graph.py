@@ -1,0 +1,105 @@
+"""The policy half of a rollout step as one captured HIP graph (ppo.py:129-140: act -> actor and critic forwards,
+the Normal sample; on_policy_runner.py:103-109 calls it once per env step).
+
+Eagerly, ActorCritic.act_and_evaluate issues ~20 host calls per step (the B-image build, the paired MLP launches
+through ctypes, the Normal sample's four torch ops): ~100 us of host time that the GPU waits out when a GPU holds
+few envs (the strong-scaling shares of config C4).  Here the same calls are captured once per configuration into a
+torch.cuda.CUDAGraph and replayed: the observation is copied into the graph's static input, the graph replays
+(image build included, so parameters updated in place between rollouts are picked up), and the outputs are the
+graph's static tensors (the actions are cloned, so a caller may keep them).
+
+Same values and the same random stream as the eager calls: the sample's normal_() draws from the default CUDA
+generator, whose offset a captured graph advances by the same increment per replay as the eager kernel does per
+call (PyTorch's graph-safe philox); tests/test_gpu_act_graph.py compares a graphed and an eager rollout bitwise.
+The first call of a configuration runs eagerly, the second captures; any capture failure falls back to the eager
+path for that configuration.  RSLRL_ACT_GRAPH=0 disables it.
+"""
+
+from __future__ import annotations
+
+import contextlib
+import os
+import warnings
+
+import torch
+from torch.distributions import Normal
+
+from .. import kernels
+from ..networks import fused_mlp
+
+
+class RolloutActGraph:
+    def __init__(self, policy):
+        self.policy = policy
+        self._key = None
+        self._seen = 0
+        self._graph = None
+        self._failed = set()
+        self._static_in = None
+        self._out = None
+
+    @staticmethod
+    def enabled() -> bool:
+        return os.environ.get("RSLRL_ACT_GRAPH", "1") != "0"
+
+    def _config(self, obs):
+        pol = self.policy
+        groups = sorted(set(pol.obs_groups["policy"]) | set(pol.obs_groups["critic"]))
+        shapes = []
+        for g in groups:
+            t = obs[g]
+            if not (isinstance(t, torch.Tensor) and t.is_cuda):
+                return None
+            shapes.append((g, tuple(t.shape), t.dtype, t.device, t.stride()))
+        ptrs = tuple(p.data_ptr() for p in pol.parameters()) + tuple(b.data_ptr() for b in pol.buffers())
+        return (tuple(shapes), ptrs, fused_mlp._mode, torch.is_inference_mode_enabled())
+
+    def __call__(self, obs):
+        """(actions, values) of the step, with policy.distribution set as act() sets it; None: run eagerly."""
+        key = self._config(obs)
+        if key is None or key in self._failed:
+            return None
+        if key != self._key:
+            self._key, self._seen, self._graph, self._static_in, self._out = key, 0, None, None, None
+        if self._graph is None:
+            self._seen += 1
+            if self._seen < 2:  # the first call of a configuration runs eagerly (lazy initialisations happen there)
+                return None
+            if not self._capture(obs, key):
+                return None
+        for g, t in self._static_in.items():
+            t.copy_(obs[g])
+        self._graph.replay()
+        actions, values, mean, scale = self._out
+        self.policy.distribution = Normal(mean, scale)
+        return actions.clone(), values
+
+    def _capture(self, obs, key) -> bool:
+        pol = self.policy
+        static_in = {g: obs[g].clone() for g in sorted(set(pol.obs_groups["policy"]) | set(pol.obs_groups["critic"]))}
+        graph = torch.cuda.CUDAGraph()
+        try:
+            with _eager_caches_off(), torch.cuda.graph(graph):
+                actions, values = pol.act_and_evaluate(static_in)
+                dist = pol.distribution
+                out = (actions, values, dist.loc, dist.scale)
+        except Exception as e:  # noqa: BLE001 -- any op that cannot be captured: stay eager for this configuration
+            self._failed.add(key)
+            warnings.warn(f"rollout act() graph capture failed, running eagerly: {e}")
+            return False
+        self._graph, self._static_in, self._out = graph, static_in, out
+        return True
+
+
+@contextlib.contextmanager
+def _eager_caches_off():
+    """No frozen-weights B-image reuse and no kernel-timer events while capturing: the image build is captured
+    into the graph (rebuilt at every replay from the current weights) and no timing event lands in it."""
+    depth, en, men = fused_mlp._frozen_depth, kernels.timer.enabled, kernels.timer.mlp_enabled
+    fused_mlp._frozen_depth = 0
+    kernels.timer.enabled = kernels.timer.mlp_enabled = False
+    try:
+        yield
+    finally:
+        fused_mlp._frozen_depth = depth
+        kernels.timer.enabled, kernels.timer.mlp_enabled = en, men

@@ -1,0 +1,48 @@
+"""The rollout's act() replayed as a captured HIP graph (modules/act_graph.py) against the eager calls: the same
+actions, values, log-probs and storage contents bit for bit over whole training iterations (the sample draws from
+the default CUDA generator in the same order), and the same parameters after the updates."""
+
+import contextlib
+import io
+
+import pytest
+import torch
+
+from rsl_rl_amd.env import SyntheticVecEnv
+from rsl_rl_amd.runners import OnPolicyRunner
+
+pytestmark = pytest.mark.gpu
+
+
+def _cfg(hidden, timeouts=False):
+    return {"num_steps_per_env": 8, "save_interval": 10**9, "obs_groups": {"policy": ["policy"], "critic": ["policy"]},
+            "policy": {"class_name": "ActorCritic", "activation": "elu", "actor_hidden_dims": hidden,
+                       "critic_hidden_dims": hidden, "init_noise_std": 1.0},
+            "algorithm": {"class_name": "PPO", "num_learning_epochs": 2, "num_mini_batches": 2}}
+
+
+def _run(graph: bool, monkeypatch, dev, hidden, n_envs, iters=3):
+    monkeypatch.setenv("RSLRL_ACT_GRAPH", "1" if graph else "0")
+    torch.manual_seed(7)
+    env = SyntheticVecEnv(n_envs, 48, 12, device=dev, seed=3, timeout_prob=0.2)
+    with contextlib.redirect_stdout(io.StringIO()):
+        runner = OnPolicyRunner(env, _cfg(hidden), log_dir=None, device=dev)
+        snaps = []
+        for _ in range(iters):
+            runner.learn(1)
+            st = runner.alg.storage
+            snaps.append({k: getattr(st, k).clone() for k in ("actions", "values", "actions_log_prob", "rewards")})
+    params = [p.detach().clone() for p in runner.alg.policy.parameters()]
+    return snaps, params, runner.alg._act_graph
+
+
+@pytest.mark.parametrize("hidden,n_envs", [([256, 256, 256], 4096), ([64, 64], 1000)])
+def test_graphed_rollout_matches_eager(hidden, n_envs, cuda_device, monkeypatch):
+    eager, p_eager, _ = _run(False, monkeypatch, cuda_device, hidden, n_envs)
+    graphed, p_graph, g = _run(True, monkeypatch, cuda_device, hidden, n_envs)
+    assert g is not None and g._graph is not None, "the graph was not captured"
+    for a, b in zip(eager, graphed):
+        for k in a:
+            assert torch.equal(a[k], b[k]), k
+    for a, b in zip(p_eager, p_graph):
+        assert torch.equal(a, b)
