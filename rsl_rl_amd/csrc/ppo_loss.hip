@@ -480,8 +480,8 @@ __device__ __forceinline__ void fold_columns(const double* __restrict__ src, int
 // (current + prefetched) of row pieces live per lane.
 constexpr int quad_waves(int apl, bool shared, bool kl) { return (apl == 1 && (shared || !kl)) ? 4 : 2; }
 
-template <int APL, bool SHARED, bool KL>
-__global__ __launch_bounds__(kBlock, quad_waves(APL, SHARED, KL)) void ppo_loss_quad_kernel(LossParams p, double* __restrict__ partials,
+template <int APL, bool SHARED, bool KL, int DEPTH = 1>
+__global__ __launch_bounds__(kBlock, DEPTH > 1 ? 1 : quad_waves(APL, SHARED, KL)) void ppo_loss_quad_kernel(LossParams p, double* __restrict__ partials,
                                                                unsigned* __restrict__ tickets, float value_loss_coef,
                                                                float entropy_coef) {
     constexpr int A = 4 * APL;
@@ -594,11 +594,12 @@ __global__ __launch_bounds__(kBlock, quad_waves(APL, SHARED, KL)) void ppo_loss_
         }
     };
     uint32_t tile = blockIdx.x * (kBlock / kWave) + wid;
-    TileIn cur;
+    TileIn cur, ahead;  // DEPTH 2: `ahead` = the tile after the next one is loaded while this one is computed
     if (tile < ntiles) load_tile(tile, cur);
+    if constexpr (DEPTH > 1) load_tile(tile + tstride, ahead);
     for (; tile < ntiles; tile += tstride) {
         TileIn nxt;
-        load_tile(tile + tstride, nxt);
+        load_tile(tile + DEPTH * tstride, nxt);
         const uint32_t base = tile * kWave;
         const uint32_t is = base + lane;
         const bool vs = is < B32;
@@ -759,7 +760,12 @@ __global__ __launch_bounds__(kBlock, quad_waves(APL, SHARED, KL)) void ppo_loss_
                 store_piece<APL>(r_gsg, iq * gsg_row + piece, gsg);
             }
         }
-        cur = nxt;
+        if constexpr (DEPTH > 1) {
+            cur = ahead;
+            ahead = nxt;
+        } else {
+            cur = nxt;
+        }
     }
 
     // ---- block partials: scalar columns by wave butterfly; sigma columns over lanes of equal q
@@ -928,10 +934,19 @@ bool use_quad(int sigma_mode) {
     return sigma_mode == 0;
 }
 
+// software-pipeline depth of the quad kernel (tiles in flight per wave beyond the one computed); RSLRL_LOSS_DEPTH
+// overrides it (read per call: A/B runs)
+int loss_depth() {
+    const char* e = std::getenv("RSLRL_LOSS_DEPTH");
+    return (e && e[0] == '2') ? 2 : 1;
+}
+
 template <int APL>
 void launch_quad(const LossParams& p, int nb, double* part, unsigned* tickets, float cv, float ce, hipStream_t st) {
     const dim3 g(nb), b(kBlock);
-    if (p.sigma_mode == 0 && p.compute_kl)
+    if (p.sigma_mode == 0 && p.compute_kl && loss_depth() == 2)
+        hipLaunchKernelGGL((ppo_loss_quad_kernel<APL, true, true, 2>), g, b, 0, st, p, part, tickets, cv, ce);
+    else if (p.sigma_mode == 0 && p.compute_kl)
         hipLaunchKernelGGL((ppo_loss_quad_kernel<APL, true, true>), g, b, 0, st, p, part, tickets, cv, ce);
     else if (p.sigma_mode == 0)
         hipLaunchKernelGGL((ppo_loss_quad_kernel<APL, true, false>), g, b, 0, st, p, part, tickets, cv, ce);

@@ -212,3 +212,22 @@ def test_shared_sigma_kl_fast_path_bit_exact(B, perturb, cuda_device, monkeypatc
         ref = O.ppo_loss(mu, np.broadcast_to(sig_vec, (B, A)), V, x, old_logp, adv, tv, R, omu, osig)
         kl = float(out["1"][0][kernels.STATS_KL])
         assert abs(kl - ref["kl_mean"]) <= RTOL * abs(ref["kl_mean"]) + 1e-7
+
+
+def test_quad_kernel_pipeline_depth_bit_identical(cuda_device, monkeypatch):
+    """RSLRL_LOSS_DEPTH 2 (two tiles in flight per wave) computes every tile the same way: identical bits."""
+    monkeypatch.setenv("RSLRL_LOSS_KERNEL", "quad")
+    torch.manual_seed(5)
+    B, A, d = 100003, 12, cuda_device
+    mu, x, omu = (torch.randn(B, A, device=d) for _ in range(3))
+    osig = (0.5 + torch.rand(A, device=d)).expand(B, A).contiguous()
+    sigma = 0.5 + torch.rand(A, device=d)
+    V, old_logp, adv, tv, R = (torch.randn(B, 1, device=d) for _ in range(5))
+    out = []
+    for depth in ("1", "2"):
+        monkeypatch.setenv("RSLRL_LOSS_DEPTH", depth)
+        res = kernels.ppo_loss_fwd_bwd(mu, sigma, V, x, old_logp, adv, tv, R, omu, osig)
+        torch.cuda.synchronize()
+        out.append([t.clone() for t in res])
+    for a, b in zip(*out):
+        assert torch.equal(a, b)
