@@ -50,7 +50,7 @@ C4_ENVS = 131072  # BASELINE.json configs[3]: the total partitioned over the ran
 # per-launch HBM traffic of the hot-path kernels from rocprofv3 FETCH_SIZE / WRITE_SIZE passes over this same
 # bench command (scripts/pmc_summary.py; raw counters next to it).  PMC passes serialise and slow the
 # run, so they are collected separately and the committed summary is reported here.
-PMC_TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r2_pmc_traffic.json")
+PMC_TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r3_pmc_traffic.json")
 
 
 def pmc_traffic(kernel):

@@ -86,6 +86,11 @@ __global__ __launch_bounds__(kBlock) void rollout_record_kernel(rslrl_rollout_ar
         const int rows = static_cast<int>(min<int64_t>(kRecRows, N - n0));
         const int total = rows * rs.r4;  // <= 64 * 64: exact float division below
         float4* dst = rs.dst0 + n0 * rs.r4;
+        // the actions / mu / sigma units of these records also go to LDS ([3][64][A], dynamic LDS): the log-prob is
+        // computed here from the values the copy already loaded, instead of the per-env threads reading the actions
+        // and mu rows a second time
+        const int seg_x = rs.nseg - 3;  // segments: obs groups, then actions, mu, sigma (host order)
+        const int A = a.A;
         // every load of a pass is issued before its stores (a store between two loads would order them)
         constexpr int kPass = 8;
         for (int k0 = threadIdx.x; k0 < total; k0 += kPass * kBlock) {
@@ -102,8 +107,34 @@ __global__ __launch_bounds__(kBlock) void rollout_record_kernel(rslrl_rollout_ar
                 }
             }
 #pragma unroll
-            for (int j = 0; j < kPass; ++j)
-                if (k0 + j * kBlock < total) dst[k0 + j * kBlock] = v[j];
+            for (int j = 0; j < kPass; ++j) {
+                const int k = k0 + j * kBlock;
+                if (k < total) {
+                    dst[k] = v[j];
+                    const int r = static_cast<int>((static_cast<float>(k) + 0.5f) * rs.rcp_r4);
+                    const int u = k - r * rs.r4;
+                    const int sg = useg[u];
+                    if (sg >= seg_x)
+                        *reinterpret_cast<float4*>(lds_w + ((sg - seg_x) * kRecRows + r) * A + 4 * (u - sstart[sg])) = v[j];
+                }
+            }
+        }
+        __syncthreads();
+        if (static_cast<int>(threadIdx.x) < rows) {
+            // log-prob of the action under Normal(mu, sigma), torch's expression (see the per-env part below)
+            const float c = 0.918938533204672742f;
+            const float* xr = lds_w + threadIdx.x * A;
+            const float* mr = lds_w + (kRecRows + threadIdx.x) * A;
+            const float* sr = lds_w + (2 * kRecRows + threadIdx.x) * A;
+            float lp = 0.f;
+            for (int j = 0; j < A; ++j) {
+                const float sj = sr[j];
+                const float d = __fsub_rn(xr[j], mr[j]);
+                const float num = -__fmul_rn(d, d);
+                const float den = __fmul_rn(2.f, __fmul_rn(sj, sj));
+                lp = __fadd_rn(lp, __fsub_rn(__fsub_rn(__fdiv_rn(num, den), logf(sj)), c));
+            }
+            a.out_logp[n0 + threadIdx.x] = lp;
         }
         return;
     }
@@ -160,18 +191,22 @@ __global__ __launch_bounds__(kBlock) void rollout_record_kernel(rslrl_rollout_ar
 
     // log-prob of the action under Normal(mu, sigma): torch's
     //   -((x - mu) ** 2) / (2 * var) - log(sigma) - log(sqrt(2 pi)),  var = sigma ** 2, summed over A
-    const float c = 0.918938533204672742f;  // math.log(math.sqrt(2 * math.pi)) rounded to fp32
+    // (record mode: computed by the copy blocks above)
+    const bool rec = a.record_floats > 0;
     float lp = 0.f;
-    const float* xr = a.actions + n * a.A;
-    const float* mr = a.mu + n * a.A;
-    const float* sr = a.sigma_mode ? a.sigma + n * a.A : a.sigma;
-    for (int j = 0; j < a.A; ++j) {
-        const float s = sr[j];
-        const float d = __fsub_rn(xr[j], mr[j]);
-        const float num = -__fmul_rn(d, d);
-        const float den = __fmul_rn(2.f, __fmul_rn(s, s));
-        const float t = __fsub_rn(__fsub_rn(__fdiv_rn(num, den), logf(s)), c);
-        lp = __fadd_rn(lp, t);
+    if (!rec) {
+        const float c = 0.918938533204672742f;  // math.log(math.sqrt(2 * math.pi)) rounded to fp32
+        const float* xr = a.actions + n * a.A;
+        const float* mr = a.mu + n * a.A;
+        const float* sr = a.sigma_mode ? a.sigma + n * a.A : a.sigma;
+        for (int j = 0; j < a.A; ++j) {
+            const float s = sr[j];
+            const float d = __fsub_rn(xr[j], mr[j]);
+            const float num = -__fmul_rn(d, d);
+            const float den = __fmul_rn(2.f, __fmul_rn(s, s));
+            const float t = __fsub_rn(__fsub_rn(__fdiv_rn(num, den), logf(s)), c);
+            lp = __fadd_rn(lp, t);
+        }
     }
 
     float reward = a.rewards[n];
@@ -219,7 +254,7 @@ __global__ __launch_bounds__(kBlock) void rollout_record_kernel(rslrl_rollout_ar
 
     a.out_rewards[n] = reward;
     a.out_values[n] = v;
-    a.out_logp[n] = lp;
+    if (!rec) a.out_logp[n] = lp;
     a.out_dones[n] = load_flag(a.dones, a.dones_dtype, n) != 0.f ? 1 : 0;
 }
 
@@ -291,10 +326,12 @@ extern "C" int rslrl_rollout_record(const rslrl_rollout_args_t* args, rslrl_stre
     const int copy_blocks = static_cast<int>(cb);
     const int64_t row_blocks = ceil_div(a.N, kBlock);
     if (row_blocks + copy_blocks > INT32_MAX) return RSLRL_E_INVALID_ARGUMENT;
+    if (a.record_floats > 0)  // the copy blocks' [3][64][A] stage of actions / mu / sigma (log-prob)
+        lds = std::max(lds, sizeof(float) * 3 * kRecRows * static_cast<size_t>(a.A));
     const dim3 grid(static_cast<unsigned>(copy_blocks + row_blocks));
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     if (!a.rnd_target)
-        hipLaunchKernelGGL(rollout_record_kernel<0>, grid, dim3(kBlock), 0, st, a, copy_blocks, rs);
+        hipLaunchKernelGGL(rollout_record_kernel<0>, grid, dim3(kBlock), lds, st, a, copy_blocks, rs);
     else if (c5)
         hipLaunchKernelGGL(rollout_record_kernel<1>, grid, dim3(kBlock), lds, st, a, copy_blocks, rs);
     else

@@ -26,6 +26,10 @@ SHORT = {
     "gather_records_kernel": "gather_rows",
     "record_fill_slot_kernel": "record_fill_slot",
     "rollout_record_kernel": "rollout_record",
+    "centered_sq_kernel": "adv_centered_sq",
+    "rnd_update_kernel": "rnd_update",
+    "rnd_fold_kernel": "rnd_fold",
+    "synthetic_env_kernel": "synthetic_env",
     "mlp_gemm_x6_kernel<1": "x6_fwd_elu",
     "mlp_gemm_x6_kernel<2": "x6_dgrad_elu",
     "wgrad_x6_kernel": "x6_wgrad",
