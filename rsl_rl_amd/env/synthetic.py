@@ -8,6 +8,8 @@ global RNG state.  `unwrapped.step_dt` is provided for the RND weight scaling (r
 
 from __future__ import annotations
 
+import os
+
 import torch
 
 from ..utils import TensorDict
@@ -35,7 +37,8 @@ class SyntheticVecEnv(VecEnv):
         # on a ROCm device one step is one launch (rslrl_synthetic_env_step: the same distributions and done /
         # time-out / episode-length rules from a counter-based generator keyed by `seed`); CPU tensors and
         # privileged observation groups keep the torch implementation below
-        self._fused = self.device.type == "cuda" and num_privileged_obs == 0 and num_obs % 4 == 0
+        self._fused = (self.device.type == "cuda" and num_privileged_obs == 0 and num_obs % 4 == 0
+                       and os.environ.get("RSLRL_SYNTH_ENV", "fused") != "torch")
         self._seed = int(seed)
         self._step_count = 0
 
