@@ -34,7 +34,7 @@ constexpr int kRows = 256;       // rows per tile (one per thread)
 constexpr int kChunk = 64;       // rows per LDS reduction chunk (one wave's rows)
 constexpr int kColStride = 68;   // floats per chunk column (64 rows + 4: the 16 x-columns a wave reads hit 16
                                  // distinct 4-bank groups)
-constexpr int kMaxGroups = 512;  // workgroups (partials rows); 2 per CU
+constexpr int kMaxGroups = 512;  // workgroups (partials rows); 2 per CU (<= the fold block's 1024 threads)
 constexpr int kFoldSlices = 16;  // fold: workgroup slices per gradient entry
 
 struct RndParams {
@@ -54,16 +54,30 @@ struct RndParams {
     double* lpart;     // [G] loss partials (sum of squared differences)
 };
 
-// the (normalised) state row of `row` into registers; zeros past `in` and for rows past B
-template <int MAXIN>
+// the (normalised) state row of `row` into registers; zeros past `in` and for rows past B.  VEC (in == MAXIN,
+// 16-byte aligned rows): unconditional 16-byte loads of a clamped row, then the zero select -- a guarded 4-byte load
+// per element issued 48 scattered-row loads per lane
+template <int MAXIN, bool VEC>
 __device__ __forceinline__ void load_state(const RndParams& p, int64_t row, bool valid, int in, float (&x)[MAXIN]) {
     const float* sr = p.state + (valid ? row : 0) * p.stride;
+    if constexpr (VEC) {
+        static_assert(MAXIN % 4 == 0, "whole 16-byte units");
 #pragma unroll
-    for (int i = 0; i < MAXIN; ++i) {
-        float v = (i < in && valid) ? sr[i] : 0.f;
-        if (p.mean && i < in)  // (x - mean) / (std + eps)
-            v = __fdiv_rn(__fsub_rn(v, p.mean[i]), __fadd_rn(p.std[i], p.eps));
-        x[i] = v;
+        for (int k = 0; k < MAXIN / 4; ++k) {
+            const float4 v = reinterpret_cast<const float4*>(sr)[k];
+            x[4 * k] = valid ? v.x : 0.f;
+            x[4 * k + 1] = valid ? v.y : 0.f;
+            x[4 * k + 2] = valid ? v.z : 0.f;
+            x[4 * k + 3] = valid ? v.w : 0.f;
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < MAXIN; ++i) x[i] = (i < in && valid) ? sr[i] : 0.f;
+    }
+    if (p.mean) {  // (x - mean) / (std + eps)
+#pragma unroll
+        for (int i = 0; i < MAXIN; ++i)
+            if (i < in) x[i] = __fdiv_rn(__fsub_rn(x[i], p.mean[i]), __fadd_rn(p.std[i], p.eps));
     }
 }
 
@@ -127,7 +141,7 @@ __global__ __launch_bounds__(kBlock) void rnd_update_kernel(RndParams p) {
         // reduction reloads it, so that only a and dz stay in registers there)
         {
             float x[INP];
-            load_state<INP>(p, row, valid, in, x);
+            load_state<INP, EXACT>(p, row, valid, in, x);
             float t[MAXQ];
             if (own_target) {  // target first: only x and t are live meanwhile
                 float zt[MAXHP];
@@ -181,7 +195,7 @@ __global__ __launch_bounds__(kBlock) void rnd_update_kernel(RndParams p) {
                     chunk[(col_a + h) * kColStride + lane] = a[h];
                 }
                 float x[INP];
-                load_state<INP>(p, row, valid, in, x);
+                load_state<INP, EXACT>(p, row, valid, in, x);
 #pragma unroll
                 for (int i = 0; i < INP; ++i)
                     if (i < in) chunk[(col_x + i) * kColStride + lane] = x[i];
@@ -274,12 +288,20 @@ __global__ __launch_bounds__(1024) void rnd_fold_kernel(const float* __restrict_
         for (int k = 1; k < kFoldSlices; ++k) t += sl[k][lane];
         grad[e] = static_cast<float>(t);
     }
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        double t = 0.0;
-        for (int g = 0; g < G; ++g) t += lpart[g];
-        const float mse = static_cast<float>(t * inv_numel);
-        if (loss) *loss = mse;
-        if (loss_sum) *loss_sum += static_cast<double>(mse);
+    if (blockIdx.x == 0) {  // the loss: G <= kMaxGroups partials over the first waves, then waves in order
+        __shared__ double wl[kFoldSlices];
+        double t = threadIdx.x < static_cast<unsigned>(G) ? lpart[threadIdx.x] : 0.0;
+        t = wave_sum(t);
+        if (lane == 0) wl[s] = t;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            double tot = 0.0;
+#pragma unroll
+            for (int k = 0; k < kFoldSlices; ++k) tot += wl[k];
+            const float mse = static_cast<float>(tot * inv_numel);
+            if (loss) *loss = mse;
+            if (loss_sum) *loss_sum += static_cast<double>(mse);
+        }
     }
 }
 
@@ -349,7 +371,8 @@ extern "C" int rslrl_rnd_update(const rslrl_rnd_update_args_t* a, void* workspac
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     const bool own = a->target_w1 != nullptr;
     int rc;
-    if (a->in == 48 && a->hidden == 48 && a->out == 1)  // config C5
+    const bool aligned_rows = (reinterpret_cast<uintptr_t>(a->state) & 15) == 0 && (a->state_stride & 3) == 0;
+    if (a->in == 48 && a->hidden == 48 && a->out == 1 && aligned_rows)  // config C5
         rc = launch<48, 48, 1, true>(p, G, own, st);
     else if (a->in <= 16 && a->hidden <= 32 && a->out <= 4)
         rc = launch<16, 32, 4, false>(p, G, own, st);

@@ -216,12 +216,24 @@ __global__ __launch_bounds__(kBlock) void rollout_record_kernel(rslrl_rollout_ar
         const int Q = RNDK == 1 ? 1 : a.rnd_out;
         float x[RS::INP];
         const float* sx = a.rnd_obs + n * a.rnd_obs_stride;
+        if constexpr (RS::EXACT) {  // 16-byte aligned rows (checked on the host): 16-byte loads
 #pragma unroll
-        for (int i = 0; i < RS::INP; ++i) {
-            float v = i < in ? sx[i] : 0.f;
-            if (a.rnd_state_mean && i < in)  // (x - mean) / (std + eps), normalization.py forward
-                v = __fdiv_rn(__fsub_rn(v, a.rnd_state_mean[i]), __fadd_rn(a.rnd_state_std[i], a.rnd_state_eps));
-            x[i] = v;
+            for (int k = 0; k < RS::INP / 4; ++k) {
+                const float4 v = reinterpret_cast<const float4*>(sx)[k];
+                x[4 * k] = v.x;
+                x[4 * k + 1] = v.y;
+                x[4 * k + 2] = v.z;
+                x[4 * k + 3] = v.w;
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < RS::INP; ++i) x[i] = i < in ? sx[i] : 0.f;
+        }
+        if (a.rnd_state_mean) {  // (x - mean) / (std + eps), normalization.py forward
+#pragma unroll
+            for (int i = 0; i < RS::INP; ++i)
+                if (i < in)
+                    x[i] = __fdiv_rn(__fsub_rn(x[i], a.rnd_state_mean[i]), __fadd_rn(a.rnd_state_std[i], a.rnd_state_eps));
         }
         float yt[RS::Q], yp[RS::Q];
         {
@@ -315,7 +327,8 @@ extern "C" int rslrl_rollout_record(const rslrl_rollout_args_t* args, rslrl_stre
             return RSLRL_E_UNSUPPORTED;
         if ((a.rnd_state_mean == nullptr) != (a.rnd_state_std == nullptr)) return RSLRL_E_INVALID_ARGUMENT;
     }
-    const bool c5 = a.rnd_target && a.rnd_in == 48 && a.rnd_hidden == 48 && a.rnd_out == 1;
+    const bool c5 = a.rnd_target && a.rnd_in == 48 && a.rnd_hidden == 48 && a.rnd_out == 1 &&
+                    (reinterpret_cast<uintptr_t>(a.rnd_obs) & 15) == 0 && (a.rnd_obs_stride & 3) == 0;
     if (a.rnd_target)
         lds = 2 * sizeof(float) * static_cast<size_t>(c5 ? rnd_net_floats(48, 48, 1) : rnd_net_floats(64, 64, a.rnd_out));
     int64_t copy_elems = a.N * a.A;
