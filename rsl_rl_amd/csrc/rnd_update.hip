@@ -186,7 +186,11 @@ __global__ __launch_bounds__(kBlock) void rnd_update_kernel(RndParams p) {
                 dz[h] = valid ? __fmul_rn(da, dz[h]) : 0.f;
             }
         }
-        // ---- reduction: wave w's rows through the LDS chunk, every thread adds them into its entries
+        // ---- reduction: wave w's rows through the LDS chunk, every thread adds them into its entries.  The state
+        // row is reloaded (L2) here, before the first barrier, so that its latency is not waited out by the other
+        // waves at the barrier of this wave's turn
+        float x[INP];
+        load_state<INP, EXACT>(p, row, valid, in, x);
         for (int w = 0; w < kBlock / kWave; ++w) {
             if (wid == w) {  // column-major: lane = row -> consecutive addresses per column
 #pragma unroll
@@ -194,8 +198,6 @@ __global__ __launch_bounds__(kBlock) void rnd_update_kernel(RndParams p) {
                     chunk[h * kColStride + lane] = dz[h];
                     chunk[(col_a + h) * kColStride + lane] = a[h];
                 }
-                float x[INP];
-                load_state<INP, EXACT>(p, row, valid, in, x);
 #pragma unroll
                 for (int i = 0; i < INP; ++i)
                     if (i < in) chunk[(col_x + i) * kColStride + lane] = x[i];
