@@ -476,6 +476,35 @@ __device__ __forceinline__ void fold_columns(const double* __restrict__ src, int
     }
 }
 
+// fold_columns for up to 256 partials per column: 16 lanes per column, each adding rows l16, l16 + 16, ..., l16 + 240
+// in that order (all 16 loads in flight first), then a 16-lane butterfly -- one memory round trip.
+template <int kMaxC>
+__device__ __forceinline__ void fold_columns_wide(const double* __restrict__ src, int ld, int n, int ncols,
+                                                  double* __restrict__ out) {
+    constexpr int kPasses = (kMaxC + 15) / 16;
+    const int l16 = threadIdx.x & 15;
+    const int cc = threadIdx.x >> 4;
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<double*>(src), 0, static_cast<int>(sizeof(double) * ncols * ld), 0x00020000);
+#pragma unroll
+    for (int ps = 0; ps < kPasses; ++ps) {
+        const int c = ps * 16 + cc;
+        double v[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int r = l16 + 16 * i;
+            const int off = (c < ncols && r < n) ? (c * ld + r) * 8 : 0x7ffffff0;  // out of range: reads 0
+            v[i] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rsrc, off, 0, 16 /* sc1 */));
+        }
+        double t = v[0];
+#pragma unroll
+        for (int i = 1; i < 16; ++i) t += v[i];
+#pragma unroll
+        for (int off = 8; off >= 1; off >>= 1) t += __shfl_xor(t, off, kWave);
+        if (l16 == 0 && c < ncols) out[c] = t;
+    }
+}
+
 // Waves per SIMD the register budget is sized for (no spills at these bounds, hipcc 7.2): two tiles
 // (current + prefetched) of row pieces live per lane.
 constexpr int quad_waves(int apl, bool shared, bool kl) { return (apl == 1 && (shared || !kl)) ? 4 : 2; }
@@ -505,34 +534,7 @@ __global__ __launch_bounds__(kBlock, DEPTH > 1 ? 1 : quad_waves(APL, SHARED, KL)
     // normal range, which the per-element test below keeps it to.  Same bits as __fdiv_rn, ~30 fewer VALU.
     float c_os[APL], c_t1[APL], c_D[APL], c_rD[APL];
     float ent_shared = 0.0f;
-    if constexpr (SHARED) {
-#pragma unroll
-        for (int k = 0; k < APL; ++k) {
-            const float s = p.sigma[a0 + k];
-            const float inv_s = 1.0f / s;
-            c_s[k] = s;
-            c_ls[k] = logf(s);
-            c_inv_den[k] = 1.0f / __fmul_rn(2.0f, __fmul_rn(s, s));
-            c_inv_s[k] = inv_s;
-            c_inv_s3[k] = inv_s * inv_s * inv_s;
-            if constexpr (KL) {
-                const float os0 = p.B > 0 ? p.old_sigma[a0 + k] : 1.0f;
-                const float D = __fmul_rn(2.0f, __fmul_rn(s, s));
-                const bool d_ok = D >= 0x1p-60f && D <= 0x1p60f;  // else: every element takes the full path
-                c_os[k] = (d_ok && p.kl_fast) ? os0 : __builtin_nanf("");  // NaN never compares equal
-                c_t1[k] = logf(__fadd_rn(__fdiv_rn(s, os0), 1.0e-5f));
-                c_D[k] = D;
-                c_rD[k] = __fdiv_rn(1.0f, D);
-            }
-        }
-#pragma unroll
-        for (int a = 0; a < A; ++a) ent_shared = __fadd_rn(ent_shared, __fadd_rn(kEntC, logf(p.sigma[a])));
-    }
     float adv_mean = 0.0f, adv_den = 1.0f;
-    if (p.normalize_adv) {
-        adv_mean = p.adv_stats[0];
-        adv_den = __fadd_rn(p.adv_stats[1], 1e-8f);  // ppo.py:223  (std + 1e-8)
-    }
 
     float acc_surr = 0.0f, acc_value = 0.0f, acc_ent = 0.0f, acc_kl = 0.0f;
     float acc_sig[APL];
@@ -597,6 +599,35 @@ __global__ __launch_bounds__(kBlock, DEPTH > 1 ? 1 : quad_waves(APL, SHARED, KL)
     TileIn cur, ahead;  // DEPTH 2: `ahead` = the tile after the next one is loaded while this one is computed
     if (tile < ntiles) load_tile(tile, cur);
     if constexpr (DEPTH > 1) load_tile(tile + tstride, ahead);
+    // the per-action constants after the first tile's loads are in flight (their loads and logf chains would
+    // otherwise delay them)
+    if constexpr (SHARED) {
+#pragma unroll
+        for (int k = 0; k < APL; ++k) {
+            const float s = p.sigma[a0 + k];
+            const float inv_s = 1.0f / s;
+            c_s[k] = s;
+            c_ls[k] = logf(s);
+            c_inv_den[k] = 1.0f / __fmul_rn(2.0f, __fmul_rn(s, s));
+            c_inv_s[k] = inv_s;
+            c_inv_s3[k] = inv_s * inv_s * inv_s;
+            if constexpr (KL) {
+                const float os0 = p.B > 0 ? p.old_sigma[a0 + k] : 1.0f;
+                const float D = __fmul_rn(2.0f, __fmul_rn(s, s));
+                const bool d_ok = D >= 0x1p-60f && D <= 0x1p60f;  // else: every element takes the full path
+                c_os[k] = (d_ok && p.kl_fast) ? os0 : __builtin_nanf("");  // NaN never compares equal
+                c_t1[k] = logf(__fadd_rn(__fdiv_rn(s, os0), 1.0e-5f));
+                c_D[k] = D;
+                c_rD[k] = __fdiv_rn(1.0f, D);
+            }
+        }
+#pragma unroll
+        for (int a = 0; a < A; ++a) ent_shared = __fadd_rn(ent_shared, __fadd_rn(kEntC, logf(p.sigma[a])));
+    }
+    if (p.normalize_adv) {
+        adv_mean = p.adv_stats[0];
+        adv_den = __fadd_rn(p.adv_stats[1], 1e-8f);  // ppo.py:223  (std + 1e-8)
+    }
     for (; tile < ntiles; tile += tstride) {
         TileIn nxt;
         load_tile(tile + DEPTH * tstride, nxt);
@@ -802,6 +833,21 @@ __global__ __launch_bounds__(kBlock, DEPTH > 1 ? 1 : quad_waves(APL, SHARED, KL)
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    if (nb <= kBlock) {  // one level: the last of the <= 256 blocks folds every partial in one round trip
+        if (threadIdx.x == 0) {
+            const unsigned t = __hip_atomic_fetch_add(tickets, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int last = (t == static_cast<unsigned>(nb) - 1);
+            if (last) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            last_flag = last;
+        }
+        __syncthreads();
+        if (!last_flag) return;
+        fold_columns_wide<kCols>(partials, nb, nb, kCols, folded);
+        __syncthreads();
+    } else {
     // level 1: the last arriver of this block's group folds the group's partials (fixed order)
     const int g = blockIdx.x / kFoldGroup;
     const int g0 = g * kFoldGroup;
@@ -841,6 +887,7 @@ __global__ __launch_bounds__(kBlock, DEPTH > 1 ? 1 : quad_waves(APL, SHARED, KL)
         if (!last_flag) return;
         fold_columns<kCols>(gpart, ng, ng, kCols, folded);
         __syncthreads();
+    }
     }
     if (threadIdx.x == 0) {
         const double Bd = static_cast<double>(p.B);

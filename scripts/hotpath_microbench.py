@@ -39,7 +39,7 @@ def main():
     args = ap.parse_args()
     only = set(args.only.split(","))
     dev = torch.device("cuda:0")
-    T, N, O, A, M = 24, 65536, 48, 12, 4
+    T, N, O, A, M = 24, int(os.environ.get("MICROBENCH_ENVS", "65536")), 48, 12, 4
     g = torch.Generator(device=dev).manual_seed(0)
     res = {}
 
