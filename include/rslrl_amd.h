@@ -31,7 +31,7 @@ extern "C" {
 
 typedef struct ihipStream_t* rslrl_stream_t; /* == hipStream_t */
 
-#define RSLRL_ABI_VERSION 7
+#define RSLRL_ABI_VERSION 8
 
 enum {
     RSLRL_OK = 0,
@@ -287,11 +287,12 @@ size_t rslrl_fold_partials_workspace_bytes(int64_t S, int64_t NK);
 int rslrl_fold_partials(const float* partials, int64_t S, int64_t NK, float* out, void* workspace,
                         size_t workspace_bytes, rslrl_stream_t stream);
 
-/* Output-layer backward in one launch (Nred <= 16, % 4 == 0; fp32 FMAs on the VALU, W rebuilt exactly from its x6
- * image -- RSLRL_OUT_BWD=mfma selects the x6 MFMA kernel): rslrl_linear_dgrad_elu's outputs plus this
- * layer's weight gradient dW[Nred, K] = dz^T h and bias gradient db[Nred] = column sums of dz, as
- * per-128-row-tile partials [rslrl_linear_tiles(M)][Nred * K + Nred] (dW row-major, then db;
- * rslrl_linear_dgrad_wgrad_partial_bytes), folded by rslrl_fold_partials over Nred * K + Nred columns.
+/* Output-layer backward in one launch (1 <= Nred <= 16, dz rows of Nred floats -- a 1-wide value head's [M, 1]
+ * gradient as it is; fp32 FMAs on the VALU, W rebuilt exactly from its x6 image -- RSLRL_OUT_BWD=mfma selects the
+ * x6 MFMA kernel, Nred % 4 == 0 only): rslrl_linear_dgrad_elu's outputs plus this layer's weight gradient
+ * dW[Nred, K] = dz^T h and bias gradient db[Nred] = column sums of dz, as per-128-row-tile partials
+ * [rslrl_linear_tiles(M)][P], P = Nred * K + Nred rounded up to a multiple of 4 (dW row-major, then db, then
+ * zeros; rslrl_linear_dgrad_wgrad_partial_bytes), folded by rslrl_fold_partials over P columns.
  * The reference runs these as three autograd GEMM/elementwise steps over the same h (mlp.py:106-114). */
 size_t rslrl_linear_dgrad_wgrad_partial_bytes(int64_t M, int32_t Nred, int32_t K);
 int rslrl_linear_dgrad_elu_wgrad(const float* dz, int64_t M, int32_t Nred, int32_t K, const float* h, float* dz_prev,
@@ -350,9 +351,11 @@ typedef struct {
 size_t rslrl_linear_bimage_h3_bytes(int32_t depth);
 size_t rslrl_amax_workspace_bytes(void);
 int rslrl_linear_gemm(const rslrl_linear_args_t* args /* host struct */, rslrl_stream_t stream);
-/* Two RSLRL_LINEAR_FWD[_ELU] problems of the same op, arithmetic, M, K and N in one launch (the rollout's actor
- * and critic layer l: at M = 65536 one problem fills half of the workgroup slots).  Results are identical to
- * two rslrl_linear_gemm calls; distinct amax workspaces when both write an amax. */
+/* Two RSLRL_LINEAR_FWD[_ELU] or RSLRL_LINEAR_DGRAD_ELU problems of the same op, arithmetic, M, K and N in one
+ * launch (the actor's and the critic's layer l: the rollout's forward, where one problem fills half of the
+ * workgroup slots at M = 65536, and the update's hidden-layer input gradients, where a problem's tile count is
+ * not a whole number of slot rounds at M <= 98,304).  Results are identical to two rslrl_linear_gemm calls; distinct
+ * amax workspaces when both write an amax. */
 int rslrl_linear_gemm_pair(const rslrl_linear_args_t* a0, const rslrl_linear_args_t* a1, rslrl_stream_t stream);
 int rslrl_linear_wgrad_ex(const float* dz, const float* dz_amax, const float* x, const float* x_amax, int64_t M,
                           int32_t N, int32_t K, int32_t arith, float* dw, void* workspace, size_t workspace_bytes,
@@ -366,6 +369,23 @@ size_t rslrl_linear_wgrad_bias_workspace_bytes(int64_t M, int32_t N, int32_t K, 
 int rslrl_linear_wgrad_bias(const float* dz, const float* dz_amax, const float* x, const float* x_amax, int64_t M,
                             int32_t N, int32_t K, int32_t arith, int32_t bias_side, float* dw_db, void* workspace,
                             size_t workspace_bytes, rslrl_stream_t stream);
+/* Two rslrl_linear_wgrad_bias problems of one shape (M, N, K, arith, bias_side) in one launch -- the actor's and
+ * the critic's layer l in the update's backward.  Each problem takes half the row slices of a single launch (the
+ * grid stays one workgroup per CU), so its partials and their fold are half as large.  Deterministic; the slice
+ * boundaries differ from rslrl_linear_wgrad_bias's, so the fp32 partial sums (not the fp64 fold) round
+ * differently.  Workspace per problem: rslrl_linear_wgrad_bias_pair_workspace_bytes. */
+typedef struct {
+    const float* dz;
+    const float* dz_amax; /* h3 only */
+    const float* x;
+    const float* x_amax;  /* h3 only */
+    float* dw_db;
+    void* workspace;
+    size_t workspace_bytes;
+} rslrl_wgrad_problem_t;
+size_t rslrl_linear_wgrad_bias_pair_workspace_bytes(int64_t M, int32_t N, int32_t K, int32_t bias_side);
+int rslrl_linear_wgrad_bias_pair(const rslrl_wgrad_problem_t* p0, const rslrl_wgrad_problem_t* p1, int64_t M,
+                                 int32_t N, int32_t K, int32_t arith, int32_t bias_side, rslrl_stream_t stream);
 
 /* ------------------------------------------------------------------------------------------------
  * Rollout-side record: for environment step t, in one launch,

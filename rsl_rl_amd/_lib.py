@@ -19,7 +19,7 @@ import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 # RSLRL_AMD_LIB: an alternative in-tree build of the same library (A/B kernel experiments)
 LIB_PATH = os.environ.get("RSLRL_AMD_LIB") or os.path.join(LIB_DIR, "librslrl_amd.so")
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 # symbols declared in include/rslrl_amd.h (tests/test_capi.py checks the header against this list)
 EXPORTED_SYMBOLS = (
@@ -62,6 +62,8 @@ EXPORTED_SYMBOLS = (
     "rslrl_linear_wgrad_ex",
     "rslrl_linear_wgrad_bias_workspace_bytes",
     "rslrl_linear_wgrad_bias",
+    "rslrl_linear_wgrad_bias_pair_workspace_bytes",
+    "rslrl_linear_wgrad_bias_pair",
     "rslrl_ppo_update_tail",
     "rslrl_adam_workspace_bytes",
     "rslrl_clip_adam_step",
@@ -257,6 +259,19 @@ class RndUpdateArgs(ctypes.Structure):
     ]
 
 
+class WgradProblem(ctypes.Structure):
+    """include/rslrl_amd.h rslrl_wgrad_problem_t"""
+    _fields_ = [
+        ("dz", ctypes.c_void_p),
+        ("dz_amax", ctypes.c_void_p),
+        ("x", ctypes.c_void_p),
+        ("x_amax", ctypes.c_void_p),
+        ("dw_db", ctypes.c_void_p),
+        ("workspace", ctypes.c_void_p),
+        ("workspace_bytes", ctypes.c_size_t),
+    ]
+
+
 RND_MAX_IN, RND_MAX_HIDDEN, RND_MAX_OUT = 64, 64, 8
 
 _lib = None
@@ -349,6 +364,11 @@ def _declare(L):
     L.rslrl_linear_wgrad_bias_workspace_bytes.argtypes = [I64, I32, I32, I32]
     L.rslrl_linear_wgrad_bias.restype = ctypes.c_int
     L.rslrl_linear_wgrad_bias.argtypes = [P, P, P, P, I64, I32, I32, I32, I32, P, P, SZ, P]
+    L.rslrl_linear_wgrad_bias_pair_workspace_bytes.restype = SZ
+    L.rslrl_linear_wgrad_bias_pair_workspace_bytes.argtypes = [I64, I32, I32, I32]
+    L.rslrl_linear_wgrad_bias_pair.restype = ctypes.c_int
+    L.rslrl_linear_wgrad_bias_pair.argtypes = [ctypes.POINTER(WgradProblem), ctypes.POINTER(WgradProblem), I64, I32,
+                                               I32, I32, I32, P]
     L.rslrl_rnd_update_workspace_bytes.restype = SZ
     L.rslrl_rnd_update_workspace_bytes.argtypes = [I64, I32, I32, I32]
     L.rslrl_rnd_update.restype = ctypes.c_int

@@ -325,18 +325,6 @@ class PPO:
             param_group["lr"] = self.learning_rate
         return kl
 
-    def _value_grad_buffer(self, value_batch):
-        """Zero-padded [B, 4] destination of d(loss)/dV for a one-column value head (kept across mini-batches: the
-        loss kernel only ever writes column 0), or None."""
-        if value_batch.dim() != 2 or value_batch.shape[1] != 1:
-            return None
-        B = value_batch.shape[0]
-        buf = getattr(self, "_gv_pad", None)
-        if buf is None or buf.shape[0] != B or buf.device != value_batch.device:
-            buf = torch.zeros(B, 4, dtype=torch.float32, device=value_batch.device)
-            self._gv_pad = buf
-        return buf
-
     def update(self):  # noqa: C901
         if self.symmetry:
             raise NotImplementedError(
@@ -401,15 +389,13 @@ class PPO:
                     if g_sigma is None:  # shared std: d sigma reduced by the loss kernel, into the std's slot
                         g_sigma = (arena.slot(self.policy.std) if self.policy.noise_std_type == "scalar"
                                    else torch.empty_like(sigma))
-                    # the value head's gradient goes straight into column 0 of a zero-padded [B, 4] buffer: the
-                    # critic's fused output-layer backward reads it without a pad copy
-                    gv_pad = self._value_grad_buffer(value_batch)
+                    # the value head's gradient: a contiguous [B, 1] (the critic's fused output-layer backward reads
+                    # its 1-wide rows as they are; a strided column of a padded buffer cost the loss ~2 us)
                     stats, g_mean, g_sigma, g_value = kernels.ppo_loss_fwd_bwd(
                         mean, sigma, value_batch, actions_batch, old_actions_log_prob_batch, advantages_batch,
                         target_values_batch, returns_batch, old_mu_batch, old_sigma_batch, grad_mu=g_mean,
-                        grad_sigma=g_sigma, grad_values=gv_pad[:, :1] if gv_pad is not None else None, **loss_kw)
-                    self.policy.train_backward(tape, g_mean, g_sigma, g_value, sigma, arena.slot, side_stream=side,
-                                               g_value_padded=gv_pad)
+                        grad_sigma=g_sigma, **loss_kw)
+                    self.policy.train_backward(tape, g_mean, g_sigma, g_value, sigma, arena.slot, side_stream=side)
                     del tape
             else:
                 # autograd path for any other policy (ppo.py:246-253, :367-372)

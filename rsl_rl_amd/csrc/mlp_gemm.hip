@@ -1210,10 +1210,10 @@ struct GemmPair {
     const uint4* img[2];
 };
 
-template <int EPI, bool FULL, int PL, int KCH = 0>
+template <int EPI, bool FULL, int PL, int KCH = 0, bool STAGE = false>
 __global__ __launch_bounds__(kThreads, 4) void mlp_gemm_x6_pair_kernel(GemmPair b) {
     const int y = blockIdx.y;
-    mlp_gemm_x6_body<EPI, FULL, 4, PL, false, KCH>(b.p[y], b.img[y]);
+    mlp_gemm_x6_body<EPI, FULL, 4, PL, STAGE, KCH>(b.p[y], b.img[y]);
 }
 
 // ---- the same x6 GEMM on v_mfma_f32_16x16x32_bf16 ("paired" x6).  Under load the chip holds a higher
@@ -1534,6 +1534,11 @@ int out_fwd_occupancy() {  // tuning knob: RSLRL_OUT_FWD_OCC=2|4 (default 4)
 // dZ rows are wave-uniform (scalar loads); four rows of H are in flight per wave.
 constexpr int kOutBwdThreads = 256;
 
+// per-tile partial row of the output-layer backward: dW [Nred][N], db [Nred], zero pad to a multiple of 4 floats
+__host__ __device__ inline int64_t dgrad_wgrad_tile_floats(int nred, int n) {
+    return (static_cast<int64_t>(nred) * n + nred + 3) / 4 * 4;
+}
+
 // CPL columns per lane (4: a wave spans a 256-column row; 2: two waves share a row, so W and the dW
 // accumulators take 2 NR registers each instead of 4 NR -- NR >= 12 needed 178+ registers at CPL 4)
 template <int NR, int CPL>
@@ -1589,12 +1594,22 @@ __global__ __launch_bounds__(kOutBwdThreads, NR >= 16 ? 3 : 4) void out_bwd_valu
     float amx = 0.f;
     // the tile's dZ rows (128 x NR floats) staged once in LDS: a per-row uniform global load is a vector load
     // the waves would wait on (the compiler cannot prove dZ read-only for the scalar cache)
+    // (p.K = Nred, the row stride of dZ: NR = Nred rounded up to 4, the missing rows staged as zeros -- a 1-wide
+    // value head reads its [M, 1] gradient as it is, no zero-padded copy)
     {
         const int64_t t0 = static_cast<int64_t>(blockIdx.x) * kBM;
-        for (int i = threadIdx.x; i < kBM * NR / 4; i += kOutBwdThreads) {
-            const int r = i / (NR / 4), q = i % (NR / 4);
-            dzt4[r][q] = t0 + r < p.M ? *reinterpret_cast<const float4*>(p.a + (t0 + r) * p.K + 4 * q)
-                                      : make_float4(0.f, 0.f, 0.f, 0.f);
+        if (p.K == NR) {
+            for (int i = threadIdx.x; i < kBM * NR / 4; i += kOutBwdThreads) {
+                const int r = i / (NR / 4), q = i % (NR / 4);
+                dzt4[r][q] = t0 + r < p.M ? *reinterpret_cast<const float4*>(p.a + (t0 + r) * p.K + 4 * q)
+                                          : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+        } else {
+            float* dzt = reinterpret_cast<float*>(dzt4);
+            for (int i = threadIdx.x; i < kBM * NR; i += kOutBwdThreads) {
+                const int r = i / NR, o = i % NR;
+                dzt[i] = (t0 + r < p.M && o < p.K) ? p.a[(t0 + r) * p.K + o] : 0.f;
+            }
         }
         __syncthreads();
     }
@@ -1651,7 +1666,7 @@ __global__ __launch_bounds__(kOutBwdThreads, NR >= 16 ? 3 : 4) void out_bwd_valu
         for (int o = 0; o < NR; ++o) dzsum[rg][o] = dzs[o];
     __syncthreads();
     const int nred = p.K;
-    const int64_t tile_floats = static_cast<int64_t>(nred) * p.N + nred;
+    const int64_t tile_floats = dgrad_wgrad_tile_floats(nred, p.N);
     float* wp = p.wpart + static_cast<int64_t>(blockIdx.x) * tile_floats;
     for (int idx = threadIdx.x; idx < (NR + 1) * kBN; idx += kOutBwdThreads) {
         const int o = idx / kBN, c = idx % kBN;
@@ -1668,6 +1683,9 @@ __global__ __launch_bounds__(kOutBwdThreads, NR >= 16 ? 3 : 4) void out_bwd_valu
         for (int g = 1; g < RG; ++g) v += dzsum[g][threadIdx.x];
         wp[static_cast<int64_t>(nred) * p.N + threadIdx.x] = v;
     }
+    // the row's pad to a 16-byte multiple (the fold reads float4 columns): zeros
+    const int pad = static_cast<int>(tile_floats - (static_cast<int64_t>(nred) * p.N + nred));
+    if (threadIdx.x < pad) wp[static_cast<int64_t>(nred) * p.N + nred + threadIdx.x] = 0.f;
     amax_publish<kOutBwdThreads>(p.amax_out, p.amax_ws, amx);
 }
 
@@ -1701,12 +1719,14 @@ int launch(const GemmParams& p, const void* bimage, hipStream_t st) {
                     constexpr int CPL = NR <= 4 ? 4 : 2;
                     hipLaunchKernelGGL((out_bwd_valu_kernel<NR, CPL>), g, dim3(kOutBwdThreads), 0, st, p, img);
                 };
-                switch (p.K) {
+                switch ((p.K + 3) / 4 * 4) {  // Nred 1..16; a partial last group of 4 is staged with zeros
                     case 4: go(std::integral_constant<int, 4>{}); break;
                     case 8: go(std::integral_constant<int, 8>{}); break;
                     case 12: go(std::integral_constant<int, 12>{}); break;
                     default: go(std::integral_constant<int, 16>{}); break;
                 }
+            } else if (p.K & 3) {
+                return RSLRL_E_UNSUPPORTED;  // the MFMA variant reads whole float4 rows of dZ
             } else {
                 auto go = [&](auto nr) {
                     constexpr int NR = decltype(nr)::value;
@@ -1830,13 +1850,13 @@ extern "C" int rslrl_linear_dgrad_elu(const float* dz, int64_t M, int32_t Nred, 
 
 extern "C" size_t rslrl_linear_dgrad_wgrad_partial_bytes(int64_t M, int32_t Nred, int32_t K) {
     if (M < 1 || Nred < 1 || K < 1) return 0;
-    return static_cast<size_t>(ceil_div(M, kBM)) * (static_cast<size_t>(Nred) * K + Nred) * sizeof(float);
+    return static_cast<size_t>(ceil_div(M, kBM)) * static_cast<size_t>(dgrad_wgrad_tile_floats(Nred, K)) * sizeof(float);
 }
 
 extern "C" int rslrl_linear_dgrad_elu_wgrad(const float* dz, int64_t M, int32_t Nred, int32_t K, const float* h,
                                             float* dz_prev, float* colsum_partials, const void* bimage,
                                             float* wgrad_partials, rslrl_stream_t stream) {
-    if (M < 0 || Nred < 1 || Nred > kMaxWgradRows || K < 1 || K > kBN || (Nred & 3)) return RSLRL_E_INVALID_ARGUMENT;
+    if (M < 0 || Nred < 1 || Nred > kMaxWgradRows || K < 1 || K > kBN) return RSLRL_E_INVALID_ARGUMENT;
     if (M == 0) return RSLRL_OK;
     if (!dz || !h || !dz_prev || !colsum_partials || !bimage || !wgrad_partials) return RSLRL_E_INVALID_ARGUMENT;
     if (!aligned16(dz) || !aligned16(bimage)) return RSLRL_E_MISALIGNED;
@@ -1892,7 +1912,9 @@ extern "C" int rslrl_linear_gemm(const rslrl_linear_args_t* a, rslrl_stream_t st
     const int op = a->op;
     const bool h3 = a->arith == RSLRL_ARITH_H3;
     if (!h3 && a->arith != RSLRL_ARITH_X6) return RSLRL_E_INVALID_ARGUMENT;
-    if (a->M < 0 || a->K < 1 || a->N < 1 || a->N > kBN || (a->K & 3) || a->K > INT32_MAX / 2)
+    // K % 4 == 0, except the output-layer backward's reduction width (Nred 1..16, dZ rows read as they are)
+    if (a->M < 0 || a->K < 1 || a->N < 1 || a->N > kBN || ((a->K & 3) && op != RSLRL_LINEAR_DGRAD_ELU_WGRAD) ||
+        a->K > INT32_MAX / 2)
         return RSLRL_E_INVALID_ARGUMENT;
     if (a->M == 0) return RSLRL_OK;
     if (!a->a || !a->bimage || (h3 && !a->a_amax)) return RSLRL_E_INVALID_ARGUMENT;
@@ -1988,9 +2010,39 @@ int launch_pair(const GemmPair& b, bool fullm, hipStream_t st) {
             return launch_status();
         }
     }
+    if constexpr (EPI == kEpiEluGrad) {  // the input gradient stages its first H block like the single launch
+        if (fullm) hipLaunchKernelGGL((mlp_gemm_x6_pair_kernel<EPI, true, PL, 0, true>), g, blk, 0, st, b);
+        else hipLaunchKernelGGL((mlp_gemm_x6_pair_kernel<EPI, false, PL, 0, true>), g, blk, 0, st, b);
+        return launch_status();
+    }
     if (fullm) hipLaunchKernelGGL((mlp_gemm_x6_pair_kernel<EPI, true, PL>), g, blk, 0, st, b);
     else hipLaunchKernelGGL((mlp_gemm_x6_pair_kernel<EPI, false, PL>), g, blk, 0, st, b);
     return launch_status();
+}
+
+// validated GemmParams of an input-gradient op (rslrl_linear_gemm's checks for RSLRL_LINEAR_DGRAD_ELU)
+int dgrad_params(const rslrl_linear_args_t* a, GemmParams& p) {
+    const bool h3 = a->arith == RSLRL_ARITH_H3;
+    if (!h3 && a->arith != RSLRL_ARITH_X6) return RSLRL_E_INVALID_ARGUMENT;
+    if (a->M < 0 || a->K < 1 || a->N < 1 || a->N > kBN || (a->K & 3) || a->K > INT32_MAX / 2)
+        return RSLRL_E_INVALID_ARGUMENT;
+    if (!a->a || !a->bimage || (h3 && !a->a_amax) || !a->h || !a->c) return RSLRL_E_INVALID_ARGUMENT;
+    if (a->amax_out && !a->amax_workspace) return RSLRL_E_INVALID_ARGUMENT;
+    if (!aligned16(a->a) || !aligned16(a->bimage)) return RSLRL_E_MISALIGNED;
+    p = GemmParams{};
+    p.a = a->a;
+    p.M = a->M;
+    p.K = a->K;
+    p.N = a->N;
+    p.a_amax = a->a_amax;
+    p.amax_out = a->amax_out;
+    p.amax_ws = static_cast<unsigned*>(a->amax_workspace);
+    p.deep = h3_deep(RSLRL_LINEAR_DGRAD_ELU);
+    p.h = a->h;
+    p.c = a->c;
+    p.colsum = a->colsum_partials;
+    p.ctiles = ceil_div(a->M, kBM);
+    return RSLRL_OK;
 }
 }  // namespace
 
@@ -2000,7 +2052,8 @@ extern "C" int rslrl_linear_gemm_pair(const rslrl_linear_args_t* a0, const rslrl
                                       rslrl_stream_t stream) {
     if (!a0 || !a1) return RSLRL_E_INVALID_ARGUMENT;
     const int op = a0->op;
-    if (a1->op != op || (op != RSLRL_LINEAR_FWD && op != RSLRL_LINEAR_FWD_ELU)) return RSLRL_E_UNSUPPORTED;
+    if (a1->op != op || (op != RSLRL_LINEAR_FWD && op != RSLRL_LINEAR_FWD_ELU && op != RSLRL_LINEAR_DGRAD_ELU))
+        return RSLRL_E_UNSUPPORTED;
     if (a0->arith != a1->arith || a0->M != a1->M || a0->K != a1->K || a0->N != a1->N) return RSLRL_E_INVALID_ARGUMENT;
     if (a0->amax_out && a1->amax_out && a0->amax_workspace == a1->amax_workspace) return RSLRL_E_INVALID_ARGUMENT;
     const bool h3 = a0->arith == RSLRL_ARITH_H3;
@@ -2010,13 +2063,15 @@ extern "C" int rslrl_linear_gemm_pair(const rslrl_linear_args_t* a0, const rslrl
     }
     GemmPair b{};
     for (int i = 0; i < 2; ++i) {
-        const int rc = fwd_params(i ? a1 : a0, b.p[i]);
+        const int rc = op == RSLRL_LINEAR_DGRAD_ELU ? dgrad_params(i ? a1 : a0, b.p[i]) : fwd_params(i ? a1 : a0, b.p[i]);
         if (rc) return rc;
         b.img[i] = static_cast<const uint4*>((i ? a1 : a0)->bimage);
     }
     if (a0->M == 0) return RSLRL_OK;
     const bool fullm = a0->M % kBM == 0 && a0->K % kKC == 0;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (op == RSLRL_LINEAR_DGRAD_ELU)
+        return h3 ? launch_pair<kEpiEluGrad, 2>(b, fullm, st) : launch_pair<kEpiEluGrad, 3>(b, fullm, st);
     if (op == RSLRL_LINEAR_FWD_ELU)
         return h3 ? launch_pair<kEpiBiasElu, 2>(b, fullm, st) : launch_pair<kEpiBiasElu, 3>(b, fullm, st);
     return h3 ? launch_pair<kEpiBias, 2>(b, fullm, st) : launch_pair<kEpiBias, 3>(b, fullm, st);

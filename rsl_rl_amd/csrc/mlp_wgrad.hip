@@ -128,7 +128,7 @@ __device__ __forceinline__ F read_frag_tr(const char* __restrict__ plane, int cb
 // share their 4 columns), folded over the 8 threads of a column quad through LDS in a fixed order and written
 // after the tile as the slice's extra partial row: part[s] = [dW (N x K) | colsum (N or K)].
 template <int TN, bool FULL, int PL = 3, bool MASKN = false, int CS = 0>
-__global__ __launch_bounds__(kThreadsW, TN <= 64 ? 4 : 2) void wgrad_x6_kernel(WgradParams p) {  // <= 64: 2 per CU
+__device__ __forceinline__ void wgrad_x6_body(const WgradParams& p) {
     static_assert(CS != 1 || TN == kTK, "column sums of the dz side need 256-row tiles");
     using Frag = typename Arith<PL>::frag;
     constexpr int WN = TN == 32 ? 1 : 2;
@@ -309,6 +309,23 @@ __global__ __launch_bounds__(kThreadsW, TN <= 64 ? 4 : 2) void wgrad_x6_kernel(W
                 if (n < p.N && k < p.K) out[n * p.K + k] = PL == 2 ? acc[i][j][r] * unscale : acc[i][j][r];
             }
         }
+}
+
+template <int TN, bool FULL, int PL = 3, bool MASKN = false, int CS = 0>
+__global__ __launch_bounds__(kThreadsW, TN <= 64 ? 4 : 2) void wgrad_x6_kernel(WgradParams p) {  // <= 64: 2 per CU
+    wgrad_x6_body<TN, FULL, PL, MASKN, CS>(p);
+}
+
+// Two weight gradients of one shape in one launch (blockIdx.y selects the problem) -- the actor's and the critic's
+// layer l in the update's backward.  With both in one grid each problem takes half the slices (twice the rows per
+// slice), so its partials (and their fold) are half as large at the same occupancy.
+struct WgradPair {
+    WgradParams p[2];
+};
+
+template <int TN, bool FULL, int PL = 3, bool MASKN = false, int CS = 0>
+__global__ __launch_bounds__(kThreadsW, TN <= 64 ? 4 : 2) void wgrad_x6_pair_kernel(WgradPair b) {
+    wgrad_x6_body<TN, FULL, PL, MASKN, CS>(b.p[blockIdx.y]);
 }
 
 // dW[e] = sum over s of part[s][e] (e < N * K), fp64, fixed order: thread (g, c) of a 256-thread block
@@ -547,4 +564,85 @@ extern "C" int rslrl_linear_wgrad(const float* dz, const float* x, int64_t M, in
                                   void* workspace, size_t workspace_bytes, rslrl_stream_t stream) {
     return rslrl_linear_wgrad_ex(dz, nullptr, x, nullptr, M, N, K, RSLRL_ARITH_X6, dw, workspace, workspace_bytes,
                                  stream);
+}
+
+// ---- two weight gradients of one shape in one launch (the actor's and the critic's layer l)
+namespace rslrl {
+namespace {
+int64_t wgrad_pair_rows_per(int64_t M, int N) {
+    const int64_t S = std::max<int64_t>(1, wgrad_slices(M, N) / 2);
+    return ceil_div(ceil_div(M, S), kMC) * kMC;
+}
+}  // namespace
+}  // namespace rslrl
+
+extern "C" size_t rslrl_linear_wgrad_bias_pair_workspace_bytes(int64_t M, int32_t N, int32_t K, int32_t bias_side) {
+    if (M < 1 || N < 1 || K < 1 || bias_side < 0 || bias_side > 2) return 0;
+    const int64_t S = ceil_div(M, wgrad_pair_rows_per(M, N));
+    const int64_t NKE = static_cast<int64_t>(N) * K + colsum_len(bias_side, N, K);
+    return static_cast<size_t>(S) * NKE * sizeof(float) + rslrl_fold_partials_workspace_bytes(S, NKE);
+}
+
+extern "C" int rslrl_linear_wgrad_bias_pair(const rslrl_wgrad_problem_t* a0, const rslrl_wgrad_problem_t* a1,
+                                            int64_t M, int32_t N, int32_t K, int32_t arith, int32_t bias_side,
+                                            rslrl_stream_t stream) {
+    if (!a0 || !a1) return RSLRL_E_INVALID_ARGUMENT;
+    if (M < 1 || N < 1 || K < 1 || N > 256 || K > kTK || (N & 3) || (K & 3)) return RSLRL_E_INVALID_ARGUMENT;
+    if (bias_side < 0 || bias_side > 2 || (bias_side == 1 && N <= 64)) return RSLRL_E_INVALID_ARGUMENT;
+    const bool h3 = arith == RSLRL_ARITH_H3;
+    if (!h3 && arith != RSLRL_ARITH_X6) return RSLRL_E_INVALID_ARGUMENT;
+    const rslrl_wgrad_problem_t* a[2] = {a0, a1};
+    const size_t need = rslrl_linear_wgrad_bias_pair_workspace_bytes(M, N, K, bias_side);
+    for (int i = 0; i < 2; ++i) {
+        if (!a[i]->dz || !a[i]->x || !a[i]->dw_db || !a[i]->workspace) return RSLRL_E_INVALID_ARGUMENT;
+        if (h3 && (!a[i]->dz_amax || !a[i]->x_amax)) return RSLRL_E_INVALID_ARGUMENT;
+        if ((reinterpret_cast<uintptr_t>(a[i]->dz) | reinterpret_cast<uintptr_t>(a[i]->x)) & 15) return RSLRL_E_MISALIGNED;
+        if (a[i]->workspace_bytes < need) return RSLRL_E_WORKSPACE_TOO_SMALL;
+    }
+    const int64_t rows_per = wgrad_pair_rows_per(M, N);
+    const int64_t S = ceil_div(M, rows_per);
+    const int64_t NKE = static_cast<int64_t>(N) * K + colsum_len(bias_side, N, K);
+    const size_t part_bytes = static_cast<size_t>(S) * NKE * sizeof(float);
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    WgradPair b{};
+    for (int i = 0; i < 2; ++i)
+        b.p[i] = WgradParams{a[i]->dz, a[i]->x, static_cast<float*>(a[i]->workspace), M, rows_per, N, K, a[i]->dz_amax,
+                             a[i]->x_amax};
+    const bool full = (M % rows_per == 0) && K == kTK && (rows_per / kMC) % kWgradDepth == 0;
+    const dim3 g(static_cast<unsigned>(S), 2), blk(kThreadsW);
+    auto go = [&](auto tn, auto pl, auto cs) {
+        constexpr int TN = decltype(tn)::value, PL = decltype(pl)::value, CS = decltype(cs)::value;
+        if constexpr (CS == 1 && TN != kTK) {
+            return;
+        } else {
+            if (full && N == TN) hipLaunchKernelGGL((wgrad_x6_pair_kernel<TN, true, PL, false, CS>), g, blk, 0, st, b);
+            else if (full && N < TN) hipLaunchKernelGGL((wgrad_x6_pair_kernel<TN, true, PL, true, CS>), g, blk, 0, st, b);
+            else hipLaunchKernelGGL((wgrad_x6_pair_kernel<TN, false, PL, false, CS>), g, blk, 0, st, b);
+        }
+    };
+    auto by_side = [&](auto tn, auto pl) {
+        using C0 = std::integral_constant<int, 0>;
+        using C1 = std::integral_constant<int, 1>;
+        using C2 = std::integral_constant<int, 2>;
+        if (bias_side == 1) go(tn, pl, C1{});
+        else if (bias_side == 2) go(tn, pl, C2{});
+        else go(tn, pl, C0{});
+    };
+    using I32 = std::integral_constant<int, 32>;
+    using I64 = std::integral_constant<int, 64>;
+    using I256 = std::integral_constant<int, 256>;
+    using P2 = std::integral_constant<int, 2>;
+    using P3 = std::integral_constant<int, 3>;
+    if (N <= 32) h3 ? by_side(I32{}, P2{}) : by_side(I32{}, P3{});
+    else if (N <= 64) h3 ? by_side(I64{}, P2{}) : by_side(I64{}, P3{});
+    else h3 ? by_side(I256{}, P2{}) : by_side(I256{}, P3{});
+    int rc = launch_status();
+    if (rc) return rc;
+    for (int i = 0; i < 2; ++i) {
+        rc = rslrl_fold_partials(static_cast<const float*>(a[i]->workspace), S, NKE, a[i]->dw_db,
+                                 static_cast<char*>(a[i]->workspace) + part_bytes, a[i]->workspace_bytes - part_bytes,
+                                 stream);
+        if (rc) return rc;
+    }
+    return RSLRL_OK;
 }

@@ -155,13 +155,19 @@ class ActorCritic(nn.Module):
         c_obs = self.critic_obs_normalizer(self.get_critic_obs(obs))
         a_obs = a_obs if a_obs.is_contiguous() else a_obs.contiguous()
         c_obs = c_obs if c_obs.is_contiguous() else c_obs.contiguous()
-        if side_stream is not None:
+        pair = None
+        if side_stream is None:  # the actor's and the critic's same-shape layers batched into one launch each
+            pair = fused_mlp.train_forward_pair(a_obs, *self._linears(self.actor), c_obs, *self._linears(self.critic))
+        if pair is not None:
+            y, tape_a, value, tape_c = pair
+        elif side_stream is not None:
             main = torch.cuda.current_stream(c_obs.device)
             side_stream.wait_stream(main)
             c_obs.record_stream(side_stream)  # kept by the critic's tape for its backward on the side stream
             with torch.cuda.stream(side_stream):
                 value, tape_c = fused_mlp.train_forward(c_obs, *self._linears(self.critic))
-        y, tape_a = fused_mlp.train_forward(a_obs, *self._linears(self.actor))
+        if pair is None:
+            y, tape_a = fused_mlp.train_forward(a_obs, *self._linears(self.actor))
         A = self.num_actions
         if self.state_dependent_std:
             mean, raw = y[:, :A], y[:, A:]  # = unbind(Unflatten([2, A])(y), dim=-2)
@@ -169,13 +175,13 @@ class ActorCritic(nn.Module):
         else:
             mean = y
             std = self.std if self.noise_std_type == "scalar" else torch.exp(self.log_std)
-        if side_stream is None:
+        if pair is None and side_stream is None:
             value, tape_c = fused_mlp.train_forward(c_obs, *self._linears(self.critic))
-        else:
+        elif side_stream is not None:
             main.wait_stream(side_stream)
             value.record_stream(main)  # allocated on the side stream, read by the loss on this one
         self.distribution = Normal(mean, std.expand_as(mean))  # for logging, as act() leaves it
-        return mean, std, value, (tape_a, tape_c, y.shape)
+        return mean, std, value, (tape_a, tape_c, y.shape, pair is not None)
 
     def train_grad_buffers(self, mean, std):
         """(d mean, d sigma) destinations for the fused loss: for a state-dependent head both are the halves of
@@ -193,7 +199,7 @@ class ActorCritic(nn.Module):
         gradient buffer (train_grad_buffers) the loss kernel wrote.  side_stream: as in train_forward (the
         critic's backward runs there; the current stream waits for it before returning).  g_value_padded: a zero-padded
         [B, 4] buffer whose column 0 is g_value (the loss kernel wrote it there), or None."""
-        tape_a, tape_c, y_shape = tape
+        tape_a, tape_c, y_shape, paired = tape
         if self.state_dependent_std:
             dy = torch.as_strided(g_mean, y_shape, (y_shape[1], 1))  # the [B, 2A] buffer behind both halves
             if self.noise_std_type == "log":  # d raw = d sigma * exp(raw) (ExpBackward: grad * result)
@@ -209,6 +215,10 @@ class ActorCritic(nn.Module):
             fused_mlp.train_backward(tp, d, outs=[(slot(w), slot(b)) for w, b in zip(ws, bs)], dy_padded=d_pad)
 
         if side_stream is None:
+            if paired and g_value_padded is None:
+                outs = [[(slot(w), slot(b)) for w, b in zip(*self._linears(m))] for m in (self.actor, self.critic)]
+                if fused_mlp.train_backward_pair(tape_a, dy, outs[0], tape_c, g_value.reshape(-1, 1), outs[1]):
+                    return
             run(self.actor, tape_a, dy)
             run(self.critic, tape_c, g_value.reshape(-1, 1), g_value_padded)
             return

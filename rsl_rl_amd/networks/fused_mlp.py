@@ -324,18 +324,37 @@ def linear_dgrad_elu_ex(dz, h, img, arith, dz_amax=None, want_amax=False, db_out
     return out, db, amax
 
 
+def linear_dgrad_elu_pair(dzs, hs, imgs, arith, dz_amaxes=(None, None), want_amax=(False, False)):
+    """linear_dgrad_elu_ex (want_db=False) of two problems of one shape in one launch (rslrl_linear_gemm_pair) --
+    e.g. the actor's and the critic's hidden layer l in the update's backward; bit-identical to two launches.
+    Returns ([out0, out1], [amax0, amax1])."""
+    M, N = dzs[0].shape
+    K = hs[0].shape[1]
+    outs = [torch.empty(M, K, device=dz.device, dtype=torch.float32) for dz in dzs]
+    amaxes = [torch.empty(1, device=dz.device, dtype=torch.float32) if w else None for dz, w in zip(dzs, want_amax)]
+    args = [_gemm_args(_lib.LINEAR_DGRAD_ELU, arith, dzs[i], dz_amaxes[i], K, imgs[i], h=hs[i], c=outs[i],
+                       amax_out=amaxes[i], slot=i) for i in range(2)]
+    with timer.span(f"linear_dgrad_pair[M={M},Nred={N},K={K}]{_tag(arith)}", dzs[0].device, 8 * M * (N + 2 * K),
+                    4 * M * K * N):
+        rc = _lib.lib().rslrl_linear_gemm_pair(ctypes.byref(args[0]), ctypes.byref(args[1]), _stream(dzs[0]))
+    _lib.check(rc, "rslrl_linear_gemm_pair")
+    return outs, amaxes
+
+
 def linear_dgrad_elu_wgrad(dz, w, h, img, want_amax=False, db_prev_out=None, dwb_out=None, want_db_prev=True):
-    """Output-layer backward in one launch (x6; dz [M, Nred <= 16, % 4]): ((dz @ w) * ELU'(h), its column sums,
-    dz^T h).  w is the layer weight [Nred, K] (only its image is read).  db_prev_out: optional [K] destination of
-    the column sums; dwb_out: optional [Nred*K + Nred] destination of dW (row-major) followed by db -- the layout
-    of a Linear's weight and bias adjacent in a gradient arena."""
+    """Output-layer backward in one launch (x6; dz [M, Nred <= 16] contiguous -- any Nred, e.g. the value head's
+    [M, 1] gradient unpadded): ((dz @ w) * ELU'(h), its column sums, dz^T h).  w is the layer weight [Nred, K] (only
+    its image is read).  db_prev_out: optional [K] destination of the column sums; dwb_out: optional [Nred*K + Nred]
+    destination of dW (row-major) followed by db -- the layout of a Linear's weight and bias adjacent in a gradient
+    arena (used when Nred*K + Nred is a multiple of 4, the kernel's padded partial row)."""
     M, N = dz.shape
     K = h.shape[1]
     L = _lib.lib()
     tiles = L.rslrl_linear_tiles(M)
+    P = (N * K + N + 3) // 4 * 4  # per tile: dW [N, K], then db [N], then zeros
     out = torch.empty(M, K, device=dz.device, dtype=torch.float32)
     part = torch.empty(K, tiles, device=dz.device, dtype=torch.float32) if want_db_prev else None
-    wpart = torch.empty(tiles, N * K + N, device=dz.device, dtype=torch.float32)  # per tile: dW [N, K], then db [N]
+    wpart = torch.empty(tiles, P, device=dz.device, dtype=torch.float32)
     amax = torch.empty(1, device=dz.device, dtype=torch.float32) if want_amax else None
     with timer.span(f"linear_dgrad_wgrad[M={M},Nred={N},K={K}]", dz.device, 4 * M * (N + 2 * K), 4 * M * K * N):
         _gemm(_lib.LINEAR_DGRAD_ELU_WGRAD, _lib.ARITH_X6, dz, None, K, img, h=h, c=out, colsum=part, wpart=wpart,
@@ -345,13 +364,15 @@ def linear_dgrad_elu_wgrad(dz, w, h, img, want_amax=False, db_prev_out=None, dwb
         db = _out_or_empty(db_prev_out, (K,), dz.device)
         rc = L.rslrl_column_sum_fold(part.data_ptr(), tiles, K, db.data_ptr(), _stream(dz))
         _lib.check(rc, "rslrl_column_sum_fold")
-    dwb = _out_or_empty(dwb_out, (N * K + N,), dz.device)
-    nbytes = L.rslrl_fold_partials_workspace_bytes(tiles, N * K + N)
+    dwb = _out_or_empty(dwb_out if P == N * K + N else None, (P,), dz.device)
+    nbytes = L.rslrl_fold_partials_workspace_bytes(tiles, P)
     ws = torch.empty(max(nbytes, 16) // 8, dtype=torch.float64, device=dz.device)
-    rc = L.rslrl_fold_partials(wpart.data_ptr(), tiles, N * K + N, dwb.data_ptr(), ws.data_ptr(), nbytes,
-                               _stream(dz))
+    rc = L.rslrl_fold_partials(wpart.data_ptr(), tiles, P, dwb.data_ptr(), ws.data_ptr(), nbytes, _stream(dz))
     _lib.check(rc, "rslrl_fold_partials")
-    dw, db_out = dwb[: N * K].view(N, K), dwb[N * K:]
+    dw, db_out = dwb[: N * K].view(N, K), dwb[N * K: N * K + N]
+    if dwb_out is not None and dwb.data_ptr() != dwb_out.data_ptr():
+        dwb_out.copy_(dwb[: N * K + N])
+        dw, db_out = dwb_out[: N * K].view(N, K), dwb_out[N * K:]
     if want_amax:
         return out, db, dw, db_out, amax
     return out, db, dw, db_out
@@ -382,6 +403,37 @@ def linear_wgrad(dz, x, arith=_lib.ARITH_X6, dz_amax=None, x_amax=None, out=None
     if not bias_side:
         return dwb
     return dwb[: N * K].view(N, K), dwb[N * K:]
+
+
+def linear_wgrad_pair(dzs, xs, arith=_lib.ARITH_X6, bias_side=0, dwb_outs=(None, None), amaxes=((None, None),) * 2):
+    """linear_wgrad of two problems of one shape in one launch (rslrl_linear_wgrad_bias_pair): returns, per problem,
+    dw (bias_side 0) or (dw, colsum).  dwb_outs: optional [N*K + E] destinations (a Linear's adjacent arena slots);
+    amaxes: per problem (max |dz|, max |x|) device scalars for h3."""
+    M, N = dzs[0].shape
+    K = xs[0].shape[1]
+    L = _lib.lib()
+    nbytes = L.rslrl_linear_wgrad_bias_pair_workspace_bytes(M, N, K, bias_side)
+    E = N if bias_side == 1 else (K if bias_side == 2 else 0)
+    wss, dwbs, probs = [], [], []
+    for i in range(2):
+        ws = torch.empty(nbytes // 4, dtype=torch.float32, device=dzs[i].device)
+        dwb = _out_or_empty(dwb_outs[i], (N * K + E,), dzs[i].device)
+        da, xa = amaxes[i]
+        if arith == _lib.ARITH_H3:
+            da = _amax(dzs[i]) if da is None else da
+            xa = _amax(xs[i]) if xa is None else xa
+        wss.append(ws)
+        dwbs.append(dwb)
+        probs.append(_lib.WgradProblem(dzs[i].data_ptr(), _ptr(da), xs[i].data_ptr(), _ptr(xa), dwb.data_ptr(),
+                                       ws.data_ptr(), nbytes))
+    with timer.span(f"linear_wgrad_pair[M={M},N={N},K={K}]{_tag(arith)}", dzs[0].device, 8 * M * (N + K),
+                    4 * M * K * N):
+        rc = L.rslrl_linear_wgrad_bias_pair(ctypes.byref(probs[0]), ctypes.byref(probs[1]), M, N, K, arith,
+                                            bias_side, _stream(dzs[0]))
+    _lib.check(rc, "rslrl_linear_wgrad_bias_pair")
+    if not bias_side:
+        return [d.view(N, K) for d in dwbs]
+    return [(d[: N * K].view(N, K), d[N * K:]) for d in dwbs]
 
 
 def _weight_grad(dz, x, x6: bool, h3=False, dz_amax=None, x_amax=None, out=None, want_bias=False, db_out=None):
@@ -557,11 +609,8 @@ def train_backward(tape, dy, need_dx=False, need_w=None, outs=None, dy_padded=No
         if fuse_w:  # output layer: dgrad + ELU' + bias grad + weight grad over one read of h (one launch)
             nred = dz.shape[1]
             K = h_in.shape[1]
-            pad = (-nred) % 4
-            if dy_padded is not None:
-                dzp = dy_padded
-            else:
-                dzp = F.pad(dz, (0, pad)) if pad else dz
+            pad = (nred * K + nred) % 4  # the kernel's partial rows are padded to 4 floats: fold into a temporary
+            dzp = dy_padded if dy_padded is not None else dz  # the kernel reads any Nred <= 16 (no pad copy)
             want = l - 1 > 0 and h3[l - 1]
             # the kernel's [dW | db] result lands directly in the arena when weight and bias are adjacent there
             dwb_out = None
@@ -626,6 +675,109 @@ def train_backward(tape, dy, need_dx=False, need_w=None, outs=None, dy_padded=No
     return dx, grads_w, grads_b
 
 
+# ---- the actor and the critic of the PPO update as one pass (same-shape hidden layers batched per launch)
+def _pairable(ws_a, ws_c, x_a, x_c) -> bool:
+    """Two MLPs whose hidden layers can share launches: the split (x6) arithmetic without h3 layers, the same depth
+    and hidden shapes, the same batch, both output layers fused (<= 16 wide, hidden width <= 256)."""
+    if _PAIR_TRAIN is False or _mode != GEMM_X6 or not _split():
+        return False
+    if len(ws_a) != len(ws_c) or len(ws_a) < 3 or x_a.shape[0] != x_c.shape[0]:
+        return False
+    if any(a.shape != c.shape for a, c in zip(ws_a[:-1], ws_c[:-1])):
+        return False
+    if not (_fuse_out_fwd(ws_a) and _fuse_out_fwd(ws_c)):
+        return False
+    return all(w.shape[0] <= 16 and w.shape[1] <= MAX_WIDTH for w in (ws_a[-1], ws_c[-1]))
+
+
+def train_forward_pair(x_a, ws_a, bs_a, x_c, ws_c, bs_c):
+    """train_forward of the actor (x_a, ws_a, bs_a) and the critic (x_c, ...) with each same-shape hidden layer of the
+    two in one launch (rslrl_linear_gemm_pair) and every B image of both passes in one launch; the output layers run
+    as two fused launches.  Values identical to two train_forward calls.  Returns (y_a, tape_a, y_c, tape_c), or None
+    when the pair does not qualify (_pairable)."""
+    if not _pairable(ws_a, ws_c, x_a, x_c):
+        return None
+    ws, bs, xs = (ws_a, ws_c), (bs_a, bs_c), (x_a, x_c)
+    nh = len(ws_a) - 1
+    h3 = [False] * len(ws_a)
+    specs = []
+    for i in range(2):  # per pass: forward images of layers 0..nh-1, transposed images of 1..nh, the output image
+        specs += [(w, False) for w in ws[i][:-1]] + [(w, True) for w in ws[i][1:]]
+        specs.append((ws[i][-1], False, _lib.BIMAGE_LAYOUT_OUT))
+    imgs = bimages(specs)
+    per = 2 * nh + 1
+    fwd = [imgs[i * per: i * per + nh] for i in range(2)]
+    dgr = [[None] + imgs[i * per + nh: i * per + 2 * nh] for i in range(2)]
+    out_img = [imgs[i * per + 2 * nh] for i in range(2)]
+    h = [x if x.is_contiguous() else x.contiguous() for x in xs]
+    hs = [[h[0]], [h[1]]]
+    y = [None, None]
+    for l in range(nh):
+        if l < nh - 1:
+            h, _ = linear_fwd_pair(h, [bs[0][l], bs[1][l]], ws[0][l].shape[0], True, [fwd[0][l], fwd[1][l]],
+                                   _lib.ARITH_X6, [None, None], [False, False])
+        else:
+            for i in range(2):
+                h[i], y[i] = linear_fwd_out_ex(h[i], bs[i][l], ws[i][l].shape[0], fwd[i][l], _lib.ARITH_X6, None,
+                                               bs[i][-1], out_img[i], store_h=True)
+        for i in range(2):
+            hs[i].append(h[i])
+    tapes = [MLPTape(hs[i], list(ws[i]), dgr[i], [None] * (nh + 1), h3, True) for i in range(2)]
+    return y[0], tapes[0], y[1], tapes[1]
+
+
+def train_backward_pair(tape_a, dy_a, outs_a, tape_c, dy_c, outs_c):
+    """train_backward of two passes of train_forward_pair, gradients into outs_* (per layer (dW, db) destinations,
+    as train_backward's outs): the output layers as two fused launches, then per hidden layer the two weight
+    gradients (rslrl_linear_wgrad_bias_pair) and the two input gradients (rslrl_linear_gemm_pair) in one launch each.
+    Input gradients are bit-identical to two train_backward calls; a weight gradient's fp32 slice partials cover
+    twice the rows (half the slices), so its rounding differs within fp32 accumulation error.  Returns False (nothing
+    done) when the tapes do not qualify."""
+    tapes, dys, outs = (tape_a, tape_c), (dy_a, dy_c), (outs_a, outs_c)
+    L = len(tape_a.ws)
+    if not (tape_a.x6 and tape_c.x6 and not any(tape_a.h3) and not any(tape_c.h3) and len(tape_c.ws) == L
+            and _FUSE_OUT and all(o is not None and all(t is not None for t in o) for ob in outs for o in ob)):
+        return False
+    if not all(_bias_from_wgrad(t.ws[l].shape[0], t.hs[l].shape[1], True) for t in tapes for l in range(L - 1)):
+        return False
+    dz = [None, None]
+    for i in range(2):  # output layer: dgrad + ELU' + its weight and bias gradients over one read of h
+        t, o = tapes[i], outs[i]
+        d = dys[i] if dys[i].is_contiguous() else dys[i].contiguous()
+        nred, K = d.shape[1], t.hs[L - 1].shape[1]
+        wo, bo = o[L - 1]
+        adjacent = ((nred * K + nred) % 4 == 0 and wo.is_contiguous()
+                    and bo.data_ptr() == wo.data_ptr() + 4 * wo.numel())
+        dwb_out = torch.as_strided(wo, (nred * K + nred,), (1,)) if adjacent else None
+        dz[i], _, dw, db = linear_dgrad_elu_wgrad(d, t.ws[L - 1], t.hs[L - 1], t.dgrad_imgs[L - 1], dwb_out=dwb_out,
+                                                  want_db_prev=False)
+        if not adjacent:
+            torch._foreach_copy_([wo, bo], [dw, db])
+    for l in range(L - 2, -1, -1):
+        h_in = [t.hs[l] for t in tapes]
+        N, K = tapes[0].ws[l].shape
+        if l > 0:  # square hidden layer: dW = dz^T h, db = column sums of dz, written into the arena slots
+            dwb_outs = []
+            for i in range(2):
+                wo, bo = outs[i][l]
+                adj = wo.is_contiguous() and bo.data_ptr() == wo.data_ptr() + 4 * wo.numel()
+                dwb_outs.append(torch.as_strided(wo, (N * K + N,), (1,)) if adj else None)
+            res = linear_wgrad_pair(dz, h_in, bias_side=1, dwb_outs=dwb_outs)
+            for i in range(2):
+                if dwb_outs[i] is None:
+                    torch._foreach_copy_(list(outs[i][l]), list(res[i]))
+            dz, _ = linear_dgrad_elu_pair(dz, h_in, [t.dgrad_imgs[l] for t in tapes], _lib.ARITH_X6)
+        else:  # first layer: (x^T dz)^T on the 64-row tiles, the bias from dz (the kernel's K side)
+            pad = (-K) % 4
+            xp = [F.pad(x, (0, pad)) if pad else x for x in h_in]
+            res = linear_wgrad_pair(xp, dz, bias_side=2)
+            for i in range(2):
+                wo, bo = outs[i][0]
+                dwt, db = res[i]
+                torch._foreach_copy_([wo, bo], [dwt[:K].t(), db])
+    return True
+
+
 class FusedMLPFunction(torch.autograd.Function):
     """y = MLP(x) for hidden ELU(alpha=1) layers; args: (x, W1, b1, ..., WL, bL)."""
 
@@ -682,6 +834,8 @@ def _unflatten(mlp, y):
 
 
 _side_streams: dict = {}
+# RSLRL_PAIR_TRAIN=0 keeps the update's actor and critic passes in separate launches (A/B)
+_PAIR_TRAIN = os.environ.get("RSLRL_PAIR_TRAIN", "1") != "0"
 
 
 def side_stream(device):

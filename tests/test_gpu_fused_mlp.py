@@ -196,7 +196,8 @@ def test_linear_wgrad(M, N, K, cuda_device):
     _close(ours, ref.float(), 1e-5)
 
 
-@pytest.mark.parametrize("M,N,K", [(393216, 12, 256), (5000, 4, 256), (3001, 16, 64), (128, 8, 48)])
+@pytest.mark.parametrize("M,N,K", [(393216, 12, 256), (5000, 4, 256), (3001, 16, 64), (128, 8, 48), (393216, 1, 256),
+                                   (3001, 3, 256), (1000, 5, 48)])
 def test_linear_dgrad_elu_wgrad(M, N, K, cuda_device):
     """Fused output-layer backward (one x6 launch): dz_prev and the bias grad as linear_dgrad_elu, and the
     layer's weight gradient dz^T h, vs fp64 (fp32-class: 2e-5 of the max, the sum runs over M rows)."""
@@ -213,6 +214,13 @@ def test_linear_dgrad_elu_wgrad(M, N, K, cuda_device):
     _close(db_out, dz.double().sum(0).float(), 1e-5)  # this layer's own bias gradient (column sums of dz)
     out2, db2, dw2, db_out2 = fused_mlp.linear_dgrad_elu_wgrad(dz, w, h, bimage(w, True))
     assert torch.equal(dw, dw2) and torch.equal(db, db2) and torch.equal(db_out, db_out2)  # deterministic
+    if N % 4:  # rows of Nred floats read as they are == the zero-padded operand (the round-2 layout), bitwise
+        pad = (-N) % 4
+        wp = torch.nn.functional.pad(w, (0, 0, 0, pad))
+        out3, db3, dw3, db_out3 = fused_mlp.linear_dgrad_elu_wgrad(torch.nn.functional.pad(dz, (0, pad)), wp, h,
+                                                                  bimage(wp, True))
+        assert torch.equal(out, out3) and torch.equal(db, db3)
+        assert torch.equal(dw, dw3[:N]) and torch.equal(db_out, db_out3[:N])
 
 
 @pytest.mark.parametrize("S,NK", [(1, 4), (7, 100), (256, 65536), (3072, 3072), (3072, 1024), (129, 20)])

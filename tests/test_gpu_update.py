@@ -192,9 +192,13 @@ def test_update_c2_width_matches_reference(golden_meta, cuda_device):
 def test_update_two_streams_bit_identical(golden_meta, cuda_device, monkeypatch):
     """The opt-in side stream for the critic's MLP launches (RSLRL_TWO_STREAMS=1, update and rollout forward)
     changes only where the launches run, not what they compute: the C2-shape update ends with bit-identical
-    parameters, learning-rate trace and loss statistics either way."""
+    parameters, learning-rate trace and loss statistics either way.  (The one-stream update otherwise pairs the
+    actor's and the critic's layers per launch, whose weight-gradient slices round differently: compared unpaired,
+    the pairing has its own test, test_gpu_pair_train.py.)"""
     from update_fixtures import build_update, run_recorded_update
+    from rsl_rl_amd.networks import fused_mlp
 
+    monkeypatch.setattr(fused_mlp, "_PAIR_TRAIN", False)
     m = golden_meta["update_c2"]
     z = np.load(golden_path("update_c2.npz"))
     res = {}
