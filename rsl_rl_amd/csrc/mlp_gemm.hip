@@ -774,20 +774,27 @@ __device__ __forceinline__ void h3_deep_loop(const GemmParams& p, int64_t row0, 
 // PL: operand planes (3: x6 bf16 on a layout-0 image; 2: h3 fp16 on a layout-2 image, A scaled from *p.a_amax).
 // KCH = 3: a kernel for K = 48 only (the first layer), whose look-ahead loop is its only main loop (one body with
 // both loop instances ran the K = 256 forward ~2 % slower)
+// bytes of each of the two LDS buffers of the x6 GEMM body
+template <int EPI, int PL>
+constexpr int x6_buf_bytes() {
+    // the fused output layer's epilogue needs 40 KiB per buffer (h stage in one, reduction tiles in the other)
+    return EPI == kEpiBiasEluOut ? 40960 : (PL * kBM * kX6RowB + PL * kX6PlaneB);
+}
+
+// lds_b0 / lds_b1: the kernel's two LDS buffers (x6_buf_bytes<EPI, PL>() each).  Two LDS objects, not one [2][bytes]
+// array: the waitcnt pass can then tell a DMA into one buffer from reads of the other (distinct alias scopes) where
+// the buffer index is a compile-time constant.  Declared by the kernel so that two bodies in one kernel (the
+// output-layer pair) share them.
 template <int EPI, bool FULL, int NR, int PL, bool STAGE = true, int KCH = 0>
-__device__ __forceinline__ void mlp_gemm_x6_body(GemmParams p, const uint4* __restrict__ bimg) {
+__device__ __forceinline__ void mlp_gemm_x6_body(GemmParams p, const uint4* __restrict__ bimg, char* lds_b0,
+                                                 char* lds_b1) {
     static_assert(PL == 3 || EPI != kEpiEluGradWgrad, "the fused output-layer backward is x6 only");
     using Frag = typename Arith<PL>::frag;
     constexpr int BM = kBM;
     constexpr int I = BM / 64;
     constexpr int planeA = BM * kX6RowB;
-    // the fused output layer's epilogue needs 40 KiB per buffer (h stage in one, reduction tiles in the other)
-    constexpr int bufBytes = EPI == kEpiBiasEluOut ? 40960 : (PL * planeA + PL * kX6PlaneB);
+    constexpr int bufBytes = x6_buf_bytes<EPI, PL>();
     static_assert(bufBytes >= PL * planeA + PL * kX6PlaneB, "LDS buffer");
-    // two LDS objects, not one [2][bytes] array: the waitcnt pass can then tell a DMA into one buffer from
-    // reads of the other (distinct alias scopes) where the buffer index is a compile-time constant
-    __shared__ __attribute__((aligned(16))) char lds_b0[bufBytes];
-    __shared__ __attribute__((aligned(16))) char lds_b1[bufBytes];
     char* lds[2];
     lds[0] = lds_b0;
     lds[1] = lds_b1;
@@ -1193,7 +1200,9 @@ __device__ __forceinline__ void mlp_gemm_x6_body(GemmParams p, const uint4* __re
 
 template <int EPI, bool FULL, int MINW, int NR = 4, int PL = 3, int KCH = 0>
 __global__ __launch_bounds__(kThreads, MINW) void mlp_gemm_x6_kernel(GemmParams p, const uint4* __restrict__ bimg) {
-    mlp_gemm_x6_body<EPI, FULL, NR, PL, true, KCH>(p, bimg);
+    __shared__ __attribute__((aligned(16))) char lds_b0[x6_buf_bytes<EPI, PL>()];
+    __shared__ __attribute__((aligned(16))) char lds_b1[x6_buf_bytes<EPI, PL>()];
+    mlp_gemm_x6_body<EPI, FULL, NR, PL, true, KCH>(p, bimg, lds_b0, lds_b1);
 }
 
 // the K = 48 kernel applies to full tiles of a forward on x6 operands with the deep loop enabled
@@ -1212,8 +1221,29 @@ struct GemmPair {
 
 template <int EPI, bool FULL, int PL, int KCH = 0, bool STAGE = false>
 __global__ __launch_bounds__(kThreads, 4) void mlp_gemm_x6_pair_kernel(GemmPair b) {
+    __shared__ __attribute__((aligned(16))) char lds_b0[x6_buf_bytes<EPI, PL>()];
+    __shared__ __attribute__((aligned(16))) char lds_b1[x6_buf_bytes<EPI, PL>()];
     const int y = blockIdx.y;
-    mlp_gemm_x6_body<EPI, FULL, 4, PL, STAGE, KCH>(b.p[y], b.img[y]);
+    mlp_gemm_x6_body<EPI, FULL, 4, PL, STAGE, KCH>(b.p[y], b.img[y], lds_b0, lds_b1);
+}
+
+// The actor's and the critic's fused last hidden + output layer in one launch (blockIdx.y): the two output widths
+// take different epilogues (NR 4: MFMA output layer, e.g. 12 actions; NR 1: VALU, <= 4 outputs, e.g. the value
+// head), one body each over the shared LDS buffers.  At the rollout's 16,384 rows per GPU each alone fills a
+// quarter of the workgroup slots.
+template <bool FULL, int MINW, int NR0, int NR1, int PL>
+__global__ __launch_bounds__(kThreads, MINW) void mlp_gemm_x6_out_pair_kernel(GemmPair b) {
+    __shared__ __attribute__((aligned(16))) char lds_b0[x6_buf_bytes<kEpiBiasEluOut, PL>()];
+    __shared__ __attribute__((aligned(16))) char lds_b1[x6_buf_bytes<kEpiBiasEluOut, PL>()];
+    // (distinct opaque markers open the two branches: otherwise the bodies' common index arithmetic is hoisted
+    // above the branch, lives through either body and spills)
+    if (blockIdx.y == 0) {
+        asm volatile("; out pair: problem 0" ::: "memory");
+        mlp_gemm_x6_body<kEpiBiasEluOut, FULL, NR0, PL>(b.p[0], b.img[0], lds_b0, lds_b1);
+    } else {
+        asm volatile("; out pair: problem 1" ::: "memory");
+        mlp_gemm_x6_body<kEpiBiasEluOut, FULL, NR1, PL>(b.p[1], b.img[1], lds_b0, lds_b1);
+    }
 }
 
 // ---- the same x6 GEMM on v_mfma_f32_16x16x32_bf16 ("paired" x6).  Under load the chip holds a higher
@@ -1514,6 +1544,18 @@ int out_fwd_nt() {  // tuning knob: RSLRL_OUT_FWD_NT=0|1
         return (e && std::atoi(e) == 1) ? 1 : 0;
     }();
     return v;
+}
+
+int cu_count() {  // compute units of the current device (cached per device)
+    static int cache[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    if (cache[dev] <= 0) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+        cache[dev] = n;
+    }
+    return cache[dev];
 }
 
 int out_fwd_occupancy() {  // tuning knob: RSLRL_OUT_FWD_OCC=2|4 (default 4)
@@ -2020,6 +2062,44 @@ int launch_pair(const GemmPair& b, bool fullm, hipStream_t st) {
     return launch_status();
 }
 
+// validated GemmParams of a fused output-layer forward (rslrl_linear_gemm's checks for RSLRL_LINEAR_FWD_OUT)
+int out_params(const rslrl_linear_args_t* a, GemmParams& p) {
+    const bool h3 = a->arith == RSLRL_ARITH_H3;
+    if (!h3 && a->arith != RSLRL_ARITH_X6) return RSLRL_E_INVALID_ARGUMENT;
+    if (a->M < 0 || a->K < 1 || a->N < 1 || a->N > kBN || (a->K & 3) || (a->N & 3) || a->K > INT32_MAX / 2)
+        return RSLRL_E_INVALID_ARGUMENT;
+    if (!a->a || !a->bimage || (h3 && !a->a_amax)) return RSLRL_E_INVALID_ARGUMENT;
+    if (a->nout < 1 || a->nout > kMaxOutWidth || !a->bias || !a->out_bias || !a->out_image || !a->y)
+        return RSLRL_E_INVALID_ARGUMENT;
+    if (a->amax_out) return RSLRL_E_UNSUPPORTED;
+    if (!aligned16(a->a) || !aligned16(a->bimage) || !aligned16(a->bias) || !aligned16(a->out_image) ||
+        (a->c && !aligned16(a->c)))
+        return RSLRL_E_MISALIGNED;
+    p = GemmParams{};
+    p.a = a->a;
+    p.M = a->M;
+    p.K = a->K;
+    p.N = a->N;
+    p.a_amax = a->a_amax;
+    p.deep = h3_deep(RSLRL_LINEAR_FWD_OUT);
+    p.bias = a->bias;
+    p.c = a->c;
+    p.oimg = static_cast<const uint4*>(a->out_image);
+    p.obias = a->out_bias;
+    p.y = a->y;
+    p.nout = a->nout;
+    p.nt = out_fwd_nt();
+    return RSLRL_OK;
+}
+
+// (MINW 2: both epilogues in one kernel do not fit 128 registers without spills; the pair is only taken when its
+// tiles are at most one per CU, where the occupancy limit costs nothing)
+template <bool FULL, int NR0>
+void launch_out_pair(const GemmPair& b, int nr1, dim3 g, hipStream_t st) {
+    if (nr1 == 1) hipLaunchKernelGGL((mlp_gemm_x6_out_pair_kernel<FULL, 2, NR0, 1, 3>), g, dim3(kThreads), 0, st, b);
+    else hipLaunchKernelGGL((mlp_gemm_x6_out_pair_kernel<FULL, 2, NR0, 4, 3>), g, dim3(kThreads), 0, st, b);
+}
+
 // validated GemmParams of an input-gradient op (rslrl_linear_gemm's checks for RSLRL_LINEAR_DGRAD_ELU)
 int dgrad_params(const rslrl_linear_args_t* a, GemmParams& p) {
     const bool h3 = a->arith == RSLRL_ARITH_H3;
@@ -2052,8 +2132,37 @@ extern "C" int rslrl_linear_gemm_pair(const rslrl_linear_args_t* a0, const rslrl
                                       rslrl_stream_t stream) {
     if (!a0 || !a1) return RSLRL_E_INVALID_ARGUMENT;
     const int op = a0->op;
-    if (a1->op != op || (op != RSLRL_LINEAR_FWD && op != RSLRL_LINEAR_FWD_ELU && op != RSLRL_LINEAR_DGRAD_ELU))
+    if (a1->op != op || (op != RSLRL_LINEAR_FWD && op != RSLRL_LINEAR_FWD_ELU && op != RSLRL_LINEAR_DGRAD_ELU &&
+                         op != RSLRL_LINEAR_FWD_OUT))
         return RSLRL_E_UNSUPPORTED;
+    if (op == RSLRL_LINEAR_FWD_OUT) {  // output widths may differ; x6 at the default occupancy, else two launches
+        if (a0->arith != a1->arith || a0->M != a1->M || a0->K != a1->K || a0->N != a1->N) return RSLRL_E_INVALID_ARGUMENT;
+        if (a0->arith != RSLRL_ARITH_X6 || x6_shape() == 16 || 2 * ceil_div(a0->M, kBM) > cu_count()) {
+            const int rc = rslrl_linear_gemm(a0, stream);
+            return rc ? rc : rslrl_linear_gemm(a1, stream);
+        }
+        GemmPair b{};
+        for (int i = 0; i < 2; ++i) {
+            const int rc = out_params(i ? a1 : a0, b.p[i]);
+            if (rc) return rc;
+            b.img[i] = static_cast<const uint4*>((i ? a1 : a0)->bimage);
+        }
+        if (a0->M == 0) return RSLRL_OK;
+        const int64_t tiles = ceil_div(a0->M, kBM);
+        if (tiles > INT32_MAX) return RSLRL_E_INVALID_ARGUMENT;
+        const dim3 g(static_cast<unsigned>(tiles), 2);
+        const bool fullm = a0->M % kBM == 0 && a0->K % kKC == 0;
+        const int nr0 = a0->nout <= 4 ? 1 : 4, nr1 = a1->nout <= 4 ? 1 : 4;
+        hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+        if (fullm) {
+            if (nr0 == 1) launch_out_pair<true, 1>(b, nr1, g, st);
+            else launch_out_pair<true, 4>(b, nr1, g, st);
+        } else {
+            if (nr0 == 1) launch_out_pair<false, 1>(b, nr1, g, st);
+            else launch_out_pair<false, 4>(b, nr1, g, st);
+        }
+        return launch_status();
+    }
     if (a0->arith != a1->arith || a0->M != a1->M || a0->K != a1->K || a0->N != a1->N) return RSLRL_E_INVALID_ARGUMENT;
     if (a0->amax_out && a1->amax_out && a0->amax_workspace == a1->amax_workspace) return RSLRL_E_INVALID_ARGUMENT;
     const bool h3 = a0->arith == RSLRL_ARITH_H3;

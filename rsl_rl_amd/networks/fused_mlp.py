@@ -267,6 +267,24 @@ def linear_fwd_out_ex(x, b, N: int, img, arith, x_amax, b_out, out_img, store_h:
     return h, y
 
 
+def linear_fwd_out_pair(xs, bs, N: int, imgs, b_outs, out_imgs, store_h: bool):
+    """linear_fwd_out_ex (x6) of two problems with the same M, K, N (output widths may differ) in one launch
+    (rslrl_linear_gemm_pair, RSLRL_LINEAR_FWD_OUT): the rollout's actor and critic heads.  The library takes the
+    pair when its tiles are at most one per CU and otherwise runs the two launches; identical results either way.
+    Returns ([h0, h1], [y0, y1])."""
+    M, K = xs[0].shape
+    hs = [torch.empty(M, N, device=x.device, dtype=torch.float32) if store_h else None for x in xs]
+    ys = [torch.empty(M, bo.shape[0], device=x.device, dtype=torch.float32) for x, bo in zip(xs, b_outs)]
+    args = [_gemm_args(_lib.LINEAR_FWD_OUT, _lib.ARITH_X6, xs[i], None, N, imgs[i], bias=bs[i], c=hs[i],
+                       out_img=out_imgs[i], out_bias=b_outs[i], y=ys[i], nout=b_outs[i].shape[0]) for i in range(2)]
+    nout = b_outs[0].shape[0] + b_outs[1].shape[0]
+    with timer.span(f"linear_fwd_out_pair[M={M},K={K},N={N},out={nout}]", xs[0].device,
+                    4 * M * (2 * K + nout + (2 * N if store_h else 0)), 2 * M * N * (2 * K + nout)):
+        rc = _lib.lib().rslrl_linear_gemm_pair(ctypes.byref(args[0]), ctypes.byref(args[1]), _stream(xs[0]))
+    _lib.check(rc, "rslrl_linear_gemm_pair")
+    return hs, ys
+
+
 def _fuse_out_fwd(ws) -> bool:
     """The last hidden layer and the output layer run as one linear_fwd_out launch (split modes only)."""
     return _FUSE_OUT_FWD and _split() and len(ws) >= 2 and ws[-1].shape[0] <= MAX_OUT_WIDTH \
@@ -836,6 +854,8 @@ def _unflatten(mlp, y):
 _side_streams: dict = {}
 # RSLRL_PAIR_TRAIN=0 keeps the update's actor and critic passes in separate launches (A/B)
 _PAIR_TRAIN = os.environ.get("RSLRL_PAIR_TRAIN", "1") != "0"
+# RSLRL_OUT_PAIR=0 keeps the rollout's two fused output-layer launches separate (A/B)
+_OUT_PAIR = os.environ.get("RSLRL_OUT_PAIR", "1") != "0"
 
 
 def side_stream(device):
@@ -897,6 +917,12 @@ def fused_mlp_forward_pair(mlp_a: nn.Sequential, x_a: torch.Tensor, mlp_b: nn.Se
         if not any(last_fused):
             h, amax = linear_fwd_pair(h, [bs[0][l], bs[1][l]], ws[0][l].shape[0], True, [imgs[0][0][l], imgs[1][0][l]],
                                       arith(l), amax, [want, want])
+            continue
+        if _OUT_PAIR and all(last_fused) and not any(h3) and side_stream(h[1].device) is None:
+            # both heads in one launch (different epilogues per output width; two launches past one tile per CU)
+            _, y = linear_fwd_out_pair(h, [bs[0][l], bs[1][l]], ws[0][l].shape[0], [imgs[0][0][l], imgs[1][0][l]],
+                                       [bs[0][-1], bs[1][-1]], [imgs[0][2], imgs[1][2]], store_h=False)
+            h = [None, None]
             continue
         # the output layer's fused launches differ per network (output width): the second network's runs on a
         # side stream beside the first's, so the two launches fill each other's tails
