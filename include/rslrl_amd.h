@@ -286,6 +286,12 @@ size_t rslrl_linear_wgrad_workspace_bytes(int64_t M, int32_t N, int32_t K);
 size_t rslrl_fold_partials_workspace_bytes(int64_t S, int64_t NK);
 int rslrl_fold_partials(const float* partials, int64_t S, int64_t NK, float* out, void* workspace,
                         size_t workspace_bytes, rslrl_stream_t stream);
+/* rslrl_fold_partials writing only the first out_len (<= NK) sums, and the leading t_rows x t_cols block of them
+ * transposed (sum e = r * t_cols + c -> out[c * t_rows + r]; t_rows = t_cols = 0: none) -- a weight gradient
+ * computed as (x^T dz) lands in W's [t_cols, t_rows] layout with its bias sums after it, and a partial row padded to
+ * a multiple of 4 lands in an exact-size destination.  out needs 4-byte alignment only. */
+int rslrl_fold_partials_ex(const float* partials, int64_t S, int64_t NK, float* out, int64_t out_len, int32_t t_rows,
+                           int32_t t_cols, void* workspace, size_t workspace_bytes, rslrl_stream_t stream);
 
 /* Output-layer backward in one launch (1 <= Nred <= 16, dz rows of Nred floats -- a 1-wide value head's [M, 1]
  * gradient as it is; fp32 FMAs on the VALU, W rebuilt exactly from its x6 image -- RSLRL_OUT_BWD=mfma selects the
@@ -382,6 +388,7 @@ typedef struct {
     float* dw_db;
     void* workspace;
     size_t workspace_bytes;
+    int32_t transpose_out; /* 1: dw_db receives dw^T ([K, N] row-major), then the column sums */
 } rslrl_wgrad_problem_t;
 size_t rslrl_linear_wgrad_bias_pair_workspace_bytes(int64_t M, int32_t N, int32_t K, int32_t bias_side);
 int rslrl_linear_wgrad_bias_pair(const rslrl_wgrad_problem_t* p0, const rslrl_wgrad_problem_t* p1, int64_t M,

@@ -64,6 +64,7 @@ EXPORTED_SYMBOLS = (
     "rslrl_linear_wgrad_bias",
     "rslrl_linear_wgrad_bias_pair_workspace_bytes",
     "rslrl_linear_wgrad_bias_pair",
+    "rslrl_fold_partials_ex",
     "rslrl_ppo_update_tail",
     "rslrl_adam_workspace_bytes",
     "rslrl_clip_adam_step",
@@ -269,6 +270,7 @@ class WgradProblem(ctypes.Structure):
         ("dw_db", ctypes.c_void_p),
         ("workspace", ctypes.c_void_p),
         ("workspace_bytes", ctypes.c_size_t),
+        ("transpose_out", ctypes.c_int32),
     ]
 
 
@@ -324,6 +326,8 @@ def _declare(L):
     L.rslrl_linear_wgrad_workspace_bytes.argtypes = [I64, I32, I32]
     L.rslrl_fold_partials.restype = ctypes.c_int
     L.rslrl_fold_partials.argtypes = [P, I64, I64, P, P, SZ, P]
+    L.rslrl_fold_partials_ex.restype = ctypes.c_int
+    L.rslrl_fold_partials_ex.argtypes = [P, I64, I64, P, I64, I32, I32, P, SZ, P]
     L.rslrl_fold_partials_workspace_bytes.restype = SZ
     L.rslrl_fold_partials_workspace_bytes.argtypes = [I64, I64]
     L.rslrl_linear_dgrad_wgrad_partial_bytes.restype = SZ

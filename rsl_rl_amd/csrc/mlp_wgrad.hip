@@ -334,9 +334,31 @@ __global__ __launch_bounds__(kThreadsW, TN <= 64 ? 4 : 2) void wgrad_x6_pair_ker
 // out[e] = sum of part[s][e] over the slices s of group blockIdx.y (per slices each) in a fixed order: four
 // interleaved fp64 accumulator groups (s % 4), combined ((g0 + g1) + g2) + g3.  IN is float (partials) or
 // double (stage-1 group sums); OUT is double (stage 1 of a two-stage fold) or float (final).
+// Where a folded fp32 value e lands: e < out_len only; the leading t_rows x t_cols block transposed
+// (e = r * t_cols + c -> out[c * t_rows + r]: the first layer's (x^T dz)^T weight gradient written as W's layout),
+// the rest (the column sums) in place.  Identity: out_len = NK, t_rows = 0.
+struct OutMap {
+    int64_t out_len;
+    int t_rows, t_cols;
+};
+
+__device__ __forceinline__ void store_mapped(float* __restrict__ out, int64_t e0, const float (&v)[4], OutMap m) {
+    if (m.t_rows == 0 && e0 + 3 < m.out_len && !(reinterpret_cast<uintptr_t>(out + e0) & 15)) {
+        *reinterpret_cast<float4*>(out + e0) = make_float4(v[0], v[1], v[2], v[3]);
+        return;
+    }
+    const int64_t tn = static_cast<int64_t>(m.t_rows) * m.t_cols;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int64_t e = e0 + k;
+        if (e >= m.out_len) break;
+        out[e < tn ? (e % m.t_cols) * m.t_rows + e / m.t_cols : e] = v[k];
+    }
+}
+
 template <typename IN, typename OUT>
 __global__ __launch_bounds__(kBlock) void fold_kernel(const IN* __restrict__ part, int S, int per, int NK,
-                                                      OUT* __restrict__ out) {
+                                                      OUT* __restrict__ out, OutMap omap) {
     __shared__ double red[4][64][4];
     const int g = threadIdx.x >> 6;
     const int c = threadIdx.x & 63;
@@ -367,10 +389,10 @@ __global__ __launch_bounds__(kBlock) void fold_kernel(const IN* __restrict__ par
 #pragma unroll
         for (int k = 0; k < 4; ++k) r[k] = ((red[0][c][k] + red[1][c][k]) + red[2][c][k]) + red[3][c][k];
         OUT* dst = out + static_cast<int64_t>(blockIdx.y) * NK + e0;
-        if constexpr (sizeof(OUT) == 4) {
-            *reinterpret_cast<float4*>(dst) =
-                make_float4(static_cast<float>(r[0]), static_cast<float>(r[1]), static_cast<float>(r[2]),
-                            static_cast<float>(r[3]));
+        if constexpr (sizeof(OUT) == 4) {  // the final stage (one group): mapped
+            const float v[4] = {static_cast<float>(r[0]), static_cast<float>(r[1]), static_cast<float>(r[2]),
+                                static_cast<float>(r[3])};
+            store_mapped(out, e0, v, omap);
         } else {
             reinterpret_cast<double2*>(dst)[0] = make_double2(r[0], r[1]);
             reinterpret_cast<double2*>(dst)[1] = make_double2(r[2], r[3]);
@@ -386,7 +408,7 @@ __global__ __launch_bounds__(kBlock) void fold_kernel(const IN* __restrict__ par
 constexpr int kWideMinBlocks = 128;  // the first layer's 48 x 256 (+ bias) partials (193 blocks): 14.4 us in
                                      // two fold_kernel stages; one pass keeps 64 KiB per CU in flight
 __global__ __launch_bounds__(kBlock) void fold_wide_kernel(const float* __restrict__ part, int S, int NK,
-                                                           float* __restrict__ out) {
+                                                           float* __restrict__ out, OutMap omap) {
     __shared__ double red[16][16][4];
     const int q = threadIdx.x & 15;
     const int ph = threadIdx.x >> 4;
@@ -416,8 +438,9 @@ __global__ __launch_bounds__(kBlock) void fold_wide_kernel(const float* __restri
         for (int p2 = 1; p2 < 16; ++p2)
 #pragma unroll
             for (int k = 0; k < 4; ++k) r[k] += red[p2][q][k];
-        *reinterpret_cast<float4*>(out + e0) = make_float4(static_cast<float>(r[0]), static_cast<float>(r[1]),
-                                                          static_cast<float>(r[2]), static_cast<float>(r[3]));
+        const float v[4] = {static_cast<float>(r[0]), static_cast<float>(r[1]), static_cast<float>(r[2]),
+                            static_cast<float>(r[3])};
+        store_mapped(out, e0, v, omap);
     }
 }
 
@@ -472,21 +495,27 @@ extern "C" size_t rslrl_linear_wgrad_workspace_bytes(int64_t M, int32_t N, int32
     return rslrl_linear_wgrad_bias_workspace_bytes(M, N, K, 0);
 }
 
-extern "C" int rslrl_fold_partials(const float* partials, int64_t S, int64_t NK, float* out, void* workspace,
-                                   size_t workspace_bytes, rslrl_stream_t stream) {
+extern "C" int rslrl_fold_partials_ex(const float* partials, int64_t S, int64_t NK, float* out, int64_t out_len,
+                                      int32_t t_rows, int32_t t_cols, void* workspace, size_t workspace_bytes,
+                                      rslrl_stream_t stream) {
     if (!partials || !out || S < 1 || S > INT32_MAX || NK < 4 || NK > INT32_MAX || (NK & 3)) return RSLRL_E_INVALID_ARGUMENT;
-    if ((reinterpret_cast<uintptr_t>(partials) | reinterpret_cast<uintptr_t>(out)) & 15) return RSLRL_E_MISALIGNED;
+    if (out_len < 1 || out_len > NK || t_rows < 0 || t_cols < 0 || (t_rows > 0) != (t_cols > 0) ||
+        static_cast<int64_t>(t_rows) * t_cols > out_len)
+        return RSLRL_E_INVALID_ARGUMENT;
+    if (reinterpret_cast<uintptr_t>(partials) & 15) return RSLRL_E_MISALIGNED;  // (out: any 4-byte alignment)
+    const OutMap omap{out_len, t_rows, t_cols};
+    const OutMap ident{NK, 0, 0};
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     if (ceil_div(NK, 64) >= kWideMinBlocks) {
         hipLaunchKernelGGL(fold_wide_kernel, dim3(static_cast<unsigned>(ceil_div(NK, 64))), dim3(kBlock), 0, st,
-                           partials, static_cast<int>(S), static_cast<int>(NK), out);
+                           partials, static_cast<int>(S), static_cast<int>(NK), out, omap);
         return launch_status();
     }
     const unsigned cols = static_cast<unsigned>(ceil_div(NK, 256));
     const int64_t G = fold_groups(S, NK);
     if (G == 1) {
         hipLaunchKernelGGL((fold_kernel<float, float>), dim3(cols), dim3(kBlock), 0, st, partials,
-                           static_cast<int>(S), static_cast<int>(S), static_cast<int>(NK), out);
+                           static_cast<int>(S), static_cast<int>(S), static_cast<int>(NK), out, omap);
         return launch_status();
     }
     if (!workspace) return RSLRL_E_INVALID_ARGUMENT;
@@ -494,12 +523,17 @@ extern "C" int rslrl_fold_partials(const float* partials, int64_t S, int64_t NK,
     if (workspace_bytes < static_cast<size_t>(G) * NK * sizeof(double)) return RSLRL_E_WORKSPACE_TOO_SMALL;
     double* ws = static_cast<double*>(workspace);
     hipLaunchKernelGGL((fold_kernel<float, double>), dim3(cols, static_cast<unsigned>(G)), dim3(kBlock), 0, st,
-                       partials, static_cast<int>(S), kFoldPer, static_cast<int>(NK), ws);
+                       partials, static_cast<int>(S), kFoldPer, static_cast<int>(NK), ws, ident);
     int rc = launch_status();
     if (rc) return rc;
     hipLaunchKernelGGL((fold_kernel<double, float>), dim3(cols), dim3(kBlock), 0, st, static_cast<const double*>(ws),
-                       static_cast<int>(G), static_cast<int>(G), static_cast<int>(NK), out);
+                       static_cast<int>(G), static_cast<int>(G), static_cast<int>(NK), out, omap);
     return launch_status();
+}
+
+extern "C" int rslrl_fold_partials(const float* partials, int64_t S, int64_t NK, float* out, void* workspace,
+                                   size_t workspace_bytes, rslrl_stream_t stream) {
+    return rslrl_fold_partials_ex(partials, S, NK, out, NK, 0, 0, workspace, workspace_bytes, stream);
 }
 
 extern "C" int rslrl_linear_wgrad_bias(const float* dz, const float* dz_amax, const float* x, const float* x_amax,
@@ -639,9 +673,10 @@ extern "C" int rslrl_linear_wgrad_bias_pair(const rslrl_wgrad_problem_t* a0, con
     int rc = launch_status();
     if (rc) return rc;
     for (int i = 0; i < 2; ++i) {
-        rc = rslrl_fold_partials(static_cast<const float*>(a[i]->workspace), S, NKE, a[i]->dw_db,
-                                 static_cast<char*>(a[i]->workspace) + part_bytes, a[i]->workspace_bytes - part_bytes,
-                                 stream);
+        const bool tr = a[i]->transpose_out != 0;
+        rc = rslrl_fold_partials_ex(static_cast<const float*>(a[i]->workspace), S, NKE, a[i]->dw_db, NKE, tr ? N : 0,
+                                    tr ? K : 0, static_cast<char*>(a[i]->workspace) + part_bytes,
+                                    a[i]->workspace_bytes - part_bytes, stream);
         if (rc) return rc;
     }
     return RSLRL_OK;

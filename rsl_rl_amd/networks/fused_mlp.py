@@ -382,15 +382,13 @@ def linear_dgrad_elu_wgrad(dz, w, h, img, want_amax=False, db_prev_out=None, dwb
         db = _out_or_empty(db_prev_out, (K,), dz.device)
         rc = L.rslrl_column_sum_fold(part.data_ptr(), tiles, K, db.data_ptr(), _stream(dz))
         _lib.check(rc, "rslrl_column_sum_fold")
-    dwb = _out_or_empty(dwb_out if P == N * K + N else None, (P,), dz.device)
+    dwb = _out_or_empty(dwb_out, (N * K + N,), dz.device)  # the fold writes exactly dW then db (no pad)
     nbytes = L.rslrl_fold_partials_workspace_bytes(tiles, P)
     ws = torch.empty(max(nbytes, 16) // 8, dtype=torch.float64, device=dz.device)
-    rc = L.rslrl_fold_partials(wpart.data_ptr(), tiles, P, dwb.data_ptr(), ws.data_ptr(), nbytes, _stream(dz))
-    _lib.check(rc, "rslrl_fold_partials")
-    dw, db_out = dwb[: N * K].view(N, K), dwb[N * K: N * K + N]
-    if dwb_out is not None and dwb.data_ptr() != dwb_out.data_ptr():
-        dwb_out.copy_(dwb[: N * K + N])
-        dw, db_out = dwb_out[: N * K].view(N, K), dwb_out[N * K:]
+    rc = L.rslrl_fold_partials_ex(wpart.data_ptr(), tiles, P, dwb.data_ptr(), N * K + N, 0, 0, ws.data_ptr(), nbytes,
+                                  _stream(dz))
+    _lib.check(rc, "rslrl_fold_partials_ex")
+    dw, db_out = dwb[: N * K].view(N, K), dwb[N * K:]
     if want_amax:
         return out, db, dw, db_out, amax
     return out, db, dw, db_out
@@ -423,10 +421,12 @@ def linear_wgrad(dz, x, arith=_lib.ARITH_X6, dz_amax=None, x_amax=None, out=None
     return dwb[: N * K].view(N, K), dwb[N * K:]
 
 
-def linear_wgrad_pair(dzs, xs, arith=_lib.ARITH_X6, bias_side=0, dwb_outs=(None, None), amaxes=((None, None),) * 2):
+def linear_wgrad_pair(dzs, xs, arith=_lib.ARITH_X6, bias_side=0, dwb_outs=(None, None), amaxes=((None, None),) * 2,
+                      transpose_out=False):
     """linear_wgrad of two problems of one shape in one launch (rslrl_linear_wgrad_bias_pair): returns, per problem,
     dw (bias_side 0) or (dw, colsum).  dwb_outs: optional [N*K + E] destinations (a Linear's adjacent arena slots);
-    amaxes: per problem (max |dz|, max |x|) device scalars for h3."""
+    amaxes: per problem (max |dz|, max |x|) device scalars for h3.  transpose_out: dw is delivered as dw^T ([K, N],
+    the first layer's (x^T dz)^T form written straight in W's layout)."""
     M, N = dzs[0].shape
     K = xs[0].shape[1]
     L = _lib.lib()
@@ -443,15 +443,16 @@ def linear_wgrad_pair(dzs, xs, arith=_lib.ARITH_X6, bias_side=0, dwb_outs=(None,
         wss.append(ws)
         dwbs.append(dwb)
         probs.append(_lib.WgradProblem(dzs[i].data_ptr(), _ptr(da), xs[i].data_ptr(), _ptr(xa), dwb.data_ptr(),
-                                       ws.data_ptr(), nbytes))
+                                       ws.data_ptr(), nbytes, 1 if transpose_out else 0))
     with timer.span(f"linear_wgrad_pair[M={M},N={N},K={K}]{_tag(arith)}", dzs[0].device, 8 * M * (N + K),
                     4 * M * K * N):
         rc = L.rslrl_linear_wgrad_bias_pair(ctypes.byref(probs[0]), ctypes.byref(probs[1]), M, N, K, arith,
                                             bias_side, _stream(dzs[0]))
     _lib.check(rc, "rslrl_linear_wgrad_bias_pair")
+    shape = (K, N) if transpose_out else (N, K)
     if not bias_side:
-        return [d.view(N, K) for d in dwbs]
-    return [(d[: N * K].view(N, K), d[N * K:]) for d in dwbs]
+        return [d.view(*shape) for d in dwbs]
+    return [(d[: N * K].view(*shape), d[N * K:]) for d in dwbs]
 
 
 def _weight_grad(dz, x, x6: bool, h3=False, dz_amax=None, x_amax=None, out=None, want_bias=False, db_out=None):
@@ -627,8 +628,10 @@ def train_backward(tape, dy, need_dx=False, need_w=None, outs=None, dy_padded=No
         if fuse_w:  # output layer: dgrad + ELU' + bias grad + weight grad over one read of h (one launch)
             nred = dz.shape[1]
             K = h_in.shape[1]
-            pad = (nred * K + nred) % 4  # the kernel's partial rows are padded to 4 floats: fold into a temporary
-            dzp = dy_padded if dy_padded is not None else dz  # the kernel reads any Nred <= 16 (no pad copy)
+            # the kernel reads any Nred <= 16 (no pad copy) and its fold writes exactly [dW | db]; a caller's padded
+            # operand computes the padded rows too (dropped below)
+            dzp = dy_padded if dy_padded is not None else dz
+            pad = dzp.shape[1] - nred
             want = l - 1 > 0 and h3[l - 1]
             # the kernel's [dW | db] result lands directly in the arena when weight and bias are adjacent there
             dwb_out = None
@@ -764,8 +767,7 @@ def train_backward_pair(tape_a, dy_a, outs_a, tape_c, dy_c, outs_c):
         d = dys[i] if dys[i].is_contiguous() else dys[i].contiguous()
         nred, K = d.shape[1], t.hs[L - 1].shape[1]
         wo, bo = o[L - 1]
-        adjacent = ((nred * K + nred) % 4 == 0 and wo.is_contiguous()
-                    and bo.data_ptr() == wo.data_ptr() + 4 * wo.numel())
+        adjacent = wo.is_contiguous() and bo.data_ptr() == wo.data_ptr() + 4 * wo.numel()
         dwb_out = torch.as_strided(wo, (nred * K + nred,), (1,)) if adjacent else None
         dz[i], _, dw, db = linear_dgrad_elu_wgrad(d, t.ws[L - 1], t.hs[L - 1], t.dgrad_imgs[L - 1], dwb_out=dwb_out,
                                                   want_db_prev=False)
@@ -788,11 +790,17 @@ def train_backward_pair(tape_a, dy_a, outs_a, tape_c, dy_c, outs_c):
         else:  # first layer: (x^T dz)^T on the 64-row tiles, the bias from dz (the kernel's K side)
             pad = (-K) % 4
             xp = [F.pad(x, (0, pad)) if pad else x for x in h_in]
-            res = linear_wgrad_pair(xp, dz, bias_side=2)
-            for i in range(2):
+            dwb_outs = []
+            for i in range(2):  # the fold writes (x^T dz)^T = dW in W's layout, then db: straight into the arena
                 wo, bo = outs[i][0]
-                dwt, db = res[i]
-                torch._foreach_copy_([wo, bo], [dwt[:K].t(), db])
+                adj = not pad and wo.is_contiguous() and bo.data_ptr() == wo.data_ptr() + 4 * wo.numel()
+                dwb_outs.append(torch.as_strided(wo, (N * K + N,), (1,)) if adj else None)
+            res = linear_wgrad_pair(xp, dz, bias_side=2, dwb_outs=dwb_outs, transpose_out=not pad)
+            for i in range(2):
+                if dwb_outs[i] is None:
+                    wo, bo = outs[i][0]
+                    dwt, db = res[i]
+                    torch._foreach_copy_([wo, bo], [dwt[:, :K] if not pad else dwt[:K].t(), db])
     return True
 
 

@@ -300,3 +300,29 @@ def test_linear_fwd_out(M, K, N, nout, store, cuda_device):
         assert h is None
     h2, y2 = fused_mlp.linear_fwd_out(x, w, b, img, wo, bo, oimg, store_h=store)
     assert torch.equal(y, y2)
+
+
+@pytest.mark.parametrize("S,R,C,E,out_len", [(37, 48, 256, 256, None), (256, 48, 256, 256, None),
+                                              (3072, 0, 0, 260, 257), (7, 0, 0, 100, 98)])
+def test_fold_partials_mapped(S, R, C, E, out_len, cuda_device):
+    """rslrl_fold_partials_ex: the leading R x C block written transposed and only out_len sums written -- bitwise
+    the identity fold's values at their mapped places, nothing past out_len touched."""
+    L = _lib.lib()
+    torch.manual_seed(S + E)
+    NK = R * C + E
+    out_len = NK if out_len is None else out_len
+    part = torch.randn(S, NK, device=cuda_device)
+    nbytes = L.rslrl_fold_partials_workspace_bytes(S, NK)
+    ws = torch.empty(max(nbytes, 16) // 8, dtype=torch.float64, device=cuda_device)
+    ident = torch.empty(NK, device=cuda_device)
+    _lib.check(L.rslrl_fold_partials(part.data_ptr(), S, NK, ident.data_ptr(), ws.data_ptr(), nbytes,
+                                     torch.cuda.current_stream().cuda_stream), "fold")
+    buf = torch.full((out_len + 3,), float("nan"), device=cuda_device)
+    dst = buf[1:]  # 4-byte aligned only
+    _lib.check(L.rslrl_fold_partials_ex(part.data_ptr(), S, NK, dst.data_ptr(), out_len, R, C, ws.data_ptr(), nbytes,
+                                        torch.cuda.current_stream().cuda_stream), "fold_ex")
+    torch.cuda.synchronize()
+    if R:
+        assert torch.equal(dst[: R * C].view(C, R), ident[: R * C].view(R, C).t())
+    assert torch.equal(dst[R * C: out_len], ident[R * C: out_len])
+    assert torch.isnan(buf[0]) and torch.isnan(buf[out_len + 1:]).all()
