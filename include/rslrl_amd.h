@@ -461,6 +461,11 @@ typedef struct {
     float* out_records;    /* record mode: the first record of step t ([N, record_floats], 16-byte aligned) */
 } rslrl_rollout_args_t;
 int rslrl_rollout_record(const rslrl_rollout_args_t* args /* host struct */, rslrl_stream_t stream);
+/* The rollout's action sample (actor_critic.py act(): Normal(mu, sigma).sample()): x [N, A] (contiguous standard
+ * normals drawn by the framework's generator, so the random stream is the reference's) <- x * scale + loc, rounded
+ * as torch's mul_ then add_ -- one launch for the pair.  scale / loc row strides in floats (0: one row for all rows). */
+int rslrl_normal_affine(float* x, const float* scale, int64_t scale_row_stride, const float* loc,
+                        int64_t loc_row_stride, int64_t N, int32_t A, rslrl_stream_t stream);
 
 /* ------------------------------------------------------------------------------------------------
  * Running normalisers, rsl_rl/networks/normalization.py.

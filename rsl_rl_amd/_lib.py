@@ -65,6 +65,7 @@ EXPORTED_SYMBOLS = (
     "rslrl_linear_wgrad_bias_pair_workspace_bytes",
     "rslrl_linear_wgrad_bias_pair",
     "rslrl_fold_partials_ex",
+    "rslrl_normal_affine",
     "rslrl_ppo_update_tail",
     "rslrl_adam_workspace_bytes",
     "rslrl_clip_adam_step",
@@ -326,6 +327,8 @@ def _declare(L):
     L.rslrl_linear_wgrad_workspace_bytes.argtypes = [I64, I32, I32]
     L.rslrl_fold_partials.restype = ctypes.c_int
     L.rslrl_fold_partials.argtypes = [P, I64, I64, P, P, SZ, P]
+    L.rslrl_normal_affine.restype = ctypes.c_int
+    L.rslrl_normal_affine.argtypes = [P, P, I64, P, I64, I64, I32, P]
     L.rslrl_fold_partials_ex.restype = ctypes.c_int
     L.rslrl_fold_partials_ex.argtypes = [P, I64, I64, P, I64, I32, I32, P, SZ, P]
     L.rslrl_fold_partials_workspace_bytes.restype = SZ

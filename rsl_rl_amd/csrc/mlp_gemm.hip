@@ -1583,15 +1583,27 @@ __host__ __device__ inline int64_t dgrad_wgrad_tile_floats(int nred, int n) {
 
 // CPL columns per lane (4: a wave spans a 256-column row; 2: two waves share a row, so W and the dW
 // accumulators take 2 NR registers each instead of 4 NR -- NR >= 12 needed 178+ registers at CPL 4)
+// LDS of one out_bwd body: red [RG][NR + 1][kBN] floats (per-row-group dW rows, then column sums), dzt4 [kBM][NR / 4]
+// float4s (the tile's dZ rows), dzsum [RG][NR] floats
 template <int NR, int CPL>
-__global__ __launch_bounds__(kOutBwdThreads, NR >= 16 ? 3 : 4) void out_bwd_valu_kernel(GemmParams p, const uint4* __restrict__ bimg) {
-    constexpr int WPR = kBN / (kWave * CPL);          // waves per row
-    constexpr int RG = (kOutBwdThreads / kWave) / WPR;  // row groups per workgroup
+struct OutBwdLds {
+    static constexpr int WPR = kBN / (kWave * CPL);          // waves per row
+    static constexpr int RG = (kOutBwdThreads / kWave) / WPR;  // row groups per workgroup
+    static constexpr int kRed = RG * (NR + 1) * kBN * 4;
+    static constexpr int kDzt = kBM * (NR / 4) * 16;
+    static constexpr int kBytes = kRed + kDzt + RG * NR * 4;
+};
+
+template <int NR, int CPL>
+__device__ __forceinline__ void out_bwd_valu_body(const GemmParams& p, const uint4* __restrict__ bimg, char* smem) {
+    using LD = OutBwdLds<NR, CPL>;
+    constexpr int WPR = LD::WPR;
+    constexpr int RG = LD::RG;
     constexpr int RPW = kBM / RG;                      // rows per wave
     using vec = typename std::conditional<CPL == 4, f32x4, f32x2>::type;
-    __shared__ float red[RG][NR + 1][kBN];  // per-row-group dW rows, then column sums (row NR)
-    __shared__ float dzsum[RG][NR];
-    __shared__ float4 dzt4[kBM][NR / 4];
+    auto red = reinterpret_cast<float (*)[NR + 1][kBN]>(smem);
+    auto dzt4 = reinterpret_cast<float4 (*)[NR / 4]>(smem + LD::kRed);
+    auto dzsum = reinterpret_cast<float (*)[NR]>(smem + LD::kRed + LD::kDzt);
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int rg = wave / WPR;
@@ -1729,6 +1741,28 @@ __global__ __launch_bounds__(kOutBwdThreads, NR >= 16 ? 3 : 4) void out_bwd_valu
     const int pad = static_cast<int>(tile_floats - (static_cast<int64_t>(nred) * p.N + nred));
     if (threadIdx.x < pad) wp[static_cast<int64_t>(nred) * p.N + nred + threadIdx.x] = 0.f;
     amax_publish<kOutBwdThreads>(p.amax_out, p.amax_ws, amx);
+}
+
+template <int NR, int CPL>
+__global__ __launch_bounds__(kOutBwdThreads, NR >= 16 ? 3 : 4) void out_bwd_valu_kernel(GemmParams p, const uint4* __restrict__ bimg) {
+    __shared__ __attribute__((aligned(16))) char smem[OutBwdLds<NR, CPL>::kBytes];
+    out_bwd_valu_body<NR, CPL>(p, bimg, smem);
+}
+
+// The actor's and the critic's output-layer backward in one launch (blockIdx.y; e.g. Nred 12 and 1), one body each
+// over one LDS area: at 98,304 rows each fills three quarters of the workgroup slots.
+template <int NR0, int CPL0, int NR1, int CPL1>
+__global__ __launch_bounds__(kOutBwdThreads, 4) void out_bwd_valu_pair_kernel(GemmPair b) {
+    constexpr int kBytes = OutBwdLds<NR0, CPL0>::kBytes > OutBwdLds<NR1, CPL1>::kBytes ? OutBwdLds<NR0, CPL0>::kBytes
+                                                                                       : OutBwdLds<NR1, CPL1>::kBytes;
+    __shared__ __attribute__((aligned(16))) char smem[kBytes];
+    if (blockIdx.y == 0) {
+        asm volatile("; out bwd pair: problem 0" ::: "memory");
+        out_bwd_valu_body<NR0, CPL0>(b.p[0], b.img[0], smem);
+    } else {
+        asm volatile("; out bwd pair: problem 1" ::: "memory");
+        out_bwd_valu_body<NR1, CPL1>(b.p[1], b.img[1], smem);
+    }
 }
 
 int out_bwd_mode() {  // tuning knob: RSLRL_OUT_BWD=mfma selects the MFMA kernel (default: VALU)
@@ -2100,6 +2134,51 @@ void launch_out_pair(const GemmPair& b, int nr1, dim3 g, hipStream_t st) {
     else hipLaunchKernelGGL((mlp_gemm_x6_out_pair_kernel<FULL, 2, NR0, 4, 3>), g, dim3(kThreads), 0, st, b);
 }
 
+// validated GemmParams of a fused output-layer backward (rslrl_linear_gemm's checks for RSLRL_LINEAR_DGRAD_ELU_WGRAD)
+int dgrad_wgrad_params(const rslrl_linear_args_t* a, GemmParams& p) {
+    if (a->arith != RSLRL_ARITH_X6) return RSLRL_E_UNSUPPORTED;
+    if (a->M < 0 || a->K < 1 || a->K > kMaxWgradRows || a->N < 1 || a->N > kBN) return RSLRL_E_INVALID_ARGUMENT;
+    if (!a->a || !a->bimage || !a->h || !a->c || !a->wgrad_partials) return RSLRL_E_INVALID_ARGUMENT;
+    if (a->amax_out && !a->amax_workspace) return RSLRL_E_INVALID_ARGUMENT;
+    if (!aligned16(a->a) || !aligned16(a->bimage)) return RSLRL_E_MISALIGNED;
+    p = GemmParams{};
+    p.a = a->a;
+    p.M = a->M;
+    p.K = a->K;
+    p.N = a->N;
+    p.amax_out = a->amax_out;
+    p.amax_ws = static_cast<unsigned*>(a->amax_workspace);
+    p.h = a->h;
+    p.c = a->c;
+    p.colsum = a->colsum_partials;
+    p.ctiles = ceil_div(a->M, kBM);
+    p.wpart = a->wgrad_partials;
+    return RSLRL_OK;
+}
+
+template <int NR0, int NR1>
+void launch_out_bwd_pair(const GemmPair& b, dim3 g, hipStream_t st) {
+    constexpr int C0 = NR0 <= 4 ? 4 : 2, C1 = NR1 <= 4 ? 4 : 2;
+    hipLaunchKernelGGL((out_bwd_valu_pair_kernel<NR0, C0, NR1, C1>), g, dim3(kOutBwdThreads), 0, st, b);
+}
+
+// (one of the two reductions <= 4 wide -- the value head -- the other any of 4 / 8 / 12 / 16)
+bool out_bwd_pair_dispatch(const GemmPair& b, int nr0, int nr1, dim3 g, hipStream_t st) {
+    auto other = [&](int nr, auto small_first) {
+        constexpr bool F = decltype(small_first)::value;
+        switch (nr) {
+            case 4: launch_out_bwd_pair<4, 4>(b, g, st); return true;
+            case 8: F ? launch_out_bwd_pair<4, 8>(b, g, st) : launch_out_bwd_pair<8, 4>(b, g, st); return true;
+            case 12: F ? launch_out_bwd_pair<4, 12>(b, g, st) : launch_out_bwd_pair<12, 4>(b, g, st); return true;
+            case 16: F ? launch_out_bwd_pair<4, 16>(b, g, st) : launch_out_bwd_pair<16, 4>(b, g, st); return true;
+            default: return false;
+        }
+    };
+    if (nr1 == 4) return other(nr0, std::false_type{});
+    if (nr0 == 4) return other(nr1, std::true_type{});
+    return false;
+}
+
 // validated GemmParams of an input-gradient op (rslrl_linear_gemm's checks for RSLRL_LINEAR_DGRAD_ELU)
 int dgrad_params(const rslrl_linear_args_t* a, GemmParams& p) {
     const bool h3 = a->arith == RSLRL_ARITH_H3;
@@ -2133,8 +2212,32 @@ extern "C" int rslrl_linear_gemm_pair(const rslrl_linear_args_t* a0, const rslrl
     if (!a0 || !a1) return RSLRL_E_INVALID_ARGUMENT;
     const int op = a0->op;
     if (a1->op != op || (op != RSLRL_LINEAR_FWD && op != RSLRL_LINEAR_FWD_ELU && op != RSLRL_LINEAR_DGRAD_ELU &&
-                         op != RSLRL_LINEAR_FWD_OUT))
+                         op != RSLRL_LINEAR_FWD_OUT && op != RSLRL_LINEAR_DGRAD_ELU_WGRAD))
         return RSLRL_E_UNSUPPORTED;
+    if (op == RSLRL_LINEAR_DGRAD_ELU_WGRAD) {  // reduction widths (K = Nred) may differ; VALU kernels only
+        if (a0->M != a1->M || a0->N != a1->N) return RSLRL_E_INVALID_ARGUMENT;
+        GemmPair b{};
+        int rc = RSLRL_OK;
+        for (int i = 0; i < 2 && rc == RSLRL_OK; ++i) {
+            rc = dgrad_wgrad_params(i ? a1 : a0, b.p[i]);
+            b.img[i] = static_cast<const uint4*>((i ? a1 : a0)->bimage);
+        }
+        if (rc == RSLRL_E_UNSUPPORTED || out_bwd_mode() != 0) {
+            rc = rslrl_linear_gemm(a0, stream);
+            return rc ? rc : rslrl_linear_gemm(a1, stream);
+        }
+        if (rc) return rc;
+        if (a0->M == 0) return RSLRL_OK;
+        const int64_t tiles = ceil_div(a0->M, kBM);
+        if (tiles > INT32_MAX) return RSLRL_E_INVALID_ARGUMENT;
+        hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+        if (!out_bwd_pair_dispatch(b, (a0->K + 3) / 4 * 4, (a1->K + 3) / 4 * 4, dim3(static_cast<unsigned>(tiles), 2),
+                                   st)) {
+            rc = rslrl_linear_gemm(a0, stream);
+            return rc ? rc : rslrl_linear_gemm(a1, stream);
+        }
+        return launch_status();
+    }
     if (op == RSLRL_LINEAR_FWD_OUT) {  // output widths may differ; x6 at the default occupancy, else two launches
         if (a0->arith != a1->arith || a0->M != a1->M || a0->K != a1->K || a0->N != a1->N) return RSLRL_E_INVALID_ARGUMENT;
         if (a0->arith != RSLRL_ARITH_X6 || x6_shape() == 16 || 2 * ceil_div(a0->M, kBM) > cu_count()) {

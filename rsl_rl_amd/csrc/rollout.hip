@@ -351,3 +351,31 @@ extern "C" int rslrl_rollout_record(const rslrl_rollout_args_t* args, rslrl_stre
         hipLaunchKernelGGL(rollout_record_kernel<2>, grid, dim3(kBlock), lds, st, a, copy_blocks, rs);
     return launch_status();
 }
+
+// ---- the rollout's action sample (ActorCritic.act: Normal(mu, sigma).sample() = normal_(0, 1) * sigma + mu, the
+// distribution.py sample of torch.normal): x <- x * scale + loc with torch's two roundings (mul, then add) -- one
+// launch for the mul_ + add_ pair.  x [N, A] contiguous (the standard normals, drawn by the framework's generator so
+// that the random stream is the reference's); scale / loc rows with their own strides (0: one row for all).
+namespace rslrl {
+namespace {
+__global__ __launch_bounds__(kBlock) void normal_affine_kernel(float* __restrict__ x, const float* __restrict__ scale,
+                                                               int64_t s_rs, const float* __restrict__ loc,
+                                                               int64_t l_rs, int64_t N, int A) {
+    const int64_t t = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    if (t >= N * A) return;
+    const int64_t n = t / A;
+    const int a = static_cast<int>(t - n * A);
+    x[t] = __fadd_rn(__fmul_rn(x[t], scale[n * s_rs + a]), loc[n * l_rs + a]);
+}
+}  // namespace
+}  // namespace rslrl
+
+extern "C" int rslrl_normal_affine(float* x, const float* scale, int64_t scale_row_stride, const float* loc,
+                                   int64_t loc_row_stride, int64_t N, int32_t A, rslrl_stream_t stream) {
+    if (N < 0 || A < 1 || scale_row_stride < 0 || loc_row_stride < 0) return RSLRL_E_INVALID_ARGUMENT;
+    if (N == 0) return RSLRL_OK;
+    if (!x || !scale || !loc) return RSLRL_E_INVALID_ARGUMENT;
+    hipLaunchKernelGGL(normal_affine_kernel, dim3(static_cast<unsigned>(ceil_div(N * A, kBlock))), dim3(kBlock), 0,
+                       reinterpret_cast<hipStream_t>(stream), x, scale, scale_row_stride, loc, loc_row_stride, N, A);
+    return launch_status();
+}

@@ -127,6 +127,22 @@ class KernelTimer:
 timer = KernelTimer()
 
 
+def normal_affine_(x: torch.Tensor, scale: torch.Tensor, loc: torch.Tensor) -> torch.Tensor:
+    """x <- x * scale + loc in place (torch's mul_ then add_ roundings) in one launch (rslrl_normal_affine): the
+    rollout's Normal sample from standard normals x [N, A] contiguous; scale / loc [N, A] with unit column stride
+    (row stride 0 for an expanded shared std)."""
+    _require_device(x, scale, loc)
+    if x.dim() != 2 or not x.is_contiguous() or scale.shape != x.shape or loc.shape != x.shape:
+        raise ValueError("normal_affine_: x [N, A] contiguous, scale / loc of its shape")
+    if (scale.stride(1) != 1 and x.shape[1] > 1) or (loc.stride(1) != 1 and x.shape[1] > 1):
+        raise ValueError("normal_affine_: scale / loc need unit column stride")
+    N, A = x.shape
+    rc = _lib.lib().rslrl_normal_affine(x.data_ptr(), scale.data_ptr(), scale.stride(0), loc.data_ptr(), loc.stride(0),
+                                        N, A, ctypes.c_void_p(_stream(x.device)))
+    _lib.check(rc, "rslrl_normal_affine")
+    return x
+
+
 # ------------------------------------------------------------------------------------------------
 # rollout_storage.py:127-149
 # ------------------------------------------------------------------------------------------------

@@ -4,9 +4,12 @@ the Normal sample; on_policy_runner.py:103-109 calls it once per env step).
 Eagerly, ActorCritic.act_and_evaluate issues ~20 host calls per step (the B-image build, the paired MLP launches
 through ctypes, the Normal sample's four torch ops): ~100 us of host time that the GPU waits out when a GPU holds
 few envs (the strong-scaling shares of config C4).  Here the same calls are captured once per configuration into a
-torch.cuda.CUDAGraph and replayed: the observation is copied into the graph's static input, the graph replays
-(image build included, so parameters updated in place between rollouts are picked up), and the outputs are the
-graph's static tensors (the actions are cloned, so a caller may keep them).
+torch.cuda.CUDAGraph and replayed: the observation is copied into the graph's static input, the graph replays, and
+the outputs are the graph's static tensors (the actions are cloned, so a caller may keep them).  Two graphs per
+configuration: one with the B-image build of the weights (replayed at the first step of each rollout -- each entry
+into an outermost fused_mlp.frozen_weights() scope -- so parameters updated in place between rollouts are picked
+up, and at every step outside such a scope) and one without it, reading the images the first one wrote (the other
+23 steps of a rollout).
 
 Same values and the same random stream as the eager calls: the sample's normal_() draws from the default CUDA
 generator, whose offset a captured graph advances by the same increment per replay as the eager kernel does per
@@ -37,6 +40,10 @@ class RolloutActGraph:
         self._failed = set()
         self._static_in = None
         self._out = None
+        self._graph_fwd = None  # the graph without the image build, and its outputs
+        self._out_fwd = None
+        self._imgs = None  # the image tensors both graphs use (written by the first one's replay)
+        self._img_gen = None  # fused_mlp._frozen_gen of the last image build
 
     @staticmethod
     def enabled() -> bool:
@@ -61,6 +68,7 @@ class RolloutActGraph:
             return None
         if key != self._key:
             self._key, self._seen, self._graph, self._static_in, self._out = key, 0, None, None, None
+            self._graph_fwd, self._out_fwd, self._imgs, self._img_gen = None, None, None, None
         if self._graph is None:
             self._seen += 1
             if self._seen < 2:  # the first call of a configuration runs eagerly (lazy initialisations happen there)
@@ -69,37 +77,60 @@ class RolloutActGraph:
                 return None
         for g, t in self._static_in.items():
             t.copy_(obs[g])
-        self._graph.replay()
-        actions, values, mean, scale = self._out
+        frozen = fused_mlp._frozen_depth > 0
+        if frozen and self._graph_fwd is not None and self._img_gen == fused_mlp._frozen_gen:
+            self._graph_fwd.replay()  # the images of this rollout's weights are current
+            actions, values, mean, scale = self._out_fwd
+        else:
+            self._graph.replay()
+            self._img_gen = fused_mlp._frozen_gen if frozen else None
+            actions, values, mean, scale = self._out
         self.policy.distribution = Normal(mean, scale)
         return actions.clone(), values
 
     def _capture(self, obs, key) -> bool:
         pol = self.policy
         static_in = {g: obs[g].clone() for g in sorted(set(pol.obs_groups["policy"]) | set(pol.obs_groups["critic"]))}
-        graph = torch.cuda.CUDAGraph()
+        graph, graph_fwd = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
         try:
-            with _eager_caches_off(), torch.cuda.graph(graph):
-                actions, values = pol.act_and_evaluate(static_in)
-                dist = pol.distribution
-                out = (actions, values, dist.loc, dist.scale)
+            with _capture_caches() as cache:
+                with torch.cuda.graph(graph):  # image build + forward + sample
+                    actions, values = pol.act_and_evaluate(static_in)
+                    dist = pol.distribution
+                    out = (actions, values, dist.loc, dist.scale)
+                imgs = [v[1] for v in cache.values()]
+                out_fwd = None
+                if imgs:  # the same step reading the cached images (no image launch in this graph)
+                    with torch.cuda.graph(graph_fwd):
+                        a2, v2 = pol.act_and_evaluate(static_in)
+                        d2 = pol.distribution
+                        out_fwd = (a2, v2, d2.loc, d2.scale)
         except Exception as e:  # noqa: BLE001 -- any op that cannot be captured: stay eager for this configuration
             self._failed.add(key)
             warnings.warn(f"rollout act() graph capture failed, running eagerly: {e}")
             return False
         self._graph, self._static_in, self._out = graph, static_in, out
+        self._graph_fwd, self._out_fwd, self._imgs = (graph_fwd, out_fwd, imgs) if out_fwd is not None else (None,) * 3
+        self._img_gen = None  # the first replay runs the image build
         return True
 
 
 @contextlib.contextmanager
-def _eager_caches_off():
-    """No frozen-weights B-image reuse and no kernel-timer events while capturing: the image build is captured
-    into the graph (rebuilt at every replay from the current weights) and no timing event lands in it."""
+def _capture_caches():
+    """While capturing: a private frozen-weights image cache (the first graph's image build fills it, the second graph
+    reads it), no kernel-timer events; the caller's cache and memo are restored afterwards."""
     depth, en, men = fused_mlp._frozen_depth, kernels.timer.enabled, kernels.timer.mlp_enabled
-    fused_mlp._frozen_depth = 0
+    cache, memo = dict(fused_mlp._bimage_cache), dict(fused_mlp._pair_memo)
+    fused_mlp._bimage_cache.clear()
+    fused_mlp._pair_memo.clear()
+    fused_mlp._frozen_depth = 1
     kernels.timer.enabled = kernels.timer.mlp_enabled = False
     try:
-        yield
+        yield fused_mlp._bimage_cache
     finally:
         fused_mlp._frozen_depth = depth
+        fused_mlp._bimage_cache.clear()
+        fused_mlp._bimage_cache.update(cache)
+        fused_mlp._pair_memo.clear()
+        fused_mlp._pair_memo.update(memo)
         kernels.timer.enabled, kernels.timer.mlp_enabled = en, men

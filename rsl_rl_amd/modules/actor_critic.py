@@ -13,6 +13,7 @@ import torch
 import torch.nn as nn
 from torch.distributions import Normal
 
+from .. import kernels
 from ..networks import MLP, EmpiricalNormalization
 from ..networks import fused_mlp
 from ..networks.fused_mlp import fused_mlp_forward_pair
@@ -241,7 +242,11 @@ class ActorCritic(nn.Module):
         # scale.min() >= 0 with a device-to-host read that stalls the launch queue every env step
         loc, scale = self.distribution.loc, self.distribution.scale
         with torch.no_grad():
-            return torch.empty_like(loc).normal_().mul_(scale).add_(loc)
+            eps = torch.empty_like(loc).normal_()
+            if (eps.is_cuda and eps.dim() == 2 and eps.is_contiguous() and scale.shape == eps.shape
+                    and loc.shape == eps.shape and scale.stride(1) == 1 and loc.stride(1) == 1):
+                return kernels.normal_affine_(eps, scale, loc)  # the mul_ + add_ pair in one launch, same bits
+            return eps.mul_(scale).add_(loc)
 
     def act_and_evaluate(self, obs):
         """(act(obs), evaluate(obs)) of the rollout step (ppo.py:155-156) with the actor's and the critic's

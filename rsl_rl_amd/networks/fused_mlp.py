@@ -102,6 +102,7 @@ def _ptr(t):
 # moving their version counter (fused Adam does not bump it), so images are rebuilt on every use except
 # inside a frozen_weights() scope, where the caller promises the weights do not change (the rollout).
 _frozen_depth = 0
+_frozen_gen = 0  # bumped on entering an outermost frozen_weights() scope (a new rollout: weights may have changed)
 _bimage_cache: dict = {}
 _pair_memo: dict = {}  # fused_mlp_forward_pair's per-pair plan inside a frozen_weights() scope
 
@@ -109,7 +110,9 @@ _pair_memo: dict = {}  # fused_mlp_forward_pair's per-pair plan inside a frozen_
 @contextlib.contextmanager
 def frozen_weights():
     """Scope in which B images of weights are built once and reused (the rollout of on_policy_runner)."""
-    global _frozen_depth
+    global _frozen_depth, _frozen_gen
+    if _frozen_depth == 0:
+        _frozen_gen += 1
     _frozen_depth += 1
     try:
         yield
@@ -392,6 +395,40 @@ def linear_dgrad_elu_wgrad(dz, w, h, img, want_amax=False, db_prev_out=None, dwb
     if want_amax:
         return out, db, dw, db_out, amax
     return out, db, dw, db_out
+
+
+def linear_dgrad_elu_wgrad_pair(dzs, hs, imgs, dwb_outs=(None, None)):
+    """linear_dgrad_elu_wgrad (want_db_prev=False, no amax) of two output layers over the same rows and hidden width
+    in one launch (rslrl_linear_gemm_pair, RSLRL_LINEAR_DGRAD_ELU_WGRAD; the reduction widths may differ, e.g. 12
+    actions and the value head).  Returns per problem (dz_prev, dw, db)."""
+    M, K = hs[0].shape
+    L = _lib.lib()
+    tiles = L.rslrl_linear_tiles(M)
+    outs, wparts, dwbs = [], [], []
+    for i in range(2):
+        N = dzs[i].shape[1]
+        P = (N * K + N + 3) // 4 * 4
+        outs.append(torch.empty(M, K, device=dzs[i].device, dtype=torch.float32))
+        wparts.append(torch.empty(tiles, P, device=dzs[i].device, dtype=torch.float32))
+        dwbs.append(_out_or_empty(dwb_outs[i], (N * K + N,), dzs[i].device))
+    args = [_gemm_args(_lib.LINEAR_DGRAD_ELU_WGRAD, _lib.ARITH_X6, dzs[i], None, K, imgs[i], h=hs[i], c=outs[i],
+                       wpart=wparts[i]) for i in range(2)]
+    nred = dzs[0].shape[1] + dzs[1].shape[1]
+    with timer.span(f"linear_dgrad_wgrad_pair[M={M},Nred={nred},K={K}]", dzs[0].device, 4 * M * (nred + 4 * K),
+                    4 * M * K * nred):
+        rc = L.rslrl_linear_gemm_pair(ctypes.byref(args[0]), ctypes.byref(args[1]), _stream(dzs[0]))
+    _lib.check(rc, "rslrl_linear_gemm_pair")
+    res = []
+    for i in range(2):
+        N = dzs[i].shape[1]
+        P = wparts[i].shape[1]
+        nbytes = L.rslrl_fold_partials_workspace_bytes(tiles, P)
+        ws = torch.empty(max(nbytes, 16) // 8, dtype=torch.float64, device=dzs[i].device)
+        rc = L.rslrl_fold_partials_ex(wparts[i].data_ptr(), tiles, P, dwbs[i].data_ptr(), N * K + N, 0, 0,
+                                      ws.data_ptr(), nbytes, _stream(dzs[i]))
+        _lib.check(rc, "rslrl_fold_partials_ex")
+        res.append((outs[i], dwbs[i][: N * K].view(N, K), dwbs[i][N * K:]))
+    return res
 
 
 def linear_wgrad(dz, x, arith=_lib.ARITH_X6, dz_amax=None, x_amax=None, out=None, bias_side=0, dwb_out=None):
@@ -761,18 +798,22 @@ def train_backward_pair(tape_a, dy_a, outs_a, tape_c, dy_c, outs_c):
         return False
     if not all(_bias_from_wgrad(t.ws[l].shape[0], t.hs[l].shape[1], True) for t in tapes for l in range(L - 1)):
         return False
-    dz = [None, None]
-    for i in range(2):  # output layer: dgrad + ELU' + its weight and bias gradients over one read of h
-        t, o = tapes[i], outs[i]
-        d = dys[i] if dys[i].is_contiguous() else dys[i].contiguous()
-        nred, K = d.shape[1], t.hs[L - 1].shape[1]
-        wo, bo = o[L - 1]
-        adjacent = wo.is_contiguous() and bo.data_ptr() == wo.data_ptr() + 4 * wo.numel()
-        dwb_out = torch.as_strided(wo, (nred * K + nred,), (1,)) if adjacent else None
-        dz[i], _, dw, db = linear_dgrad_elu_wgrad(d, t.ws[L - 1], t.hs[L - 1], t.dgrad_imgs[L - 1], dwb_out=dwb_out,
-                                                  want_db_prev=False)
-        if not adjacent:
-            torch._foreach_copy_([wo, bo], [dw, db])
+    # output layers: dgrad + ELU' + their weight and bias gradients over one read of h, both in one launch
+    ds = [d if d.is_contiguous() else d.contiguous() for d in dys]
+    K = tape_a.hs[L - 1].shape[1]
+    dwb_outs, adjacent = [], []
+    for i in range(2):
+        nred = ds[i].shape[1]
+        wo, bo = outs[i][L - 1]
+        adj = wo.is_contiguous() and bo.data_ptr() == wo.data_ptr() + 4 * wo.numel()
+        adjacent.append(adj)
+        dwb_outs.append(torch.as_strided(wo, (nred * K + nred,), (1,)) if adj else None)
+    res = linear_dgrad_elu_wgrad_pair(ds, [t.hs[L - 1] for t in tapes], [t.dgrad_imgs[L - 1] for t in tapes],
+                                      dwb_outs)
+    dz = [r[0] for r in res]
+    for i in range(2):
+        if not adjacent[i]:
+            torch._foreach_copy_(list(outs[i][L - 1]), [res[i][1], res[i][2]])
     for l in range(L - 2, -1, -1):
         h_in = [t.hs[l] for t in tapes]
         N, K = tapes[0].ws[l].shape
