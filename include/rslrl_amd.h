@@ -292,6 +292,18 @@ int rslrl_fold_partials(const float* partials, int64_t S, int64_t NK, float* out
  * a multiple of 4 lands in an exact-size destination.  out needs 4-byte alignment only. */
 int rslrl_fold_partials_ex(const float* partials, int64_t S, int64_t NK, float* out, int64_t out_len, int32_t t_rows,
                            int32_t t_cols, void* workspace, size_t workspace_bytes, rslrl_stream_t stream);
+/* Up to 16 folds in one launch, each as rslrl_fold_partials_ex (one pass: 64 columns per workgroup, every slice of
+ * them; fp64 in a fixed order that depends on S alone).  The folds of one backward pass (every layer of the actor
+ * and the critic) run as one launch instead of one or two each. */
+typedef struct {
+    const float* partials; /* [S][NK], 16-byte aligned */
+    int64_t S;
+    int64_t NK;            /* multiple of 4 */
+    float* out;
+    int64_t out_len;
+    int32_t t_rows, t_cols;
+} rslrl_fold_job_t;
+int rslrl_fold_partials_batch(const rslrl_fold_job_t* jobs, int32_t n, rslrl_stream_t stream);
 
 /* Output-layer backward in one launch (1 <= Nred <= 16, dz rows of Nred floats -- a 1-wide value head's [M, 1]
  * gradient as it is; fp32 FMAs on the VALU, W rebuilt exactly from its x6 image -- RSLRL_OUT_BWD=mfma selects the
@@ -391,8 +403,14 @@ typedef struct {
     int32_t transpose_out; /* 1: dw_db receives dw^T ([K, N] row-major), then the column sums */
 } rslrl_wgrad_problem_t;
 size_t rslrl_linear_wgrad_bias_pair_workspace_bytes(int64_t M, int32_t N, int32_t K, int32_t bias_side);
+/* flags RSLRL_WGRAD_NO_FOLD: leave each problem's [S][N * K + E] fp32 partials at the start of its workspace
+ * (S = rslrl_linear_wgrad_bias_pair_slices(M, N)) for the caller to fold (rslrl_fold_partials_batch: the folds of a
+ * whole backward pass in one launch); transpose_out / dw_db are then unused. */
+#define RSLRL_WGRAD_NO_FOLD 1
+int64_t rslrl_linear_wgrad_bias_pair_slices(int64_t M, int32_t N);
 int rslrl_linear_wgrad_bias_pair(const rslrl_wgrad_problem_t* p0, const rslrl_wgrad_problem_t* p1, int64_t M,
-                                 int32_t N, int32_t K, int32_t arith, int32_t bias_side, rslrl_stream_t stream);
+                                 int32_t N, int32_t K, int32_t arith, int32_t bias_side, int32_t flags,
+                                 rslrl_stream_t stream);
 
 /* ------------------------------------------------------------------------------------------------
  * Rollout-side record: for environment step t, in one launch,

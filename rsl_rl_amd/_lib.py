@@ -65,6 +65,8 @@ EXPORTED_SYMBOLS = (
     "rslrl_linear_wgrad_bias_pair_workspace_bytes",
     "rslrl_linear_wgrad_bias_pair",
     "rslrl_fold_partials_ex",
+    "rslrl_fold_partials_batch",
+    "rslrl_linear_wgrad_bias_pair_slices",
     "rslrl_normal_affine",
     "rslrl_ppo_update_tail",
     "rslrl_adam_workspace_bytes",
@@ -261,6 +263,23 @@ class RndUpdateArgs(ctypes.Structure):
     ]
 
 
+class FoldJob(ctypes.Structure):
+    """include/rslrl_amd.h rslrl_fold_job_t"""
+    _fields_ = [
+        ("partials", ctypes.c_void_p),
+        ("S", ctypes.c_int64),
+        ("NK", ctypes.c_int64),
+        ("out", ctypes.c_void_p),
+        ("out_len", ctypes.c_int64),
+        ("t_rows", ctypes.c_int32),
+        ("t_cols", ctypes.c_int32),
+    ]
+
+
+MAX_FOLD_JOBS = 16
+WGRAD_NO_FOLD = 1
+
+
 class WgradProblem(ctypes.Structure):
     """include/rslrl_amd.h rslrl_wgrad_problem_t"""
     _fields_ = [
@@ -375,7 +394,11 @@ def _declare(L):
     L.rslrl_linear_wgrad_bias_pair_workspace_bytes.argtypes = [I64, I32, I32, I32]
     L.rslrl_linear_wgrad_bias_pair.restype = ctypes.c_int
     L.rslrl_linear_wgrad_bias_pair.argtypes = [ctypes.POINTER(WgradProblem), ctypes.POINTER(WgradProblem), I64, I32,
-                                               I32, I32, I32, P]
+                                               I32, I32, I32, I32, P]
+    L.rslrl_linear_wgrad_bias_pair_slices.restype = I64
+    L.rslrl_linear_wgrad_bias_pair_slices.argtypes = [I64, I32]
+    L.rslrl_fold_partials_batch.restype = ctypes.c_int
+    L.rslrl_fold_partials_batch.argtypes = [ctypes.POINTER(FoldJob), I32, P]
     L.rslrl_rnd_update_workspace_bytes.restype = SZ
     L.rslrl_rnd_update_workspace_bytes.argtypes = [I64, I32, I32, I32]
     L.rslrl_rnd_update.restype = ctypes.c_int

@@ -444,6 +444,59 @@ __global__ __launch_bounds__(kBlock) void fold_wide_kernel(const float* __restri
     }
 }
 
+// Several folds in one launch (rslrl_fold_partials_batch): block b belongs to the job whose range of 64-column blocks
+// holds it; each block runs fold_wide's body (16 slice phases x 16 column quads, fp64, phase order) -- the same
+// summation order as fold_wide_kernel for any S, so a job's result does not depend on its batch.
+constexpr int kMaxFoldJobs = 16;
+struct FoldJobs {
+    const float* part[kMaxFoldJobs];
+    float* out[kMaxFoldJobs];
+    OutMap omap[kMaxFoldJobs];
+    int S[kMaxFoldJobs];
+    int NK[kMaxFoldJobs];
+    int first_block[kMaxFoldJobs + 1];
+    int n;
+};
+
+__global__ __launch_bounds__(kBlock) void fold_batch_kernel(FoldJobs jobs) {
+    __shared__ double red[16][16][4];
+    int j = 0;
+    while (j + 1 < jobs.n && static_cast<int>(blockIdx.x) >= jobs.first_block[j + 1]) ++j;  // wave-uniform
+    const int NK = jobs.NK[j], S = jobs.S[j];
+    const int q = threadIdx.x & 15;
+    const int ph = threadIdx.x >> 4;
+    const int e0 = (static_cast<int>(blockIdx.x) - jobs.first_block[j]) * 64 + 4 * q;
+    double a[4] = {0.0, 0.0, 0.0, 0.0};
+    if (e0 < NK) {
+        const float* src = jobs.part[j] + e0;
+        for (int s0 = ph; s0 < S; s0 += 16 * 16) {
+            float4 v[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                const int s = s0 + 16 * k;
+                v[k] = s < S ? *reinterpret_cast<const float4*>(src + static_cast<int64_t>(s) * NK)
+                             : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                a[0] += v[k].x; a[1] += v[k].y; a[2] += v[k].z; a[3] += v[k].w;
+            }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) red[ph][q][k] = a[k];
+    __syncthreads();
+    if (ph == 0 && e0 < NK) {
+        double r[4] = {red[0][q][0], red[0][q][1], red[0][q][2], red[0][q][3]};
+        for (int p2 = 1; p2 < 16; ++p2)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) r[k] += red[p2][q][k];
+        const float v[4] = {static_cast<float>(r[0]), static_cast<float>(r[1]), static_cast<float>(r[2]),
+                            static_cast<float>(r[3])};
+        store_mapped(jobs.out[j], e0, v, jobs.omap[j]);
+    }
+}
+
 // Two-stage fold when one pass would leave the chip idle (few columns, many slices -- e.g. the output
 // layer's per-tile partials: 3072 slices x 3072 columns): stage 1 sums groups of kFoldPer slices into fp64
 // [G][NK], stage 2 sums the G groups.  The order is fixed by (S, NK) alone: deterministic.
@@ -536,6 +589,34 @@ extern "C" int rslrl_fold_partials(const float* partials, int64_t S, int64_t NK,
     return rslrl_fold_partials_ex(partials, S, NK, out, NK, 0, 0, workspace, workspace_bytes, stream);
 }
 
+extern "C" int rslrl_fold_partials_batch(const rslrl_fold_job_t* jobs, int32_t n, rslrl_stream_t stream) {
+    if (!jobs || n < 1 || n > kMaxFoldJobs) return RSLRL_E_INVALID_ARGUMENT;
+    FoldJobs fj{};
+    fj.n = n;
+    int64_t blocks = 0;
+    for (int i = 0; i < n; ++i) {
+        const rslrl_fold_job_t& j = jobs[i];
+        if (!j.partials || !j.out || j.S < 1 || j.S > INT32_MAX || j.NK < 4 || j.NK > INT32_MAX || (j.NK & 3))
+            return RSLRL_E_INVALID_ARGUMENT;
+        if (j.out_len < 1 || j.out_len > j.NK || j.t_rows < 0 || j.t_cols < 0 || (j.t_rows > 0) != (j.t_cols > 0) ||
+            static_cast<int64_t>(j.t_rows) * j.t_cols > j.out_len)
+            return RSLRL_E_INVALID_ARGUMENT;
+        if (reinterpret_cast<uintptr_t>(j.partials) & 15) return RSLRL_E_MISALIGNED;
+        fj.part[i] = j.partials;
+        fj.out[i] = j.out;
+        fj.omap[i] = OutMap{j.out_len, j.t_rows, j.t_cols};
+        fj.S[i] = static_cast<int>(j.S);
+        fj.NK[i] = static_cast<int>(j.NK);
+        fj.first_block[i] = static_cast<int>(blocks);
+        blocks += ceil_div(j.NK, 64);
+        if (blocks > INT32_MAX) return RSLRL_E_INVALID_ARGUMENT;
+    }
+    fj.first_block[n] = static_cast<int>(blocks);
+    hipLaunchKernelGGL(fold_batch_kernel, dim3(static_cast<unsigned>(blocks)), dim3(kBlock), 0,
+                       reinterpret_cast<hipStream_t>(stream), fj);
+    return launch_status();
+}
+
 extern "C" int rslrl_linear_wgrad_bias(const float* dz, const float* dz_amax, const float* x, const float* x_amax,
                                        int64_t M, int32_t N, int32_t K, int32_t arith, int32_t bias_side, float* dw_db,
                                        void* workspace, size_t workspace_bytes, rslrl_stream_t stream) {
@@ -617,9 +698,14 @@ extern "C" size_t rslrl_linear_wgrad_bias_pair_workspace_bytes(int64_t M, int32_
     return static_cast<size_t>(S) * NKE * sizeof(float) + rslrl_fold_partials_workspace_bytes(S, NKE);
 }
 
+extern "C" int64_t rslrl_linear_wgrad_bias_pair_slices(int64_t M, int32_t N) {
+    return M < 1 || N < 1 ? 0 : ceil_div(M, wgrad_pair_rows_per(M, N));
+}
+
 extern "C" int rslrl_linear_wgrad_bias_pair(const rslrl_wgrad_problem_t* a0, const rslrl_wgrad_problem_t* a1,
                                             int64_t M, int32_t N, int32_t K, int32_t arith, int32_t bias_side,
-                                            rslrl_stream_t stream) {
+                                            int32_t flags, rslrl_stream_t stream) {
+    if (flags & ~RSLRL_WGRAD_NO_FOLD) return RSLRL_E_INVALID_ARGUMENT;
     if (!a0 || !a1) return RSLRL_E_INVALID_ARGUMENT;
     if (M < 1 || N < 1 || K < 1 || N > 256 || K > kTK || (N & 3) || (K & 3)) return RSLRL_E_INVALID_ARGUMENT;
     if (bias_side < 0 || bias_side > 2 || (bias_side == 1 && N <= 64)) return RSLRL_E_INVALID_ARGUMENT;
@@ -671,7 +757,7 @@ extern "C" int rslrl_linear_wgrad_bias_pair(const rslrl_wgrad_problem_t* a0, con
     else if (N <= 64) h3 ? by_side(I64{}, P2{}) : by_side(I64{}, P3{});
     else h3 ? by_side(I256{}, P2{}) : by_side(I256{}, P3{});
     int rc = launch_status();
-    if (rc) return rc;
+    if (rc || (flags & RSLRL_WGRAD_NO_FOLD)) return rc;
     for (int i = 0; i < 2; ++i) {
         const bool tr = a[i]->transpose_out != 0;
         rc = rslrl_fold_partials_ex(static_cast<const float*>(a[i]->workspace), S, NKE, a[i]->dw_db, NKE, tr ? N : 0,

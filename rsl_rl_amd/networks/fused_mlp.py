@@ -397,10 +397,11 @@ def linear_dgrad_elu_wgrad(dz, w, h, img, want_amax=False, db_prev_out=None, dwb
     return out, db, dw, db_out
 
 
-def linear_dgrad_elu_wgrad_pair(dzs, hs, imgs, dwb_outs=(None, None)):
+def linear_dgrad_elu_wgrad_pair(dzs, hs, imgs, dwb_outs=(None, None), defer=None):
     """linear_dgrad_elu_wgrad (want_db_prev=False, no amax) of two output layers over the same rows and hidden width
     in one launch (rslrl_linear_gemm_pair, RSLRL_LINEAR_DGRAD_ELU_WGRAD; the reduction widths may differ, e.g. 12
-    actions and the value head).  Returns per problem (dz_prev, dw, db)."""
+    actions and the value head).  Returns per problem (dz_prev, dw, db).  defer: a _FoldBatch -- the weight-gradient
+    folds are queued there (dw, db valid after its run()) instead of launched here."""
     M, K = hs[0].shape
     L = _lib.lib()
     tiles = L.rslrl_linear_tiles(M)
@@ -422,6 +423,10 @@ def linear_dgrad_elu_wgrad_pair(dzs, hs, imgs, dwb_outs=(None, None)):
     for i in range(2):
         N = dzs[i].shape[1]
         P = wparts[i].shape[1]
+        if defer is not None:
+            defer.add(wparts[i], tiles, P, dwbs[i], N * K + N)
+            res.append((outs[i], dwbs[i][: N * K].view(N, K), dwbs[i][N * K:]))
+            continue
         nbytes = L.rslrl_fold_partials_workspace_bytes(tiles, P)
         ws = torch.empty(max(nbytes, 16) // 8, dtype=torch.float64, device=dzs[i].device)
         rc = L.rslrl_fold_partials_ex(wparts[i].data_ptr(), tiles, P, dwbs[i].data_ptr(), N * K + N, 0, 0,
@@ -459,11 +464,12 @@ def linear_wgrad(dz, x, arith=_lib.ARITH_X6, dz_amax=None, x_amax=None, out=None
 
 
 def linear_wgrad_pair(dzs, xs, arith=_lib.ARITH_X6, bias_side=0, dwb_outs=(None, None), amaxes=((None, None),) * 2,
-                      transpose_out=False):
+                      transpose_out=False, defer=None):
     """linear_wgrad of two problems of one shape in one launch (rslrl_linear_wgrad_bias_pair): returns, per problem,
     dw (bias_side 0) or (dw, colsum).  dwb_outs: optional [N*K + E] destinations (a Linear's adjacent arena slots);
     amaxes: per problem (max |dz|, max |x|) device scalars for h3.  transpose_out: dw is delivered as dw^T ([K, N],
-    the first layer's (x^T dz)^T form written straight in W's layout)."""
+    the first layer's (x^T dz)^T form written straight in W's layout).  defer: a _FoldBatch -- the folds are queued
+    there (the results are valid after its run()) instead of launched here."""
     M, N = dzs[0].shape
     K = xs[0].shape[1]
     L = _lib.lib()
@@ -484,8 +490,13 @@ def linear_wgrad_pair(dzs, xs, arith=_lib.ARITH_X6, bias_side=0, dwb_outs=(None,
     with timer.span(f"linear_wgrad_pair[M={M},N={N},K={K}]{_tag(arith)}", dzs[0].device, 8 * M * (N + K),
                     4 * M * K * N):
         rc = L.rslrl_linear_wgrad_bias_pair(ctypes.byref(probs[0]), ctypes.byref(probs[1]), M, N, K, arith,
-                                            bias_side, _stream(dzs[0]))
+                                            bias_side, _lib.WGRAD_NO_FOLD if defer is not None else 0,
+                                            _stream(dzs[0]))
     _lib.check(rc, "rslrl_linear_wgrad_bias_pair")
+    if defer is not None:
+        S = L.rslrl_linear_wgrad_bias_pair_slices(M, N)
+        for i in range(2):
+            defer.add(wss[i], S, N * K + E, dwbs[i], N * K + E, (N, K) if transpose_out else None)
     shape = (K, N) if transpose_out else (N, K)
     if not bias_side:
         return [d.view(*shape) for d in dwbs]
@@ -733,6 +744,30 @@ def train_backward(tape, dy, need_dx=False, need_w=None, outs=None, dy_padded=No
     return dx, grads_w, grads_b
 
 
+class _FoldBatch:
+    """Weight-gradient folds queued during a backward pass and launched together (rslrl_fold_partials_batch): no fold
+    is needed before the optimizer step, so the pass's 8 folds (4 layers x 2 networks) take one launch."""
+
+    def __init__(self):
+        self.jobs, self.keep, self.after = [], [], []
+
+    def add(self, partials, S, NK, out, out_len, transpose=None):
+        t_rows, t_cols = transpose if transpose is not None else (0, 0)
+        self.jobs.append(_lib.FoldJob(partials.data_ptr(), S, NK, out.data_ptr(), out_len, t_rows, t_cols))
+        self.keep += [partials, out]
+
+    def run(self, device):
+        L = _lib.lib()
+        for start in range(0, len(self.jobs), _lib.MAX_FOLD_JOBS):
+            part = self.jobs[start:start + _lib.MAX_FOLD_JOBS]
+            arr = (_lib.FoldJob * len(part))(*part)
+            st = ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+            _lib.check(L.rslrl_fold_partials_batch(arr, len(part), st), "rslrl_fold_partials_batch")
+        for fn in self.after:
+            fn()
+        self.jobs, self.keep, self.after = [], [], []
+
+
 # ---- the actor and the critic of the PPO update as one pass (same-shape hidden layers batched per launch)
 def _pairable(ws_a, ws_c, x_a, x_c) -> bool:
     """Two MLPs whose hidden layers can share launches: the split (x6) arithmetic without h3 layers, the same depth
@@ -808,12 +843,13 @@ def train_backward_pair(tape_a, dy_a, outs_a, tape_c, dy_c, outs_c):
         adj = wo.is_contiguous() and bo.data_ptr() == wo.data_ptr() + 4 * wo.numel()
         adjacent.append(adj)
         dwb_outs.append(torch.as_strided(wo, (nred * K + nred,), (1,)) if adj else None)
+    folds = _FoldBatch()
     res = linear_dgrad_elu_wgrad_pair(ds, [t.hs[L - 1] for t in tapes], [t.dgrad_imgs[L - 1] for t in tapes],
-                                      dwb_outs)
+                                      dwb_outs, defer=folds)
     dz = [r[0] for r in res]
     for i in range(2):
         if not adjacent[i]:
-            torch._foreach_copy_(list(outs[i][L - 1]), [res[i][1], res[i][2]])
+            folds.after.append(lambda o=outs[i][L - 1], r=res[i]: torch._foreach_copy_(list(o), [r[1], r[2]]))
     for l in range(L - 2, -1, -1):
         h_in = [t.hs[l] for t in tapes]
         N, K = tapes[0].ws[l].shape
@@ -823,10 +859,10 @@ def train_backward_pair(tape_a, dy_a, outs_a, tape_c, dy_c, outs_c):
                 wo, bo = outs[i][l]
                 adj = wo.is_contiguous() and bo.data_ptr() == wo.data_ptr() + 4 * wo.numel()
                 dwb_outs.append(torch.as_strided(wo, (N * K + N,), (1,)) if adj else None)
-            res = linear_wgrad_pair(dz, h_in, bias_side=1, dwb_outs=dwb_outs)
+            res = linear_wgrad_pair(dz, h_in, bias_side=1, dwb_outs=dwb_outs, defer=folds)
             for i in range(2):
                 if dwb_outs[i] is None:
-                    torch._foreach_copy_(list(outs[i][l]), list(res[i]))
+                    folds.after.append(lambda o=outs[i][l], r=res[i]: torch._foreach_copy_(list(o), list(r)))
             dz, _ = linear_dgrad_elu_pair(dz, h_in, [t.dgrad_imgs[l] for t in tapes], _lib.ARITH_X6)
         else:  # first layer: (x^T dz)^T on the 64-row tiles, the bias from dz (the kernel's K side)
             pad = (-K) % 4
@@ -836,12 +872,14 @@ def train_backward_pair(tape_a, dy_a, outs_a, tape_c, dy_c, outs_c):
                 wo, bo = outs[i][0]
                 adj = not pad and wo.is_contiguous() and bo.data_ptr() == wo.data_ptr() + 4 * wo.numel()
                 dwb_outs.append(torch.as_strided(wo, (N * K + N,), (1,)) if adj else None)
-            res = linear_wgrad_pair(xp, dz, bias_side=2, dwb_outs=dwb_outs, transpose_out=not pad)
+            res = linear_wgrad_pair(xp, dz, bias_side=2, dwb_outs=dwb_outs, transpose_out=not pad, defer=folds)
             for i in range(2):
                 if dwb_outs[i] is None:
-                    wo, bo = outs[i][0]
-                    dwt, db = res[i]
-                    torch._foreach_copy_([wo, bo], [dwt[:, :K] if not pad else dwt[:K].t(), db])
+                    def copy(o=outs[i][0], r=res[i]):
+                        dwt, db = r
+                        torch._foreach_copy_(list(o), [dwt[:, :K] if not pad else dwt[:K].t(), db])
+                    folds.after.append(copy)
+    folds.run(dz[0].device)
     return True
 
 

@@ -326,3 +326,29 @@ def test_fold_partials_mapped(S, R, C, E, out_len, cuda_device):
         assert torch.equal(dst[: R * C].view(C, R), ident[: R * C].view(R, C).t())
     assert torch.equal(dst[R * C: out_len], ident[R * C: out_len])
     assert torch.isnan(buf[0]) and torch.isnan(buf[out_len + 1:]).all()
+
+
+def test_fold_partials_batch(cuda_device):
+    """rslrl_fold_partials_batch: several folds (wide and narrow, mapped and not) in one launch -- each bitwise the
+    one-pass wide fold of its job and within fp32 rounding of an fp64 sum."""
+    L = _lib.lib()
+    torch.manual_seed(3)
+    specs = [(256, 48 * 256 + 256, 48, 256), (128, 65536 + 256, 0, 0), (3072, 3084, 0, 0), (768, 260, 0, 0), (5, 8, 0, 0)]
+    parts, outs, jobs = [], [], []
+    for S, NK, tr, tc in specs:
+        part = torch.randn(S, NK, device=cuda_device)
+        out_len = NK - 3 if NK == 260 else NK
+        out = torch.full((out_len,), float("nan"), device=cuda_device)
+        parts.append(part)
+        outs.append(out)
+        jobs.append(_lib.FoldJob(part.data_ptr(), S, NK, out.data_ptr(), out_len, tr, tc))
+    arr = (_lib.FoldJob * len(jobs))(*jobs)
+    _lib.check(L.rslrl_fold_partials_batch(arr, len(jobs), torch.cuda.current_stream().cuda_stream), "batch")
+    torch.cuda.synchronize()
+    for (S, NK, tr, tc), part, out in zip(specs, parts, outs):
+        ref = part.double().sum(0)
+        if tr:
+            ref = torch.cat([ref[: tr * tc].view(tr, tc).t().reshape(-1), ref[tr * tc:]])
+        ref = ref[: out.numel()]
+        assert not torch.isnan(out).any()
+        assert ((out.double() - ref).abs() <= 1e-6 * ref.abs() + 1e-6).all()
