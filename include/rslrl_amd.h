@@ -292,9 +292,12 @@ int rslrl_fold_partials(const float* partials, int64_t S, int64_t NK, float* out
  * a multiple of 4 lands in an exact-size destination.  out needs 4-byte alignment only. */
 int rslrl_fold_partials_ex(const float* partials, int64_t S, int64_t NK, float* out, int64_t out_len, int32_t t_rows,
                            int32_t t_cols, void* workspace, size_t workspace_bytes, rslrl_stream_t stream);
-/* Up to 16 folds in one launch, each as rslrl_fold_partials_ex (one pass: 64 columns per workgroup, every slice of
- * them; fp64 in a fixed order that depends on S alone).  The folds of one backward pass (every layer of the actor
- * and the critic) run as one launch instead of one or two each. */
+/* Up to 16 folds in one launch, each as rslrl_fold_partials_ex (64 columns per workgroup; a narrow job with more
+ * than 256 slices is also split into up to 16 slice groups whose fp64 sums the last-arriving group adds in order;
+ * fp64 in a fixed order that depends on S alone).  The folds of one backward pass (every layer of the actor and the
+ * critic) run as one launch instead of one or two each.  Workspace: rslrl_fold_partials_batch_workspace_bytes(jobs,
+ * n) bytes, 256-byte aligned, ZERO-FILLED before its first use (its leading arrival counters are left zero by every
+ * call; reuse one buffer per stream); NULL when that size is <= 256. */
 typedef struct {
     const float* partials; /* [S][NK], 16-byte aligned */
     int64_t S;
@@ -303,7 +306,9 @@ typedef struct {
     int64_t out_len;
     int32_t t_rows, t_cols;
 } rslrl_fold_job_t;
-int rslrl_fold_partials_batch(const rslrl_fold_job_t* jobs, int32_t n, rslrl_stream_t stream);
+size_t rslrl_fold_partials_batch_workspace_bytes(const rslrl_fold_job_t* jobs, int32_t n);
+int rslrl_fold_partials_batch(const rslrl_fold_job_t* jobs, int32_t n, void* workspace, size_t workspace_bytes,
+                              rslrl_stream_t stream);
 
 /* Output-layer backward in one launch (1 <= Nred <= 16, dz rows of Nred floats -- a 1-wide value head's [M, 1]
  * gradient as it is; fp32 FMAs on the VALU, W rebuilt exactly from its x6 image -- RSLRL_OUT_BWD=mfma selects the

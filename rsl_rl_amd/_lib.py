@@ -66,6 +66,7 @@ EXPORTED_SYMBOLS = (
     "rslrl_linear_wgrad_bias_pair",
     "rslrl_fold_partials_ex",
     "rslrl_fold_partials_batch",
+    "rslrl_fold_partials_batch_workspace_bytes",
     "rslrl_linear_wgrad_bias_pair_slices",
     "rslrl_normal_affine",
     "rslrl_ppo_update_tail",
@@ -398,7 +399,9 @@ def _declare(L):
     L.rslrl_linear_wgrad_bias_pair_slices.restype = I64
     L.rslrl_linear_wgrad_bias_pair_slices.argtypes = [I64, I32]
     L.rslrl_fold_partials_batch.restype = ctypes.c_int
-    L.rslrl_fold_partials_batch.argtypes = [ctypes.POINTER(FoldJob), I32, P]
+    L.rslrl_fold_partials_batch.argtypes = [ctypes.POINTER(FoldJob), I32, P, SZ, P]
+    L.rslrl_fold_partials_batch_workspace_bytes.restype = SZ
+    L.rslrl_fold_partials_batch_workspace_bytes.argtypes = [ctypes.POINTER(FoldJob), I32]
     L.rslrl_rnd_update_workspace_bytes.restype = SZ
     L.rslrl_rnd_update_workspace_bytes.argtypes = [I64, I32, I32, I32]
     L.rslrl_rnd_update.restype = ctypes.c_int

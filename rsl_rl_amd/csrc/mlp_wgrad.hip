@@ -444,38 +444,59 @@ __global__ __launch_bounds__(kBlock) void fold_wide_kernel(const float* __restri
     }
 }
 
-// Several folds in one launch (rslrl_fold_partials_batch): block b belongs to the job whose range of 64-column blocks
-// holds it; each block runs fold_wide's body (16 slice phases x 16 column quads, fp64, phase order) -- the same
-// summation order as fold_wide_kernel for any S, so a job's result does not depend on its batch.
+// Several folds in one launch (rslrl_fold_partials_batch).  Job j spans CB = ceil(NK / 64) column blocks x G slice
+// groups; block (cb, g) runs fold_wide's body over its group's slices (16 slice phases x 16 column quads, fp64,
+// phase order).  G = 1 (many columns or <= 256 slices): the block writes its 64 outputs.  G > 1 (a narrow job with
+// many slices, e.g. the value head's 3072 tile partials of 260 columns, which one pass would leave to 5 blocks): the
+// groups' fp64 sums go to the workspace and the last-arriving group of the column block adds them in group order.
+// Deterministic: the order depends on (S, G) alone.
 constexpr int kMaxFoldJobs = 16;
+constexpr int kFoldGroupSlices = 256;
 struct FoldJobs {
     const float* part[kMaxFoldJobs];
     float* out[kMaxFoldJobs];
     OutMap omap[kMaxFoldJobs];
     int S[kMaxFoldJobs];
     int NK[kMaxFoldJobs];
+    int G[kMaxFoldJobs];
+    int64_t ws_off[kMaxFoldJobs];  // doubles
+    int t_off[kMaxFoldJobs];       // tickets
     int first_block[kMaxFoldJobs + 1];
     int n;
+    double* ws;
+    unsigned* tickets;
 };
+
+int fold_batch_groups(int64_t S, int64_t NK) {
+    const int64_t cb = ceil_div(NK, 64);
+    if (S <= kFoldGroupSlices || cb >= 128) return 1;
+    return static_cast<int>(std::min<int64_t>(ceil_div(S, kFoldGroupSlices), 16));
+}
 
 __global__ __launch_bounds__(kBlock) void fold_batch_kernel(FoldJobs jobs) {
     __shared__ double red[16][16][4];
+    __shared__ int last_flag;
     int j = 0;
     while (j + 1 < jobs.n && static_cast<int>(blockIdx.x) >= jobs.first_block[j + 1]) ++j;  // wave-uniform
-    const int NK = jobs.NK[j], S = jobs.S[j];
+    const int NK = jobs.NK[j], S = jobs.S[j], G = jobs.G[j];
+    const int CB = (NK + 63) / 64;
+    const int li = static_cast<int>(blockIdx.x) - jobs.first_block[j];
+    const int cb = li % CB, g = li / CB;
+    const int per = (S + G - 1) / G;
+    const int s_lo = g * per, s_hi = min(S, s_lo + per);
     const int q = threadIdx.x & 15;
     const int ph = threadIdx.x >> 4;
-    const int e0 = (static_cast<int>(blockIdx.x) - jobs.first_block[j]) * 64 + 4 * q;
+    const int e0 = cb * 64 + 4 * q;
     double a[4] = {0.0, 0.0, 0.0, 0.0};
     if (e0 < NK) {
         const float* src = jobs.part[j] + e0;
-        for (int s0 = ph; s0 < S; s0 += 16 * 16) {
+        for (int s0 = s_lo + ph; s0 < s_hi; s0 += 16 * 16) {
             float4 v[16];
 #pragma unroll
             for (int k = 0; k < 16; ++k) {
                 const int s = s0 + 16 * k;
-                v[k] = s < S ? *reinterpret_cast<const float4*>(src + static_cast<int64_t>(s) * NK)
-                             : make_float4(0.f, 0.f, 0.f, 0.f);
+                v[k] = s < s_hi ? *reinterpret_cast<const float4*>(src + static_cast<int64_t>(s) * NK)
+                                : make_float4(0.f, 0.f, 0.f, 0.f);
             }
 #pragma unroll
             for (int k = 0; k < 16; ++k) {
@@ -486,11 +507,50 @@ __global__ __launch_bounds__(kBlock) void fold_batch_kernel(FoldJobs jobs) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) red[ph][q][k] = a[k];
     __syncthreads();
-    if (ph == 0 && e0 < NK) {
-        double r[4] = {red[0][q][0], red[0][q][1], red[0][q][2], red[0][q][3]};
+    double r[4] = {0.0, 0.0, 0.0, 0.0};
+    if (ph == 0) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) r[k] = red[0][q][k];
         for (int p2 = 1; p2 < 16; ++p2)
 #pragma unroll
             for (int k = 0; k < 4; ++k) r[k] += red[p2][q][k];
+    }
+    if (G > 1) {
+        double* wp = jobs.ws + jobs.ws_off[j];
+        if (ph == 0 && e0 < NK) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                __hip_atomic_store(reinterpret_cast<unsigned long long*>(wp + static_cast<int64_t>(g) * NK + e0 + k),
+                                   __double_as_longlong(r[k]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            unsigned* t = jobs.tickets + jobs.t_off[j] + cb;
+            const unsigned k = __hip_atomic_fetch_add(t, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int last = k == static_cast<unsigned>(G) - 1;
+            if (last) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __hip_atomic_store(t, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed for the next call
+            }
+            last_flag = last;
+        }
+        __syncthreads();
+        if (!last_flag) return;
+        if (ph == 0 && e0 < NK) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                double t = 0.0;
+                for (int g2 = 0; g2 < G; ++g2)
+                    t += __longlong_as_double(__hip_atomic_load(
+                        reinterpret_cast<unsigned long long*>(wp + static_cast<int64_t>(g2) * NK + e0 + k),
+                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                r[k] = t;
+            }
+        }
+    }
+    if (ph == 0 && e0 < NK) {
         const float v[4] = {static_cast<float>(r[0]), static_cast<float>(r[1]), static_cast<float>(r[2]),
                             static_cast<float>(r[3])};
         store_mapped(jobs.out[j], e0, v, jobs.omap[j]);
@@ -589,7 +649,38 @@ extern "C" int rslrl_fold_partials(const float* partials, int64_t S, int64_t NK,
     return rslrl_fold_partials_ex(partials, S, NK, out, NK, 0, 0, workspace, workspace_bytes, stream);
 }
 
-extern "C" int rslrl_fold_partials_batch(const rslrl_fold_job_t* jobs, int32_t n, rslrl_stream_t stream) {
+namespace rslrl {
+namespace {
+// workspace of a batch: tickets (one per column block of every grouped job) first -- the region a zero-filled
+// buffer keeps zero across calls -- then the grouped jobs' fp64 group sums
+int64_t fold_batch_layout(const rslrl_fold_job_t* jobs, int32_t n, FoldJobs* fj) {
+    int64_t tickets = 0, doubles = 0;
+    for (int i = 0; i < n; ++i) {
+        const int G = fold_batch_groups(jobs[i].S, jobs[i].NK);
+        if (fj) {
+            fj->G[i] = G;
+            fj->t_off[i] = static_cast<int>(tickets);
+        }
+        if (G > 1) tickets += ceil_div(jobs[i].NK, 64);
+    }
+    const int64_t ticket_bytes = (tickets * 4 + 255) / 256 * 256;
+    for (int i = 0; i < n; ++i) {
+        const int G = fold_batch_groups(jobs[i].S, jobs[i].NK);
+        if (fj) fj->ws_off[i] = ticket_bytes / 8 + doubles;
+        if (G > 1) doubles += static_cast<int64_t>(G) * jobs[i].NK;
+    }
+    return ticket_bytes + doubles * 8;
+}
+}  // namespace
+}  // namespace rslrl
+
+extern "C" size_t rslrl_fold_partials_batch_workspace_bytes(const rslrl_fold_job_t* jobs, int32_t n) {
+    if (!jobs || n < 1 || n > kMaxFoldJobs) return 0;
+    return static_cast<size_t>(fold_batch_layout(jobs, n, nullptr));
+}
+
+extern "C" int rslrl_fold_partials_batch(const rslrl_fold_job_t* jobs, int32_t n, void* workspace,
+                                         size_t workspace_bytes, rslrl_stream_t stream) {
     if (!jobs || n < 1 || n > kMaxFoldJobs) return RSLRL_E_INVALID_ARGUMENT;
     FoldJobs fj{};
     fj.n = n;
@@ -602,13 +693,24 @@ extern "C" int rslrl_fold_partials_batch(const rslrl_fold_job_t* jobs, int32_t n
             static_cast<int64_t>(j.t_rows) * j.t_cols > j.out_len)
             return RSLRL_E_INVALID_ARGUMENT;
         if (reinterpret_cast<uintptr_t>(j.partials) & 15) return RSLRL_E_MISALIGNED;
+    }
+    const int64_t need = fold_batch_layout(jobs, n, &fj);
+    if (need > 256) {  // some job is grouped: the workspace holds its tickets (zero) and group sums
+        if (!workspace) return RSLRL_E_INVALID_ARGUMENT;
+        if (workspace_bytes < static_cast<size_t>(need)) return RSLRL_E_WORKSPACE_TOO_SMALL;
+        if (reinterpret_cast<uintptr_t>(workspace) & 255) return RSLRL_E_MISALIGNED;
+    }
+    fj.tickets = static_cast<unsigned*>(workspace);
+    fj.ws = static_cast<double*>(workspace);
+    for (int i = 0; i < n; ++i) {
+        const rslrl_fold_job_t& j = jobs[i];
         fj.part[i] = j.partials;
         fj.out[i] = j.out;
         fj.omap[i] = OutMap{j.out_len, j.t_rows, j.t_cols};
         fj.S[i] = static_cast<int>(j.S);
         fj.NK[i] = static_cast<int>(j.NK);
         fj.first_block[i] = static_cast<int>(blocks);
-        blocks += ceil_div(j.NK, 64);
+        blocks += ceil_div(j.NK, 64) * fj.G[i];
         if (blocks > INT32_MAX) return RSLRL_E_INVALID_ARGUMENT;
     }
     fj.first_block[n] = static_cast<int>(blocks);

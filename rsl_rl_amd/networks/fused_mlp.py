@@ -744,6 +744,11 @@ def train_backward(tape, dy, need_dx=False, need_w=None, outs=None, dy_padded=No
     return dx, grads_w, grads_b
 
 
+def _kernels_ws():
+    from ..kernels import _ws
+    return _ws
+
+
 class _FoldBatch:
     """Weight-gradient folds queued during a backward pass and launched together (rslrl_fold_partials_batch): no fold
     is needed before the optimizer step, so the pass's 8 folds (4 layers x 2 networks) take one launch."""
@@ -762,7 +767,10 @@ class _FoldBatch:
             part = self.jobs[start:start + _lib.MAX_FOLD_JOBS]
             arr = (_lib.FoldJob * len(part))(*part)
             st = ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
-            _lib.check(L.rslrl_fold_partials_batch(arr, len(part), st), "rslrl_fold_partials_batch")
+            nbytes = L.rslrl_fold_partials_batch_workspace_bytes(arr, len(part))
+            ws = _kernels_ws().get(device, "fold_batch", nbytes)  # zero-filled once, counters left zero
+            _lib.check(L.rslrl_fold_partials_batch(arr, len(part), ws.data_ptr(), ws.numel(), st),
+                       "rslrl_fold_partials_batch")
         for fn in self.after:
             fn()
         self.jobs, self.keep, self.after = [], [], []

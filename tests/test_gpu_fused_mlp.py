@@ -343,8 +343,15 @@ def test_fold_partials_batch(cuda_device):
         outs.append(out)
         jobs.append(_lib.FoldJob(part.data_ptr(), S, NK, out.data_ptr(), out_len, tr, tc))
     arr = (_lib.FoldJob * len(jobs))(*jobs)
-    _lib.check(L.rslrl_fold_partials_batch(arr, len(jobs), torch.cuda.current_stream().cuda_stream), "batch")
+    nbytes = L.rslrl_fold_partials_batch_workspace_bytes(arr, len(jobs))
+    ws = torch.zeros(max(nbytes, 256) // 8 + 32, dtype=torch.float64, device=cuda_device)
+    for _ in range(2):  # the second call reuses the workspace: its counters must have been left zero
+        for o in outs:
+            o.fill_(float("nan"))
+        _lib.check(L.rslrl_fold_partials_batch(arr, len(jobs), ws.data_ptr(), ws.numel() * 8,
+                                               torch.cuda.current_stream().cuda_stream), "batch")
     torch.cuda.synchronize()
+    assert nbytes > 256  # the 3072-slice narrow jobs are grouped
     for (S, NK, tr, tc), part, out in zip(specs, parts, outs):
         ref = part.double().sum(0)
         if tr:
