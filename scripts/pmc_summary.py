@@ -30,6 +30,8 @@ SHORT = {
     "rnd_update_kernel": "rnd_update",
     "rnd_fold_kernel": "rnd_fold",
     "synthetic_env_kernel": "synthetic_env",
+    "fold_batch_kernel": "fold_batch",
+    "normal_affine_kernel": "normal_affine",
     "mlp_gemm_x6_kernel<1": "x6_fwd_elu",
     "mlp_gemm_x6_kernel<2": "x6_dgrad_elu",
     "wgrad_x6_kernel": "x6_wgrad",
@@ -37,7 +39,7 @@ SHORT = {
     "__amd_rocclr_copyBuffer": "copyBuffer",
 }
 # kernels launched at several shapes are keyed "<short>@grid=<threads>"
-BY_GRID = {"x6_fwd_elu", "x6_dgrad_elu", "x6_wgrad", "wgrad_fold", "h3_fwd_elu", "h3_dgrad_elu", "h3_fwd_out",
+BY_GRID = {"x6_fwd_elu", "x6_fwd_elu_pair", "x6_fwd_out", "x6_fwd", "x6_dgrad_elu", "x6_wgrad", "wgrad_fold", "h3_fwd_elu", "h3_dgrad_elu", "h3_fwd_out",
            "x6_dgrad_wgrad", "h3_wgrad256", "x6_wgrad64", "x6_fwd_out", "x6_fwd_elu_pair", "h3_fwd_elu_pair"}
 
 
@@ -47,15 +49,24 @@ EPI_NAMES = {0: "fwd", 1: "fwd_elu", 2: "dgrad_elu", 3: "dgrad_wgrad", 4: "fwd_o
 def gemm_name(kernel):
     """mlp_gemm_x6_kernel<EPI, FULL, MINW, NR, PL> / wgrad_x6_kernel<TN, FULL, PL>: arithmetic (PL 2 = h3,
     3 = x6) and epilogue in the key."""
-    m = re.search(r"mlp_gemm_x6_kernel<(\d+), \w+, \d+, \d+, (\d+)>", kernel)
+    m = re.search(r"mlp_gemm_x6_kernel<(\d+), \w+, \d+, \d+, (\d+)[,>]", kernel)
     if m:
         return f"{'h3' if m.group(2) == '2' else 'x6'}_{EPI_NAMES.get(int(m.group(1)), m.group(1))}"
-    m = re.search(r"mlp_gemm_x6_pair_kernel<(\d+), \w+, (\d+)>", kernel)
+    m = re.search(r"mlp_gemm_x6_pair_kernel<(\d+), \w+, (\d+)[,>]", kernel)
     if m:  # two problems per launch (grid y = 2): bytes per launch cover both
         return f"{'h3' if m.group(2) == '2' else 'x6'}_{EPI_NAMES.get(int(m.group(1)), m.group(1))}_pair"
     m = re.search(r"out_bwd_valu_kernel<(\d+), (\d+)>", kernel)
     if m:  # output-layer backward on the VALU, keyed by its reduction width
         return f"out_bwd_valu_nr{m.group(1)}"
+    m = re.search(r"out_bwd_valu_pair_kernel<(\d+), \d+, (\d+), \d+>", kernel)
+    if m:
+        return f"out_bwd_valu_pair_nr{m.group(1)}_{m.group(2)}"
+    m = re.search(r"mlp_gemm_x6_out_pair_kernel<\w+, \d+, (\d+), (\d+), \d+>", kernel)
+    if m:
+        return f"x6_fwd_out_pair_nr{m.group(1)}_{m.group(2)}"
+    m = re.search(r"wgrad_x6_pair_kernel<(\d+), \w+, (\d+)", kernel)
+    if m:
+        return f"{'h3' if m.group(2) == '2' else 'x6'}_wgrad{m.group(1)}_pair"
     m = re.search(r"wgrad_x6_kernel<(\d+), \w+, (\d+)>", kernel)
     if m:
         return f"{'h3' if m.group(2) == '2' else 'x6'}_wgrad{m.group(1)}"
