@@ -11,9 +11,11 @@ into an outermost fused_mlp.frozen_weights() scope -- so parameters updated in p
 up, and at every step outside such a scope) and one without it, reading the images the first one wrote (the other
 23 steps of a rollout).
 
-Same values and the same random stream as the eager calls: the sample's normal_() draws from the default CUDA
-generator, whose offset a captured graph advances by the same increment per replay as the eager kernel does per
-call (PyTorch's graph-safe philox); tests/test_gpu_act_graph.py compares a graphed and an eager rollout bitwise.
+Same values and the same random stream as the eager calls: the sample's standard normals are drawn eagerly into a
+static buffer right before each replay (the same normal_() on the same [N, A] shape from the default generator as
+the eager step draws -- outside the graph, so a replay does not need the two generator-state fill launches of a
+captured draw), and the graph scales and shifts them; tests/test_gpu_act_graph.py compares a graphed and an eager
+rollout bitwise.
 The first call of a configuration runs eagerly, the second captures; any capture failure falls back to the eager
 path for that configuration.  RSLRL_ACT_GRAPH=0 disables it.
 """
@@ -44,6 +46,7 @@ class RolloutActGraph:
         self._out_fwd = None
         self._imgs = None  # the image tensors both graphs use (written by the first one's replay)
         self._img_gen = None  # fused_mlp._frozen_gen of the last image build
+        self._eps = None  # the sample's standard normals, drawn before each replay
 
     @staticmethod
     def enabled() -> bool:
@@ -68,7 +71,7 @@ class RolloutActGraph:
             return None
         if key != self._key:
             self._key, self._seen, self._graph, self._static_in, self._out = key, 0, None, None, None
-            self._graph_fwd, self._out_fwd, self._imgs, self._img_gen = None, None, None, None
+            self._graph_fwd, self._out_fwd, self._imgs, self._img_gen, self._eps = None, None, None, None, None
         if self._graph is None:
             self._seen += 1
             if self._seen < 2:  # the first call of a configuration runs eagerly (lazy initialisations happen there)
@@ -77,6 +80,7 @@ class RolloutActGraph:
                 return None
         for g, t in self._static_in.items():
             t.copy_(obs[g])
+        self._eps.normal_()  # the draw the eager step makes (same generator, same shape, same order)
         frozen = fused_mlp._frozen_depth > 0
         if frozen and self._graph_fwd is not None and self._img_gen == fused_mlp._frozen_gen:
             self._graph_fwd.replay()  # the images of this rollout's weights are current
@@ -92,6 +96,9 @@ class RolloutActGraph:
         pol = self.policy
         static_in = {g: obs[g].clone() for g in sorted(set(pol.obs_groups["policy"]) | set(pol.obs_groups["critic"]))}
         graph, graph_fwd = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        loc = pol.distribution.loc  # the eager first call's distribution: the sample's shape
+        eps = torch.empty(loc.shape, dtype=loc.dtype, device=loc.device)
+        pol._static_eps = eps
         try:
             with _capture_caches() as cache:
                 with torch.cuda.graph(graph):  # image build + forward + sample
@@ -109,7 +116,9 @@ class RolloutActGraph:
             self._failed.add(key)
             warnings.warn(f"rollout act() graph capture failed, running eagerly: {e}")
             return False
-        self._graph, self._static_in, self._out = graph, static_in, out
+        finally:
+            pol._static_eps = None
+        self._graph, self._static_in, self._out, self._eps = graph, static_in, out, eps
         self._graph_fwd, self._out_fwd, self._imgs = (graph_fwd, out_fwd, imgs) if out_fwd is not None else (None,) * 3
         self._img_gen = None  # the first replay runs the image build
         return True

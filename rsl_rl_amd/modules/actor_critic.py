@@ -242,7 +242,9 @@ class ActorCritic(nn.Module):
         # scale.min() >= 0 with a device-to-host read that stalls the launch queue every env step
         loc, scale = self.distribution.loc, self.distribution.scale
         with torch.no_grad():
-            eps = torch.empty_like(loc).normal_()
+            eps = getattr(self, "_static_eps", None)  # a captured rollout graph's standard normals, drawn before replay
+            if eps is None or eps.shape != loc.shape:
+                eps = torch.empty_like(loc).normal_()
             if (eps.is_cuda and eps.dim() == 2 and eps.is_contiguous() and scale.shape == eps.shape
                     and loc.shape == eps.shape and scale.stride(1) == 1 and loc.stride(1) == 1):
                 return kernels.normal_affine_(eps, scale, loc)  # the mul_ + add_ pair in one launch, same bits
