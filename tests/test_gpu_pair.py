@@ -75,3 +75,44 @@ def test_act_and_evaluate_matches_two_calls(critic_width, state_dependent_std, c
     assert len(calls) == (2 if critic_width == 48 else 0)
     assert torch.equal(a, a_ref) and torch.equal(v, v_ref)
     assert torch.equal(pol.action_mean, mean_ref) and torch.equal(pol.action_std, std_ref)
+
+
+@pytest.mark.parametrize("M", [1000, 16384, 65536])
+def test_out_pair_matches_two_launches(M, cuda_device):
+    """The two fused output layers (12 outputs on the MFMA epilogue, 1 on the VALU one) through the pair entry --
+    one launch while the tiles fit one per CU (M <= 16384 here), two launches past that -- bit-identical to two
+    linear_fwd_out_ex calls, full and partial tiles."""
+    dev = cuda_device
+    g = torch.Generator(device=dev).manual_seed(5)
+    K, N = 256, 256
+    xs = [torch.nn.functional.elu(torch.randn(M, K, device=dev, generator=g)) for _ in range(2)]
+    ws = [torch.randn(N, K, device=dev, generator=g) / 16 for _ in range(2)]
+    bs = [torch.randn(N, device=dev, generator=g) * 0.1 for _ in range(2)]
+    wo = [torch.randn(n, N, device=dev, generator=g) / 16 for n in (12, 1)]
+    bo = [torch.randn(n, device=dev, generator=g) * 0.1 for n in (12, 1)]
+    imgs = fused_mlp.bimages([(w, False) for w in ws] + [(w, False, _lib.BIMAGE_LAYOUT_OUT) for w in wo])
+    for store_h in (False, True):
+        ref = [fused_mlp.linear_fwd_out_ex(xs[i], bs[i], N, imgs[i], _lib.ARITH_X6, None, bo[i], imgs[2 + i],
+                                           store_h=store_h) for i in range(2)]
+        hs, ys = fused_mlp.linear_fwd_out_pair(xs, bs, N, imgs[:2], bo, imgs[2:], store_h=store_h)
+        torch.cuda.synchronize()
+        for i in range(2):
+            assert torch.equal(ys[i], ref[i][1])
+            if store_h:
+                assert torch.equal(hs[i], ref[i][0])
+
+
+@pytest.mark.parametrize("M", [777, 98304])
+def test_dgrad_pair_matches_two_launches(M, cuda_device):
+    """Two hidden-layer input gradients (dz W) * ELU'(h) in one launch, bit-identical to two launches."""
+    dev = cuda_device
+    g = torch.Generator(device=dev).manual_seed(6)
+    dzs = [torch.randn(M, 256, device=dev, generator=g) for _ in range(2)]
+    hs = [torch.nn.functional.elu(torch.randn(M, 256, device=dev, generator=g)) for _ in range(2)]
+    ws = [torch.randn(256, 256, device=dev, generator=g) / 16 for _ in range(2)]
+    imgs = [fused_mlp.bimage(w, True) for w in ws]
+    ref = [fused_mlp.linear_dgrad_elu_ex(dzs[i], hs[i], imgs[i], _lib.ARITH_X6, want_db=False)[0] for i in range(2)]
+    outs, _ = fused_mlp.linear_dgrad_elu_pair(dzs, hs, imgs, _lib.ARITH_X6)
+    torch.cuda.synchronize()
+    for i in range(2):
+        assert torch.equal(outs[i], ref[i])
