@@ -555,17 +555,17 @@ __global__ __launch_bounds__(kBlock) void bimage_kernel(BImageBatch batch) {
 
 // A chunk: BM rows x 16 k = BM / 128 float4 per thread (unit u = t + 512 i: row u >> 2, k-quad u & 3).
 // FULL: the tile's rows exist and K % 16 == 0 -> no masks.
-template <int BM>
+template <int BM, int NT = kThreads>
 struct AStage {
-    float4 v[BM / 128];
+    float4 v[BM * 4 / NT];
 };
 
-template <int BM, bool FULL>
-__device__ __forceinline__ AStage<BM> load_a(const GemmParams& p, int64_t row0, int k0) {
-    AStage<BM> s;
+template <int BM, bool FULL, int NT = kThreads>
+__device__ __forceinline__ AStage<BM, NT> load_a(const GemmParams& p, int64_t row0, int k0) {
+    AStage<BM, NT> s;
 #pragma unroll
-    for (int i = 0; i < BM / 128; ++i) {
-        const int u = threadIdx.x + kThreads * i;
+    for (int i = 0; i < BM * 4 / NT; ++i) {
+        const int u = threadIdx.x + NT * i;
         const int k = k0 + 4 * (u & 3);
         const int64_t row = row0 + (u >> 2);
         if constexpr (FULL) {
@@ -579,12 +579,12 @@ __device__ __forceinline__ AStage<BM> load_a(const GemmParams& p, int64_t row0, 
 }
 
 // PL planes (3: x6 bf16, 2: h3 fp16 of the operand scaled by sc, a power of two)
-template <int BM, int PL>
-__device__ __forceinline__ void store_a_split(const AStage<BM>& s, char* __restrict__ a_lds, float sc) {
+template <int BM, int PL, int NT = kThreads>
+__device__ __forceinline__ void store_a_split(const AStage<BM, NT>& s, char* __restrict__ a_lds, float sc) {
     constexpr int plane = BM * kX6RowB;
 #pragma unroll
-    for (int i = 0; i < BM / 128; ++i) {
-        const int u = threadIdx.x + kThreads * i;
+    for (int i = 0; i < BM * 4 / NT; ++i) {
+        const int u = threadIdx.x + NT * i;
         const int q = u & 3;
         const int r = u >> 2;
         const int off = swz(r, q >> 1) + 8 * (q & 1);
@@ -641,26 +641,26 @@ __device__ __forceinline__ void amax_commit(const GemmParams& p, float amx) {
 // vmcnt(0) before every LDS read (it cannot tell the DMA's buffer from the one being read), which would drain
 // the A look-ahead every chunk.  Per chunk c: read every fragment of chunk c, write A(c+1) and B(c+1) into the
 // other buffer, fetch A(c+1+D) and B(c+2), MFMAs, barrier (LDS writes only: lgkmcnt(0)).
-template <int PL>
+template <int PL, int NT = kThreads>
 struct BStage {
-    uint4 u[PL];
+    uint4 u[PL * kThreads / NT];
 };
 
-template <int PL>
-__device__ __forceinline__ BStage<PL> load_b_regs(const uint4* __restrict__ img, int c) {
+template <int PL, int NT = kThreads>
+__device__ __forceinline__ BStage<PL, NT> load_b_regs(const uint4* __restrict__ img, int c) {
     const uint4* src = img + static_cast<int64_t>(c) * (PL * kX6PlaneB / 16);
-    BStage<PL> b;
+    BStage<PL, NT> b;
 #pragma unroll
-    for (int i = 0; i < PL; ++i) b.u[i] = src[threadIdx.x + kThreads * i];
+    for (int i = 0; i < PL * kThreads / NT; ++i) b.u[i] = src[threadIdx.x + NT * i];
     return b;
 }
 
-template <int PL>
-__device__ __forceinline__ void store_b_regs(BStage<PL>& b, char* b_lds) {
+template <int PL, int NT = kThreads>
+__device__ __forceinline__ void store_b_regs(BStage<PL, NT>& b, char* b_lds) {
 #pragma unroll
-    for (int i = 0; i < PL; ++i) {
+    for (int i = 0; i < PL * kThreads / NT; ++i) {
         asm volatile("" : "+v"(b.u[i].x), "+v"(b.u[i].y), "+v"(b.u[i].z), "+v"(b.u[i].w));
-        *reinterpret_cast<uint4*>(b_lds + 16 * (threadIdx.x + kThreads * i)) = b.u[i];
+        *reinterpret_cast<uint4*>(b_lds + 16 * (threadIdx.x + NT * i)) = b.u[i];
     }
 }
 
@@ -672,21 +672,21 @@ struct NoHook {
 
 // last_hook(free_buffer): called before the last chunk's compute with the LDS buffer no chunk reads any more
 // (a compile-time object: a DMA into it does not make the compiler wait for it before the other buffer's reads)
-template <int BM, int PL, int NCH, int D, typename Compute, typename Hook = NoHook>
+template <int BM, int PL, int NCH, int D, typename Compute, typename Hook = NoHook, int NT = kThreads>
 __device__ __forceinline__ void deep_pipeline(const GemmParams& p, int64_t row0, const uint4* __restrict__ bimg,
                                               char* (&lds)[2], float sa, Compute&& compute, Hook&& last_hook = Hook{}) {
     constexpr int planeA = BM * kX6RowB;
-    AStage<BM> sa_[D];
-    BStage<PL> sb;
+    AStage<BM, NT> sa_[D];
+    BStage<PL, NT> sb;
     {
-        BStage<PL> b0 = load_b_regs<PL>(bimg, 0);
-        store_b_regs<PL>(b0, lds[0] + PL * planeA);
+        BStage<PL, NT> b0 = load_b_regs<PL, NT>(bimg, 0);
+        store_b_regs<PL, NT>(b0, lds[0] + PL * planeA);
     }
-    store_a_split<BM, PL>(load_a<BM, true>(p, row0, 0), lds[0], sa);
+    store_a_split<BM, PL, NT>(load_a<BM, true, NT>(p, row0, 0), lds[0], sa);
 #pragma unroll
     for (int d = 1; d <= D; ++d)
-        if (d < NCH) sa_[d % D] = load_a<BM, true>(p, row0, d * kKC);
-    if (NCH > 1) sb = load_b_regs<PL>(bimg, 1);
+        if (d < NCH) sa_[d % D] = load_a<BM, true, NT>(p, row0, d * kKC);
+    if (NCH > 1) sb = load_b_regs<PL, NT>(bimg, 1);
     __syncthreads();
     constexpr bool kHook = !std::is_same_v<std::decay_t<Hook>, NoHook>;
 #pragma unroll
@@ -697,14 +697,14 @@ __device__ __forceinline__ void deep_pipeline(const GemmParams& p, int64_t row0,
             // pin the use of the prefetched registers here: otherwise the scheduler hoists the scaling
             // multiply right behind the load and the wave waits out the look-ahead right away
 #pragma unroll
-            for (int u = 0; u < BM / 128; ++u) {
+            for (int u = 0; u < BM * 4 / NT; ++u) {
                 float4& v = sa_[(c + 1) % D].v[u];
                 asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w));
             }
-            store_a_split<BM, PL>(sa_[(c + 1) % D], lds[(c + 1) & 1], sa);
-            store_b_regs<PL>(sb, lds[(c + 1) & 1] + PL * planeA);
-            if (c + 1 + D < NCH) sa_[(c + 1) % D] = load_a<BM, true>(p, row0, (c + 1 + D) * kKC);
-            if (c + 2 < NCH) sb = load_b_regs<PL>(bimg, c + 2);
+            store_a_split<BM, PL, NT>(sa_[(c + 1) % D], lds[(c + 1) & 1], sa);
+            store_b_regs<PL, NT>(sb, lds[(c + 1) & 1] + PL * planeA);
+            if (c + 1 + D < NCH) sa_[(c + 1) % D] = load_a<BM, true, NT>(p, row0, (c + 1 + D) * kKC);
+            if (c + 2 < NCH) sb = load_b_regs<PL, NT>(bimg, c + 2);
         }
         // only LDS writes to retire (lgkmcnt); __syncthreads' release fence would also wait vmcnt(0) and drain
         // the look-ahead every chunk
@@ -2075,6 +2075,73 @@ int fwd_params(const rslrl_linear_args_t* a, GemmParams& p) {
     return RSLRL_OK;
 }
 
+// ---- "w4": the same x6 GEMM with 4 waves per workgroup side by side (1 x 4), each 128 x 64 = 4 x 2 MFMA tiles, on
+// the 128 x 256 tile: a B fragment feeds 4 MFMAs and an A fragment 2 (0.375 ds_read_b128 per MFMA instead of 0.5),
+// two workgroups per CU at <= 256 registers (2 waves per SIMD).  Full tiles, x6, K = 256, no column sums or amax
+// (the paired update's hidden forward and input gradient); RSLRL_W4 selects it (A/B).
+constexpr int kThreadsW4 = 256;
+#ifndef RSLRL_W4_DEPTH
+#define RSLRL_W4_DEPTH 2
+#endif
+constexpr int kW4Depth = RSLRL_W4_DEPTH;  // A look-ahead (chunks): the 256-register budget has room for 2
+
+template <int EPI>
+__device__ __forceinline__ void mlp_gemm_x6_w4_body(const GemmParams& p, const uint4* __restrict__ bimg, char* lds_b0,
+                                                    char* lds_b1) {
+    constexpr int BM = kBM, PL = 3, I = 4;
+    constexpr int planeA = BM * kX6RowB;
+    using Frag = typename Arith<PL>::frag;
+    char* lds[2];
+    lds[0] = lds_b0;
+    lds[1] = lds_b1;
+    const int lane = threadIdx.x & 63;
+    const int wn = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // cols wn * 64
+    const int h = lane >> 5;
+    const int l32 = lane & 31;
+    const int64_t row0 = static_cast<int64_t>(blockIdx.x) * BM;
+    f32x16 acc[I][2];
+#pragma unroll
+    for (int i = 0; i < I; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
+    auto compute = [&](const char* a_lds, const char* b_lds) {
+        Frag bf[2][PL];
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int q = 0; q < PL; ++q) bf[j][q] = read_frag<Frag>(b_lds + q * kX6PlaneB, wn * 64 + j * 32 + l32, h);
+#pragma unroll
+        for (int i = 0; i < I; ++i) {
+            Frag af[PL];
+#pragma unroll
+            for (int q = 0; q < PL; ++q) af[q] = read_frag<Frag>(a_lds + q * planeA, i * 32 + l32, h);
+#pragma unroll
+            for (int j = 0; j < 2; ++j) acc[i][j] = Arith<PL>::mfma(af, bf[j], acc[i][j]);
+        }
+    };
+    deep_pipeline<BM, PL, 16, kW4Depth, decltype(compute)&, NoHook, kThreadsW4>(p, row0, bimg, lds, 1.f, compute);
+    float colpart[2];
+    float amx = 0.f;
+    epilogue_tiles<EPI, I, 2>(p, acc, row0, wn * 64, true, colpart, amx);
+}
+
+template <int EPI>
+__global__ __launch_bounds__(kThreadsW4, 2) void mlp_gemm_x6_w4_pair_kernel(GemmPair b) {
+    __shared__ __attribute__((aligned(16))) char lds_b0[x6_buf_bytes<EPI, 3>()];
+    __shared__ __attribute__((aligned(16))) char lds_b1[x6_buf_bytes<EPI, 3>()];
+    mlp_gemm_x6_w4_body<EPI>(b.p[blockIdx.y], b.img[blockIdx.y], lds_b0, lds_b1);
+}
+
+// RSLRL_W4 (read per call: A/B in one process): 1 = every eligible launch, 0 = none; unset = the input gradient at
+// >= 2048 tiles per problem (measured, scripts/w4_probe.py: dgrad pair at 393,216 rows 669 -> 642 us; the hidden
+// forward 607 -> 617 us and both equal within noise at 98,304 rows)
+bool w4_enabled(int epi, int64_t tiles) {
+    const char* e = std::getenv("RSLRL_W4");
+    if (e && e[0] == '1') return true;
+    if (e && e[0] == '0') return false;
+    return epi == kEpiEluGrad && tiles >= 2048;
+}
+
 template <int EPI, int PL>
 int launch_pair(const GemmPair& b, bool fullm, hipStream_t st) {
     const int64_t tiles = ceil_div(b.p[0].M, kBM);
@@ -2083,6 +2150,14 @@ int launch_pair(const GemmPair& b, bool fullm, hipStream_t st) {
     if constexpr (PL == 3 && (EPI == kEpiBias || EPI == kEpiBiasElu)) {
         if (k48_deep<EPI>(b.p[0], fullm, PL)) {  // both problems share the shape and the op
             hipLaunchKernelGGL((mlp_gemm_x6_pair_kernel<EPI, true, PL, 3>), g, blk, 0, st, b);
+            return launch_status();
+        }
+    }
+    if constexpr (PL == 3 && (EPI == kEpiBiasElu || EPI == kEpiEluGrad)) {
+        const bool plain = b.p[0].colsum == nullptr && b.p[1].colsum == nullptr && b.p[0].amax_out == nullptr &&
+                           b.p[1].amax_out == nullptr;
+        if (w4_enabled(EPI, tiles) && fullm && plain && b.p[0].K == 16 * kKC && b.p[0].N == kBN && b.p[0].deep) {
+            hipLaunchKernelGGL((mlp_gemm_x6_w4_pair_kernel<EPI>), g, dim3(kThreadsW4), 0, st, b);
             return launch_status();
         }
     }

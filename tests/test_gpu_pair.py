@@ -102,9 +102,12 @@ def test_out_pair_matches_two_launches(M, cuda_device):
                 assert torch.equal(hs[i], ref[i][0])
 
 
-@pytest.mark.parametrize("M", [777, 98304])
-def test_dgrad_pair_matches_two_launches(M, cuda_device):
-    """Two hidden-layer input gradients (dz W) * ELU'(h) in one launch, bit-identical to two launches."""
+@pytest.mark.parametrize("M,w4", [(777, None), (98304, None), (262144, None), (98304, "1")])
+def test_dgrad_pair_matches_two_launches(M, w4, cuda_device, monkeypatch):
+    """Two hidden-layer input gradients (dz W) * ELU'(h) in one launch, bit-identical to two launches -- including the
+    4-wave 128 x 64 layout ("w4": the default at >= 2048 tiles per problem, forced with RSLRL_W4=1)."""
+    if w4 is not None:
+        monkeypatch.setenv("RSLRL_W4", w4)
     dev = cuda_device
     g = torch.Generator(device=dev).manual_seed(6)
     dzs = [torch.randn(M, 256, device=dev, generator=g) for _ in range(2)]
@@ -116,3 +119,21 @@ def test_dgrad_pair_matches_two_launches(M, cuda_device):
     torch.cuda.synchronize()
     for i in range(2):
         assert torch.equal(outs[i], ref[i])
+
+
+def test_w4_forward_pair_matches(cuda_device, monkeypatch):
+    """The opt-in w4 layout on the hidden forward (RSLRL_W4=1) gives the default launch's bits."""
+    dev = cuda_device
+    g = torch.Generator(device=dev).manual_seed(7)
+    M = 65536
+    xs = [torch.nn.functional.elu(torch.randn(M, 256, device=dev, generator=g)) for _ in range(2)]
+    ws = [torch.randn(256, 256, device=dev, generator=g) / 16 for _ in range(2)]
+    bs = [torch.randn(256, device=dev, generator=g) * 0.1 for _ in range(2)]
+    imgs = fused_mlp.bimages([(w, False) for w in ws])
+    monkeypatch.setenv("RSLRL_W4", "0")
+    ref, _ = fused_mlp.linear_fwd_pair(xs, bs, 256, True, imgs, _lib.ARITH_X6, [None, None], [False, False])
+    monkeypatch.setenv("RSLRL_W4", "1")
+    ys, _ = fused_mlp.linear_fwd_pair(xs, bs, 256, True, imgs, _lib.ARITH_X6, [None, None], [False, False])
+    torch.cuda.synchronize()
+    for i in range(2):
+        assert torch.equal(ys[i], ref[i])
