@@ -31,7 +31,7 @@ extern "C" {
 
 typedef struct ihipStream_t* rslrl_stream_t; /* == hipStream_t */
 
-#define RSLRL_ABI_VERSION 8
+#define RSLRL_ABI_VERSION 9
 
 enum {
     RSLRL_OK = 0,
@@ -59,6 +59,18 @@ int rslrl_compute_returns(const float* values, const float* rewards, const uint8
                           const float* last_values, float gamma, float lam, int64_t T, int64_t N,
                           int32_t normalize_advantage, float* returns, float* advantages,
                           void* workspace, size_t workspace_bytes, rslrl_stream_t stream);
+
+/* rslrl_compute_returns with normalize_advantage = 1 whose normalisation pass also fills every env-step's
+ * transition-record slot (see rslrl_record_fill_slot below): records[i][slot_offset : slot_offset + 8] =
+ * {values[i], log_prob[i], returns[i], advantages[i] (normalised), 0, 0, 0, 0}, i < T*N.  The storage then needs no
+ * slot copy per update (rollout_storage.py:127-149 then :168-197; values identical to rslrl_compute_returns
+ * followed by rslrl_record_fill_slot).  records: [T*N, record_floats] fp32, 16-byte aligned, record_floats and
+ * slot_offset multiples of 4, slot_offset + 8 <= record_floats; log_prob: [T, N] fp32. */
+int rslrl_compute_returns_records(const float* values, const float* rewards, const uint8_t* dones,
+                                  const float* last_values, float gamma, float lam, int64_t T, int64_t N,
+                                  float* returns, float* advantages, const float* log_prob, float* records,
+                                  int64_t record_floats, int64_t slot_offset, void* workspace,
+                                  size_t workspace_bytes, rslrl_stream_t stream);
 
 /* Advantage statistics + in-place normalisation of an arbitrary fp32 vector (the normalisation half
  * of rollout_storage.py:148-149; ppo.py:221-223 uses the same expression per mini-batch).          */

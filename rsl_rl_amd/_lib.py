@@ -19,7 +19,7 @@ import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 # RSLRL_AMD_LIB: an alternative in-tree build of the same library (A/B kernel experiments)
 LIB_PATH = os.environ.get("RSLRL_AMD_LIB") or os.path.join(LIB_DIR, "librslrl_amd.so")
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 # symbols declared in include/rslrl_amd.h (tests/test_capi.py checks the header against this list)
 EXPORTED_SYMBOLS = (
@@ -27,6 +27,7 @@ EXPORTED_SYMBOLS = (
     "rslrl_status_string",
     "rslrl_compute_returns_workspace_bytes",
     "rslrl_compute_returns",
+    "rslrl_compute_returns_records",
     "rslrl_normalize_workspace_bytes",
     "rslrl_normalize_advantages",
     "rslrl_randperm_mt19937",
@@ -311,6 +312,8 @@ def _declare(L):
     L.rslrl_compute_returns_workspace_bytes.argtypes = [I64, I64]
     L.rslrl_compute_returns.restype = ctypes.c_int
     L.rslrl_compute_returns.argtypes = [P, P, P, P, F, F, I64, I64, I32, P, P, P, SZ, P]
+    L.rslrl_compute_returns_records.restype = ctypes.c_int
+    L.rslrl_compute_returns_records.argtypes = [P, P, P, P, F, F, I64, I64, P, P, P, P, I64, I64, P, SZ, P]
     L.rslrl_normalize_workspace_bytes.restype = SZ
     L.rslrl_normalize_workspace_bytes.argtypes = [I64]
     L.rslrl_normalize_advantages.restype = ctypes.c_int

@@ -183,6 +183,32 @@ __global__ __launch_bounds__(kBlock) void adv_normalize_kernel(float* __restrict
     for (int64_t i = nvec * 4 + tid; i < n; i += stride) adv[i] = __fdiv_rn(__fsub_rn(adv[i], mean), denom);
 }
 
+// adv_normalize_kernel that also writes each env-step's transition-record slot {value, log-prob, return, advantage,
+// 0, 0, 0, 0} (RolloutStorage's per-update slot, rollout_storage.py field semantics unchanged): the pass that
+// produces the final advantages is the one that places them, so no separate slot copy runs per update.  Two
+// consecutive lanes write one 32-byte slot (unit 0 the four scalars, unit 1 zeros): each slot leaves the store whole.
+__global__ __launch_bounds__(kBlock) void adv_normalize_slot_kernel(float* __restrict__ adv, int64_t n,
+                                                                    const double2* __restrict__ partials, int np,
+                                                                    float eps, const float* __restrict__ values,
+                                                                    const float* __restrict__ logp,
+                                                                    const float* __restrict__ returns,
+                                                                    float* __restrict__ rec, int64_t R, int64_t off) {
+    float mean, std;
+    fold_moments(partials, np, n, &mean, &std);
+    const float denom = __fadd_rn(std, eps);  // rollout_storage.py:149  (std + 1e-8)
+    const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
+    for (int64_t k = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; k < 2 * n; k += stride) {
+        const int64_t i = k >> 1;
+        float4 u = make_float4(0.f, 0.f, 0.f, 0.f);
+        if ((k & 1) == 0) {
+            const float a = __fdiv_rn(__fsub_rn(adv[i], mean), denom);
+            adv[i] = a;
+            u = make_float4(values[i], logp[i], returns[i], a);
+        }
+        *reinterpret_cast<float4*>(rec + i * R + off + 4 * (k & 1)) = u;
+    }
+}
+
 int scan_blocks(int64_t N) { return static_cast<int>(std::min<int64_t>(ceil_div(N, kBlock), kMaxPartials)); }
 
 int elementwise_blocks(int64_t n) {
@@ -216,10 +242,19 @@ extern "C" size_t rslrl_normalize_workspace_bytes(int64_t n) {
     return sizeof(double2) * kMaxPartials;
 }
 
-extern "C" int rslrl_compute_returns(const float* values, const float* rewards, const uint8_t* dones,
-                                     const float* last_values, float gamma, float lam, int64_t T, int64_t N,
-                                     int32_t normalize_advantage, float* returns, float* advantages,
-                                     void* workspace, size_t workspace_bytes, rslrl_stream_t stream) {
+namespace {
+// RecordSlot: optional destination of the normalisation pass (rslrl_compute_returns_records)
+struct RecordSlot {
+    const float* log_prob;
+    float* records;
+    int64_t record_floats;
+    int64_t offset;
+};
+
+int compute_returns_impl(const float* values, const float* rewards, const uint8_t* dones, const float* last_values,
+                         float gamma, float lam, int64_t T, int64_t N, int32_t normalize_advantage, float* returns,
+                         float* advantages, void* workspace, size_t workspace_bytes, rslrl_stream_t stream,
+                         const RecordSlot* slot) {
     if (T < 0 || N < 0 || T > INT32_MAX) return RSLRL_E_INVALID_ARGUMENT;
     if (T == 0 || N == 0) return RSLRL_OK;
     if (!values || !rewards || !dones || !last_values || !returns || !advantages) return RSLRL_E_INVALID_ARGUMENT;
@@ -249,9 +284,39 @@ extern "C" int rslrl_compute_returns(const float* values, const float* rewards, 
     hipLaunchKernelGGL(centered_sq_kernel, dim3(nb), dim3(kBlock), 0, st, advantages, n, part);
     rc = launch_status();
     if (rc != RSLRL_OK) return rc;
-    hipLaunchKernelGGL(adv_normalize_kernel, dim3(elementwise_blocks(n)), dim3(kBlock), 0, st, advantages, n, part,
-                       nb, 1e-8f);
+    if (slot) {
+        const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(ceil_div(2 * n, kBlock), 4096));
+        hipLaunchKernelGGL(adv_normalize_slot_kernel, dim3(static_cast<unsigned>(blocks)), dim3(kBlock), 0, st,
+                           advantages, n, part, nb, 1e-8f, values, slot->log_prob, returns, slot->records,
+                           slot->record_floats, slot->offset);
+    } else {
+        hipLaunchKernelGGL(adv_normalize_kernel, dim3(elementwise_blocks(n)), dim3(kBlock), 0, st, advantages, n, part,
+                           nb, 1e-8f);
+    }
     return launch_status();
+}
+}  // namespace
+
+extern "C" int rslrl_compute_returns(const float* values, const float* rewards, const uint8_t* dones,
+                                     const float* last_values, float gamma, float lam, int64_t T, int64_t N,
+                                     int32_t normalize_advantage, float* returns, float* advantages,
+                                     void* workspace, size_t workspace_bytes, rslrl_stream_t stream) {
+    return compute_returns_impl(values, rewards, dones, last_values, gamma, lam, T, N, normalize_advantage, returns,
+                                advantages, workspace, workspace_bytes, stream, nullptr);
+}
+
+extern "C" int rslrl_compute_returns_records(const float* values, const float* rewards, const uint8_t* dones,
+                                             const float* last_values, float gamma, float lam, int64_t T, int64_t N,
+                                             float* returns, float* advantages, const float* log_prob, float* records,
+                                             int64_t record_floats, int64_t slot_offset, void* workspace,
+                                             size_t workspace_bytes, rslrl_stream_t stream) {
+    if (!log_prob || !records || record_floats <= 0 || (record_floats & 3) || slot_offset < 0 || (slot_offset & 3) ||
+        slot_offset + 8 > record_floats)
+        return RSLRL_E_INVALID_ARGUMENT;
+    if (reinterpret_cast<uintptr_t>(records) & 15) return RSLRL_E_MISALIGNED;
+    const RecordSlot slot{log_prob, records, record_floats, slot_offset};
+    return compute_returns_impl(values, rewards, dones, last_values, gamma, lam, T, N, 1, returns, advantages,
+                                workspace, workspace_bytes, stream, &slot);
 }
 
 extern "C" int rslrl_normalize_advantages(float* advantages, int64_t n, float eps, void* workspace,

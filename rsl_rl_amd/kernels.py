@@ -16,6 +16,7 @@ from . import _lib
 
 __all__ = [
     "compute_returns",
+    "compute_returns_records",
     "normalize_advantages_",
     "randperm_mt19937",
     "gather_rows",
@@ -172,6 +173,37 @@ def compute_returns(values, rewards, dones, last_values, gamma, lam, normalize_a
             ws.numel(), ctypes.c_void_p(_stream(dev)),
         )
     _lib.check(rc, "rslrl_compute_returns")
+
+
+def compute_returns_records(values, rewards, dones, last_values, gamma, lam, returns, advantages, log_prob, records,
+                            slot_offset: int):
+    """compute_returns with normalisation whose last pass also writes every record's slot
+    {value, log-prob, return, advantage, 0, 0, 0, 0} at `slot_offset` (include/rslrl_amd.h
+    rslrl_compute_returns_records): records [T, N, R] contiguous fp32, log_prob [T, N, 1] contiguous fp32."""
+    _require_device(values, rewards, dones, last_values, returns, advantages, log_prob, records)
+    T, N = values.shape[0], values.shape[1]
+    for t, dt in ((values, torch.float32), (rewards, torch.float32), (dones, torch.uint8), (last_values, torch.float32),
+                  (returns, torch.float32), (advantages, torch.float32), (log_prob, torch.float32),
+                  (records, torch.float32)):
+        if t.dtype != dt or not t.is_contiguous():
+            raise ValueError(f"compute_returns_records: expected contiguous {dt}, got {t.dtype} "
+                             f"(contiguous={t.is_contiguous()})")
+    if (values.numel() != T * N or last_values.numel() != N or dones.numel() != T * N or rewards.numel() != T * N
+            or log_prob.numel() != T * N or records.dim() != 3 or records.shape[:2] != values.shape[:2]):
+        raise ValueError("compute_returns_records: inconsistent shapes")
+    R = records.shape[2]
+    L = _lib.lib()
+    dev = values.device
+    ws = _ws.get(dev, "gae", L.rslrl_compute_returns_workspace_bytes(T, N))
+    # scan (17 B + 4 B per env) + normalisation reading adv / value / log-prob / return and writing adv + the slot
+    moved = 17 * T * N + 4 * N + (4 * 4 + 4 + 32) * T * N
+    with timer.span("compute_returns", dev, moved):
+        rc = L.rslrl_compute_returns_records(
+            _ptr(values), _ptr(rewards), _ptr(dones), _ptr(last_values), ctypes.c_float(gamma), ctypes.c_float(lam),
+            T, N, _ptr(returns), _ptr(advantages), _ptr(log_prob), _ptr(records), R, int(slot_offset), _ptr(ws),
+            ws.numel(), ctypes.c_void_p(_stream(dev)),
+        )
+    _lib.check(rc, "rslrl_compute_returns_records")
 
 
 def normalize_advantages_(adv: torch.Tensor, eps: float = 1e-8) -> torch.Tensor:

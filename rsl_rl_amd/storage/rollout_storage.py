@@ -24,8 +24,9 @@ env-step sit side by side in one fp32 record padded to whole 128-byte lines ([T,
 observation groups, actions, mu and sigma (written by the rollout; `observations[k]`, `actions`, `mu`,
 `sigma` are strided views of the records, same shapes and values as the reference's buffers), then a
 32-byte slot {value, log-prob, return, advantage, 0, 0, 0, 0} filled once per update from the contiguous
-[T, N, 1] scalar buffers (GAE wants those contiguous).  A randomly drawn row then reads its record's own
-lines (1.09x the used bytes at C3) instead of at least one line per field (2.2x with one buffer per field).
+[T, N, 1] scalar buffers (GAE wants those contiguous): by compute_returns' normalisation pass itself when it
+normalises (rslrl_compute_returns_records), else by a slot copy at the first mini_batch_generator after it.
+A randomly drawn row then reads its record's own lines (1.09x the used bytes at C3) instead of at least one line per field (2.2x with one buffer per field).
 RSLRL_RECORD_LAYOUT=0 keeps one buffer per field.
 
 The host draw (1.57M elements at C3: ~4.7 ms, with the GPU idle behind it) is computed ahead: right after a
@@ -104,6 +105,8 @@ class RolloutStorage:
         self.saved_hidden_states_a = None
         self.saved_hidden_states_c = None
         self.step = 0
+        self._fills = 0  # transitions added so far (any path): a record slot written before the last one is stale
+        self._slot_key = None  # what the records' slots were filled from (compute_returns), or None
 
         # mini-batch machinery (allocated on first use)
         self.perm_generator: torch.Generator | None = None
@@ -165,6 +168,7 @@ class RolloutStorage:
             self.sigma[t].copy_(transition.action_sigma)
         self._save_hidden_states(transition.hidden_states)
         self.step += 1
+        self._fills += 1
 
     def fused_record_ok(self, transition) -> bool:
         """The fused rollout record (kernels.rollout_record) covers the RL transition of a feed-forward
@@ -205,6 +209,7 @@ class RolloutStorage:
         for src, dst in late:
             dst.copy_(src)
         self.step += 1
+        self._fills += 1
 
     def _save_hidden_states(self, hidden_states):
         if hidden_states is None or hidden_states == (None, None):
@@ -227,8 +232,23 @@ class RolloutStorage:
         last_values = last_values.detach()
         if not last_values.is_contiguous():
             last_values = last_values.contiguous()
+        if self.records is not None and normalize_advantage:
+            # the normalisation pass also writes every record's slot {value, log-prob, return, advantage}: the
+            # mini-batch generator then gathers the records as they are (no slot copy per update)
+            kernels.compute_returns_records(self.values, self.rewards, self.dones, last_values, float(gamma),
+                                            float(lam), self.returns, self.advantages, self.actions_log_prob,
+                                            self.records, self.record_layout[1]["slot"])
+            self._slot_key = self._slot_sources()
+            return
+        self._slot_key = None
         kernels.compute_returns(self.values, self.rewards, self.dones, last_values, float(gamma), float(lam),
                                 normalize_advantage, self.returns, self.advantages)
+
+    def _slot_sources(self):
+        """What the record slots hold: the transition count and the in-place versions of the four scalar buffers
+        (any later add_transitions or in-place write to values / log-prob / returns / advantages invalidates them)."""
+        return (self._fills, self.values._version, self.actions_log_prob._version, self.returns._version,
+                self.advantages._version)
 
     # ------------------------------------------------------------------ distillation (rollout_storage.py:152-157)
     def generator(self):
@@ -333,9 +353,12 @@ class RolloutStorage:
             R, offs = self.record_layout
             A = self.actions_shape[0]
             o = offs["slot"]
-            # the scalar fields' final values into each record's slot, then one gather of whole records
-            kernels.record_fill_slot(self.records, o, offs["slot_floats"],
-                                     columns=[self.values, self.actions_log_prob, self.returns, self.advantages])
+            # the scalar fields' final values into each record's slot (unless compute_returns already wrote them
+            # and nothing changed since), then one gather of whole records
+            if self._slot_key is None or self._slot_key != self._slot_sources():
+                kernels.record_fill_slot(self.records, o, offs["slot_floats"],
+                                         columns=[self.values, self.actions_log_prob, self.returns, self.advantages])
+                self._slot_key = self._slot_sources()
             fields = [(offs["obs/" + k], v.shape[-1], p["obs"][k]) for k, v in self.observations.items()]
             fields += [(offs["actions"], A, p["actions"]), (o, 1, p["values"]), (o + 1, 1, p["actions_log_prob"]),
                        (o + 2, 1, p["returns"]), (o + 3, 1, p["advantages"]), (offs["mu"], A, p["mu"]),

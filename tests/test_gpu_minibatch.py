@@ -179,3 +179,60 @@ def test_record_storage_minibatches_bit_exact(cuda_device, monkeypatch):
         for nm, a, b in zip(names, g[1:8], r[1:8]):
             assert torch.equal(a.cpu(), b.cpu()), (j, nm)
             assert torch.equal(a.cpu(), flat[nm][sel]), (j, nm)
+
+
+@pytest.mark.parametrize("T,N", [(24, 4096), (5, 1031), (1, 3)])
+def test_compute_returns_records_matches_scan_plus_slot_copy(T, N, cuda_device):
+    """rslrl_compute_returns_records == rslrl_compute_returns (normalised) + rslrl_record_fill_slot, bit for bit:
+    the contiguous returns / advantages and every record (the slot written whole, the rest untouched)."""
+    rng = np.random.default_rng(T * N)
+    R, off = 96, 88
+    f = lambda *s: torch.from_numpy(rng.standard_normal(s, dtype=np.float32)).to(cuda_device)  # noqa: E731
+    values, rewards, logp, last = f(T, N, 1), f(T, N, 1), f(T, N, 1), f(N, 1)
+    dones = torch.from_numpy((rng.random((T, N, 1)) < 0.05).astype(np.uint8)).to(cuda_device)
+    rec0 = f(T, N, R)
+    ret_a, adv_a = torch.empty_like(values), torch.empty_like(values)
+    ret_b, adv_b = torch.empty_like(values), torch.empty_like(values)
+    rec_a, rec_b = rec0.clone(), rec0.clone()
+    kernels.compute_returns(values, rewards, dones, last, 0.99, 0.95, True, ret_a, adv_a)
+    kernels.record_fill_slot(rec_a, off, 8, columns=[values, logp, ret_a, adv_a])
+    kernels.compute_returns_records(values, rewards, dones, last, 0.99, 0.95, ret_b, adv_b, logp, rec_b, off)
+    assert torch.equal(ret_a, ret_b) and torch.equal(adv_a, adv_b)
+    assert torch.equal(rec_a, rec_b)
+
+
+def test_storage_slot_from_compute_returns_and_invalidation(cuda_device, monkeypatch):
+    """The record storage's slots written by compute_returns give the same mini-batches as the per-field layout;
+    an in-place write to a scalar buffer after compute_returns (or a new transition) makes the generator copy the
+    slots again instead of gathering stale ones."""
+    T, N, A, M = 4, 257, 8, 2
+    groups = {"policy": 20}
+    obs0 = {k: torch.zeros(N, d) for k, d in groups.items()}
+    st = RolloutStorage("rl", N, T, obs0, [A], cuda_device)
+    monkeypatch.setenv("RSLRL_RECORD_LAYOUT", "0")
+    soa = RolloutStorage("rl", N, T, obs0, [A], cuda_device)
+    assert st.records is not None and soa.records is None
+    _fill_storage(st, np.random.default_rng(8), T, N, groups, A)
+    _fill_storage(soa, np.random.default_rng(8), T, N, groups, A)
+    for s in (st, s2 := soa):
+        s.rewards.copy_(torch.linspace(-1, 1, T * N).view(T, N, 1))
+        s.dones.zero_()
+    last = torch.linspace(0, 1, N, device=cuda_device).view(N, 1)
+    calls = []
+    real = kernels.record_fill_slot
+    monkeypatch.setattr(kernels, "record_fill_slot", lambda *a, **k: (calls.append(1), real(*a, **k))[1])
+
+    def batches(s, seed):
+        s.perm_generator = torch.Generator().manual_seed(seed)
+        return [tuple(t.cpu() for t in b[1:8]) for b in s.mini_batch_generator(M, 1)]
+
+    for s in (st, s2):
+        s.compute_returns(last, 0.99, 0.95, normalize_advantage=True)
+    assert all(torch.equal(a, b) for x, y in zip(batches(st, 1), batches(s2, 1)) for a, b in zip(x, y))
+    assert not calls  # the slots came from compute_returns
+    for s in (st, s2):
+        s.returns.mul_(2.0)  # an in-place edit between compute_returns and the update
+    assert all(torch.equal(a, b) for x, y in zip(batches(st, 2), batches(s2, 2)) for a, b in zip(x, y))
+    assert len(calls) == 1
+    assert all(torch.equal(a, b) for x, y in zip(batches(st, 3), batches(s2, 3)) for a, b in zip(x, y))
+    assert len(calls) == 1  # still valid: nothing changed since the copy
