@@ -31,7 +31,7 @@ extern "C" {
 
 typedef struct ihipStream_t* rslrl_stream_t; /* == hipStream_t */
 
-#define RSLRL_ABI_VERSION 9
+#define RSLRL_ABI_VERSION 10
 
 enum {
     RSLRL_OK = 0,
@@ -392,6 +392,28 @@ int rslrl_linear_gemm(const rslrl_linear_args_t* args /* host struct */, rslrl_s
  * not a whole number of slot rounds at M <= 98,304).  Results are identical to two rslrl_linear_gemm calls; distinct
  * amax workspaces when both write an amax. */
 int rslrl_linear_gemm_pair(const rslrl_linear_args_t* a0, const rslrl_linear_args_t* a1, rslrl_stream_t stream);
+
+/* The critic's last hidden layer, value head, value-loss gradient and the value head's backward in one launch:
+ * rsl_rl/networks/mlp.py:106-114 (the critic's last Linear + ELU and the 1-wide output Linear), ppo.py:305-313 (value
+ * loss, clipped or not) and the backward of ppo.py:367 through the value head.  a: an RSLRL_LINEAR_FWD_OUT problem
+ * (x6, nout = 1, N = K = 256, M a multiple of 128) whose `y` receives V = the critic's output and whose `c` receives
+ * dZ = (dV w) * ELU'(H), the gradient at the last hidden layer's pre-activation (H itself is not stored); with
+ * g = value_loss_coef / M, dV is the loss kernel's d loss / dV (rslrl_ppo_loss_fwd_bwd; same bits).
+ * wgrad_partials: [M / 128][260] per-tile rows [sum dV H (256) | sum dV | 0 0 0] -- the layout of the
+ * RSLRL_LINEAR_DGRAD_ELU_WGRAD partials, folded by rslrl_fold_partials* into the head's [dW | db].
+ * colsum_partials: optional [M / 128][256] per-tile column sums of dZ (the last hidden layer's bias gradient).
+ * RSLRL_E_UNSUPPORTED (nothing launched) for any other shape. */
+typedef struct {
+    const float* target_values; /* [M] */
+    const float* returns;       /* [M] */
+    const float* out_weight;    /* [256] the value head's weight row, 16-byte aligned */
+    float clip_param;
+    float value_loss_coef;
+    int32_t use_clipped_value_loss;
+    float* wgrad_partials;  /* [M / 128][260] */
+    float* colsum_partials; /* [M / 128][256] or NULL */
+} rslrl_value_head_args_t;
+int rslrl_value_head_fwd_bwd(const rslrl_linear_args_t* a, const rslrl_value_head_args_t* v, rslrl_stream_t stream);
 int rslrl_linear_wgrad_ex(const float* dz, const float* dz_amax, const float* x, const float* x_amax, int64_t M,
                           int32_t N, int32_t K, int32_t arith, float* dw, void* workspace, size_t workspace_bytes,
                           rslrl_stream_t stream);

@@ -19,7 +19,7 @@ import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 # RSLRL_AMD_LIB: an alternative in-tree build of the same library (A/B kernel experiments)
 LIB_PATH = os.environ.get("RSLRL_AMD_LIB") or os.path.join(LIB_DIR, "librslrl_amd.so")
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 # symbols declared in include/rslrl_amd.h (tests/test_capi.py checks the header against this list)
 EXPORTED_SYMBOLS = (
@@ -60,6 +60,7 @@ EXPORTED_SYMBOLS = (
     "rslrl_amax_workspace_bytes",
     "rslrl_linear_gemm",
     "rslrl_linear_gemm_pair",
+    "rslrl_value_head_fwd_bwd",
     "rslrl_linear_wgrad_ex",
     "rslrl_linear_wgrad_bias_workspace_bytes",
     "rslrl_linear_wgrad_bias",
@@ -112,6 +113,7 @@ BIMAGE_LAYOUT_H3 = 2
 
 ARITH_X6, ARITH_H3 = 1, 2
 LINEAR_FWD, LINEAR_FWD_ELU, LINEAR_DGRAD_ELU, LINEAR_DGRAD_ELU_WGRAD, LINEAR_FWD_OUT = 0, 1, 2, 3, 4
+E_UNSUPPORTED = -3  # RSLRL_E_UNSUPPORTED
 
 
 ADAM_MAX_TENSORS = 24
@@ -153,6 +155,21 @@ class LinearArgs(ctypes.Structure):
         ("amax_out", ctypes.c_void_p),
         ("amax_workspace", ctypes.c_void_p),
     ]
+
+
+class ValueHeadArgs(ctypes.Structure):
+    """rslrl_value_head_args_t (include/rslrl_amd.h)."""
+    _fields_ = [
+        ("target_values", ctypes.c_void_p),
+        ("returns", ctypes.c_void_p),
+        ("out_weight", ctypes.c_void_p),
+        ("clip_param", ctypes.c_float),
+        ("value_loss_coef", ctypes.c_float),
+        ("use_clipped_value_loss", ctypes.c_int32),
+        ("wgrad_partials", ctypes.c_void_p),
+        ("colsum_partials", ctypes.c_void_p),
+    ]
+
 
 DTYPE_F32, DTYPE_U8, DTYPE_I32, DTYPE_I64 = 0, 1, 2, 3
 ROLLOUT_MAX_OBS = 4
@@ -382,6 +399,8 @@ def _declare(L):
     L.rslrl_linear_gemm.argtypes = [ctypes.POINTER(LinearArgs), P]
     L.rslrl_linear_gemm_pair.restype = ctypes.c_int
     L.rslrl_linear_gemm_pair.argtypes = [ctypes.POINTER(LinearArgs), ctypes.POINTER(LinearArgs), P]
+    L.rslrl_value_head_fwd_bwd.restype = ctypes.c_int
+    L.rslrl_value_head_fwd_bwd.argtypes = [ctypes.POINTER(LinearArgs), ctypes.POINTER(ValueHeadArgs), P]
     L.rslrl_adam_workspace_bytes.restype = SZ
     L.rslrl_adam_workspace_bytes.argtypes = []
     L.rslrl_clip_adam_step.restype = ctypes.c_int

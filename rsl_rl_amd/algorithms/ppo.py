@@ -384,7 +384,12 @@ class PPO:
                 # (ppo.py:246-253 forward, :221-223 + :259-315 loss, :367-368 backward)
                 with torch.no_grad():
                     side = self._side_stream(dev)
-                    mean, sigma, value_batch, tape = self.policy.train_forward(obs_batch, side_stream=side)
+                    # the critic's last launch also runs d(value loss)/dV and the value head's backward (the same
+                    # values as the loss kernel's d/dV followed by the output-layer backward)
+                    vh = fused_mlp.ValueHead(target_values_batch, returns_batch, self.clip_param, self.value_loss_coef,
+                                             self.use_clipped_value_loss)
+                    mean, sigma, value_batch, tape = self.policy.train_forward(obs_batch, side_stream=side,
+                                                                               value_head=vh)
                     g_mean, g_sigma = self.policy.train_grad_buffers(mean, sigma)
                     if g_sigma is None:  # shared std: d sigma reduced by the loss kernel, into the std's slot
                         g_sigma = (arena.slot(self.policy.std) if self.policy.noise_std_type == "scalar"

@@ -69,7 +69,35 @@ struct GemmParams {
     float* amax_out;      // optional: max |C| over the stored output (device scalar, for an h3 consumer)
     unsigned* amax_ws;    // with amax_out: {running max bits, arrival ticket}, zero before and after the launch
     int deep;             // K = 256: the unrolled look-ahead main loop (h3_deep_loop; x6 and h3)
+    // value head with its backward (mlp_gemm_x6_value_head_kernel, rslrl_value_head_fwd_bwd)
+    const float* vh_tv;   // [M] target values (the rollout's values)
+    const float* vh_ret;  // [M] returns
+    const float* vh_w;    // [N] the value head's fp32 weight row
+    float vh_clip;        // clip_param
+    float vh_g;           // value_loss_coef / M
+    int vh_clipped;       // use_clipped_value_loss
 };
+
+// d(loss)/dV of one sample (ppo.py:305-313, :367 backward): the loss kernel's expression and operation order
+// (ppo_loss.hip, ppo_loss_quad_kernel; both compiled with -ffp-contract=off), so both produce the same bits.
+__device__ __forceinline__ float value_loss_grad(float V, float tv, float R, int clipped, float clip, float g_value) {
+    if (clipped) {
+        const float dv = V - tv;
+        const float vc = tv + fminf(fmaxf(dv, -clip), clip);
+        const float e1 = V - R;
+        const float e2 = vc - R;
+        const float vl = e1 * e1;
+        const float vlc = e2 * e2;
+        const float half = __fmul_rn(g_value, 0.5f);  // max(): ties split the gradient 1/2 : 1/2
+        const float g1 = (vl > vlc) ? g_value : ((vl == vlc) ? half : 0.0f);
+        const float g2 = (vlc > vl) ? g_value : ((vl == vlc) ? half : 0.0f);
+        float dV = 2.0f * g1 * e1;
+        if (dv >= -clip && dv <= clip) dV += 2.0f * g2 * e2;
+        return dV;
+    }
+    const float e = R - V;
+    return -2.0f * g_value * e;
+}
 
 // global -> registers for one K chunk: A: 128 x 16 floats = 512 float4 (1 per thread); B: 256 x 16 = 1024
 // float4 (2 per thread, only the first N rows real).  Rows >= M / N and k >= K read as zero.
@@ -785,7 +813,8 @@ constexpr int x6_buf_bytes() {
 // array: the waitcnt pass can then tell a DMA into one buffer from reads of the other (distinct alias scopes) where
 // the buffer index is a compile-time constant.  Declared by the kernel so that two bodies in one kernel (the
 // output-layer pair) share them.
-template <int EPI, bool FULL, int NR, int PL, bool STAGE = true, int KCH = 0>
+// HEAD (kEpiBiasEluOut, NR 1, full tiles): the value head's backward fused behind it (mlp_gemm_x6_value_head_kernel)
+template <int EPI, bool FULL, int NR, int PL, bool STAGE = true, int KCH = 0, bool HEAD = false>
 __device__ __forceinline__ void mlp_gemm_x6_body(GemmParams p, const uint4* __restrict__ bimg, char* lds_b0,
                                                  char* lds_b1) {
     static_assert(PL == 3 || EPI != kEpiEluGradWgrad, "the fused output-layer backward is x6 only");
@@ -804,6 +833,7 @@ __device__ __forceinline__ void mlp_gemm_x6_body(GemmParams p, const uint4* __re
     // past the main loop's operands and past the epilogue's H stage / reduction tiles (8 waves x 4 KiB)
     constexpr int kXsOff = PL * planeA + PL * kX6PlaneB > 8 * 4096 ? PL * planeA + PL * kX6PlaneB : 8 * 4096;
     constexpr int kXsOut = 1;  // the value head
+    constexpr int kVhWOff = kBN + kOutImageThreads / 32 * kXsOut * 8;  // HEAD: floats from xs to the value weights
     if constexpr (EPI == kEpiBiasEluOut) {
         static_assert(kXsOff + 4 * (kBN + kOutImageThreads / 32 * kXsOut * 8) <= bufBytes, "LDS side area");
         float* xs = reinterpret_cast<float*>(lds_b0 + kXsOff);
@@ -820,6 +850,24 @@ __device__ __forceinline__ void mlp_gemm_x6_body(GemmParams p, const uint4* __re
                 const bool ok = o < p.nout;
                 dst[0] = ok ? src[0] : make_float4(0.f, 0.f, 0.f, 0.f);
                 dst[1] = ok ? src[1] : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+        }
+        if constexpr (HEAD) {
+            // after the side area: the value weight row in column order [N], then the tile's target values and returns
+            // [BM] each, DMA'd now (no registers held through the main loop; its final barrier drains them) -- the
+            // epilogue replaces the targets by dV
+            static_assert(kXsOff + 4 * (kVhWOff + kBN + 2 * BM) <= bufBytes, "LDS side area (value head)");
+            if (t >= 128 && t < 128 + kBN / 4)
+                reinterpret_cast<float4*>(xs + kVhWOff)[t - 128] = *reinterpret_cast<const float4*>(p.vh_w + 4 * (t - 128));
+            if (t < BM) {
+                const int w = t >> 6;  // waves 0 and 1: 64 rows each, lane l -> row 64 w + l
+                const int64_t r = static_cast<int64_t>(blockIdx.x) * BM + t;
+                __builtin_amdgcn_global_load_lds(
+                    (const __attribute__((address_space(1))) void*)(p.vh_tv + r),
+                    (__attribute__((address_space(3))) void*)(xs + kVhWOff + kBN + 64 * w), 4, 0, 0);
+                __builtin_amdgcn_global_load_lds(
+                    (const __attribute__((address_space(1))) void*)(p.vh_ret + r),
+                    (__attribute__((address_space(3))) void*)(xs + kVhWOff + kBN + BM + 64 * w), 4, 0, 0);
             }
         }
     }
@@ -1018,6 +1066,137 @@ __device__ __forceinline__ void mlp_gemm_x6_body(GemmParams p, const uint4* __re
                     if (o < p.K && col < p.N) out[o * p.N + col] = red[o * kBN + col] + wacc[o][j];
                 }
         }
+    } else if constexpr (EPI == kEpiBiasEluOut && HEAD) {
+        // The critic's head with its backward.  V = ELU(acc + b) w^T + b_out exactly as the plain value-head epilogue
+        // below computes it (same operations, same order: the same bits), then dV = d loss / dV per row
+        // (value_loss_grad), then the output layer's backward over the H tile still in registers (acc holds H after
+        // the first pass): dZ = (dV w) * ELU'(H) -> p.c through the per-wave stage (whole-line stores), and this
+        // tile's partial row of p.wpart = [dW = sum dV H | db = sum dV | 0 pad] (out_bwd_valu_body's layout; the
+        // reduction order over the tile's rows differs).  dZ per element is out_bwd_valu_body's expression: the same
+        // bits.  H never reaches HBM, and the output layer's backward reads nothing back.
+        static_assert(NR == 1 && FULL && PL == 3, "value head: full x6 tiles, the VALU value head");
+        float* xsb = reinterpret_cast<float*>(lds_b0 + kXsOff);
+        float* wvl = xsb + kVhWOff;  // [N] value weights, column order
+        float* dvl = wvl + kBN;      // [BM] the tile's target values (prologue DMA), replaced by dV
+        const float* retl = dvl + BM;  // [BM] the tile's returns (prologue DMA)
+        float* red = reinterpret_cast<float*>(lds[1]);  // [wm][wn][i][32] V partials
+        float* stage = reinterpret_cast<float*>(lds[0]) + wave * 1024;
+#pragma unroll
+        for (int i = 0; i < I; ++i) {
+            float oval = 0.f;
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int cb = wn * 64 + j * 32 + 4 * h;
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const float4 b4 = *reinterpret_cast<const float4*>(xsb + cb + 8 * g);
+                    float t[4] = {acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
+                    t[0] += b4.x;
+                    t[1] += b4.y;
+                    t[2] += b4.z;
+                    t[3] += b4.w;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const float n = elu_neg(fminf(t[e], 0.f));
+                        acc[i][j][4 * g + e] = t[e] > 0.f ? t[e] : n;
+                    }
+                }
+                const float4* wl = reinterpret_cast<const float4*>(xsb + kBN) + 2 * ((((wn * 2 + j) * 2) * 2 + h) * kXsOut);
+#pragma unroll
+                for (int s2 = 0; s2 < 2; ++s2) {
+                    const float4* q = wl + 2 * (s2 * 2 * kXsOut);
+                    const float4 w0 = q[0], w1 = q[1];
+                    const float w[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+#pragma unroll
+                    for (int t = 0; t < 8; ++t) oval = fmaf(acc[i][j][8 * s2 + t], w[t], oval);
+                }
+            }
+            const float tsum = oval + __shfl_xor(oval, 32, 64);
+            if (h == 0) red[((wm * 4 + wn) * I + i) * 32 + l32] = tsum;
+        }
+        __syncthreads();
+        if (threadIdx.x < BM) {  // the four wn partials in the plain epilogue's order
+            const int rl = threadIdx.x;
+            const float tv = dvl[rl], ret = retl[rl];
+            const float* b = red + (rl >> 6) * 4 * I * 32 + ((rl & 63) >> 5) * 32 + (rl & 31);
+            const float sum = ((b[0] + b[I * 32]) + b[2 * I * 32]) + b[3 * I * 32];
+            const float V = sum + p.obias[0];
+            p.y[row0 + rl] = V;
+            dvl[rl] = value_loss_grad(V, tv, ret, p.vh_clipped, p.vh_clip, p.vh_g);
+        }
+        __syncthreads();
+        const int cq = lane & 7;
+        float* hred = reinterpret_cast<float*>(lds[1]) + 1024;  // [dZ sums wm 0, 1 | dW sums wm 0, 1][N]
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            float cs[4] = {0.f, 0.f, 0.f, 0.f}, wsum[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int i = 0; i < I; ++i) {
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const f32x4 hv = {acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
+                    *reinterpret_cast<f32x4*>(stage + l32 * 32 + 4 * ((2 * g + h) ^ ((l32 >> 1) & 7))) = hv;
+                }
+                __builtin_amdgcn_wave_barrier();  // one wave's LDS accesses execute in order
+                const int64_t trow = row0 + wm * (BM / 2) + i * 32;
+                float* ct = p.c + trow * p.N + (wn * 64 + j * 32);
+                const float4 w4 = *reinterpret_cast<const float4*>(wvl + wn * 64 + j * 32 + 4 * cq);
+                const float w[4] = {w4.x, w4.y, w4.z, w4.w};
+#pragma unroll 1
+                for (int k = 0; k < 4; ++k) {
+                    const int sr = 8 * k + (lane >> 3);
+                    const f32x4 hq = *reinterpret_cast<const f32x4*>(stage + sr * 32 + 4 * (cq ^ ((sr >> 1) & 7)));
+                    const float hh4[4] = {hq[0], hq[1], hq[2], hq[3]};
+                    const float dv = dvl[wm * (BM / 2) + i * 32 + sr];
+                    float o[4];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const float hh = hh4[e];
+                        const float z = __fmaf_rn(dv, w[e], 0.f);  // out_bwd_valu_body's fma chain of one term
+                        const float v = hh > 0.f ? z : z * (hh + 1.f);  // ELU'(x) = 1 if h > 0 else h + 1
+                        o[e] = v;
+                        cs[e] += v;
+                        wsum[e] = fmaf(dv, hh, wsum[e]);
+                    }
+                    const f32x4 ov = {o[0], o[1], o[2], o[3]};
+                    f32x4* dst = reinterpret_cast<f32x4*>(ct + static_cast<uint32_t>(sr * p.N + 4 * cq));
+                    if (p.nt) __builtin_nontemporal_store(ov, dst);
+                    else *dst = ov;
+                }
+                __builtin_amdgcn_wave_barrier();
+            }
+            // column sums over the wave's 64 rows: lanes of one column quad (lane & 7) differ in lane >> 3
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+#pragma unroll
+                for (int off = 8; off < 64; off <<= 1) {
+                    cs[e] += __shfl_xor(cs[e], off, 64);
+                    wsum[e] += __shfl_xor(wsum[e], off, 64);
+                }
+            if (lane < 8) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int col = wn * 64 + j * 32 + 4 * lane + e;
+                    hred[wm * kBN + col] = cs[e];
+                    hred[(2 + wm) * kBN + col] = wsum[e];
+                }
+            }
+        }
+        __syncthreads();
+        const int64_t tile_floats = (static_cast<int64_t>(p.N) + 1 + 3) / 4 * 4;  // dgrad_wgrad_tile_floats(1, N)
+        float* wp = p.wpart + static_cast<int64_t>(blockIdx.x) * tile_floats;
+        if (threadIdx.x < kBN) {
+            const int c = threadIdx.x;
+            wp[c] = hred[2 * kBN + c] + hred[3 * kBN + c];
+            if (p.colsum) p.colsum[static_cast<int64_t>(blockIdx.x) * p.N + c] = hred[c] + hred[kBN + c];
+        }
+        if (threadIdx.x < 64) {  // db = sum of the tile's dV (fixed butterfly order)
+            float sv = dvl[lane] + dvl[lane + 64];
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) sv += __shfl_xor(sv, off, 64);
+            if (lane == 0) wp[kBN] = sv;
+            else if (lane < static_cast<int>(tile_floats - kBN)) wp[kBN + lane] = 0.f;
+        }
     } else if constexpr (EPI == kEpiBiasEluOut) {
         // C^T tiles: lane (l32, h) holds row l32 of the tile, columns (r & 3) + 8 (r >> 2) + 4 h (r < 16).
         // h = ELU(acc + b) is stored (when wanted) as float4 column quads, split into bf16 planes in
@@ -1203,6 +1382,14 @@ __global__ __launch_bounds__(kThreads, MINW) void mlp_gemm_x6_kernel(GemmParams 
     __shared__ __attribute__((aligned(16))) char lds_b0[x6_buf_bytes<EPI, PL>()];
     __shared__ __attribute__((aligned(16))) char lds_b1[x6_buf_bytes<EPI, PL>()];
     mlp_gemm_x6_body<EPI, FULL, NR, PL, true, KCH>(p, bimg, lds_b0, lds_b1);
+}
+
+// The critic's last hidden layer + value head + d(value loss)/dV + the value head's backward (dZ of the last hidden
+// layer and the head's weight-gradient partials) in one launch (rslrl_value_head_fwd_bwd): full 128-row tiles, x6.
+__global__ __launch_bounds__(kThreads, 4) void mlp_gemm_x6_value_head_kernel(GemmParams p, const uint4* __restrict__ bimg) {
+    __shared__ __attribute__((aligned(16))) char lds_b0[x6_buf_bytes<kEpiBiasEluOut, 3>()];
+    __shared__ __attribute__((aligned(16))) char lds_b1[x6_buf_bytes<kEpiBiasEluOut, 3>()];
+    mlp_gemm_x6_body<kEpiBiasEluOut, true, 1, 3, true, 0, true>(p, bimg, lds_b0, lds_b1);
 }
 
 // the K = 48 kernel applies to full tiles of a forward on x6 operands with the deep loop enabled
@@ -2279,6 +2466,36 @@ int dgrad_params(const rslrl_linear_args_t* a, GemmParams& p) {
     return RSLRL_OK;
 }
 }  // namespace
+
+// The critic's last hidden layer, value head, value-loss gradient and value-head backward in one launch
+// (include/rslrl_amd.h).  Unsupported shapes return RSLRL_E_UNSUPPORTED before anything is launched (the caller
+// then runs the separate launches).
+extern "C" int rslrl_value_head_fwd_bwd(const rslrl_linear_args_t* a, const rslrl_value_head_args_t* v,
+                                        rslrl_stream_t stream) {
+    if (!a || !v || a->op != RSLRL_LINEAR_FWD_OUT) return RSLRL_E_INVALID_ARGUMENT;
+    GemmParams p;
+    const int rc = out_params(a, p);
+    if (rc) return rc;
+    if (a->arith != RSLRL_ARITH_X6 || a->nout != 1 || a->N != kBN || a->K != 16 * kKC || a->M % kBM != 0 || !p.deep)
+        return RSLRL_E_UNSUPPORTED;
+    if (!a->c || !v->target_values || !v->returns || !v->out_weight || !v->wgrad_partials)
+        return RSLRL_E_INVALID_ARGUMENT;
+    if (!aligned16(v->out_weight)) return RSLRL_E_MISALIGNED;
+    p.vh_tv = v->target_values;
+    p.vh_ret = v->returns;
+    p.vh_w = v->out_weight;
+    p.vh_clip = v->clip_param;
+    p.vh_g = v->value_loss_coef / static_cast<float>(a->M);  // the loss kernel's g_value (ppo_loss.hip)
+    p.vh_clipped = v->use_clipped_value_loss ? 1 : 0;
+    p.wpart = v->wgrad_partials;
+    p.colsum = v->colsum_partials;
+    if (a->M == 0) return RSLRL_OK;
+    const int64_t tiles = ceil_div(a->M, kBM);
+    if (tiles > INT32_MAX) return RSLRL_E_INVALID_ARGUMENT;
+    hipLaunchKernelGGL(mlp_gemm_x6_value_head_kernel, dim3(static_cast<unsigned>(tiles)), dim3(kThreads), 0,
+                       reinterpret_cast<hipStream_t>(stream), p, static_cast<const uint4*>(a->bimage));
+    return launch_status();
+}
 
 // Two forward problems of one shape (op, arithmetic, M, K, N) in one launch -- e.g. the actor's and the
 // critic's layer l in the rollout.  Each keeps its own operands, bias, output, amax and amax workspace.

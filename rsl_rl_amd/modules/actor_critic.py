@@ -144,21 +144,26 @@ class ActorCritic(nn.Module):
         lin = [m for m in mlp if isinstance(m, nn.Linear)]
         return [m.weight for m in lin], [m.bias for m in lin]
 
-    def train_forward(self, obs, side_stream=None):
+    def train_forward(self, obs, side_stream=None, value_head=None):
         """The update's forward (ppo.py:246-253) without an autograd graph: returns (mean [B, A], sigma, value
         [B, 1], tape) with sigma the shared [A] std (scalar / exp(log_std)) or the per-row [B, A] std of a
         state-dependent head (strided views of the actor output).  Call under torch.no_grad().
 
         side_stream: a second stream of the device for the critic's MLP -- the actor's and the critic's launch
         chains are independent, so each fills the other's launch tails; the current stream waits for it before
-        returning (the results are the same values either way)."""
+        returning (the results are the same values either way).
+
+        value_head: a fused_mlp.ValueHead of the mini-batch (target values, returns, value-loss settings): the critic's
+        last launch then also computes d(value loss)/dV and the value head's backward (networks/fused_mlp.py
+        value_head_fwd_bwd; paired passes only) -- train_backward then takes the critic's gradient from the tape."""
         a_obs = self.actor_obs_normalizer(self.get_actor_obs(obs))
         c_obs = self.critic_obs_normalizer(self.get_critic_obs(obs))
         a_obs = a_obs if a_obs.is_contiguous() else a_obs.contiguous()
         c_obs = c_obs if c_obs.is_contiguous() else c_obs.contiguous()
         pair = None
         if side_stream is None:  # the actor's and the critic's same-shape layers batched into one launch each
-            pair = fused_mlp.train_forward_pair(a_obs, *self._linears(self.actor), c_obs, *self._linears(self.critic))
+            pair = fused_mlp.train_forward_pair(a_obs, *self._linears(self.actor), c_obs, *self._linears(self.critic),
+                                                value_head=value_head)
         if pair is not None:
             y, tape_a, value, tape_c = pair
         elif side_stream is not None:
@@ -220,6 +225,9 @@ class ActorCritic(nn.Module):
                 outs = [[(slot(w), slot(b)) for w, b in zip(*self._linears(m))] for m in (self.actor, self.critic)]
                 if fused_mlp.train_backward_pair(tape_a, dy, outs[0], tape_c, g_value.reshape(-1, 1), outs[1]):
                     return
+            if tape_c.head is not None:
+                raise RuntimeError("train_backward: the critic's head ran fused (value_head) but the paired backward "
+                                   "does not apply to these gradient destinations")
             run(self.actor, tape_a, dy)
             run(self.critic, tape_c, g_value.reshape(-1, 1), g_value_padded)
             return

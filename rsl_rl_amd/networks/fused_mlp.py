@@ -288,6 +288,49 @@ def linear_fwd_out_pair(xs, bs, N: int, imgs, b_outs, out_imgs, store_h: bool):
     return hs, ys
 
 
+class ValueHead:
+    """What the critic's fused head (value_head_fwd_bwd) needs from the PPO loss of the mini-batch: its target values
+    and returns and the value-loss configuration (ppo.py:305-313)."""
+
+    __slots__ = ("target_values", "returns", "clip_param", "value_loss_coef", "use_clipped")
+
+    def __init__(self, target_values, returns, clip_param, value_loss_coef, use_clipped):
+        self.target_values, self.returns = target_values, returns
+        self.clip_param, self.value_loss_coef, self.use_clipped = clip_param, value_loss_coef, use_clipped
+
+
+_VALUE_HEAD = os.environ.get("RSLRL_VALUE_HEAD", "1") != "0"
+
+
+def value_head_fwd_bwd(x, b, N: int, img, b_out, out_img, w_out, head: ValueHead):
+    """The critic's last hidden layer, value head, d(value loss)/dV and the head's backward in one launch
+    (rslrl_value_head_fwd_bwd): returns (dz [M, N], y [M, 1], wpart [tiles, P]) -- dz the gradient at the last hidden
+    layer's pre-activation, y the values (the bits linear_fwd_out_ex gives), wpart the head's [dW | db] partials for
+    the fold -- or None when the shape is not covered (nothing launched)."""
+    M, K = x.shape
+    tv, ret = head.target_values, head.returns
+    if (w_out.shape[0] != 1 or not w_out.is_contiguous() or w_out.data_ptr() % 16 or tv.numel() != M
+            or ret.numel() != M or not tv.is_contiguous() or not ret.is_contiguous()):
+        return None
+    L = _lib.lib()
+    tiles = L.rslrl_linear_tiles(M)
+    P = (N + 1 + 3) // 4 * 4
+    dz = torch.empty(M, N, device=x.device, dtype=torch.float32)
+    y = torch.empty(M, 1, device=x.device, dtype=torch.float32)
+    wpart = torch.empty(tiles, P, device=x.device, dtype=torch.float32)
+    args = _gemm_args(_lib.LINEAR_FWD_OUT, _lib.ARITH_X6, x, None, N, img, bias=b, c=dz, out_img=out_img,
+                      out_bias=b_out, y=y, nout=1)
+    vargs = _lib.ValueHeadArgs(tv.data_ptr(), ret.data_ptr(), w_out.data_ptr(), float(head.clip_param),
+                               float(head.value_loss_coef), int(bool(head.use_clipped)), wpart.data_ptr(), None)
+    with timer.span(f"linear_value_head[M={M},K={K},N={N}]", x.device, 4 * M * (K + N + 3) + 4 * tiles * P,
+                    2 * M * N * (K + 2)):
+        rc = L.rslrl_value_head_fwd_bwd(ctypes.byref(args), ctypes.byref(vargs), _stream(x))
+    if rc == _lib.E_UNSUPPORTED:
+        return None
+    _lib.check(rc, "rslrl_value_head_fwd_bwd")
+    return dz, y, wpart
+
+
 def _fuse_out_fwd(ws) -> bool:
     """The last hidden layer and the output layer run as one linear_fwd_out launch (split modes only)."""
     return _FUSE_OUT_FWD and _split() and len(ws) >= 2 and ws[-1].shape[0] <= MAX_OUT_WIDTH \
@@ -434,6 +477,33 @@ def linear_dgrad_elu_wgrad_pair(dzs, hs, imgs, dwb_outs=(None, None), defer=None
         _lib.check(rc, "rslrl_fold_partials_ex")
         res.append((outs[i], dwbs[i][: N * K].view(N, K), dwbs[i][N * K:]))
     return res
+
+
+def linear_dgrad_elu_wgrad_deferred(dz, h, img, dwb_out, defer):
+    """linear_dgrad_elu_wgrad (want_db_prev=False, no amax) of one output layer with its fold queued on `defer` (a
+    _FoldBatch); bit-identical input gradient to problem 0 of linear_dgrad_elu_wgrad_pair.  Returns (dz_prev, dw, db)
+    (dw, db valid after defer.run())."""
+    M, N = dz.shape
+    K = h.shape[1]
+    tiles = _lib.lib().rslrl_linear_tiles(M)
+    P = (N * K + N + 3) // 4 * 4
+    out = torch.empty(M, K, device=dz.device, dtype=torch.float32)
+    wpart = torch.empty(tiles, P, device=dz.device, dtype=torch.float32)
+    dwb = _out_or_empty(dwb_out, (N * K + N,), dz.device)
+    with timer.span(f"linear_dgrad_wgrad[M={M},Nred={N},K={K}]", dz.device, 4 * M * (N + 2 * K), 4 * M * K * N):
+        _gemm(_lib.LINEAR_DGRAD_ELU_WGRAD, _lib.ARITH_X6, dz, None, K, img, h=h, c=out, wpart=wpart)
+    defer.add(wpart, tiles, P, dwb, N * K + N)
+    return out, dwb[: N * K].view(N, K), dwb[N * K:]
+
+
+def _head_result(tape, dwb_out, defer):
+    """(dz_prev, dw, db) of a critic tape whose head ran value_head_fwd_bwd: its dz, and the fold of its partials
+    queued on `defer`."""
+    dz, wpart = tape.head
+    K = dz.shape[1]
+    dwb = _out_or_empty(dwb_out, (K + 1,), dz.device)
+    defer.add(wpart, wpart.shape[0], wpart.shape[1], dwb, K + 1)
+    return dz, dwb[:K].view(1, K), dwb[K:]
 
 
 def linear_wgrad(dz, x, arith=_lib.ARITH_X6, dz_amax=None, x_amax=None, out=None, bias_side=0, dwb_out=None):
@@ -618,10 +688,11 @@ class MLPTape:
     """What the backward of one MLP pass needs: the layer inputs (hs[l] = input of linear l), the weights, the
     transposed B images of the input gradients, the published max |H| of h3 layers and the per-layer plan."""
 
-    __slots__ = ("hs", "ws", "dgrad_imgs", "amaxes", "h3", "x6")
+    __slots__ = ("hs", "ws", "dgrad_imgs", "amaxes", "h3", "x6", "head")
 
-    def __init__(self, hs, ws, dgrad_imgs, amaxes, h3, x6):
+    def __init__(self, hs, ws, dgrad_imgs, amaxes, h3, x6, head=None):
         self.hs, self.ws, self.dgrad_imgs, self.amaxes, self.h3, self.x6 = hs, ws, dgrad_imgs, amaxes, h3, x6
+        self.head = head  # (dz of the last hidden layer, the head's weight-gradient partials): value_head_fwd_bwd
 
 
 def train_forward(x, ws, bs):
@@ -791,11 +862,15 @@ def _pairable(ws_a, ws_c, x_a, x_c) -> bool:
     return all(w.shape[0] <= 16 and w.shape[1] <= MAX_WIDTH for w in (ws_a[-1], ws_c[-1]))
 
 
-def train_forward_pair(x_a, ws_a, bs_a, x_c, ws_c, bs_c):
+def train_forward_pair(x_a, ws_a, bs_a, x_c, ws_c, bs_c, value_head: ValueHead | None = None):
     """train_forward of the actor (x_a, ws_a, bs_a) and the critic (x_c, ...) with each same-shape hidden layer of the
     two in one launch (rslrl_linear_gemm_pair) and every B image of both passes in one launch; the output layers run
     as two fused launches.  Values identical to two train_forward calls.  Returns (y_a, tape_a, y_c, tape_c), or None
-    when the pair does not qualify (_pairable)."""
+    when the pair does not qualify (_pairable).
+
+    value_head: the mini-batch's value-loss inputs -- the critic's last launch then also runs the value loss's gradient
+    and the value head's backward (value_head_fwd_bwd): its tape carries the last hidden layer's dz instead of that
+    layer's activation, and train_backward_pair ignores the critic's dy (the same values the loss kernel writes)."""
     if not _pairable(ws_a, ws_c, x_a, x_c):
         return None
     ws, bs, xs = (ws_a, ws_c), (bs_a, bs_c), (x_a, x_c)
@@ -813,17 +888,25 @@ def train_forward_pair(x_a, ws_a, bs_a, x_c, ws_c, bs_c):
     h = [x if x.is_contiguous() else x.contiguous() for x in xs]
     hs = [[h[0]], [h[1]]]
     y = [None, None]
+    head = None
     for l in range(nh):
         if l < nh - 1:
             h, _ = linear_fwd_pair(h, [bs[0][l], bs[1][l]], ws[0][l].shape[0], True, [fwd[0][l], fwd[1][l]],
                                    _lib.ARITH_X6, [None, None], [False, False])
         else:
             for i in range(2):
+                if i == 1 and value_head is not None and _VALUE_HEAD:
+                    res = value_head_fwd_bwd(h[1], bs[1][l], ws[1][l].shape[0], fwd[1][l], bs[1][-1], out_img[1],
+                                             ws[1][-1], value_head)
+                    if res is not None:
+                        head, y[1], h[1] = (res[0], res[2]), res[1], None
+                        continue
                 h[i], y[i] = linear_fwd_out_ex(h[i], bs[i][l], ws[i][l].shape[0], fwd[i][l], _lib.ARITH_X6, None,
                                                bs[i][-1], out_img[i], store_h=True)
         for i in range(2):
             hs[i].append(h[i])
     tapes = [MLPTape(hs[i], list(ws[i]), dgr[i], [None] * (nh + 1), h3, True) for i in range(2)]
+    tapes[1].head = head
     return y[0], tapes[0], y[1], tapes[1]
 
 
@@ -852,8 +935,12 @@ def train_backward_pair(tape_a, dy_a, outs_a, tape_c, dy_c, outs_c):
         adjacent.append(adj)
         dwb_outs.append(torch.as_strided(wo, (nred * K + nred,), (1,)) if adj else None)
     folds = _FoldBatch()
-    res = linear_dgrad_elu_wgrad_pair(ds, [t.hs[L - 1] for t in tapes], [t.dgrad_imgs[L - 1] for t in tapes],
-                                      dwb_outs, defer=folds)
+    if tape_c.head is not None:  # the critic's head ran its backward in the forward launch (value_head_fwd_bwd)
+        res = [linear_dgrad_elu_wgrad_deferred(ds[0], tape_a.hs[L - 1], tape_a.dgrad_imgs[L - 1], dwb_outs[0], folds),
+               _head_result(tape_c, dwb_outs[1], folds)]
+    else:
+        res = linear_dgrad_elu_wgrad_pair(ds, [t.hs[L - 1] for t in tapes], [t.dgrad_imgs[L - 1] for t in tapes],
+                                          dwb_outs, defer=folds)
     dz = [r[0] for r in res]
     for i in range(2):
         if not adjacent[i]:
