@@ -1079,10 +1079,25 @@ __device__ __forceinline__ void mlp_gemm_x6_body(GemmParams p, const uint4* __re
         float* wvl = xsb + kVhWOff;  // [N] value weights, column order
         float* dvl = wvl + kBN;      // [BM] the tile's target values (prologue DMA), replaced by dV
         const float* retl = dvl + BM;  // [BM] the tile's returns (prologue DMA)
-        float* red = reinterpret_cast<float*>(lds[1]);  // [wm][wn][i][32] V partials
-        float* stage = reinterpret_cast<float*>(lds[0]) + wave * 1024;
+        float* red = reinterpret_cast<float*>(lds[1]);  // [wm][wn][i][32] V partials (2 KiB)
+        float* hred = reinterpret_cast<float*>(lds[1]) + 1024;  // [dZ sums wm 0, 1 | dW sums wm 0, 1][N] (4 KiB)
+        // two 32 x 32 H blocks per wave in LDS (the i = 1 row of blocks, written in the first pass: 32 registers fewer
+        // held through the dV step): area A = buffer 0 (block j = 1), area B = buffer 1 past red / hred (block j = 0);
+        // each later stages one of the wave's i = 0 blocks.  Layout of the whole-line store stage: float4 column quads
+        // XOR-swizzled by (row >> 1) & 7.
+        float* const area0 = reinterpret_cast<float*>(lds[1] + 8192) + wave * 1024;
+        float* const area1 = reinterpret_cast<float*>(lds[0]) + wave * 1024;
+        static_assert(8192 + 8 * 4096 <= bufBytes, "value head: H blocks in LDS");
+        auto stage_block = [&](float* blk, f32x16 v) {
 #pragma unroll
-        for (int i = 0; i < I; ++i) {
+            for (int g = 0; g < 4; ++g) {
+                const f32x4 hv = {v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]};
+                *reinterpret_cast<f32x4*>(blk + l32 * 32 + 4 * ((2 * g + h) ^ ((l32 >> 1) & 7))) = hv;
+            }
+        };
+#pragma unroll
+        for (int ii = 0; ii < I; ++ii) {
+            const int i = I - 1 - ii;  // the parked row of blocks first: its registers die before the other's H forms
             float oval = 0.f;
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
@@ -1110,6 +1125,7 @@ __device__ __forceinline__ void mlp_gemm_x6_body(GemmParams p, const uint4* __re
 #pragma unroll
                     for (int t = 0; t < 8; ++t) oval = fmaf(acc[i][j][8 * s2 + t], w[t], oval);
                 }
+                if (i == I - 1) stage_block(j ? area1 : area0, acc[i][j]);
             }
             const float tsum = oval + __shfl_xor(oval, 32, 64);
             if (h == 0) red[((wm * 4 + wn) * I + i) * 32 + l32] = tsum;
@@ -1126,45 +1142,43 @@ __device__ __forceinline__ void mlp_gemm_x6_body(GemmParams p, const uint4* __re
         }
         __syncthreads();
         const int cq = lane & 7;
-        float* hred = reinterpret_cast<float*>(lds[1]) + 1024;  // [dZ sums wm 0, 1 | dW sums wm 0, 1][N]
+        // dZ of one staged block (i, j): lane (row 8 k + lane >> 3, column quad cq) -> whole-line stores
+        auto block_bwd = [&](const float* blk, int i, int j, float (&cs)[4], float (&wsum)[4]) {
+            const int64_t trow = row0 + wm * (BM / 2) + i * 32;
+            float* ct = p.c + trow * p.N + (wn * 64 + j * 32);
+            const float4 w4 = *reinterpret_cast<const float4*>(wvl + wn * 64 + j * 32 + 4 * cq);
+            const float w[4] = {w4.x, w4.y, w4.z, w4.w};
+#pragma unroll 1
+            for (int k = 0; k < 4; ++k) {
+                const int sr = 8 * k + (lane >> 3);
+                const f32x4 hq = *reinterpret_cast<const f32x4*>(blk + sr * 32 + 4 * (cq ^ ((sr >> 1) & 7)));
+                const float hh4[4] = {hq[0], hq[1], hq[2], hq[3]};
+                const float dv = dvl[wm * (BM / 2) + i * 32 + sr];
+                float o[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float hh = hh4[e];
+                    const float z = __fmaf_rn(dv, w[e], 0.f);  // out_bwd_valu_body's fma chain of one term
+                    const float v = hh > 0.f ? z : z * (hh + 1.f);  // ELU'(x) = 1 if h > 0 else h + 1
+                    o[e] = v;
+                    cs[e] += v;
+                    wsum[e] = fmaf(dv, hh, wsum[e]);
+                }
+                const f32x4 ov = {o[0], o[1], o[2], o[3]};
+                f32x4* dst = reinterpret_cast<f32x4*>(ct + static_cast<uint32_t>(sr * p.N + 4 * cq));
+                if (p.nt) __builtin_nontemporal_store(ov, dst);
+                else *dst = ov;
+            }
+        };
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             float cs[4] = {0.f, 0.f, 0.f, 0.f}, wsum[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int i = 0; i < I; ++i) {
-#pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    const f32x4 hv = {acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
-                    *reinterpret_cast<f32x4*>(stage + l32 * 32 + 4 * ((2 * g + h) ^ ((l32 >> 1) & 7))) = hv;
-                }
-                __builtin_amdgcn_wave_barrier();  // one wave's LDS accesses execute in order
-                const int64_t trow = row0 + wm * (BM / 2) + i * 32;
-                float* ct = p.c + trow * p.N + (wn * 64 + j * 32);
-                const float4 w4 = *reinterpret_cast<const float4*>(wvl + wn * 64 + j * 32 + 4 * cq);
-                const float w[4] = {w4.x, w4.y, w4.z, w4.w};
-#pragma unroll 1
-                for (int k = 0; k < 4; ++k) {
-                    const int sr = 8 * k + (lane >> 3);
-                    const f32x4 hq = *reinterpret_cast<const f32x4*>(stage + sr * 32 + 4 * (cq ^ ((sr >> 1) & 7)));
-                    const float hh4[4] = {hq[0], hq[1], hq[2], hq[3]};
-                    const float dv = dvl[wm * (BM / 2) + i * 32 + sr];
-                    float o[4];
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        const float hh = hh4[e];
-                        const float z = __fmaf_rn(dv, w[e], 0.f);  // out_bwd_valu_body's fma chain of one term
-                        const float v = hh > 0.f ? z : z * (hh + 1.f);  // ELU'(x) = 1 if h > 0 else h + 1
-                        o[e] = v;
-                        cs[e] += v;
-                        wsum[e] = fmaf(dv, hh, wsum[e]);
-                    }
-                    const f32x4 ov = {o[0], o[1], o[2], o[3]};
-                    f32x4* dst = reinterpret_cast<f32x4*>(ct + static_cast<uint32_t>(sr * p.N + 4 * cq));
-                    if (p.nt) __builtin_nontemporal_store(ov, dst);
-                    else *dst = ov;
-                }
-                __builtin_amdgcn_wave_barrier();
-            }
+            float* const blk = j ? area1 : area0;
+            block_bwd(blk, I - 1, j, cs, wsum);  // the block parked in the first pass
+            __builtin_amdgcn_wave_barrier();     // one wave's LDS accesses execute in order
+            stage_block(blk, acc[0][j]);         // then block (0, j) through the same area
+            __builtin_amdgcn_wave_barrier();
+            block_bwd(blk, 0, j, cs, wsum);
             // column sums over the wave's 64 rows: lanes of one column quad (lane & 7) differ in lane >> 3
 #pragma unroll
             for (int e = 0; e < 4; ++e)
