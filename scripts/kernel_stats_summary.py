@@ -22,7 +22,8 @@ FAMILIES = [
     ("colsum_fold", r"colsum_fold"),
     ("ppo_loss", r"ppo_loss_kernel"),
     ("gae_scan", r"gae_scan_kernel"),
-    ("adv_normalize", r"adv_normalize_kernel|moments_kernel"),
+    ("adv_normalize (+ record slots)", r"adv_normalize_kernel|adv_normalize_slot_kernel|moments_kernel"),
+    ("x6 value head (fwd + d value loss + head bwd)", r"value_head_kernel"),
     ("gather_rows", r"gather_rows_kernel|gather_records_kernel"),
     ("record_fill_slot", r"record_fill_slot_kernel"),
     ("hipBLASLt GEMM", r"^Cijk_"),

@@ -21,6 +21,10 @@ SHORT = {
     "ppo_loss_quad_kernel": "ppo_loss",
     "gae_scan_kernel": "gae_scan",
     "adv_normalize_kernel": "adv_normalize",
+    "adv_normalize_slot_kernel": "adv_normalize_slot",
+    "mlp_gemm_x6_value_head_kernel": "x6_value_head",
+    "out_bwd_valu_kernel": "out_bwd",
+    "out_bwd_valu_pair_kernel": "out_bwd_pair",
     "moments_kernel": "moments",
     "gather_rows_kernel": "gather_rows",
     "gather_records_kernel": "gather_rows",
