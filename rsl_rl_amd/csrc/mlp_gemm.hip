@@ -1870,7 +1870,10 @@ __device__ __forceinline__ void out_bwd_valu_body(const GemmParams& p, const uin
     }
     const int64_t row0 = static_cast<int64_t>(blockIdx.x) * kBM + rg * RPW;
     const int64_t rows = p.M - row0 < RPW ? (p.M - row0 > 0 ? p.M - row0 : 0) : RPW;
-    constexpr int U = 4;  // rows of H in flight per wave
+#ifndef RSLRL_OUTBWD_U
+#define RSLRL_OUTBWD_U 4  // (8: 188.4 us, 16: 223 us, 4: 185.5 us -- the actor's 393,216 rows, scripts/outbwd_u_ab.sh)
+#endif
+    constexpr int U = RSLRL_OUTBWD_U;  // rows of H in flight per wave
     for (int r0 = 0; r0 < rows; r0 += U) {
         vec hv[U];
 #pragma unroll
