@@ -31,7 +31,7 @@ extern "C" {
 
 typedef struct ihipStream_t* rslrl_stream_t; /* == hipStream_t */
 
-#define RSLRL_ABI_VERSION 10
+#define RSLRL_ABI_VERSION 11
 
 enum {
     RSLRL_OK = 0,
@@ -599,6 +599,17 @@ int rslrl_rnd_update(const rslrl_rnd_update_args_t* args /* host struct */, void
 int rslrl_synthetic_env_step(float* obs, int32_t num_obs, float* rewards, int64_t* dones, float* time_outs,
                              int64_t* episode_length, int64_t N, uint64_t seed, uint32_t step, float done_prob,
                              float timeout_prob, int64_t max_episode_length, rslrl_stream_t stream);
+
+/* ------------------------------------------------------------------------------------------------
+ * Live launch timing (measurement, not a reference interface; ABI 11): rslrl_launch_timing_enable(capacity > 0)
+ * arms the next `capacity` launches of the PPO loss kernel (rslrl_ppo_loss_fwd_bwd's quad-layout path) to carry a
+ * (start, stop) HIP event pair bound to the dispatch itself (hipExtLaunchKernel), so each elapsed time is the
+ * kernel's begin-to-end duration as rocprofv3 reports it; launches on a capturing stream are never bound.
+ * capacity 0 disarms and keeps the recorded launches.  rslrl_launch_timing_read synchronises the recorded
+ * events and returns their summed duration (ms) and count.
+ * ----------------------------------------------------------------------------------------------*/
+int rslrl_launch_timing_enable(int32_t capacity);
+int rslrl_launch_timing_read(double* total_ms, int64_t* launches);
 
 #ifdef __cplusplus
 }

@@ -19,7 +19,7 @@ import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 # RSLRL_AMD_LIB: an alternative in-tree build of the same library (A/B kernel experiments)
 LIB_PATH = os.environ.get("RSLRL_AMD_LIB") or os.path.join(LIB_DIR, "librslrl_amd.so")
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 # symbols declared in include/rslrl_amd.h (tests/test_capi.py checks the header against this list)
 EXPORTED_SYMBOLS = (
@@ -77,6 +77,8 @@ EXPORTED_SYMBOLS = (
     "rslrl_rnd_update_workspace_bytes",
     "rslrl_rnd_update",
     "rslrl_synthetic_env_step",
+    "rslrl_launch_timing_enable",
+    "rslrl_launch_timing_read",
 )
 
 MAX_GATHER_FIELDS = 16
@@ -430,6 +432,10 @@ def _declare(L):
     L.rslrl_rnd_update.argtypes = [ctypes.POINTER(RndUpdateArgs), P, SZ, P]
     L.rslrl_synthetic_env_step.restype = ctypes.c_int
     L.rslrl_synthetic_env_step.argtypes = [P, I32, P, P, P, P, I64, ctypes.c_uint64, ctypes.c_uint32, F, F, I64, P]
+    L.rslrl_launch_timing_enable.restype = ctypes.c_int
+    L.rslrl_launch_timing_enable.argtypes = [I32]
+    L.rslrl_launch_timing_read.restype = ctypes.c_int
+    L.rslrl_launch_timing_read.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)]
 
 
 def lib():

@@ -15,9 +15,15 @@
 // Bytes per sample (sigma shared): read 4A (mu) + 4A (actions) + 8A (old mu, sigma) + 20 (old_logp,
 // adv, target V, returns, V), write 4A (d mu) + 4 (d V) = 20A + 24.
 
+#include <hip/hip_ext.h>
+
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
+#include <mutex>
 #include <string>
+#include <utility>
+#include <vector>
 
 #include "common.h"
 
@@ -988,19 +994,59 @@ int loss_depth() {
     return (e && e[0] == '2') ? 2 : 1;
 }
 
+// Live launch timing (rslrl_launch_timing_*, bench.py's roofline): while armed, each quad-kernel launch is bound to
+// a (start, stop) event pair through hipExtLaunchKernelGGL, so the elapsed time is the dispatch's own begin / end --
+// the duration rocprofv3 reports -- rather than a marker-event span around the C-ABI call (which adds the dispatch
+// latency of the markers, ~3-5 us on a ~30 us kernel).  Never bound while the stream is being captured.
+struct LaunchTiming {
+    std::mutex mu;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> pool;
+    size_t used = 0, cap = 0;
+    std::atomic<bool> on{false};
+};
+
+LaunchTiming& launch_timing() {
+    static LaunchTiming t;
+    return t;
+}
+
+template <typename K, typename... Args>
+void launch_timed(K kernel, dim3 g, dim3 b, hipStream_t st, Args... args) {
+    LaunchTiming& t = launch_timing();
+    if (t.on.load(std::memory_order_relaxed)) {
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        if (hipStreamIsCapturing(st, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone) {
+            hipEvent_t e0 = nullptr, e1 = nullptr;
+            {
+                std::lock_guard<std::mutex> lk(t.mu);
+                if (t.used < t.cap) {
+                    e0 = t.pool[t.used].first;
+                    e1 = t.pool[t.used].second;
+                    ++t.used;
+                }
+            }
+            if (e0) {
+                hipExtLaunchKernelGGL(kernel, g, b, 0, st, e0, e1, 0, args...);
+                return;
+            }
+        }
+    }
+    hipLaunchKernelGGL(kernel, g, b, 0, st, args...);
+}
+
 template <int APL>
 void launch_quad(const LossParams& p, int nb, double* part, unsigned* tickets, float cv, float ce, hipStream_t st) {
     const dim3 g(nb), b(kBlock);
     if (p.sigma_mode == 0 && p.compute_kl && loss_depth() == 2)
-        hipLaunchKernelGGL((ppo_loss_quad_kernel<APL, true, true, 2>), g, b, 0, st, p, part, tickets, cv, ce);
+        launch_timed(ppo_loss_quad_kernel<APL, true, true, 2>, g, b, st, p, part, tickets, cv, ce);
     else if (p.sigma_mode == 0 && p.compute_kl)
-        hipLaunchKernelGGL((ppo_loss_quad_kernel<APL, true, true>), g, b, 0, st, p, part, tickets, cv, ce);
+        launch_timed(ppo_loss_quad_kernel<APL, true, true>, g, b, st, p, part, tickets, cv, ce);
     else if (p.sigma_mode == 0)
-        hipLaunchKernelGGL((ppo_loss_quad_kernel<APL, true, false>), g, b, 0, st, p, part, tickets, cv, ce);
+        launch_timed(ppo_loss_quad_kernel<APL, true, false>, g, b, st, p, part, tickets, cv, ce);
     else if (p.compute_kl)
-        hipLaunchKernelGGL((ppo_loss_quad_kernel<APL, false, true>), g, b, 0, st, p, part, tickets, cv, ce);
+        launch_timed(ppo_loss_quad_kernel<APL, false, true>, g, b, st, p, part, tickets, cv, ce);
     else
-        hipLaunchKernelGGL((ppo_loss_quad_kernel<APL, false, false>), g, b, 0, st, p, part, tickets, cv, ce);
+        launch_timed(ppo_loss_quad_kernel<APL, false, false>, g, b, st, p, part, tickets, cv, ce);
 }
 
 template <int MAXA, bool EXACT>
@@ -1185,4 +1231,46 @@ extern "C" int rslrl_ppo_update_tail(const float* stats, const float* kl, double
     hipLaunchKernelGGL(ppo_tail_kernel, dim3(1), dim3(64), 0, reinterpret_cast<hipStream_t>(stream), stats, kl, lr,
                        lr32, round_fp32, kl_hi, kl_lo, sums);
     return launch_status();
+}
+
+extern "C" int rslrl_launch_timing_enable(int32_t capacity) {
+    if (capacity < 0) return RSLRL_E_INVALID_ARGUMENT;
+    LaunchTiming& t = launch_timing();
+    std::lock_guard<std::mutex> lk(t.mu);
+    if (capacity == 0) {  // disarm; the recorded launches stay readable
+        t.on.store(false);
+        return RSLRL_OK;
+    }
+    t.on.store(false);
+    while (t.pool.size() < static_cast<size_t>(capacity)) {
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        hipError_t err = hipEventCreate(&e0);
+        if (err == hipSuccess) err = hipEventCreate(&e1);
+        if (err != hipSuccess) {
+            if (e0) (void)hipEventDestroy(e0);
+            return static_cast<int>(err);
+        }
+        t.pool.emplace_back(e0, e1);
+    }
+    t.used = 0;
+    t.cap = static_cast<size_t>(capacity);
+    t.on.store(true);
+    return RSLRL_OK;
+}
+
+extern "C" int rslrl_launch_timing_read(double* total_ms, int64_t* launches) {
+    if (!total_ms || !launches) return RSLRL_E_INVALID_ARGUMENT;
+    LaunchTiming& t = launch_timing();
+    std::lock_guard<std::mutex> lk(t.mu);
+    double sum = 0.0;
+    for (size_t i = 0; i < t.used; ++i) {
+        hipError_t err = hipEventSynchronize(t.pool[i].second);
+        float ms = 0.0f;
+        if (err == hipSuccess) err = hipEventElapsedTime(&ms, t.pool[i].first, t.pool[i].second);
+        if (err != hipSuccess) return static_cast<int>(err);
+        sum += static_cast<double>(ms);
+    }
+    *total_ms = sum;
+    *launches = static_cast<int64_t>(t.used);
+    return RSLRL_OK;
 }

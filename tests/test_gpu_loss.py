@@ -231,3 +231,36 @@ def test_quad_kernel_pipeline_depth_bit_identical(cuda_device, monkeypatch):
         out.append([t.clone() for t in res])
     for a, b in zip(*out):
         assert torch.equal(a, b)
+
+
+def test_launch_bound_event_timing(cuda_device, monkeypatch):
+    """rslrl_launch_timing_*: while armed, each quad-kernel launch carries its own event pair (one record per
+    launch, up to the capacity); the results are the same bits as an unarmed launch; each bound duration is positive
+    and no longer than the marker span around the C-ABI call; disarming keeps the records readable."""
+    monkeypatch.setenv("RSLRL_LOSS_KERNEL", "quad")
+    torch.manual_seed(9)
+    B, A, d = 393216, 12, cuda_device
+    mu, x, omu = (torch.randn(B, A, device=d) for _ in range(3))
+    osig = (0.5 + torch.rand(A, device=d)).expand(B, A).contiguous()
+    sigma = 0.5 + torch.rand(A, device=d)
+    V, old_logp, adv, tv, R = (torch.randn(B, 1, device=d) for _ in range(5))
+    args = (mu, sigma, V, x, old_logp, adv, tv, R, omu, osig)
+    plain = [t.clone() for t in kernels.ppo_loss_fwd_bwd(*args)]
+    kernels.timer.arm_launch_events(3)
+    try:
+        spans = []
+        for _ in range(4):  # the 4th launch is past the capacity: unbound
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            out = kernels.ppo_loss_fwd_bwd(*args)
+            e.record()
+            spans.append((s, e))
+        torch.cuda.synchronize()
+    finally:
+        kernels.timer.disarm_launch_events()
+    for a, b in zip(plain, out):
+        assert torch.equal(a, b)
+    total_ms, n = kernels.timer.launch_events()
+    assert n == 3
+    span_ms = sum(s.elapsed_time(e) for s, e in spans[:3])
+    assert 0.0 < total_ms <= span_ms * 1.001
