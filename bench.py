@@ -1,6 +1,6 @@
 """PPO env-steps/sec (rollout + GAE + update) on MI355X -- BASELINE.json's headline metric.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W]     (N > 1: starts its own N ranks via torch.distributed.run)
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...
 
 Workload.  N=1 (the metric's configuration, C3 = BASELINE.json configs[2]): 65536 synthetic envs, T=24 steps/env,
@@ -175,6 +175,28 @@ def cpu_baseline(args):
     }
 
 
+def _free_port():
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n):
+    """One process per GPU for `python bench.py --gpus N` run without a launcher: torch.distributed.run as a child
+    process (one node, N ranks, rendezvous on 127.0.0.1) re-running this script with the same arguments; each rank
+    reads RANK / LOCAL_RANK / WORLD_SIZE and takes cuda:LOCAL_RANK.  Returns the launcher's exit code."""
+    import subprocess
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC for RCCL (the box's driver has no legacy IPC)
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -197,11 +219,21 @@ def main():
                     help="skip the secondary configurations (C5, f32 / h3 GEMMs, C4 total on one GPU)")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # `python bench.py --gpus N`: start the N ranks here (this process has not touched the GPU)
+        sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 through torch.distributed.run")
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if os.environ.get("RSLRL_BENCH_RANK_ENV_ONLY") == "1":  # launcher check (tests/test_bench_launch.py): no GPU
+        print(json.dumps({k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE",
+                                                         "MASTER_ADDR", "MASTER_PORT")}), flush=True)
+        return
+    visible = torch.cuda.device_count()  # does not initialise the GPU on this image
+    if local_rank >= visible:
+        raise SystemExit(f"bench.py rank {rank}: --gpus {world} needs {world} GPUs on this node, {visible} visible")
     torch.cuda.set_device(local_rank)
     device = f"cuda:{local_rank}"
     if args.num_envs is not None:

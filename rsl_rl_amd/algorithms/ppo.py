@@ -354,10 +354,12 @@ class PPO:
         # arena's RND span
         rnd_params = [p for p in self.rnd.predictor.parameters() if p.requires_grad] if self.rnd else []
         rnd_fused = None  # decided at the first mini-batch (needs the observation batch and the arena)
-        target_cache = {}  # RND target embedding per mini-batch slice of this update's gathered storage
+        # RND target embedding per mini-batch slice of this update's gathered storage, keyed by the slice's index
+        # within an epoch: every epoch walks the same permutation's slices in the same order
+        target_cache = {}
 
         generator = self.storage.mini_batch_generator(self.num_mini_batches, self.num_learning_epochs)
-        for (
+        for mb_index, (
             obs_batch,
             actions_batch,
             target_values_batch,
@@ -368,7 +370,7 @@ class PPO:
             old_sigma_batch,
             hid_states_batch,
             masks_batch,
-        ) in generator:
+        ) in enumerate(generator):
             if manual is None:
                 manual = (isinstance(self.policy, ActorCritic) and self.policy.manual_update_ok(obs_batch)
                           and all(p.requires_grad for p in self.policy.parameters()))
@@ -428,7 +430,8 @@ class PPO:
                 # one launch pair: predictor forward, detached target (computed in the first epoch, then read from
                 # the per-update cache -- its weights and inputs do not change within update()), MSE, backward
                 # straight into the predictor's arena span; the loss statistic accumulates into sums[3]
-                self._rnd_update_fused(obs_batch, arena.span(rnd_params), sums, target_cache)
+                self._rnd_update_fused(obs_batch, arena.span(rnd_params), sums, target_cache,
+                                       mb_index % self.num_mini_batches)
             elif self.rnd:
                 with torch.no_grad():
                     rnd_state_batch = self.rnd.get_rnd_state(obs_batch)
@@ -536,12 +539,15 @@ class PPO:
             return s if s.dim() == 2 and s.stride(1) == 1 else None
         return self.rnd.get_rnd_state(obs_batch)
 
-    def _rnd_update_fused(self, obs_batch, grad_span, sums, target_cache):
+    def _rnd_update_fused(self, obs_batch, grad_span, sums, target_cache, slice_index):
+        """slice_index: the mini-batch's slice of the update's permutation (its index within the epoch).  The cache
+        is keyed by it, not by the state's address: with several rnd_state groups the state is a fresh torch.cat per
+        mini-batch, and the caching allocator hands the next mini-batch's cat the same address."""
         rnd = self.rnd
         state = self._rnd_state(obs_batch)
         B = state.shape[0]
         pred, targ = kernels.rnd_linears(rnd.predictor), kernels.rnd_linears(rnd.target)
-        key = (state.data_ptr(), B, state.stride(0))
+        key = (slice_index, B)
         temb = target_cache.get(key)
         compute_target = temb is None
         if compute_target:

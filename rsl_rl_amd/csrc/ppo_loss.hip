@@ -1261,16 +1261,22 @@ extern "C" int rslrl_launch_timing_enable(int32_t capacity) {
 extern "C" int rslrl_launch_timing_read(double* total_ms, int64_t* launches) {
     if (!total_ms || !launches) return RSLRL_E_INVALID_ARGUMENT;
     LaunchTiming& t = launch_timing();
-    std::lock_guard<std::mutex> lk(t.mu);
+    // the used event pairs are copied under the lock and synchronised after it is released: a loss launch on
+    // another thread (launch_timed takes the same lock) never waits for this read's event synchronisations
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> pairs;
+    {
+        std::lock_guard<std::mutex> lk(t.mu);
+        pairs.assign(t.pool.begin(), t.pool.begin() + static_cast<std::ptrdiff_t>(t.used));
+    }
     double sum = 0.0;
-    for (size_t i = 0; i < t.used; ++i) {
-        hipError_t err = hipEventSynchronize(t.pool[i].second);
+    for (const auto& pr : pairs) {
+        hipError_t err = hipEventSynchronize(pr.second);
         float ms = 0.0f;
-        if (err == hipSuccess) err = hipEventElapsedTime(&ms, t.pool[i].first, t.pool[i].second);
+        if (err == hipSuccess) err = hipEventElapsedTime(&ms, pr.first, pr.second);
         if (err != hipSuccess) return static_cast<int>(err);
         sum += static_cast<double>(ms);
     }
     *total_ms = sum;
-    *launches = static_cast<int64_t>(t.used);
+    *launches = static_cast<int64_t>(pairs.size());
     return RSLRL_OK;
 }

@@ -89,8 +89,10 @@ class RolloutActGraph:
             self._graph.replay()
             self._img_gen = fused_mlp._frozen_gen if frozen else None
             actions, values, mean, scale = self._out
+        # actions and values are cloned (the next replay overwrites the graph's static outputs); the distribution's
+        # mean / scale stay the static tensors, valid until the next call (the eager path allocates new ones)
         self.policy.distribution = Normal(mean, scale)
-        return actions.clone(), values
+        return actions.clone(), values.clone()
 
     def _capture(self, obs, key) -> bool:
         pol = self.policy

@@ -169,6 +169,7 @@ class RolloutStorage:
         self._save_hidden_states(transition.hidden_states)
         self.step += 1
         self._fills += 1
+        self._slot_key = None  # values / log-prob rewritten: the record slots are stale
 
     def fused_record_ok(self, transition) -> bool:
         """The fused rollout record (kernels.rollout_record) covers the RL transition of a feed-forward
@@ -210,6 +211,7 @@ class RolloutStorage:
             dst.copy_(src)
         self.step += 1
         self._fills += 1
+        self._slot_key = None  # written through data_ptr (no _version bump): the record slots are stale
 
     def _save_hidden_states(self, hidden_states):
         if hidden_states is None or hidden_states == (None, None):
@@ -246,7 +248,11 @@ class RolloutStorage:
 
     def _slot_sources(self):
         """What the record slots hold: the transition count and the in-place versions of the four scalar buffers
-        (any later add_transitions or in-place write to values / log-prob / returns / advantages invalidates them)."""
+        (any later add_transitions or in-place write to values / log-prob / returns / advantages invalidates them).
+
+        Invariant: a C-ABI kernel that writes values / log-prob / returns / advantages through data_ptr does not bump
+        their torch _version, so every storage method that launches one must set self._slot_key itself (None, or
+        the new sources after it rewrote the slots too): add_transitions, add_transition_fused, compute_returns."""
         return (self._fills, self.values._version, self.actions_log_prob._version, self.returns._version,
                 self.advantages._version)
 

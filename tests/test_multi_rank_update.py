@@ -14,8 +14,9 @@ Per rank: learning-rate trace exact, loss means rtol 1e-4, the first mini-batch'
 parameters within the width's tolerance (tests/update_fixtures.check_update); and every rank ends with
 bit-identical parameters (they must, as in the reference: the same averaged gradients and lr on every rank).
 
-test_two_ranks_c4_share: two ranks x 16384 envs (C4's per-GPU share at N = 8) through a real rollout on the
-synthetic VecEnv and one update at 3x256: finite losses, identical learning-rate traces, bit-identical parameters.
+test_ranks_c4_share: 2 and 8 ranks x 16384 envs (C4's per-GPU share at N = 8; 8 ranks = C4's whole 131,072-env
+workload) through a real rollout on the synthetic VecEnv and one update at 3x256: finite losses, identical
+learning-rate traces, bit-identical parameters.  test_rccl_update_path_world1: the same path over RCCL.
 """
 
 import os
@@ -40,7 +41,7 @@ def _free_port():
     return p
 
 
-def _setup(rank, world, port):
+def _setup(rank, world, port, backend="gloo"):
     import sys
 
     for p in (ROOT, os.path.join(ROOT, "tests")):
@@ -51,7 +52,7 @@ def _setup(rank, world, port):
     import torch.distributed as dist
 
     torch.cuda.set_device(0)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group(backend, rank=rank, world_size=world)
     return dist
 
 
@@ -102,8 +103,8 @@ def test_multi_rank_update_matches_reference(case, golden_meta, cuda_device):
             assert torch.equal(v, res[r]["rnd_final"][k]), (r, "rnd", k)
 
 
-def _share_worker(rank, world, port, n_envs, out_dir):
-    dist = _setup(rank, world, port)
+def _share_worker(rank, world, port, n_envs, out_dir, backend="gloo"):
+    dist = _setup(rank, world, port, backend)
     try:
         from rsl_rl_amd.algorithms import PPO
         from rsl_rl_amd.env import SyntheticVecEnv
@@ -137,25 +138,50 @@ def _share_worker(rank, world, port, n_envs, out_dir):
         dist.destroy_process_group()
 
 
-def test_two_ranks_c4_share(cuda_device):
-    """C4's data-parallel path at its per-GPU size: two ranks x 16384 envs (the share of each of 8 GPUs), T = 24,
-    3x256 actor/critic: one rollout through the fused record kernel, GAE, and an update whose 20 mini-batches of
-    98,304 rows each issue one all-reduce of the gradient arena + KL.  Size-independent properties: every loss
-    finite, the same learning-rate trace on both ranks (the KL is averaged before the lr rule), bit-identical
-    parameters on both ranks after the update, and the parameters moved."""
-    world, n = 2, 16384
+def _run_share(world, n, backend="gloo"):
     with tempfile.TemporaryDirectory() as d:
-        mp.start_processes(_share_worker, args=(world, _free_port(), n, d), nprocs=world, join=True,
+        mp.start_processes(_share_worker, args=(world, _free_port(), n, d, backend), nprocs=world, join=True,
                            start_method="spawn")
-        res = [torch.load(os.path.join(d, f"rank{r}.pt"), weights_only=True) for r in range(world)]
+        return [torch.load(os.path.join(d, f"rank{r}.pt"), weights_only=True) for r in range(world)]
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("world", [2, 8])
+def test_ranks_c4_share(world, cuda_device):
+    """C4's data-parallel path at its per-GPU size: `world` ranks x 16384 envs (the share of each of 8 GPUs; at
+    world 8 this is C4's whole 131,072-env workload), T = 24, 3x256 actor/critic: one rollout through the fused
+    record kernel, GAE, and an update whose 20 mini-batches of 98,304 rows each issue one all-reduce of the
+    gradient arena + KL.  Size-independent properties: every loss finite, the same learning-rate trace on every
+    rank (the KL is averaged before the lr rule), bit-identical parameters on every rank after the update, and the
+    parameters moved."""
+    n = 16384
+    res = _run_share(world, n)
     for out in res:
         assert all(np.isfinite(v) for v in out["loss"].values()), out["loss"]
         assert len(out["lr_trace"]) == 20
-    assert res[0]["lr_trace"] == res[1]["lr_trace"]
+    for r in range(1, world):
+        assert res[0]["lr_trace"] == res[r]["lr_trace"], r
+        for k, v in res[0]["final"].items():
+            assert torch.isfinite(v).all(), k
+            assert torch.equal(v, res[r]["final"][k]), (r, k)
+            assert torch.equal(res[0]["init"][k], res[r]["init"][k]), (r, k)  # broadcast_parameters
     for k, v in res[0]["final"].items():
-        assert torch.isfinite(v).all(), k
-        assert torch.equal(v, res[1]["final"][k]), k
-        assert torch.equal(res[0]["init"][k], res[1]["init"][k]), k  # broadcast_parameters
         assert not torch.equal(v, res[0]["init"][k]), k
     # the losses are per-rank means over each rank's own shard: they differ between ranks (different envs)
-    assert res[0]["loss"] != res[1]["loss"]
+    assert all(res[0]["loss"] != res[r]["loss"] for r in range(1, world))
+
+
+@pytest.mark.timeout(600)
+def test_rccl_update_path_world1(cuda_device):
+    """The multi-GPU update path on RCCL ("nccl", the backend the runner and bench.py use) on a real device: a
+    world-1 group, so broadcast_parameters, the per-mini-batch arena + KL all-reduce and the fp32 lr rounding all
+    run through RCCL (two ranks cannot share one device under RCCL).  A world-1 SUM and the division by 1 are
+    exact, so the result must be bit-identical to the same run over gloo."""
+    n = 16384
+    rccl = _run_share(1, n, "nccl")[0]
+    gloo = _run_share(1, n, "gloo")[0]
+    assert rccl["lr_trace"] == gloo["lr_trace"]
+    assert rccl["loss"] == gloo["loss"]
+    for k, v in rccl["final"].items():
+        assert torch.equal(v, gloo["final"][k]), k
+        assert not torch.equal(v, rccl["init"][k]), k
