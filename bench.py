@@ -51,6 +51,26 @@ C4_ENVS = 131072  # BASELINE.json configs[3]: the total partitioned over the ran
 # bench command (scripts/pmc_summary.py; raw counters next to it).  PMC passes serialise and slow the
 # run, so they are collected separately and the committed summary is reported here.
 PMC_TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r3_pmc_traffic.json")
+# the MLP GEMM pairs' counters (scripts/mlp_pmc.sh + scripts/mlp_pmc_summary.py over scripts/mlp_pair_probe.py at C3's
+# 393,216-row mini-batch): FETCH_SIZE / WRITE_SIZE corrected by factors calibrated on the box in each kernel's own
+# access pattern (scripts/pmc_pattern_probe.hip), plus clock and MFMA-pipe utilisation from the SQ counters
+MLP_PMC_FILE = os.path.join(ROOT, "profiles", "r4_mlp_pmc.json")
+MLP_PMC_NAMES = {"linear_dgrad_pair[M=393216,Nred=256,K=256]": "x6_dgrad_pair_w4",
+                 "linear_fwd_pair[M=393216,K=256,N=256]": "x6_fwd_elu_pair",
+                 "linear_wgrad_pair[M=393216,N=256,K=256]": "x6_wgrad_pair"}
+
+
+def mlp_pmc(kernel):
+    try:
+        with open(MLP_PMC_FILE) as f:
+            k = json.load(f)["kernels"].get(MLP_PMC_NAMES.get(kernel, ""))
+    except (OSError, ValueError, KeyError):
+        return None
+    if not k:
+        return None
+    return {"traffic_bytes": k.get("traffic_bytes"), "traffic_over_algorithmic": k.get("traffic_over_algorithmic"),
+            "clock_GHz": k.get("clock_GHz"), "mfma_pipe_util": k.get("mfma_pipe_util"),
+            "source": os.path.relpath(MLP_PMC_FILE, ROOT)}
 
 
 def pmc_traffic(kernel):
@@ -141,7 +161,9 @@ def cpu_baseline(args):
     rate, secs, parts = torch_cpu_ppo.time_iterations(4096, args.num_obs, args.num_actions, T=args.num_steps_per_env,
                                                       iters=1, warmup=1, threads=threads)
     out["C2"] = {"env_steps_per_s": round(rate, 1), "num_envs": 4096, "timed_seconds": round(secs, 2),
-                 "update_env_steps_per_s": round(parts["update_env_steps_per_s"], 1), "phase_seconds": parts["seconds"]}
+                 "update_env_steps_per_s": round(parts["update_env_steps_per_s"], 1), "phase_seconds": parts["seconds"],
+                 # the C3 sample's extrapolation rule applied to this whole C2 iteration's own mini-batch times
+                 "extrapolation_check": parts["extrapolation_check"]}
     n = args.num_envs_local
     rate, secs, parts = torch_cpu_ppo.time_full_size_sample(n, args.num_obs, args.num_actions,
                                                             T=args.num_steps_per_env,
@@ -164,13 +186,16 @@ def cpu_baseline(args):
         "update_env_steps_per_s": big["update_env_steps_per_s"],
         "samples": out,
         "thread_probe_c2_env_steps_per_s": {str(k): round(v, 1) for k, v in probe.items()},
+        "extrapolation_error_on_whole_c2_update": out["C2"]["extrapolation_check"].get(
+            f"first_{args.cpu_mini_batches}", {}).get("rel_error"),
         "cpu_share": share,
         "sample": f"the reference's algorithm in torch-CPU ops (oracle/torch_cpu_ppo.py: rollout, compute_returns loop, "
                   f"randperm + per-mini-batch gathers, Normal log-prob/entropy/KL, clipped losses, autograd, "
                   f"clip_grad_norm_, Adam) at the bench workload's full size N={n}, T={args.num_steps_per_env}, obs "
                   f"{args.num_obs}, act {args.num_actions}, 3x256 MLP: the whole rollout + compute_returns timed, then "
                   f"{args.cpu_mini_batches} of the 20 update mini-batches, the update extrapolated as first + 19 x "
-                  f"mean(rest) (value); plus one whole C2 iteration (N 4096); {threads} threads (the faster of the "
+                  f"mean(rest) (value); plus one whole C2 iteration (N 4096), on which the same extrapolation is checked "
+                  f"against its measured update (extrapolation_error_on_whole_c2_update); {threads} threads (the faster of the "
                   f"{share}-CPU affinity/cgroup share and half of it on a C2 probe); CPU: {model}",
     }
 
@@ -354,8 +379,10 @@ def main():
             peak, arith = X6_PEAK_TFLOPS, "x6 split-bf16 (fp32-class, DESIGN.md s5); peak = bf16 dense / 6"
         else:
             peak, arith = FP32_MFMA_PEAK_TFLOPS, "fp32 MFMA"
+        pmc = mlp_pmc(dm)
         roofline_mlp = {"kernel": dm, "bound": "mfma", "achieved": ach, "peak": round(peak, 1), "unit": "TFLOP/s",
-                        "frac": round(ach / peak, 4), "traffic": None,
+                        "frac": round(ach / peak, 4), "traffic": pmc["traffic_bytes"] if pmc else None,
+                        "pmc": pmc,
                         "flops_per_launch": mlp[dm]["flops_per_launch"], "mean_launch_us": mlp[dm]["mean_us"],
                         "arithmetic": arith, "fp32_mfma_peak": FP32_MFMA_PEAK_TFLOPS,
                         "mlp_ms_per_step": round(sum(e["ms_per_step"] for e in mlp.values()), 3),

@@ -191,10 +191,20 @@ def time_iterations(N, O=48, A=12, T=24, iters=1, warmup=1, threads=None):
             agg[k] += tm[k]
     steps = N * T * iters
     hot = agg["returns"] + agg["hot_loss_and_batches"]
+    # the full-size sample's extrapolation (time_full_size_sample: first + (E*M - 1) x mean of the next k - 1
+    # mini-batches) applied to this whole iteration's own mini-batch times, against its measured update
+    mbs = tm["mini_batch_seconds"]
+    check = {}
+    for k in (3, 5):
+        if len(mbs) > k:
+            est = mbs[0] + (len(mbs) - 1) * sum(mbs[1:k]) / (k - 1)
+            check[f"first_{k}"] = {"update_extrapolated": round(est, 3), "update_measured": round(sum(mbs), 3),
+                                   "rel_error": round(est / sum(mbs) - 1.0, 4)}
     return steps / agg["total"], agg["total"], {
         "update_env_steps_per_s": steps / (agg["returns"] + agg["update"]),
         "hot_path_env_steps_per_s": steps / hot,
         "seconds": {k: round(v, 3) for k, v in agg.items()},
+        "extrapolation_check": check,
     }
 
 

@@ -65,7 +65,10 @@ class RolloutActGraph:
         return (tuple(shapes), ptrs, fused_mlp._mode, torch.is_inference_mode_enabled())
 
     def __call__(self, obs):
-        """(actions, values) of the step, with policy.distribution set as act() sets it; None: run eagerly."""
+        """(actions, values) of the step, with policy.distribution set as act() sets it; None: run eagerly.
+
+        actions is a fresh tensor; values and policy.distribution's mean / scale are the graph's static outputs and
+        stay valid only until the next call."""
         key = self._config(obs)
         if key is None or key in self._failed:
             return None
@@ -89,10 +92,13 @@ class RolloutActGraph:
             self._graph.replay()
             self._img_gen = fused_mlp._frozen_gen if frozen else None
             actions, values, mean, scale = self._out
-        # actions and values are cloned (the next replay overwrites the graph's static outputs); the distribution's
-        # mean / scale stay the static tensors, valid until the next call (the eager path allocates new ones)
+        # Aliasing contract: actions are cloned; the returned values and the distribution's mean / scale ARE the
+        # graph's static outputs, valid only until the next call (the next replay overwrites them; the eager path
+        # allocates new tensors).  PPO.act keeps them in its transition only until process_env_step copies them into
+        # the storage in the same env step.  (A clone of values would add one launch per env step to the
+        # host-bound rollout at the 16384-env share.)
         self.policy.distribution = Normal(mean, scale)
-        return actions.clone(), values.clone()
+        return actions.clone(), values
 
     def _capture(self, obs, key) -> bool:
         pol = self.policy

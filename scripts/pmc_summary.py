@@ -43,7 +43,8 @@ SHORT = {
     "__amd_rocclr_copyBuffer": "copyBuffer",
 }
 # kernels launched at several shapes are keyed "<short>@grid=<threads>"
-BY_GRID = {"x6_fwd_elu", "x6_fwd_elu_pair", "x6_fwd_out", "x6_fwd", "x6_dgrad_elu", "x6_wgrad", "wgrad_fold", "h3_fwd_elu", "h3_dgrad_elu", "h3_fwd_out",
+BY_GRID = {"x6_fwd_elu", "x6_fwd_elu_pair", "x6_dgrad_elu_pair_w4", "x6_fwd_elu_pair_w4", "x6_dgrad_elu_pair_w8",
+           "x6_fwd_elu_pair_w8", "x6_dgrad_elu_pair", "x6_wgrad256_pair", "x6_fwd_out", "x6_fwd", "x6_dgrad_elu", "x6_wgrad", "wgrad_fold", "h3_fwd_elu", "h3_dgrad_elu", "h3_fwd_out",
            "x6_dgrad_wgrad", "h3_wgrad256", "x6_wgrad64", "x6_fwd_out", "x6_fwd_elu_pair", "h3_fwd_elu_pair"}
 
 
@@ -56,6 +57,9 @@ def gemm_name(kernel):
     m = re.search(r"mlp_gemm_x6_kernel<(\d+), \w+, \d+, \d+, (\d+)[,>]", kernel)
     if m:
         return f"{'h3' if m.group(2) == '2' else 'x6'}_{EPI_NAMES.get(int(m.group(1)), m.group(1))}"
+    m = re.search(r"mlp_gemm_x6_w([48])_pair_kernel<(\d+)>", kernel)
+    if m:  # the 4-wave (128 x 64 per wave) and 256-row-tile layouts of the paired update GEMMs
+        return f"x6_{EPI_NAMES.get(int(m.group(2)), m.group(2))}_pair_w{m.group(1)}"
     m = re.search(r"mlp_gemm_x6_pair_kernel<(\d+), \w+, (\d+)[,>]", kernel)
     if m:  # two problems per launch (grid y = 2): bytes per launch cover both
         return f"{'h3' if m.group(2) == '2' else 'x6'}_{EPI_NAMES.get(int(m.group(1)), m.group(1))}_pair"
