@@ -215,9 +215,14 @@ __device__ __forceinline__ void epilogue_tiles_impl(const GemmParams& p, f32x16 
         auto soff = [&](int i, int r) { return (i * 32 + 8 * (r >> 2)) * kBN * 4; };
         auto load_hb = [&](int b, float (&dst)[16]) {
             const int i = b / J, j = b % J;
+#ifdef RSLRL_DBG_NOHLOAD  // diagnostic build only: the input gradient's H loads replaced by register values
+#pragma unroll
+            for (int r = 0; r < 16; ++r) dst[r] = __builtin_bit_cast(float, voff(j, r) ^ soff(i, r)) - 0.5f;
+#else
 #pragma unroll
             for (int r = 0; r < 16; ++r)
                 dst[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rh, voff(j, r), soff(i, r), 0));
+#endif
         };
         if constexpr (EPI == kEpiEluGrad) {
             if (dzo) {  // block 0 was staged in LDS during the last main-loop chunk (row-major 32 x 32)
@@ -256,8 +261,12 @@ __device__ __forceinline__ void epilogue_tiles_impl(const GemmParams& p, f32x16 
                     colpart[j] += v;
                 }
                 amx = fmaxf(amx, fabsf(v));
+#ifdef RSLRL_DBG_NOSTORE  // diagnostic build only: the full-tile epilogue's stores skipped (values kept live)
+                asm volatile("" ::"v"(v));
+#else
                 __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), rc, voff(j, r), soff(i, r),
                                                       2 /* nt */);
+#endif
             }
             if constexpr (GRAD) {
 #pragma unroll
@@ -332,6 +341,111 @@ __device__ __forceinline__ void epilogue_tiles_impl(const GemmParams& p, f32x16 
         if constexpr (GRAD) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) hcur[r] = hnext[r];
+        }
+    }
+}
+
+// Full-tile forward (bias + ELU) / input-gradient (ELU') epilogue through a per-wave LDS stage of 4 KiB: each 32 x 32
+// block is written in the MFMA's C layout (lane = column, ds_write_b32), read back as 8 rows x 128 B per instruction
+// (lane: row 8 k + (lane >> 3), column quad lane & 7; quads XOR-swizzled by (row >> 1) & 7 -- conflict-free both ways)
+// and meets HBM as 16-byte accesses: per block 4 loads of H and 4 stores where the C-layout epilogue issues 16 + 16
+// 4-byte ones.  The elementwise operations are epilogue_tiles_impl's: the same bits.  Plain launches only (no column
+// sums, no amax).  Measured on the input-gradient pair: skipping its H loads and stores altogether took it from 662 to
+// 526 us at 393,216 rows (diagnostic builds, RSLRL_DBG_NOSTORE / RSLRL_DBG_NOHLOAD), the I/O's share this attacks --
+// but the 16-byte form measured no faster than the 4-byte C-layout one (dgrad pair 629-631 vs 623-624 us, forward
+// 634-637 vs 622-626 us, the K = 48 first layer 230 vs 211 us; profiles/r4_staged_epilogue_ab.json): the epilogue's
+// cost is its bytes (the clock falls 9 % with them, profiles/r4_epilogue_io_diag.json), not its instruction count.
+// Kept as a build knob (RSLRL_STAGED_EPI=1), bit-identical to the default epilogue.
+#ifndef RSLRL_STAGED_EPI
+#define RSLRL_STAGED_EPI 0  // measured no faster (profiles/r4_staged_epilogue_ab.json): a build knob, off
+#endif
+constexpr bool kStagedEpi = RSLRL_STAGED_EPI != 0;
+using u32x4 = __attribute__((ext_vector_type(4))) unsigned int;
+
+template <int EPI, int I, int J>
+__device__ __forceinline__ void epilogue_tiles_staged(const GemmParams& p, f32x16 (&acc)[I][J], int64_t wrow0,
+                                                      int wcol0, float* __restrict__ stage) {
+    static_assert(EPI == kEpiBiasElu || EPI == kEpiEluGrad, "staged epilogue: forward ELU or input gradient");
+    constexpr bool GRAD = EPI == kEpiEluGrad;
+    const int lane = threadIdx.x & 63;
+    const int h = lane >> 5;
+    const int l32 = lane & 31;
+    const int cq = lane & 7;   // read layout: column quad
+    const int rr = lane >> 3;  // read layout: row within an 8-row group
+    const int wr = __builtin_amdgcn_readfirstlane(static_cast<int>(wrow0));  // rows < 2^31 (launch)
+    const int wc = __builtin_amdgcn_readfirstlane(wcol0);
+    const int64_t ubase = static_cast<int64_t>(wr) * kBN + wc;
+    const uint32_t rbytes = static_cast<uint32_t>(I * 32 * kBN * 4);
+    const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(p.c + ubase, 0, rbytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rh =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(GRAD ? p.h + ubase : p.c), 0, rbytes, 0x00020000);
+    auto voff = [&](int j) { return static_cast<int>((rr * kBN + j * 32 + 4 * cq) * 4); };
+    auto soff = [&](int i, int k) { return (i * 32 + 8 * k) * kBN * 4; };
+    f32x4 hcur[4], hnext[4];
+    auto load_h = [&](int b, f32x4 (&dst)[4]) {
+        const int i = b / J, j = b % J;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            dst[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rh, voff(j), soff(i, k), 0));
+    };
+    f32x4 bias[J];
+    if constexpr (!GRAD) {
+#pragma unroll
+        for (int j = 0; j < J; ++j) bias[j] = *reinterpret_cast<const f32x4*>(p.bias + wc + j * 32 + 4 * cq);
+    } else {
+        load_h(0, hcur);
+    }
+#pragma unroll
+    for (int b = 0; b < I * J; ++b) {
+        const int i = b / J, j = b % J;
+        if constexpr (GRAD) {
+            if (b + 1 < I * J) load_h(b + 1, hnext);
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int row = 4 * h + (r & 3) + 8 * (r >> 2);
+#ifdef RSLRL_STAGE_NOSWZ  // diagnostic
+            stage[row * 32 + l32] = acc[i][j][r];
+#else
+            stage[row * 32 + 4 * ((l32 >> 2) ^ ((row >> 1) & 7)) + (l32 & 3)] = acc[i][j][r];
+#endif
+        }
+        // the stage's dword writes retire before its 16-byte reads (without this wait a few elements per tile read
+        // stale data on the box: a b32-write / b128-read order is not kept by the LDS on its own)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int row = 8 * k + rr;
+#ifdef RSLRL_STAGE_NOSWZ
+            f32x4 v = *reinterpret_cast<const f32x4*>(stage + row * 32 + 4 * cq);
+#else
+            f32x4 v = *reinterpret_cast<const f32x4*>(stage + row * 32 + 4 * (cq ^ ((row >> 1) & 7)));
+#endif
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                if constexpr (GRAD) {
+                    const float hv = hcur[k][e];
+                    const float g = v[e] * (hv + 1.f);
+                    v[e] = hv > 0.f ? v[e] : g;
+                } else {
+                    const float t = v[e] + bias[j][e];
+                    const float n = elu_neg(fminf(t, 0.f));  // evaluated on every lane: a select, not a branch
+                    v[e] = t > 0.f ? t : n;
+                }
+            }
+            const u32x4 sv = __builtin_bit_cast(u32x4, v);
+            __builtin_amdgcn_raw_buffer_store_b128(sv, rc, voff(j), soff(i, k), 2 /* nt */);
+            // VMEM store-data hazard: the 16-byte store reads its data VGPRs after it issues, and hipcc (ROCm 7.2,
+            // gfx950) put a VALU write of the first data register right behind it with no wait state -- the stored
+            // element 0 of some lanes then came from the next computation (non-deterministic outputs on the box).
+            // The asm keeps the data registers live past wait states of its own (ordered after the store by the
+            // memory clobber).
+            asm volatile("s_nop 3" ::"v"(sv) : "memory");
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the stage's reads are done before the next writes
+        if constexpr (GRAD) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) hcur[k] = hnext[k];
         }
     }
 }
@@ -692,6 +806,11 @@ __device__ __forceinline__ void store_b_regs(BStage<PL, NT>& b, char* b_lds) {
     }
 }
 
+#ifndef RSLRL_B_FIRST
+#define RSLRL_B_FIRST 1
+#endif
+constexpr bool kBFirst = RSLRL_B_FIRST != 0;  // deep_pipeline's issue order of the look-ahead loads (A/B build knob)
+
 // The pipeline alone, for any fragment schedule: compute(a_lds, b_lds) reads one chunk's fragments from the
 // LDS buffer and issues its MFMAs.
 struct NoHook {
@@ -731,8 +850,16 @@ __device__ __forceinline__ void deep_pipeline(const GemmParams& p, int64_t row0,
             }
             store_a_split<BM, PL, NT>(sa_[(c + 1) % D], lds[(c + 1) & 1], sa);
             store_b_regs<PL, NT>(sb, lds[(c + 1) & 1] + PL * planeA);
-            if (c + 1 + D < NCH) sa_[(c + 1) % D] = load_a<BM, true, NT>(p, row0, (c + 1 + D) * kKC);
-            if (c + 2 < NCH) sb = load_b_regs<PL, NT>(bimg, c + 2);
+            if constexpr (kBFirst) {
+                // B (one chunk ahead) issued before A (D chunks ahead): vmcnt retires in issue order, so the next
+                // chunk's wait for this B leaves the younger A loads in flight.  Issued after A, that wait was a
+                // vmcnt(0) every chunk -- the A look-ahead drained down to one chunk (the .s of the w4 kernel).
+                if (c + 2 < NCH) sb = load_b_regs<PL, NT>(bimg, c + 2);
+                if (c + 1 + D < NCH) sa_[(c + 1) % D] = load_a<BM, true, NT>(p, row0, (c + 1 + D) * kKC);
+            } else {
+                if (c + 1 + D < NCH) sa_[(c + 1) % D] = load_a<BM, true, NT>(p, row0, (c + 1 + D) * kKC);
+                if (c + 2 < NCH) sb = load_b_regs<PL, NT>(bimg, c + 2);
+            }
         }
         // only LDS writes to retire (lgkmcnt); __syncthreads' release fence would also wait vmcnt(0) and drain
         // the look-ahead every chunk
@@ -1355,8 +1482,18 @@ __device__ __forceinline__ void mlp_gemm_x6_body(GemmParams p, const uint4* __re
             if (row < p.M) p.y[row * nout + o] = sum + p.obias[o];
         }
     } else {
-        epilogue_tiles<EPI, I, 2>(p, acc, row0 + wm * (BM / 2), wn * 64, full, colpart, amx,
-                                  stage_h0 && full ? reinterpret_cast<const float*>(lds[0]) : nullptr);
+        bool staged = false;
+        if constexpr (kStagedEpi && PL == 3 && EPI == kEpiBiasElu) {
+            // plain full tiles (the paired update launches): 16-byte I/O through a per-wave stage in buffer 0 (the
+            // input gradient takes the w4 kernel's staged epilogue instead: beside the 128-register one here it spilled)
+            staged = full && p.colsum == nullptr && p.amax_out == nullptr && !stage_h0;
+            if (staged)
+                epilogue_tiles_staged<EPI, I, 2>(p, acc, row0 + wm * (BM / 2), wn * 64,
+                                                 reinterpret_cast<float*>(lds[0]) + wave * 1024);
+        }
+        if (!staged)
+            epilogue_tiles<EPI, I, 2>(p, acc, row0 + wm * (BM / 2), wn * 64, full, colpart, amx,
+                                      stage_h0 && full ? reinterpret_cast<const float*>(lds[0]) : nullptr);
     }
 #ifdef RSLRL_STAMPS
     {
@@ -2324,9 +2461,13 @@ __device__ __forceinline__ void mlp_gemm_x6_w4_body(const GemmParams& p, const u
         }
     };
     deep_pipeline<BM, PL, 16, kW4Depth, decltype(compute)&, NoHook, kThreadsW4>(p, row0, bimg, lds, 1.f, compute);
-    float colpart[2];
-    float amx = 0.f;
-    epilogue_tiles<EPI, I, 2>(p, acc, row0, wn * 64, true, colpart, amx);
+    if constexpr (kStagedEpi) {  // after deep_pipeline's final barrier no wave reads the LDS buffers any more
+        epilogue_tiles_staged<EPI, I, 2>(p, acc, row0, wn * 64, reinterpret_cast<float*>(lds_b0) + wn * 1024);
+    } else {
+        float colpart[2];
+        float amx = 0.f;
+        epilogue_tiles<EPI, I, 2>(p, acc, row0, wn * 64, true, colpart, amx);
+    }
 }
 
 template <int EPI>
@@ -2334,6 +2475,70 @@ __global__ __launch_bounds__(kThreadsW4, 2) void mlp_gemm_x6_w4_pair_kernel(Gemm
     __shared__ __attribute__((aligned(16))) char lds_b0[x6_buf_bytes<EPI, 3>()];
     __shared__ __attribute__((aligned(16))) char lds_b1[x6_buf_bytes<EPI, 3>()];
     mlp_gemm_x6_w4_body<EPI>(b.p[blockIdx.y], b.img[blockIdx.y], lds_b0, lds_b1);
+}
+
+// ---- "w8": 256 x 256 tiles, 8 waves as 2 (M) x 4 (N) of the w4 wave tile (128 x 64), one workgroup per CU at <= 256
+// registers.  Each B-image chunk is staged once per 256 rows instead of once per 128: the image (384 KiB per tile, from
+// L2) is the kernels' largest stream -- at 128-row tiles 2.36 GB per input-gradient pair launch against 2.4 GB of HBM
+// traffic, 2.4 M of the launch's 6.3 M vector-memory instructions (SQ counters, profiles/r4_mlp_pmc_base.json).
+constexpr int kBMW8 = 256;
+#ifndef RSLRL_W8_DEPTH
+#define RSLRL_W8_DEPTH 2
+#endif
+constexpr int kW8Depth = RSLRL_W8_DEPTH;  // A look-ahead (chunks)
+
+template <int EPI>
+__device__ __forceinline__ void mlp_gemm_x6_w8_body(const GemmParams& p, const uint4* __restrict__ bimg, char* lds_b0,
+                                                    char* lds_b1) {
+    constexpr int BM = kBMW8, PL = 3, I = 4;
+    constexpr int planeA = BM * kX6RowB;
+    using Frag = typename Arith<PL>::frag;
+    char* lds[2];
+    lds[0] = lds_b0;
+    lds[1] = lds_b1;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wm = wave >> 2;  // rows wm * 128
+    const int wn = wave & 3;   // cols wn * 64
+    const int h = lane >> 5;
+    const int l32 = lane & 31;
+    const int64_t row0 = static_cast<int64_t>(blockIdx.x) * BM;
+    f32x16 acc[I][2];
+#pragma unroll
+    for (int i = 0; i < I; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
+    auto compute = [&](const char* a_lds, const char* b_lds) {
+        Frag bf[2][PL];
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int q = 0; q < PL; ++q) bf[j][q] = read_frag<Frag>(b_lds + q * kX6PlaneB, wn * 64 + j * 32 + l32, h);
+#pragma unroll
+        for (int i = 0; i < I; ++i) {
+            Frag af[PL];
+#pragma unroll
+            for (int q = 0; q < PL; ++q) af[q] = read_frag<Frag>(a_lds + q * planeA, wm * 128 + i * 32 + l32, h);
+#pragma unroll
+            for (int j = 0; j < 2; ++j) acc[i][j] = Arith<PL>::mfma(af, bf[j], acc[i][j]);
+        }
+    };
+    deep_pipeline<BM, PL, 16, kW8Depth, decltype(compute)&, NoHook, kThreads>(p, row0, bimg, lds, 1.f, compute);
+    if constexpr (kStagedEpi) {
+        epilogue_tiles_staged<EPI, I, 2>(p, acc, row0 + wm * 128, wn * 64, reinterpret_cast<float*>(lds_b0) + wave * 1024);
+    } else {
+        float colpart[2];
+        float amx = 0.f;
+        epilogue_tiles<EPI, I, 2>(p, acc, row0 + wm * 128, wn * 64, true, colpart, amx);
+    }
+}
+
+template <int EPI>
+__global__ __launch_bounds__(kThreads, 2) void mlp_gemm_x6_w8_pair_kernel(GemmPair b) {
+    constexpr int bytes = 3 * kBMW8 * kX6RowB + 3 * kX6PlaneB;
+    __shared__ __attribute__((aligned(16))) char lds_b0[bytes];
+    __shared__ __attribute__((aligned(16))) char lds_b1[bytes];
+    mlp_gemm_x6_w8_body<EPI>(b.p[blockIdx.y], b.img[blockIdx.y], lds_b0, lds_b1);
 }
 
 // RSLRL_W4 (read per call: A/B in one process): 1 = every eligible launch, 0 = none; unset = the input gradient at
@@ -2344,6 +2549,13 @@ bool w4_enabled(int epi, int64_t tiles) {
     if (e && e[0] == '1') return true;
     if (e && e[0] == '0') return false;
     return epi == kEpiEluGrad && tiles >= 2048;
+}
+
+// RSLRL_W8 (read per call): 1 = the 256-row tiles for every eligible launch (M % 256 == 0), 0 = none (default)
+bool w8_enabled(int epi, int64_t M) {
+    (void)epi;
+    const char* e = std::getenv("RSLRL_W8");
+    return e && e[0] == '1' && M % kBMW8 == 0;
 }
 
 template <int EPI, int PL>
@@ -2360,6 +2572,11 @@ int launch_pair(const GemmPair& b, bool fullm, hipStream_t st) {
     if constexpr (PL == 3 && (EPI == kEpiBiasElu || EPI == kEpiEluGrad)) {
         const bool plain = b.p[0].colsum == nullptr && b.p[1].colsum == nullptr && b.p[0].amax_out == nullptr &&
                            b.p[1].amax_out == nullptr;
+        if (w8_enabled(EPI, b.p[0].M) && plain && b.p[0].K == 16 * kKC && b.p[0].N == kBN && b.p[0].deep) {
+            hipLaunchKernelGGL((mlp_gemm_x6_w8_pair_kernel<EPI>), dim3(static_cast<unsigned>(b.p[0].M / kBMW8), 2),
+                               dim3(kThreads), 0, st, b);
+            return launch_status();
+        }
         if (w4_enabled(EPI, tiles) && fullm && plain && b.p[0].K == 16 * kKC && b.p[0].N == kBN && b.p[0].deep) {
             hipLaunchKernelGGL((mlp_gemm_x6_w4_pair_kernel<EPI>), g, dim3(kThreadsW4), 0, st, b);
             return launch_status();

@@ -935,6 +935,9 @@ def train_backward_pair(tape_a, dy_a, outs_a, tape_c, dy_c, outs_c):
         adjacent.append(adj)
         dwb_outs.append(torch.as_strided(wo, (nred * K + nred,), (1,)) if adj else None)
     folds = _FoldBatch()
+    # RSLRL_FOLD_EAGER=1 (read per call): each weight-gradient launch's folds run right behind it, while its partials
+    # are still in the Infinity Cache, instead of one batched fold after the pass (which reads them back from HBM)
+    eager = os.environ.get("RSLRL_FOLD_EAGER", "0") == "1"
     if tape_c.head is not None:  # the critic's head ran its backward in the forward launch (value_head_fwd_bwd)
         res = [linear_dgrad_elu_wgrad_deferred(ds[0], tape_a.hs[L - 1], tape_a.dgrad_imgs[L - 1], dwb_outs[0], folds),
                _head_result(tape_c, dwb_outs[1], folds)]
@@ -945,6 +948,8 @@ def train_backward_pair(tape_a, dy_a, outs_a, tape_c, dy_c, outs_c):
     for i in range(2):
         if not adjacent[i]:
             folds.after.append(lambda o=outs[i][L - 1], r=res[i]: torch._foreach_copy_(list(o), [r[1], r[2]]))
+    if eager:
+        folds.run(dz[0].device)
     for l in range(L - 2, -1, -1):
         h_in = [t.hs[l] for t in tapes]
         N, K = tapes[0].ws[l].shape
@@ -958,6 +963,8 @@ def train_backward_pair(tape_a, dy_a, outs_a, tape_c, dy_c, outs_c):
             for i in range(2):
                 if dwb_outs[i] is None:
                     folds.after.append(lambda o=outs[i][l], r=res[i]: torch._foreach_copy_(list(o), list(r)))
+            if eager:
+                folds.run(dz[0].device)
             dz, _ = linear_dgrad_elu_pair(dz, h_in, [t.dgrad_imgs[l] for t in tapes], _lib.ARITH_X6)
         else:  # first layer: (x^T dz)^T on the 64-row tiles, the bias from dz (the kernel's K side)
             pad = (-K) % 4
