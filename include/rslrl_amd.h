@@ -31,7 +31,7 @@ extern "C" {
 
 typedef struct ihipStream_t* rslrl_stream_t; /* == hipStream_t */
 
-#define RSLRL_ABI_VERSION 11
+#define RSLRL_ABI_VERSION 12
 
 enum {
     RSLRL_OK = 0,
@@ -71,6 +71,17 @@ int rslrl_compute_returns_records(const float* values, const float* rewards, con
                                   float* returns, float* advantages, const float* log_prob, float* records,
                                   int64_t record_floats, int64_t slot_offset, void* workspace,
                                   size_t workspace_bytes, rslrl_stream_t stream);
+
+/* rslrl_compute_returns with normalize_advantage = 1 whose normalisation pass also writes the update's scalar slot
+ * array (ABI 12): slots[i] = {values[i], log_prob[i], returns[i], advantages[i] (normalised)}, i < T*N, one contiguous
+ * 16-byte unit per env-step (slots: [T*N, 4] fp32, 16-byte aligned) -- coalesced stores where the in-record slots
+ * of rslrl_compute_returns_records are 32-byte pieces at the record stride.  The mini-batch gather reads each drawn
+ * row's slot beside its record (rslrl_gather_records_side).  Replaces rollout_storage.py:127-149 like
+ * rslrl_compute_returns. */
+int rslrl_compute_returns_slots(const float* values, const float* rewards, const uint8_t* dones,
+                                const float* last_values, float gamma, float lam, int64_t T, int64_t N,
+                                float* returns, float* advantages, const float* log_prob, float* slots,
+                                void* workspace, size_t workspace_bytes, rslrl_stream_t stream);
 
 /* Advantage statistics + in-place normalisation of an arbitrary fp32 vector (the normalisation half
  * of rollout_storage.py:148-149; ppo.py:221-223 uses the same expression per mini-batch).          */
@@ -126,6 +137,14 @@ typedef struct {
 
 int rslrl_gather_records(const float* records, int64_t record_floats, const rslrl_record_field_t* fields /* host */,
                          int32_t num_fields, const int32_t* indices, int64_t num_rows, rslrl_stream_t stream);
+/* rslrl_gather_records plus one 16-byte unit per row from a side array (ABI 12): for each side field g,
+ * dst_g[r] = side[indices[r]][offset_g : offset_g + width_g] (offset_g + width_g <= 4; side: [n, 4] fp32, 16-byte
+ * aligned) -- RolloutStorage's scalar slot array {value, log-prob, return, advantage} (rslrl_compute_returns_slots).
+ * num_fields + num_side_fields <= RSLRL_MAX_GATHER_FIELDS. */
+int rslrl_gather_records_side(const float* records, int64_t record_floats, const rslrl_record_field_t* fields,
+                              int32_t num_fields, const float* side, const rslrl_record_field_t* side_fields,
+                              int32_t num_side_fields, const int32_t* indices, int64_t num_rows,
+                              rslrl_stream_t stream);
 int rslrl_record_fill_slot(float* records, int64_t record_floats, int64_t offset, int32_t slot_floats,
                            const float* row_src, int32_t row_width,
                            const float* const* columns /* host array of device pointers */, int32_t num_columns,

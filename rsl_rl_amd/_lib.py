@@ -19,7 +19,7 @@ import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 # RSLRL_AMD_LIB: an alternative in-tree build of the same library (A/B kernel experiments)
 LIB_PATH = os.environ.get("RSLRL_AMD_LIB") or os.path.join(LIB_DIR, "librslrl_amd.so")
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 # symbols declared in include/rslrl_amd.h (tests/test_capi.py checks the header against this list)
 EXPORTED_SYMBOLS = (
@@ -28,11 +28,13 @@ EXPORTED_SYMBOLS = (
     "rslrl_compute_returns_workspace_bytes",
     "rslrl_compute_returns",
     "rslrl_compute_returns_records",
+    "rslrl_compute_returns_slots",
     "rslrl_normalize_workspace_bytes",
     "rslrl_normalize_advantages",
     "rslrl_randperm_mt19937",
     "rslrl_gather_rows",
     "rslrl_gather_records",
+    "rslrl_gather_records_side",
     "rslrl_record_fill_slot",
     "rslrl_ppo_loss_workspace_bytes",
     "rslrl_ppo_loss_fwd_bwd",
@@ -343,6 +345,11 @@ def _declare(L):
     L.rslrl_gather_rows.argtypes = [ctypes.POINTER(GatherField), I32, P, I64, P]
     L.rslrl_gather_records.restype = ctypes.c_int
     L.rslrl_gather_records.argtypes = [P, I64, ctypes.POINTER(RecordField), I32, P, I64, P]
+    L.rslrl_gather_records_side.restype = ctypes.c_int
+    L.rslrl_gather_records_side.argtypes = [P, I64, ctypes.POINTER(RecordField), I32, P, ctypes.POINTER(RecordField),
+                                            I32, P, I64, P]
+    L.rslrl_compute_returns_slots.restype = ctypes.c_int
+    L.rslrl_compute_returns_slots.argtypes = [P, P, P, P, F, F, I64, I64, P, P, P, P, P, SZ, P]
     L.rslrl_record_fill_slot.restype = ctypes.c_int
     L.rslrl_record_fill_slot.argtypes = [P, I64, I64, I32, P, I32, ctypes.POINTER(ctypes.c_void_p), I32, I64, P]
     L.rslrl_ppo_loss_workspace_bytes.restype = SZ

@@ -209,6 +209,27 @@ __global__ __launch_bounds__(kBlock) void adv_normalize_slot_kernel(float* __res
     }
 }
 
+// adv_normalize_kernel that also writes the update's scalar slot array {value, log-prob, return, advantage} (one
+// float4 per env-step, contiguous [T*N, 4]): every store is a coalesced 16-byte unit, where the in-record slots above
+// are 32-byte pieces at the record stride (~1.6 TB/s: 49 us of the 72 us compute_returns at C3, profiles/r3_*).  The
+// mini-batch gather takes each row's slot from this array beside the record (rslrl_gather_records_side).
+__global__ __launch_bounds__(kBlock) void adv_normalize_slots_kernel(float* __restrict__ adv, int64_t n,
+                                                                     const double2* __restrict__ partials, int np,
+                                                                     float eps, const float* __restrict__ values,
+                                                                     const float* __restrict__ logp,
+                                                                     const float* __restrict__ returns,
+                                                                     float4* __restrict__ slots) {
+    float mean, std;
+    fold_moments(partials, np, n, &mean, &std);
+    const float denom = __fadd_rn(std, eps);  // rollout_storage.py:149  (std + 1e-8)
+    const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
+    for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < n; i += stride) {
+        const float a = __fdiv_rn(__fsub_rn(adv[i], mean), denom);
+        adv[i] = a;
+        slots[i] = make_float4(values[i], logp[i], returns[i], a);
+    }
+}
+
 int scan_blocks(int64_t N) { return static_cast<int>(std::min<int64_t>(ceil_div(N, kBlock), kMaxPartials)); }
 
 int elementwise_blocks(int64_t n) {
@@ -246,7 +267,7 @@ namespace {
 // RecordSlot: optional destination of the normalisation pass (rslrl_compute_returns_records)
 struct RecordSlot {
     const float* log_prob;
-    float* records;
+    float* records;         // records (record_floats > 0) or the contiguous float4 slot array (record_floats == 0)
     int64_t record_floats;
     int64_t offset;
 };
@@ -284,7 +305,12 @@ int compute_returns_impl(const float* values, const float* rewards, const uint8_
     hipLaunchKernelGGL(centered_sq_kernel, dim3(nb), dim3(kBlock), 0, st, advantages, n, part);
     rc = launch_status();
     if (rc != RSLRL_OK) return rc;
-    if (slot) {
+    if (slot && slot->record_floats == 0) {
+        const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, kBlock), 4096));
+        hipLaunchKernelGGL(adv_normalize_slots_kernel, dim3(static_cast<unsigned>(blocks)), dim3(kBlock), 0, st,
+                           advantages, n, part, nb, 1e-8f, values, slot->log_prob, returns,
+                           reinterpret_cast<float4*>(slot->records));
+    } else if (slot) {
         const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(ceil_div(2 * n, kBlock), 4096));
         hipLaunchKernelGGL(adv_normalize_slot_kernel, dim3(static_cast<unsigned>(blocks)), dim3(kBlock), 0, st,
                            advantages, n, part, nb, 1e-8f, values, slot->log_prob, returns, slot->records,
@@ -315,6 +341,17 @@ extern "C" int rslrl_compute_returns_records(const float* values, const float* r
         return RSLRL_E_INVALID_ARGUMENT;
     if (reinterpret_cast<uintptr_t>(records) & 15) return RSLRL_E_MISALIGNED;
     const RecordSlot slot{log_prob, records, record_floats, slot_offset};
+    return compute_returns_impl(values, rewards, dones, last_values, gamma, lam, T, N, 1, returns, advantages,
+                                workspace, workspace_bytes, stream, &slot);
+}
+
+extern "C" int rslrl_compute_returns_slots(const float* values, const float* rewards, const uint8_t* dones,
+                                           const float* last_values, float gamma, float lam, int64_t T, int64_t N,
+                                           float* returns, float* advantages, const float* log_prob, float* slots,
+                                           void* workspace, size_t workspace_bytes, rslrl_stream_t stream) {
+    if (!log_prob || !slots) return RSLRL_E_INVALID_ARGUMENT;
+    if (reinterpret_cast<uintptr_t>(slots) & 15) return RSLRL_E_MISALIGNED;
+    const RecordSlot slot{log_prob, slots, 0, 0};
     return compute_returns_impl(values, rewards, dones, last_values, gamma, lam, T, N, 1, returns, advantages,
                                 workspace, workspace_bytes, stream, &slot);
 }

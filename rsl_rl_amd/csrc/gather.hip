@@ -122,6 +122,7 @@ struct RecParams {
     int32_t units;  // 16-byte units read per record
     int32_t tile;   // rows per block
     int32_t r4;     // record stride in 16-byte units
+    const float4* side;  // optional: one 16-byte unit per row index (the slot array), staged after the record's units
 };
 
 __global__ __launch_bounds__(kBlock) void gather_records_kernel(RecParams p, const float4* __restrict__ rec,
@@ -132,8 +133,9 @@ __global__ __launch_bounds__(kBlock) void gather_records_kernel(RecParams p, con
     const int nrows = static_cast<int>(min<int64_t>(p.tile, num_rows - row0));
     for (int r = threadIdx.x; r < nrows; r += kBlock) ridx[r] = indices[row0 + r];
     __syncthreads();
-    const unsigned U = static_cast<unsigned>(p.units);
-    const int s4 = p.units + 1;
+    const unsigned RU = static_cast<unsigned>(p.units);  // record units of a row
+    const unsigned U = RU + (p.side ? 1u : 0u);            // + the side unit (slot array) when present
+    const int s4 = static_cast<int>(U) + 1;
     const unsigned total = static_cast<unsigned>(nrows) * U;
     // four independent 16-byte loads in flight per thread before their LDS stores
     for (unsigned k0 = threadIdx.x; k0 < total; k0 += 4 * kBlock) {
@@ -145,7 +147,8 @@ __global__ __launch_bounds__(kBlock) void gather_records_kernel(RecParams p, con
             const unsigned kk = k < total ? k : total - 1;
             const unsigned r = kk / U, u = kk - r * U;
             slot[j] = r * s4 + u;
-            v[j] = rec[static_cast<int64_t>(ridx[r]) * p.r4 + u];
+            const int64_t src = static_cast<int64_t>(ridx[r]);
+            v[j] = u < RU ? rec[src * p.r4 + u] : p.side[src];
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j)
@@ -203,27 +206,41 @@ __global__ __launch_bounds__(kBlock) void record_fill_slot_kernel(float* __restr
 }  // namespace
 }  // namespace rslrl
 
-extern "C" int rslrl_gather_records(const float* records, int64_t record_floats, const rslrl_record_field_t* fields,
-                                    int32_t num_fields, const int32_t* indices, int64_t num_rows,
-                                    rslrl_stream_t stream) {
-    if (num_fields < 0 || num_fields > RSLRL_MAX_GATHER_FIELDS || num_rows < 0) return RSLRL_E_INVALID_ARGUMENT;
-    if (num_rows == 0 || num_fields == 0) return RSLRL_OK;
-    if (!records || !fields || !indices || record_floats <= 0 || (record_floats & 3)) return RSLRL_E_INVALID_ARGUMENT;
-    if (reinterpret_cast<uintptr_t>(records) & 15) return RSLRL_E_MISALIGNED;
+namespace {
+int gather_records_impl(const float* records, int64_t record_floats, const rslrl_record_field_t* fields,
+                        int32_t num_fields, const float* side, const rslrl_record_field_t* side_fields,
+                        int32_t num_side, const int32_t* indices, int64_t num_rows, rslrl_stream_t stream) {
+    if (num_fields < 0 || num_side < 0 || num_fields + num_side > RSLRL_MAX_GATHER_FIELDS || num_rows < 0)
+        return RSLRL_E_INVALID_ARGUMENT;
+    if (num_rows == 0 || num_fields + num_side == 0) return RSLRL_OK;
+    if (!records || (num_fields && !fields) || !indices || record_floats <= 0 || (record_floats & 3))
+        return RSLRL_E_INVALID_ARGUMENT;
+    if (num_side && (!side || !side_fields)) return RSLRL_E_INVALID_ARGUMENT;
+    if ((reinterpret_cast<uintptr_t>(records) & 15) || (side && (reinterpret_cast<uintptr_t>(side) & 15)))
+        return RSLRL_E_MISALIGNED;
     RecParams p{};
-    p.nf = num_fields;
+    p.nf = num_fields + num_side;
     int64_t used = 0;
     for (int i = 0; i < num_fields; ++i) {
         const rslrl_record_field_t& f = fields[i];
         if (!f.dst || f.width < 1 || f.offset < 0 || f.offset + f.width > record_floats) return RSLRL_E_INVALID_ARGUMENT;
         used = std::max<int64_t>(used, f.offset + f.width);
-        const bool v16 = (f.width % 4 == 0) && (f.offset % 4 == 0) && ((reinterpret_cast<uintptr_t>(f.dst) & 15) == 0);
-        p.f[i] = RecField{static_cast<int32_t>(f.offset), static_cast<int32_t>(f.width), v16 ? 1 : 0, f.dst};
     }
     if (used > RSLRL_MAX_RECORD_FLOATS) return RSLRL_E_UNSUPPORTED;
     p.units = static_cast<int32_t>((used + 3) / 4);
-    p.tile = p.units <= 32 ? kRecTile : kRecTile / 2;
-    if (static_cast<int64_t>(p.tile) * (p.units + 1) > kRecLdsUnits) return RSLRL_E_UNSUPPORTED;
+    const int64_t side_off = 4 * static_cast<int64_t>(p.units);  // the side unit's floats follow the record's units
+    for (int i = 0; i < num_fields + num_side; ++i) {
+        const bool is_side = i >= num_fields;
+        const rslrl_record_field_t& f = is_side ? side_fields[i - num_fields] : fields[i];
+        if (is_side && (!f.dst || f.width < 1 || f.offset < 0 || f.offset + f.width > 4)) return RSLRL_E_INVALID_ARGUMENT;
+        const int64_t off = is_side ? side_off + f.offset : f.offset;
+        const bool v16 = (f.width % 4 == 0) && (off % 4 == 0) && ((reinterpret_cast<uintptr_t>(f.dst) & 15) == 0);
+        p.f[i] = RecField{static_cast<int32_t>(off), static_cast<int32_t>(f.width), v16 ? 1 : 0, f.dst};
+    }
+    p.side = num_side ? reinterpret_cast<const float4*>(side) : nullptr;
+    const int32_t units_all = p.units + (num_side ? 1 : 0);
+    p.tile = units_all <= 32 ? kRecTile : kRecTile / 2;
+    if (static_cast<int64_t>(p.tile) * (units_all + 1) > kRecLdsUnits) return RSLRL_E_UNSUPPORTED;
     if (record_floats / 4 > INT32_MAX) return RSLRL_E_INVALID_ARGUMENT;
     p.r4 = static_cast<int32_t>(record_floats / 4);
     const int64_t nb = ceil_div(num_rows, p.tile);
@@ -232,6 +249,22 @@ extern "C" int rslrl_gather_records(const float* records, int64_t record_floats,
                        reinterpret_cast<hipStream_t>(stream), p, reinterpret_cast<const float4*>(records), indices,
                        num_rows);
     return launch_status();
+}
+}  // namespace
+
+extern "C" int rslrl_gather_records(const float* records, int64_t record_floats, const rslrl_record_field_t* fields,
+                                    int32_t num_fields, const int32_t* indices, int64_t num_rows,
+                                    rslrl_stream_t stream) {
+    return gather_records_impl(records, record_floats, fields, num_fields, nullptr, nullptr, 0, indices, num_rows,
+                               stream);
+}
+
+extern "C" int rslrl_gather_records_side(const float* records, int64_t record_floats,
+                                         const rslrl_record_field_t* fields, int32_t num_fields, const float* side,
+                                         const rslrl_record_field_t* side_fields, int32_t num_side_fields,
+                                         const int32_t* indices, int64_t num_rows, rslrl_stream_t stream) {
+    return gather_records_impl(records, record_floats, fields, num_fields, side, side_fields, num_side_fields, indices,
+                               num_rows, stream);
 }
 
 extern "C" int rslrl_record_fill_slot(float* records, int64_t record_floats, int64_t offset, int32_t slot_floats,

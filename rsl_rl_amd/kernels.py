@@ -221,6 +221,36 @@ def compute_returns_records(values, rewards, dones, last_values, gamma, lam, ret
     _lib.check(rc, "rslrl_compute_returns_records")
 
 
+def compute_returns_slots(values, rewards, dones, last_values, gamma, lam, returns, advantages, log_prob, slots):
+    """compute_returns with normalisation whose last pass also writes the scalar slot array
+    slots[t, n] = {value, log-prob, return, advantage} (include/rslrl_amd.h rslrl_compute_returns_slots): slots
+    [T, N, 4] contiguous fp32, log_prob [T, N, 1] contiguous fp32."""
+    _require_device(values, rewards, dones, last_values, returns, advantages, log_prob, slots)
+    T, N = values.shape[0], values.shape[1]
+    for t, dt in ((values, torch.float32), (rewards, torch.float32), (dones, torch.uint8), (last_values, torch.float32),
+                  (returns, torch.float32), (advantages, torch.float32), (log_prob, torch.float32),
+                  (slots, torch.float32)):
+        if t.dtype != dt or not t.is_contiguous():
+            raise ValueError(f"compute_returns_slots: expected contiguous {dt}, got {t.dtype} "
+                             f"(contiguous={t.is_contiguous()})")
+    if (values.numel() != T * N or last_values.numel() != N or dones.numel() != T * N or rewards.numel() != T * N
+            or log_prob.numel() != T * N or slots.numel() != 4 * T * N):
+        raise ValueError("compute_returns_slots: inconsistent shapes")
+    L = _lib.lib()
+    dev = values.device
+    ws = _ws.get(dev, "gae", L.rslrl_compute_returns_workspace_bytes(T, N))
+    # scan (17 B + 4 B per env) + centred squares (4 B) + normalisation reading adv / value / log-prob / return and
+    # writing adv + the 16-byte slot
+    moved = 17 * T * N + 4 * N + 4 * T * N + (4 * 4 + 4 + 16) * T * N
+    with timer.span("compute_returns", dev, moved):
+        rc = L.rslrl_compute_returns_slots(
+            _ptr(values), _ptr(rewards), _ptr(dones), _ptr(last_values), ctypes.c_float(gamma), ctypes.c_float(lam),
+            T, N, _ptr(returns), _ptr(advantages), _ptr(log_prob), _ptr(slots), _ptr(ws), ws.numel(),
+            ctypes.c_void_p(_stream(dev)),
+        )
+    _lib.check(rc, "rslrl_compute_returns_slots")
+
+
 def normalize_advantages_(adv: torch.Tensor, eps: float = 1e-8) -> torch.Tensor:
     """In-place (adv - mean) / (std_unbiased + eps) over all elements (rollout_storage.py:149)."""
     _require_device(adv)
@@ -324,6 +354,38 @@ def gather_records(records: torch.Tensor, fields, indices: torch.Tensor):
         rc = _lib.lib().rslrl_gather_records(_ptr(records), R, arr, len(fields), _ptr(indices), count,
                                              ctypes.c_void_p(_stream(dev)))
     _lib.check(rc, "rslrl_gather_records")
+
+
+def gather_records_side(records: torch.Tensor, fields, side: torch.Tensor, side_fields, indices: torch.Tensor):
+    """gather_records plus fields of a side array (include/rslrl_amd.h rslrl_gather_records_side): side [..., 4]
+    contiguous fp32 (one 16-byte unit per record index); side_fields: (offset, width, dst) with offset + width <= 4,
+    dst[r] = side.view(-1, 4)[indices[r], offset:offset+width]."""
+    if len(fields) + len(side_fields) > _lib.MAX_GATHER_FIELDS:
+        raise ValueError(f"gather_records_side: at most {_lib.MAX_GATHER_FIELDS} fields per launch")
+    _require_device(records, side, indices, *[f[2] for f in fields], *[f[2] for f in side_fields])
+    if records.dtype != torch.float32 or not records.is_contiguous():
+        raise ValueError("gather_records_side: records must be contiguous fp32")
+    if side.dtype != torch.float32 or not side.is_contiguous() or side.shape[-1] != 4 or \
+            side.numel() // 4 != records.numel() // records.shape[-1]:
+        raise ValueError("gather_records_side: side must be contiguous fp32 [..., 4], one row per record")
+    if indices.dtype != torch.int32 or not indices.is_contiguous():
+        raise ValueError("gather_records_side: indices must be contiguous int32")
+    R = records.shape[-1]
+    count = indices.numel()
+    arrs, moved = [], 0
+    for fl in (fields, side_fields):
+        arr = (_lib.RecordField * max(len(fl), 1))()
+        for i, (off, width, dst) in enumerate(fl):
+            if dst.dtype != torch.float32 or not dst.is_contiguous() or dst.numel() != count * width:
+                raise ValueError("gather_records_side: dst must be contiguous fp32 [count, width]")
+            arr[i] = _lib.RecordField(int(off), int(width), dst.data_ptr())
+            moved += 8 * width * count
+        arrs.append(arr)
+    dev = indices.device
+    with timer.span("gather_rows", dev, moved + 4 * count):
+        rc = _lib.lib().rslrl_gather_records_side(_ptr(records), R, arrs[0], len(fields), _ptr(side), arrs[1],
+                                                  len(side_fields), _ptr(indices), count, ctypes.c_void_p(_stream(dev)))
+    _lib.check(rc, "rslrl_gather_records_side")
 
 
 def record_fill_slot(records: torch.Tensor, offset: int, slot_floats: int, row=None, columns=()):

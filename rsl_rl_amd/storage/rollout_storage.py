@@ -22,11 +22,13 @@ reproducible under torch.manual_seed and bit-exact with the reference run on CPU
 Transition records (ROCm storages of feed-forward RL with 4-multiple widths): the gathered fields of an
 env-step sit side by side in one fp32 record padded to whole 128-byte lines ([T, N, R]; 96 floats at C3):
 observation groups, actions, mu and sigma (written by the rollout; `observations[k]`, `actions`, `mu`,
-`sigma` are strided views of the records, same shapes and values as the reference's buffers), then a
-32-byte slot {value, log-prob, return, advantage, 0, 0, 0, 0} filled once per update from the contiguous
-[T, N, 1] scalar buffers (GAE wants those contiguous): by compute_returns' normalisation pass itself when it
-normalises (rslrl_compute_returns_records), else by a slot copy at the first mini_batch_generator after it.
-A randomly drawn row then reads its record's own lines (1.09x the used bytes at C3) instead of at least one line per field (2.2x with one buffer per field).
+`sigma` are strided views of the records, same shapes and values as the reference's buffers).  The update's
+scalars {value, log-prob, return, advantage} of an env-step sit in one 16-byte unit of a contiguous slot array
+([T, N, 4]), filled once per update from the contiguous [T, N, 1] scalar buffers (GAE wants those contiguous): by
+compute_returns' normalisation pass itself when it normalises (rslrl_compute_returns_slots, coalesced stores), else
+by a slot copy at the first mini_batch_generator after it; the gather reads a drawn row's slot beside its record
+(rslrl_gather_records_side).  A randomly drawn row then reads its record's own lines plus one 16-byte unit instead
+of at least one line per field (2.2x the used bytes with one buffer per field).
 RSLRL_RECORD_LAYOUT=0 keeps one buffer per field.
 
 The host draw (1.57M elements at C3: ~4.7 ms, with the GPU idle behind it) is computed ahead: right after a
@@ -86,6 +88,9 @@ class RolloutStorage:
             self.actions = view("actions", actions_shape[0])
             self.mu = view("mu", actions_shape[0])
             self.sigma = view("sigma", actions_shape[0])
+            # the update's scalar slot array {value, log-prob, return, advantage}: one contiguous 16-byte unit per
+            # env-step, written by compute_returns' normalisation pass and gathered beside each drawn record
+            self.slots = zeros(T, N, 4)
         else:
             self.observations = TensorDict({k: zeros(T, *v.shape) for k, v in obs.items()}, batch_size=[T, N],
                                            device=device)
@@ -105,8 +110,8 @@ class RolloutStorage:
         self.saved_hidden_states_a = None
         self.saved_hidden_states_c = None
         self.step = 0
-        self._fills = 0  # transitions added so far (any path): a record slot written before the last one is stale
-        self._slot_key = None  # what the records' slots were filled from (compute_returns), or None
+        self._fills = 0  # transitions added so far (any path): a slot written before the last one is stale
+        self._slot_key = None  # what the slot array was filled from (compute_returns), or None
 
         # mini-batch machinery (allocated on first use)
         self.perm_generator: torch.Generator | None = None
@@ -140,15 +145,11 @@ class RolloutStorage:
         for name, w in widths:
             offs[name] = used
             used += w
-        # the per-update slot {value, log-prob, return, advantage, 0, 0, 0, 0}: a 32-byte piece of its own
-        # (measured on MI355X: writing it whole costs no more than the 16 bytes alone; a 64-byte slot that also
-        # carries sigma, copied per update from a buffer of its own, cost more in the rollout than it saved)
-        offs["slot"] = -(-used // 8) * 8
-        offs["slot_floats"] = 8
-        used = offs["slot"] + 4
+        # (round 4: the per-update scalars {value, log-prob, return, advantage} moved out of the record into the
+        # contiguous slot array: a 32-byte slot per 384-byte record was written at ~1.6 TB/s, the array at HBM rate)
         if used > 256:
             return None
-        return -(-(offs["slot"] + 8) // 32) * 32, offs
+        return -(-used // 32) * 32, offs
 
     # ------------------------------------------------------------------ filling (rollout_storage.py:77-125)
     def add_transitions(self, transition: Transition):
@@ -169,7 +170,7 @@ class RolloutStorage:
         self._save_hidden_states(transition.hidden_states)
         self.step += 1
         self._fills += 1
-        self._slot_key = None  # values / log-prob rewritten: the record slots are stale
+        self._slot_key = None  # values / log-prob rewritten: the slots are stale
 
     def fused_record_ok(self, transition) -> bool:
         """The fused rollout record (kernels.rollout_record) covers the RL transition of a feed-forward
@@ -211,7 +212,7 @@ class RolloutStorage:
             dst.copy_(src)
         self.step += 1
         self._fills += 1
-        self._slot_key = None  # written through data_ptr (no _version bump): the record slots are stale
+        self._slot_key = None  # written through data_ptr (no _version bump): the slots are stale
 
     def _save_hidden_states(self, hidden_states):
         if hidden_states is None or hidden_states == (None, None):
@@ -235,11 +236,11 @@ class RolloutStorage:
         if not last_values.is_contiguous():
             last_values = last_values.contiguous()
         if self.records is not None and normalize_advantage:
-            # the normalisation pass also writes every record's slot {value, log-prob, return, advantage}: the
-            # mini-batch generator then gathers the records as they are (no slot copy per update)
-            kernels.compute_returns_records(self.values, self.rewards, self.dones, last_values, float(gamma),
-                                            float(lam), self.returns, self.advantages, self.actions_log_prob,
-                                            self.records, self.record_layout[1]["slot"])
+            # the normalisation pass also writes the slot array {value, log-prob, return, advantage} (coalesced
+            # 16-byte units): the mini-batch generator gathers it beside the records (no slot copy per update)
+            kernels.compute_returns_slots(self.values, self.rewards, self.dones, last_values, float(gamma),
+                                          float(lam), self.returns, self.advantages, self.actions_log_prob,
+                                          self.slots)
             self._slot_key = self._slot_sources()
             return
         self._slot_key = None
@@ -247,7 +248,7 @@ class RolloutStorage:
                                 normalize_advantage, self.returns, self.advantages)
 
     def _slot_sources(self):
-        """What the record slots hold: the transition count and the in-place versions of the four scalar buffers
+        """What the slot array holds: the transition count and the in-place versions of the four scalar buffers
         (any later add_transitions or in-place write to values / log-prob / returns / advantages invalidates them).
 
         Invariant: a C-ABI kernel that writes values / log-prob / returns / advantages through data_ptr does not bump
@@ -358,18 +359,16 @@ class RolloutStorage:
         if self.records is not None:
             R, offs = self.record_layout
             A = self.actions_shape[0]
-            o = offs["slot"]
-            # the scalar fields' final values into each record's slot (unless compute_returns already wrote them
-            # and nothing changed since), then one gather of whole records
+            # the scalar fields' final values into the slot array (unless compute_returns already wrote them and
+            # nothing changed since), then one gather of the records' used prefixes with each row's slot beside it
             if self._slot_key is None or self._slot_key != self._slot_sources():
-                kernels.record_fill_slot(self.records, o, offs["slot_floats"],
+                kernels.record_fill_slot(self.slots, 0, 4,
                                          columns=[self.values, self.actions_log_prob, self.returns, self.advantages])
                 self._slot_key = self._slot_sources()
             fields = [(offs["obs/" + k], v.shape[-1], p["obs"][k]) for k, v in self.observations.items()]
-            fields += [(offs["actions"], A, p["actions"]), (o, 1, p["values"]), (o + 1, 1, p["actions_log_prob"]),
-                       (o + 2, 1, p["returns"]), (o + 3, 1, p["advantages"]), (offs["mu"], A, p["mu"]),
-                       (offs["sigma"], A, p["sigma"])]
-            kernels.gather_records(self.records, fields, indices)
+            fields += [(offs["actions"], A, p["actions"]), (offs["mu"], A, p["mu"]), (offs["sigma"], A, p["sigma"])]
+            side = [(0, 1, p["values"]), (1, 1, p["actions_log_prob"]), (2, 1, p["returns"]), (3, 1, p["advantages"])]
+            kernels.gather_records_side(self.records, fields, self.slots, side, indices)
         else:
             flat = lambda t: t.flatten(0, 1)  # noqa: E731
             pairs = [(flat(v), p["obs"][k]) for k, v in self.observations.items()]

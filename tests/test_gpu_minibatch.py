@@ -156,7 +156,7 @@ def test_record_storage_minibatches_bit_exact(cuda_device, monkeypatch):
     groups = {"policy": 20, "critic": 12}
     obs0 = {k: torch.zeros(N, d) for k, d in groups.items()}
     st = RolloutStorage("rl", N, T, obs0, [A], cuda_device)
-    assert st.records is not None and st.records.shape[-1] == 64  # 20 + 12 + 24, the 8-float slot at 56 -> 64
+    assert st.records is not None and st.records.shape[-1] == 64  # 20 + 12 + 24 = 56 used floats -> 64
     monkeypatch.setenv("RSLRL_RECORD_LAYOUT", "0")
     soa = RolloutStorage("rl", N, T, obs0, [A], cuda_device)
     assert soa.records is None
@@ -199,6 +199,45 @@ def test_compute_returns_records_matches_scan_plus_slot_copy(T, N, cuda_device):
     kernels.compute_returns_records(values, rewards, dones, last, 0.99, 0.95, ret_b, adv_b, logp, rec_b, off)
     assert torch.equal(ret_a, ret_b) and torch.equal(adv_a, adv_b)
     assert torch.equal(rec_a, rec_b)
+
+
+@pytest.mark.parametrize("T,N", [(24, 4096), (5, 1031), (1, 3)])
+def test_compute_returns_slots_matches_scan_plus_stack(T, N, cuda_device):
+    """rslrl_compute_returns_slots == rslrl_compute_returns (normalised) followed by stacking {value, log-prob, return,
+    advantage} per env-step, bit for bit (returns, advantages and the whole slot array)."""
+    rng = np.random.default_rng(T * N + 1)
+    f = lambda *s: torch.from_numpy(rng.standard_normal(s, dtype=np.float32)).to(cuda_device)  # noqa: E731
+    values, rewards, logp, last = f(T, N, 1), f(T, N, 1), f(T, N, 1), f(N, 1)
+    dones = torch.from_numpy((rng.random((T, N, 1)) < 0.05).astype(np.uint8)).to(cuda_device)
+    ret_a, adv_a = torch.empty_like(values), torch.empty_like(values)
+    ret_b, adv_b = torch.empty_like(values), torch.empty_like(values)
+    slots = torch.full((T, N, 4), float("nan"), device=cuda_device)
+    kernels.compute_returns(values, rewards, dones, last, 0.99, 0.95, True, ret_a, adv_a)
+    kernels.compute_returns_slots(values, rewards, dones, last, 0.99, 0.95, ret_b, adv_b, logp, slots)
+    assert torch.equal(ret_a, ret_b) and torch.equal(adv_a, adv_b)
+    assert torch.equal(slots, torch.cat([values, logp, ret_a, adv_a], dim=-1))
+
+
+@pytest.mark.parametrize("R,used", [(96, 84), (64, 56), (256, 252)])
+def test_gather_records_side_bit_exact(R, used, cuda_device):
+    """rslrl_gather_records_side: record fields and the side array's units of each drawn row, bit for bit
+    (incl. a record that fills all 256 floats, misaligned scalar destinations and a ragged row count)."""
+    g = torch.Generator(device=cuda_device).manual_seed(R)
+    n, rows = 3 * 1031, 2 * 1031 + 5
+    rec = torch.randn(n, R, device=cuda_device, generator=g)
+    side = torch.randn(n, 4, device=cuda_device, generator=g)
+    idx = torch.randint(0, n, (rows,), device=cuda_device, generator=g, dtype=torch.int32)
+    widths = [(0, used - 24), (used - 24, 12), (used - 12, 12)]
+    dst = [torch.empty(rows, w, device=cuda_device) for _, w in widths]
+    big = torch.empty(rows * 4 + 1, device=cuda_device)
+    sdst = [big[1 + k * rows: 1 + (k + 1) * rows].view(rows, 1) for k in range(4)]  # 4-byte aligned only
+    kernels.gather_records_side(rec, [(o, w, d) for (o, w), d in zip(widths, dst)], side,
+                                [(k, 1, sdst[k]) for k in range(4)], idx)
+    il = idx.long()
+    for (o, w), d in zip(widths, dst):
+        assert torch.equal(d, rec[il, o:o + w])
+    for k in range(4):
+        assert torch.equal(sdst[k][:, 0], side[il, k])
 
 
 def test_storage_slot_from_compute_returns_and_invalidation(cuda_device, monkeypatch):

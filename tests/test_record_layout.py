@@ -12,13 +12,14 @@ layout = RolloutStorage._record_layout
 def test_c3_record():
     R, offs = layout("rl", {"policy": torch.zeros(4, 48)}, [12], "cuda")
     assert R == 96  # 384 bytes: three 128-byte lines
-    assert offs == {"obs/policy": 0, "actions": 48, "mu": 60, "sigma": 72, "slot": 88, "slot_floats": 8}
+    # the per-update scalars live in the contiguous slot array (RolloutStorage.slots), not in the record
+    assert offs == {"obs/policy": 0, "actions": 48, "mu": 60, "sigma": 72}
 
 
-def test_fields_in_order_and_slot_is_a_32_byte_piece():
+def test_fields_in_order_and_records_are_whole_lines():
     R, offs = layout("rl", {"policy": torch.zeros(4, 20), "critic": torch.zeros(4, 12)}, [8], "cuda:0")
     assert [offs[k] for k in ("obs/policy", "obs/critic", "actions", "mu", "sigma")] == [0, 20, 32, 40, 48]
-    assert offs["slot"] % 8 == 0 and offs["slot"] >= 56 and offs["slot"] + 8 <= R and R % 32 == 0
+    assert R == 64 and R % 32 == 0
 
 
 @pytest.mark.parametrize("kw", [
