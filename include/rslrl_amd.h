@@ -31,7 +31,7 @@ extern "C" {
 
 typedef struct ihipStream_t* rslrl_stream_t; /* == hipStream_t */
 
-#define RSLRL_ABI_VERSION 12
+#define RSLRL_ABI_VERSION 13
 
 enum {
     RSLRL_OK = 0,
@@ -433,6 +433,50 @@ typedef struct {
     float* colsum_partials; /* [M / 128][256] or NULL */
 } rslrl_value_head_args_t;
 int rslrl_value_head_fwd_bwd(const rslrl_linear_args_t* a, const rslrl_value_head_args_t* v, rslrl_stream_t stream);
+
+/* The actor's last hidden layer, its 12-wide output layer (the action mean), the whole PPO loss of the mini-batch and
+ * the backward through the output layer in one launch (ABI 13): rsl_rl/networks/mlp.py:106-114 (the actor's last
+ * Linear + ELU and the output Linear), ppo.py:259-315 (KL for the adaptive schedule, clipped surrogate, value loss
+ * and entropy terms, total loss; the statistics rslrl_ppo_loss_fwd_bwd writes, d loss / d sigma of the shared std)
+ * and the backward of ppo.py:367 down to the actor's last hidden pre-activation.  Replaces, for that shape, the
+ * sequence rslrl_linear_gemm(RSLRL_LINEAR_FWD_OUT) -> rslrl_ppo_loss_fwd_bwd -> rslrl_linear_gemm(
+ * RSLRL_LINEAR_DGRAD_ELU_WGRAD): H and d loss / d mu never reach HBM.
+ * a: an RSLRL_LINEAR_FWD_OUT problem (x6, nout = 12, N = K = 256, M a multiple of 128, at most 4096 tiles) whose
+ * `y` receives mu [M, 12] (the bits rslrl_linear_gemm gives) and whose `c` receives dZ [M, 256] = (d mu W_out) *
+ * ELU'(H).  d mu is the loss kernel's (same bits); dZ comes from x6 products of d mu and W_out (fp32-faithful, the
+ * separate output-layer backward's fp32 FMA chain differs in rounding).  Shared std only (sigma [12]); per-mini-batch
+ * advantage normalisation is not fused (RSLRL_E_UNSUPPORTED: use the separate launches).
+ * wgrad_partials: [M / 128][3084] per-tile rows [sum d mu^T H (12 x 256) | sum d mu (12)] -- the
+ * RSLRL_LINEAR_DGRAD_ELU_WGRAD partial layout, folded by rslrl_fold_partials* into the output layer's [dW | db].
+ * stats [8] and grad_sigma [12] as rslrl_ppo_loss_fwd_bwd writes them (loss-term sums fold in fp64 per 128-row tile:
+ * within fp32 rounding of the loss kernel's).  grad_mu: optional [M, 12] copy of d loss / d mu (tests).
+ * workspace: rslrl_actor_head_workspace_bytes(M), 16-byte aligned, zero-filled before its first use (the launch
+ * leaves it re-armed). */
+typedef struct {
+    const float* actions;        /* [M, 12] */
+    const float* old_log_prob;   /* [M] */
+    const float* advantages;     /* [M] */
+    const float* values;         /* [M] V of the mini-batch (the critic's output of this pass) */
+    const float* target_values;  /* [M] */
+    const float* returns;        /* [M] */
+    const float* old_mu;         /* [M, 12] */
+    const float* old_sigma;      /* [M, 12] */
+    const float* sigma;          /* [12] the shared std */
+    int32_t num_actions;         /* 12 */
+    float clip_param;
+    float value_loss_coef;
+    float entropy_coef;
+    int32_t use_clipped_value_loss;
+    int32_t compute_kl;
+    const void* out_weight_t_image; /* x6 B image (layout 0) of W_out^T: rslrl_linear_prepare_bimage(W_out, 12, 256, 1) */
+    float* wgrad_partials;       /* [M / 128][3084] */
+    float* grad_sigma;           /* [12] */
+    float* stats;                /* [8] */
+    float* grad_mu;              /* [M, 12] or NULL */
+} rslrl_actor_head_args_t;
+size_t rslrl_actor_head_workspace_bytes(int64_t M);
+int rslrl_actor_head_fwd_bwd(const rslrl_linear_args_t* a, const rslrl_actor_head_args_t* h, void* workspace,
+                             size_t workspace_bytes, rslrl_stream_t stream);
 int rslrl_linear_wgrad_ex(const float* dz, const float* dz_amax, const float* x, const float* x_amax, int64_t M,
                           int32_t N, int32_t K, int32_t arith, float* dw, void* workspace, size_t workspace_bytes,
                           rslrl_stream_t stream);

@@ -19,7 +19,7 @@ import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 # RSLRL_AMD_LIB: an alternative in-tree build of the same library (A/B kernel experiments)
 LIB_PATH = os.environ.get("RSLRL_AMD_LIB") or os.path.join(LIB_DIR, "librslrl_amd.so")
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 # symbols declared in include/rslrl_amd.h (tests/test_capi.py checks the header against this list)
 EXPORTED_SYMBOLS = (
@@ -63,6 +63,8 @@ EXPORTED_SYMBOLS = (
     "rslrl_linear_gemm",
     "rslrl_linear_gemm_pair",
     "rslrl_value_head_fwd_bwd",
+    "rslrl_actor_head_workspace_bytes",
+    "rslrl_actor_head_fwd_bwd",
     "rslrl_linear_wgrad_ex",
     "rslrl_linear_wgrad_bias_workspace_bytes",
     "rslrl_linear_wgrad_bias",
@@ -174,6 +176,34 @@ class ValueHeadArgs(ctypes.Structure):
         ("colsum_partials", ctypes.c_void_p),
     ]
 
+
+class ActorHeadArgs(ctypes.Structure):
+    """rslrl_actor_head_args_t (include/rslrl_amd.h)."""
+    _fields_ = [
+        ("actions", ctypes.c_void_p),
+        ("old_log_prob", ctypes.c_void_p),
+        ("advantages", ctypes.c_void_p),
+        ("values", ctypes.c_void_p),
+        ("target_values", ctypes.c_void_p),
+        ("returns", ctypes.c_void_p),
+        ("old_mu", ctypes.c_void_p),
+        ("old_sigma", ctypes.c_void_p),
+        ("sigma", ctypes.c_void_p),
+        ("num_actions", ctypes.c_int32),
+        ("clip_param", ctypes.c_float),
+        ("value_loss_coef", ctypes.c_float),
+        ("entropy_coef", ctypes.c_float),
+        ("use_clipped_value_loss", ctypes.c_int32),
+        ("compute_kl", ctypes.c_int32),
+        ("out_weight_t_image", ctypes.c_void_p),
+        ("wgrad_partials", ctypes.c_void_p),
+        ("grad_sigma", ctypes.c_void_p),
+        ("stats", ctypes.c_void_p),
+        ("grad_mu", ctypes.c_void_p),
+    ]
+
+
+ACTOR_HEAD_ACTIONS = 12  # the fused actor head's output width (rslrl_actor_head_fwd_bwd)
 
 DTYPE_F32, DTYPE_U8, DTYPE_I32, DTYPE_I64 = 0, 1, 2, 3
 ROLLOUT_MAX_OBS = 4
@@ -410,6 +440,10 @@ def _declare(L):
     L.rslrl_linear_gemm_pair.argtypes = [ctypes.POINTER(LinearArgs), ctypes.POINTER(LinearArgs), P]
     L.rslrl_value_head_fwd_bwd.restype = ctypes.c_int
     L.rslrl_value_head_fwd_bwd.argtypes = [ctypes.POINTER(LinearArgs), ctypes.POINTER(ValueHeadArgs), P]
+    L.rslrl_actor_head_workspace_bytes.restype = ctypes.c_size_t
+    L.rslrl_actor_head_workspace_bytes.argtypes = [I64]
+    L.rslrl_actor_head_fwd_bwd.restype = ctypes.c_int
+    L.rslrl_actor_head_fwd_bwd.argtypes = [ctypes.POINTER(LinearArgs), ctypes.POINTER(ActorHeadArgs), P, ctypes.c_size_t, P]
     L.rslrl_adam_workspace_bytes.restype = SZ
     L.rslrl_adam_workspace_bytes.argtypes = []
     L.rslrl_clip_adam_step.restype = ctypes.c_int

@@ -390,18 +390,34 @@ class PPO:
                     # values as the loss kernel's d/dV followed by the output-layer backward)
                     vh = fused_mlp.ValueHead(target_values_batch, returns_batch, self.clip_param, self.value_loss_coef,
                                              self.use_clipped_value_loss)
+                    # the actor's last launch may also run the loss and the output layer's backward (shared std, no
+                    # per-mini-batch advantage normalisation): the same statistics and d sigma as the loss kernel
+                    ah = None
+                    if (not self.normalize_advantage_per_mini_batch and not self.policy.state_dependent_std
+                            and actions_batch.shape[-1] == fused_mlp.ACTOR_HEAD_ACTIONS):
+                        ah_gs = (arena.slot(self.policy.std) if self.policy.noise_std_type == "scalar"
+                                 else torch.empty(actions_batch.shape[-1], device=dev, dtype=torch.float32))
+                        ah = fused_mlp.ActorHead(
+                            actions_batch, old_actions_log_prob_batch, advantages_batch, target_values_batch,
+                            returns_batch, old_mu_batch, old_sigma_batch, None, clip_param=self.clip_param,
+                            value_loss_coef=self.value_loss_coef, entropy_coef=self.entropy_coef,
+                            use_clipped=self.use_clipped_value_loss, compute_kl=adaptive, grad_sigma=ah_gs,
+                            stats=stats_buf)
                     mean, sigma, value_batch, tape = self.policy.train_forward(obs_batch, side_stream=side,
-                                                                               value_head=vh)
-                    g_mean, g_sigma = self.policy.train_grad_buffers(mean, sigma)
-                    if g_sigma is None:  # shared std: d sigma reduced by the loss kernel, into the std's slot
-                        g_sigma = (arena.slot(self.policy.std) if self.policy.noise_std_type == "scalar"
-                                   else torch.empty_like(sigma))
-                    # the value head's gradient: a contiguous [B, 1] (the critic's fused output-layer backward reads
-                    # its 1-wide rows as they are; a strided column of a padded buffer cost the loss ~2 us)
-                    stats, g_mean, g_sigma, g_value = kernels.ppo_loss_fwd_bwd(
-                        mean, sigma, value_batch, actions_batch, old_actions_log_prob_batch, advantages_batch,
-                        target_values_batch, returns_batch, old_mu_batch, old_sigma_batch, grad_mu=g_mean,
-                        grad_sigma=g_sigma, **loss_kw)
+                                                                               value_head=vh, actor_head=ah)
+                    if ah is not None and ah.done:  # loss and d loss / d mu ran inside the actor's launch
+                        stats, g_mean, g_sigma, g_value = stats_buf, mean, ah.grad_sigma, value_batch
+                    else:
+                        g_mean, g_sigma = self.policy.train_grad_buffers(mean, sigma)
+                        if g_sigma is None:  # shared std: d sigma reduced by the loss kernel, into the std's slot
+                            g_sigma = (arena.slot(self.policy.std) if self.policy.noise_std_type == "scalar"
+                                       else torch.empty_like(sigma))
+                        # the value head's gradient: a contiguous [B, 1] (the critic's fused output-layer backward
+                        # reads its 1-wide rows as they are; a strided column of a padded buffer cost the loss ~2 us)
+                        stats, g_mean, g_sigma, g_value = kernels.ppo_loss_fwd_bwd(
+                            mean, sigma, value_batch, actions_batch, old_actions_log_prob_batch, advantages_batch,
+                            target_values_batch, returns_batch, old_mu_batch, old_sigma_batch, grad_mu=g_mean,
+                            grad_sigma=g_sigma, **loss_kw)
                     self.policy.train_backward(tape, g_mean, g_sigma, g_value, sigma, arena.slot, side_stream=side)
                     del tape
             else:

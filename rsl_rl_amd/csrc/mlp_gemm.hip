@@ -26,6 +26,7 @@
 #include "common.h"
 #include "amax.h"
 #include "x6_split.h"
+#include "ppo_loss_common.h"
 
 namespace rslrl {
 namespace {
@@ -76,6 +77,32 @@ struct GemmParams {
     float vh_clip;        // clip_param
     float vh_g;           // value_loss_coef / M
     int vh_clipped;       // use_clipped_value_loss
+};
+
+// The actor head with the PPO loss and its backward (mlp_gemm_x6_actor_head_kernel, rslrl_actor_head_fwd_bwd): the
+// loss inputs of the mini-batch, the output layer's transposed image and the loss outputs.
+constexpr int kActA = 12;                              // actions: 3 per lane of a row's quad
+constexpr int kActCols = 4 + kActA;                    // loss partial columns: surrogate, value, entropy, KL, d sigma
+constexpr int kActTileFloats = kActA * kBN + kActA;    // per-tile [dW (12 x 256) | db (12)] (a multiple of 4)
+struct ActorParams {
+    const float* actions;    // [M, 12]
+    const float* old_mu;     // [M, 12]
+    const float* old_sigma;  // [M, 12]
+    const float* sigma;      // [12] shared std
+    const float* old_logp;   // [M]
+    const float* adv;        // [M]
+    const float* values;     // [M]
+    const float* target_values;  // [M]
+    const float* returns;    // [M]
+    const uint4* w_t_img;    // x6 image of W_out^T (layout 0): row n = hidden column, k = action
+    float* wpart;            // [tiles][kActTileFloats]
+    float* grad_sigma;       // [12]
+    float* stats;            // [8]
+    float* grad_mu;          // [M, 12] or null
+    double* partials;        // [kActCols][tiles], then [kActCols][groups]
+    unsigned* tickets;       // 1 + groups, zero between launches
+    float clip, ratio_lo, ratio_hi, g_surr, g_ent, value_loss_coef, entropy_coef;
+    int clipped_value, compute_kl, kl_fast;
 };
 
 // d(loss)/dV of one sample (ppo.py:305-313, :367 backward): the loss kernel's expression and operation order
@@ -936,14 +963,354 @@ constexpr int x6_buf_bytes() {
     return EPI == kEpiBiasEluOut ? 40960 : (PL * kBM * kX6RowB + PL * kX6PlaneB);
 }
 
+// ---- The actor head: last hidden layer + output layer + PPO loss + output-layer backward (one 128-row tile) ----------
+// Called after the main loop of a full x6 C^T tile (acc: lane (l32, h) holds row l32 of block i, columns (r & 3) +
+// 8 (r >> 2) + 4 h of block j).  Phases (LDS: buffer 0 = b0, buffer 1 = b1, 40 KiB each):
+//  1. H = ELU(acc + b) in place; the output layer's partial tiles (x6 MFMA, the fused forward's epilogue: the same
+//     bits) -> red [wm][wn][i][12][32] (b0 [0, 24K)).
+//  2. mu of row t >> 2, actions 3 (t & 3) .. +2 (the wn partials added in the fused forward's order), then the loss of
+//     the row on its quad of lanes: ppo_loss_quad_kernel's arithmetic (shared std; same d mu bits) -> d mu tile
+//     [128][16] (b1 [32K, 40K), columns 12..15 zero) and per-wave fp64 loss partials (b0 [32K, 33K)).  The i = 1
+//     half of H waits in LDS meanwhile (32 registers fewer through the loss).
+//  3. per half i (1, then 0): H staged as [32 rows][256] per wave row wm (b0 / b1 [0, 32K), float4 quads XOR-swizzled
+//     in their 8-quad group by row & 7); dW[o][c] += d mu[r][o] H[r][c] over the half's 64 rows, thread (c, o half)
+//     with 6 accumulators; then dZ = (d mu W_out) * ELU'(H): x6 MFMA of the W_out^T image (A) and the split d mu
+//     rows (B) gives the C^T layout of acc, ELU' from H, and the result leaves in place through the stage as
+//     whole-line stores.
+//  4. per-tile [dW | db] partials; loss partials folded over the grid (fold_grid_partials) -> stats, d sigma.
+__device__ __forceinline__ int act_stage_idx(int l, int quad) { return l * kBN + 4 * (quad ^ (l & 7)); }
+
+__device__ __forceinline__ void actor_head_epilogue(const GemmParams& p, const ActorParams& ap, f32x16 (&acc)[2][2],
+                                                    char* lds0, char* lds1, const float* xsb, int wm, int wn, int lane,
+                                                    int wave, int64_t row0) {
+    const int l32 = lane & 31, h = lane >> 5;
+    const int t = threadIdx.x;
+    float* red = reinterpret_cast<float*>(lds0);
+    float* dmu = reinterpret_cast<float*>(lds1 + 32768);
+    double* wstat = reinterpret_cast<double*>(lds0 + 32768);  // [8 waves][kActCols]
+    double* folded = wstat + 8 * kActCols;                    // [kActCols]
+    int* flag = reinterpret_cast<int*>(folded + kActCols);
+    float* const stg = reinterpret_cast<float*>(wm ? lds1 : lds0);  // this wave row's half-tile H stage
+    // ---- 1. H and the output layer's partials
+    const uint4* oimg = p.oimg + wn * (2 * 2 * 3 * 64);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        f32x16 oacc = f32x16{};
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int cb = wn * 64 + j * 32 + 4 * h;
+            float v[16];
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const float4 b4 = *reinterpret_cast<const float4*>(xsb + cb + 8 * g);
+                float tt[4] = {acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
+                tt[0] += b4.x;
+                tt[1] += b4.y;
+                tt[2] += b4.z;
+                tt[3] += b4.w;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float n = elu_neg(fminf(tt[e], 0.f));
+                    v[4 * g + e] = tt[e] > 0.f ? tt[e] : n;
+                    acc[i][j][4 * g + e] = v[4 * g + e];
+                }
+            }
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) {
+                bf16x8 vb[3], wa[3];
+                uint2 lo[3], hi[3];
+                split4(make_float4(v[8 * s2], v[8 * s2 + 1], v[8 * s2 + 2], v[8 * s2 + 3]), lo[0], lo[1], lo[2]);
+                split4(make_float4(v[8 * s2 + 4], v[8 * s2 + 5], v[8 * s2 + 6], v[8 * s2 + 7]), hi[0], hi[1], hi[2]);
+#pragma unroll
+                for (int q = 0; q < 3; ++q) {
+                    vb[q] = __builtin_bit_cast(bf16x8, make_uint4(lo[q].x, lo[q].y, hi[q].x, hi[q].y));
+                    wa[q] = __builtin_bit_cast(bf16x8, oimg[((j * 2 + s2) * 3 + q) * 64 + lane]);
+                }
+                oacc = mfma_x6(wa, vb, oacc);
+                __builtin_amdgcn_sched_barrier(0);  // one k step at a time: its planes die before the next split
+            }
+        }
+        float* rd = red + ((wm * 4 + wn) * 2 + i) * (kActA * 32);
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            const int o = (r & 3) + 8 * (r >> 2) + 4 * h;
+            if (o < kActA) rd[o * 32 + l32] = oacc[r];
+        }
+    }
+    // ---- 2. mu and the loss of row rl on lanes q = 0..3 (actions a0 .. a0 + 2)
+    const int rl = t >> 2, q = t & 3, a0 = 3 * q;
+    const int64_t row = row0 + rl;
+    const float* xact = xsb + kBN;  // [obias | sigma | old_sigma of sample 0] x 12 (prologue)
+    __syncthreads();  // red complete
+    float mu[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const float* b = red + ((rl >> 6) * 4 * 2 + ((rl & 63) >> 5)) * (kActA * 32) + (a0 + k) * 32 + (rl & 31);
+        const float sum = ((b[0] + b[2 * kActA * 32]) + b[4 * kActA * 32]) + b[6 * kActA * 32];
+        mu[k] = sum + xact[a0 + k];
+        p.y[row * kActA + a0 + k] = mu[k];
+    }
+    float x[3], om[3], os[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        x[k] = ap.actions[row * kActA + a0 + k];
+        om[k] = ap.old_mu[row * kActA + a0 + k];
+        os[k] = ap.old_sigma[row * kActA + a0 + k];
+    }
+    const float old_logp = ap.old_logp[row], adv = ap.adv[row], V = ap.values[row], tv = ap.target_values[row],
+                R = ap.returns[row];
+    __syncthreads();  // red read: buffer 0 takes the H stage
+    auto stage_half = [&](int i) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const f32x4 hv = {acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
+                *reinterpret_cast<f32x4*>(stg + act_stage_idx(l32, wn * 16 + j * 8 + 2 * g + h)) = hv;
+            }
+    };
+    stage_half(1);
+    // per-action constants (ppo_loss_quad_kernel, SHARED = true)
+    float c_s[3], c_ls[3], c_inv_den[3], c_inv_s[3], c_inv_s3[3], c_os[3], c_t1[3], c_D[3], c_rD[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const float s = xact[kActA + a0 + k], os0 = xact[2 * kActA + a0 + k];
+        const float inv_s = 1.0f / s;
+        c_s[k] = s;
+        c_ls[k] = logf(s);
+        c_inv_den[k] = 1.0f / __fmul_rn(2.0f, __fmul_rn(s, s));
+        c_inv_s[k] = inv_s;
+        c_inv_s3[k] = inv_s * inv_s * inv_s;
+        const float D = __fmul_rn(2.0f, __fmul_rn(s, s));
+        const bool d_ok = D >= 0x1p-60f && D <= 0x1p60f;
+        c_os[k] = (d_ok && ap.kl_fast) ? os0 : __builtin_nanf("");
+        c_t1[k] = logf(__fadd_rn(__fdiv_rn(s, os0), 1.0e-5f));
+        c_D[k] = D;
+        c_rD[k] = __fdiv_rn(1.0f, D);
+    }
+    float ent_shared = 0.0f;  // sum over the 12 actions in order (the quad's lanes hold 3 each)
+#pragma unroll
+    for (int a = 0; a < kActA; ++a)
+        ent_shared = __fadd_rn(ent_shared, __fadd_rn(kEntC, __shfl(c_ls[a % 3], (lane & ~3) + a / 3, kWave)));
+    float d[3], lpart = 0.0f, klpart = 0.0f;
+    bool kl_slow = false;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const float dd = x[k] - mu[k];
+        d[k] = dd;
+        lpart += (-(dd * dd) * c_inv_den[k] - c_ls[k]) - kLogSqrt2Pi;
+        const float osk = os[k];
+        const float dm = __fsub_rn(om[k], mu[k]);
+        const float n = __fadd_rn(__fmul_rn(osk, osk), __fmul_rn(dm, dm));
+        const float t1 = c_t1[k];
+        const float q0 = __fmul_rn(n, c_rD[k]);
+        const float t2 = __builtin_fmaf(__builtin_fmaf(-q0, c_D[k], n), c_rD[k], q0);
+        kl_slow |= !(osk == c_os[k] && n >= 0x1p-60f && n <= 0x1p60f);
+        klpart = __fadd_rn(klpart, __fsub_rn(__fadd_rn(t1, t2), 0.5f));
+    }
+    if (ap.compute_kl && kl_slow) {  // the reference's exact expression for every element of this lane (rare)
+        klpart = 0.0f;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const float s = c_s[k], osk = os[k];
+            const float dm = __fsub_rn(om[k], mu[k]);
+            const float t1 = logf(__fadd_rn(__fdiv_rn(s, osk), 1.0e-5f));
+            const float t2 = __fdiv_rn(__fadd_rn(__fmul_rn(osk, osk), __fmul_rn(dm, dm)), __fmul_rn(2.0f, __fmul_rn(s, s)));
+            klpart = __fadd_rn(klpart, __fsub_rn(__fadd_rn(t1, t2), 0.5f));
+        }
+    }
+    const float logp = quad_sum(lpart);
+    // surrogate (ppo.py:297-302)
+    const float ratio = expf(logp - old_logp);
+    const float nadv = -adv;
+    const float surr = nadv * ratio;
+    const float rc = fminf(fmaxf(ratio, ap.ratio_lo), ap.ratio_hi);
+    const float surr_c = nadv * rc;
+    float g_s, g_sc;
+    max_grads(surr, surr_c, ap.g_surr, g_s, g_sc);
+    const bool in_clip = (ratio >= ap.ratio_lo) && (ratio <= ap.ratio_hi);
+    const float g_ratio = g_s * nadv + (in_clip ? g_sc * nadv : 0.0f);
+    const float gj = g_ratio * ratio;
+    // value loss term (ppo.py:305-313; its gradient is the critic head's, rslrl_value_head_fwd_bwd)
+    float vterm;
+    if (ap.clipped_value) {
+        const float dv = V - tv;
+        const float vc = tv + fminf(fmaxf(dv, -ap.clip), ap.clip);
+        const float e1 = V - R;
+        const float e2 = vc - R;
+        vterm = fmaxf(e1 * e1, e2 * e2);
+    } else {
+        const float e = R - V;
+        vterm = e * e;
+    }
+    const float g2 = 2.0f * gj;
+    float gsg[3];
+    {
+        float gm[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const float dd = d[k];
+            gm[k] = g2 * dd * c_inv_den[k];
+            gsg[k] = gj * (dd * dd * c_inv_s3[k] - c_inv_s[k]) + ap.g_ent * c_inv_s[k];
+            dmu[rl * 16 + a0 + k] = gm[k];
+            if (ap.grad_mu) ap.grad_mu[row * kActA + a0 + k] = gm[k];
+        }
+        if (q == 3) *reinterpret_cast<float4*>(dmu + rl * 16 + kActA) = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    {
+        const double s_surr = wave_sum(static_cast<double>(q == 0 ? fmaxf(surr, surr_c) : 0.0f));
+        const double s_val = wave_sum(static_cast<double>(q == 0 ? vterm : 0.0f));
+        const double s_ent = wave_sum(static_cast<double>(q == 0 ? ent_shared : 0.0f));
+        const double s_kl = wave_sum(static_cast<double>(ap.compute_kl ? klpart : 0.0f));
+        if (lane == 0) {
+            wstat[wave * kActCols + 0] = s_surr;
+            wstat[wave * kActCols + 1] = s_val;
+            wstat[wave * kActCols + 2] = s_ent;
+            wstat[wave * kActCols + 3] = s_kl;
+        }
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            double v = static_cast<double>(gsg[k]);
+#pragma unroll
+            for (int off = 4; off < kWave; off <<= 1) v += __shfl_xor(v, off, kWave);
+            if (lane < 4) wstat[wave * kActCols + 4 + 3 * lane + k] = v;
+        }
+    }
+    __syncthreads();  // the d mu tile and the i = 1 stage complete
+    // ---- 3. output-layer backward, half i = 1 (staged) then i = 0 (registers)
+    float* wp = ap.wpart + static_cast<int64_t>(blockIdx.x) * kActTileFloats;
+    if (wave == 0) {  // db = column sums of d mu: lane (o, quarter) adds its 32 rows in order, then the quarters
+        const int o = lane & 15, part = lane >> 4;
+        float s = 0.f;
+#pragma unroll 8
+        for (int r = 32 * part; r < 32 * part + 32; ++r) s += dmu[r * 16 + o];
+        s += __shfl_xor(s, 16, kWave);
+        s += __shfl_xor(s, 32, kWave);
+        if (lane < kActA) wp[kActA * kBN + lane] = s;
+    }
+    const int c = t & (kBN - 1), oh = t >> 8;  // dW columns c, actions 6 oh .. 6 oh + 5 (oh wave-uniform)
+    float wacc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    auto dw_pass = [&](int i) {
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            const float* sb = reinterpret_cast<const float*>(b ? lds1 : lds0);
+#pragma unroll 4
+            for (int l = 0; l < 32; ++l) {
+                const float hv = sb[act_stage_idx(l, c >> 2) + (c & 3)];
+                const float* dr = dmu + (b * 64 + i * 32 + l) * 16 + 6 * oh;
+#pragma unroll
+                for (int k = 0; k < 6; ++k) wacc[k] = fmaf(dr[k], hv, wacc[k]);
+            }
+        }
+    };
+    bf16x8 wa[2][3];
+    auto load_wa = [&]() {
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int qq = 0; qq < 3; ++qq)
+                wa[j][qq] = read_frag<bf16x8>(reinterpret_cast<const char*>(ap.w_t_img) + qq * kX6PlaneB,
+                                              wn * 64 + j * 32 + l32, h);
+    };
+    auto dmu_frag = [&](int i, bf16x8 (&vb)[3]) {
+        const float* r = dmu + (wm * 64 + i * 32 + l32) * 16 + 8 * h;
+        const float4 v0 = *reinterpret_cast<const float4*>(r);
+        const float4 v1 = *reinterpret_cast<const float4*>(r + 4);
+        uint2 lo[3], hi[3];
+        split4(v0, lo[0], lo[1], lo[2]);
+        split4(v1, hi[0], hi[1], hi[2]);
+#pragma unroll
+        for (int qq = 0; qq < 3; ++qq) vb[qq] = __builtin_bit_cast(bf16x8, make_uint4(lo[qq].x, lo[qq].y, hi[qq].x, hi[qq].y));
+    };
+    // dZ of block (i, j) from H values hv (C^T layout): in place over the wave's stage positions, then whole lines out
+    auto dz_block = [&](int i, int j, const bf16x8 (&vb)[3], const f32x16& hv) {
+        const f32x16 dacc = mfma_x6(wa[j], vb, f32x16{});
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            f32x4 o;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float z = dacc[4 * g + e], hh = hv[4 * g + e];
+                o[e] = hh > 0.f ? z : z * (hh + 1.f);  // ELU'(x) = 1 if h > 0 else h + 1
+            }
+            *reinterpret_cast<f32x4*>(stg + act_stage_idx(l32, wn * 16 + j * 8 + 2 * g + h)) = o;
+        }
+        __builtin_amdgcn_wave_barrier();  // one wave's LDS accesses execute in order
+        float* ct = p.c + (row0 + wm * 64 + i * 32) * kBN + (wn * 64 + j * 32);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int sr = 8 * k + (lane >> 3), cq = lane & 7;
+            const f32x4 v = *reinterpret_cast<const f32x4*>(stg + act_stage_idx(sr, wn * 16 + j * 8 + cq));
+            f32x4* dst = reinterpret_cast<f32x4*>(ct + static_cast<uint32_t>(sr * kBN + 4 * cq));
+            if (p.nt) __builtin_nontemporal_store(v, dst);
+            else *dst = v;
+        }
+        __builtin_amdgcn_wave_barrier();
+    };
+    load_wa();
+    dw_pass(1);
+    __syncthreads();  // every wave's reads of the i = 1 stage done
+    {
+        bf16x8 vb[3];
+        dmu_frag(1, vb);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            f32x16 hv;
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const f32x4 h4 = *reinterpret_cast<const f32x4*>(stg + act_stage_idx(l32, wn * 16 + j * 8 + 2 * g + h));
+#pragma unroll
+                for (int e = 0; e < 4; ++e) hv[4 * g + e] = h4[e];
+            }
+            dz_block(1, j, vb, hv);
+        }
+    }
+    stage_half(0);
+    __syncthreads();  // the i = 0 stage complete
+    dw_pass(0);
+    __syncthreads();  // every wave's reads of the i = 0 stage done
+    {
+        bf16x8 vb[3];
+        dmu_frag(0, vb);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) dz_block(0, j, vb, acc[0][j]);
+    }
+    // ---- 4. per-tile partials: dW rows (coalesced over c), then the loss terms over the grid
+#pragma unroll
+    for (int k = 0; k < 6; ++k) wp[(6 * oh + k) * kBN + c] = wacc[k];
+    double v = 0.0;
+    if (t < kActCols) {
+        v = wstat[t];
+#pragma unroll
+        for (int w = 1; w < 8; ++w) v += wstat[w * kActCols + t];
+    }
+    if (fold_grid_partials<kActCols>(ap.partials, ap.tickets, static_cast<int>(gridDim.x), kActCols, v, folded, flag)) {
+        if (t == 0) {
+            const double Bd = static_cast<double>(p.M);
+            float* stats = ap.stats;
+            stats[1] = static_cast<float>(folded[0] / Bd);
+            stats[2] = static_cast<float>(folded[1] / Bd);
+            stats[3] = static_cast<float>(folded[2] / Bd);
+            stats[4] = static_cast<float>(folded[3] / Bd);
+            stats[0] = __fsub_rn(__fadd_rn(stats[1], __fmul_rn(ap.value_loss_coef, stats[2])),
+                                 __fmul_rn(ap.entropy_coef, stats[3]));
+            stats[5] = 0.0f;
+            stats[6] = 0.0f;
+            stats[7] = 0.0f;
+            __hip_atomic_store(ap.tickets, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm (stream-ordered)
+        }
+        if (t < kActA) ap.grad_sigma[t] = static_cast<float>(folded[4 + t]);
+    }
+}
+
 // lds_b0 / lds_b1: the kernel's two LDS buffers (x6_buf_bytes<EPI, PL>() each).  Two LDS objects, not one [2][bytes]
 // array: the waitcnt pass can then tell a DMA into one buffer from reads of the other (distinct alias scopes) where
 // the buffer index is a compile-time constant.  Declared by the kernel so that two bodies in one kernel (the
 // output-layer pair) share them.
 // HEAD (kEpiBiasEluOut, NR 1, full tiles): the value head's backward fused behind it (mlp_gemm_x6_value_head_kernel)
-template <int EPI, bool FULL, int NR, int PL, bool STAGE = true, int KCH = 0, bool HEAD = false>
+template <int EPI, bool FULL, int NR, int PL, bool STAGE = true, int KCH = 0, int HEAD = 0>
 __device__ __forceinline__ void mlp_gemm_x6_body(GemmParams p, const uint4* __restrict__ bimg, char* lds_b0,
-                                                 char* lds_b1) {
+                                                 char* lds_b1, const ActorParams* ap = nullptr) {
     static_assert(PL == 3 || EPI != kEpiEluGradWgrad, "the fused output-layer backward is x6 only");
     using Frag = typename Arith<PL>::frag;
     constexpr int BM = kBM;
@@ -979,7 +1346,17 @@ __device__ __forceinline__ void mlp_gemm_x6_body(GemmParams p, const uint4* __re
                 dst[1] = ok ? src[1] : make_float4(0.f, 0.f, 0.f, 0.f);
             }
         }
-        if constexpr (HEAD) {
+        if constexpr (HEAD == 2) {
+            // the actor head: [output bias | shared std | old std of the mini-batch's sample 0] per action after the bias
+            // (actor_head_epilogue's mu and per-action loss constants)
+            if (t >= 64 && t < 64 + kActA) {
+                const int a = t - 64;
+                xs[kBN + a] = p.obias[a];
+                xs[kBN + kActA + a] = ap->sigma[a];
+                xs[kBN + 2 * kActA + a] = ap->old_sigma[a];
+            }
+        }
+        if constexpr (HEAD == 1) {
             // after the side area: the value weight row in column order [N], then the tile's target values and returns
             // [BM] each, DMA'd now (no registers held through the main loop; its final barrier drains them) -- the
             // epilogue replaces the targets by dV
@@ -1193,7 +1570,11 @@ __device__ __forceinline__ void mlp_gemm_x6_body(GemmParams p, const uint4* __re
                     if (o < p.K && col < p.N) out[o * p.N + col] = red[o * kBN + col] + wacc[o][j];
                 }
         }
-    } else if constexpr (EPI == kEpiBiasEluOut && HEAD) {
+    } else if constexpr (EPI == kEpiBiasEluOut && HEAD == 2) {
+        static_assert(FULL && PL == 3, "actor head: full x6 tiles");
+        actor_head_epilogue(p, *ap, acc, lds_b0, lds_b1, reinterpret_cast<const float*>(lds_b0 + kXsOff), wm, wn, lane,
+                            wave, row0);
+    } else if constexpr (EPI == kEpiBiasEluOut && HEAD == 1) {
         // The critic's head with its backward.  V = ELU(acc + b) w^T + b_out exactly as the plain value-head epilogue
         // below computes it (same operations, same order: the same bits), then dV = d loss / dV per row
         // (value_loss_grad), then the output layer's backward over the H tile still in registers (acc holds H after
@@ -1540,7 +1921,16 @@ __global__ __launch_bounds__(kThreads, MINW) void mlp_gemm_x6_kernel(GemmParams 
 __global__ __launch_bounds__(kThreads, 4) void mlp_gemm_x6_value_head_kernel(GemmParams p, const uint4* __restrict__ bimg) {
     __shared__ __attribute__((aligned(16))) char lds_b0[x6_buf_bytes<kEpiBiasEluOut, 3>()];
     __shared__ __attribute__((aligned(16))) char lds_b1[x6_buf_bytes<kEpiBiasEluOut, 3>()];
-    mlp_gemm_x6_body<kEpiBiasEluOut, true, 1, 3, true, 0, true>(p, bimg, lds_b0, lds_b1);
+    mlp_gemm_x6_body<kEpiBiasEluOut, true, 1, 3, true, 0, 1>(p, bimg, lds_b0, lds_b1);
+}
+
+// The actor's last hidden layer + output layer + the PPO loss + the output layer's backward in one launch
+// (rslrl_actor_head_fwd_bwd; actor_head_epilogue): full 128-row tiles, x6.
+__global__ __launch_bounds__(kThreads, 4) void mlp_gemm_x6_actor_head_kernel(GemmParams p, const uint4* __restrict__ bimg,
+                                                                           ActorParams ap) {
+    __shared__ __attribute__((aligned(16))) char lds_b0[x6_buf_bytes<kEpiBiasEluOut, 3>()];
+    __shared__ __attribute__((aligned(16))) char lds_b1[x6_buf_bytes<kEpiBiasEluOut, 3>()];
+    mlp_gemm_x6_body<kEpiBiasEluOut, true, 4, 3, true, 0, 2>(p, bimg, lds_b0, lds_b1, &ap);
 }
 
 // the K = 48 kernel applies to full tiles of a forward on x6 operands with the deep loop enabled
@@ -2728,6 +3118,68 @@ extern "C" int rslrl_value_head_fwd_bwd(const rslrl_linear_args_t* a, const rslr
     if (tiles > INT32_MAX) return RSLRL_E_INVALID_ARGUMENT;
     hipLaunchKernelGGL(mlp_gemm_x6_value_head_kernel, dim3(static_cast<unsigned>(tiles)), dim3(kThreads), 0,
                        reinterpret_cast<hipStream_t>(stream), p, static_cast<const uint4*>(a->bimage));
+    return launch_status();
+}
+
+// The actor's last hidden layer, output layer, the PPO loss and the output layer's backward in one launch
+// (include/rslrl_amd.h).  Unsupported shapes return RSLRL_E_UNSUPPORTED before anything is launched.
+extern "C" size_t rslrl_actor_head_workspace_bytes(int64_t M) {
+    const int64_t tiles = ceil_div(M > 0 ? M : 0, kBM);
+    const int64_t groups = ceil_div(tiles, kFoldGroup);
+    return 1024 + sizeof(double) * static_cast<size_t>(kActCols * (tiles + groups));
+}
+
+extern "C" int rslrl_actor_head_fwd_bwd(const rslrl_linear_args_t* a, const rslrl_actor_head_args_t* h,
+                                        void* workspace, size_t workspace_bytes, rslrl_stream_t stream) {
+    if (!a || !h || a->op != RSLRL_LINEAR_FWD_OUT) return RSLRL_E_INVALID_ARGUMENT;
+    GemmParams p;
+    const int rc = out_params(a, p);
+    if (rc) return rc;
+    const int64_t tiles = ceil_div(a->M, kBM);
+    if (a->arith != RSLRL_ARITH_X6 || a->nout != kActA || h->num_actions != kActA || a->N != kBN ||
+        a->K != 16 * kKC || a->M % kBM != 0 || a->M < 1 || !p.deep || tiles > int64_t{kFoldGroup} * kFoldGroup)
+        return RSLRL_E_UNSUPPORTED;
+    if (!a->c || !h->actions || !h->old_log_prob || !h->advantages || !h->values || !h->target_values ||
+        !h->returns || !h->old_mu || !h->old_sigma || !h->sigma || !h->out_weight_t_image || !h->wgrad_partials ||
+        !h->grad_sigma || !h->stats || !workspace)
+        return RSLRL_E_INVALID_ARGUMENT;
+    if (!aligned16(a->c) || !aligned16(h->out_weight_t_image) || !aligned16(workspace)) return RSLRL_E_MISALIGNED;
+    if (workspace_bytes < rslrl_actor_head_workspace_bytes(a->M)) return RSLRL_E_WORKSPACE_TOO_SMALL;
+    ActorParams ap{};
+    ap.actions = h->actions;
+    ap.old_mu = h->old_mu;
+    ap.old_sigma = h->old_sigma;
+    ap.sigma = h->sigma;
+    ap.old_logp = h->old_log_prob;
+    ap.adv = h->advantages;
+    ap.values = h->values;
+    ap.target_values = h->target_values;
+    ap.returns = h->returns;
+    ap.w_t_img = static_cast<const uint4*>(h->out_weight_t_image);
+    ap.wpart = h->wgrad_partials;
+    ap.grad_sigma = h->grad_sigma;
+    ap.stats = h->stats;
+    ap.grad_mu = h->grad_mu;
+    ap.tickets = static_cast<unsigned*>(workspace);
+    ap.partials = reinterpret_cast<double*>(static_cast<char*>(workspace) + 1024);
+    // the loss kernel's scalars (rslrl_ppo_loss_fwd_bwd)
+    const float Bf = static_cast<float>(a->M);
+    ap.clip = h->clip_param;
+    ap.ratio_lo = static_cast<float>(1.0 - static_cast<double>(h->clip_param));
+    ap.ratio_hi = static_cast<float>(1.0 + static_cast<double>(h->clip_param));
+    ap.g_surr = 1.0f / Bf;
+    ap.g_ent = -h->entropy_coef / Bf;
+    ap.value_loss_coef = h->value_loss_coef;
+    ap.entropy_coef = h->entropy_coef;
+    ap.clipped_value = h->use_clipped_value_loss ? 1 : 0;
+    ap.compute_kl = h->compute_kl ? 1 : 0;
+    {  // RSLRL_KL_FAST=0 disables the per-action-constant KL (as in the loss kernel)
+        const char* e = std::getenv("RSLRL_KL_FAST");
+        ap.kl_fast = (e && e[0] == '0') ? 0 : 1;
+    }
+    if (tiles > INT32_MAX) return RSLRL_E_INVALID_ARGUMENT;
+    hipLaunchKernelGGL(mlp_gemm_x6_actor_head_kernel, dim3(static_cast<unsigned>(tiles)), dim3(kThreads), 0,
+                       reinterpret_cast<hipStream_t>(stream), p, static_cast<const uint4*>(a->bimage), ap);
     return launch_status();
 }
 

@@ -26,13 +26,12 @@
 #include <vector>
 
 #include "common.h"
+#include "ppo_loss_common.h"
 
 namespace rslrl {
 namespace {
 
 constexpr int kMaxBlocks = 512;  // a lane handles ~3 samples at C3; the last block folds <= 512 partials
-constexpr float kLogSqrt2Pi = 0.91893853320467274178f;  // log(sqrt(2*pi)), normal.py log_prob
-constexpr float kEntC = 1.41893853320467274178f;         // 0.5 + 0.5*log(2*pi), normal.py entropy
 
 struct LossParams {
     int64_t B;
@@ -103,12 +102,6 @@ __device__ __forceinline__ void store_row(float* __restrict__ p, int A, const fl
     }
 }
 
-// torch.max(a, b) backward (derivatives.yaml, maximum): ties give each side grad / 2.
-__device__ __forceinline__ void max_grads(float a, float b, float g, float& ga, float& gb) {
-    const float half = __fmul_rn(g, 0.5f);
-    ga = (a > b) ? g : ((a == b) ? half : 0.0f);
-    gb = (b > a) ? g : ((a == b) ? half : 0.0f);
-}
 
 // Loss-term columns of the per-block partials; shared-sigma gradient columns follow.
 enum { kColSurr = 0, kColValue, kColEnt, kColKl, kNumScalarCols };
@@ -379,7 +372,6 @@ __global__ __launch_bounds__(kBlock) void ppo_loss_kernel(LossParams p, double* 
 // Partials fold in two levels so that the grid can cover one tile per wave: groups of kFoldGroup
 // blocks (last arriver of a group folds the group, fixed order), then the last group folds the groups.
 
-constexpr int kFoldGroup = 64;
 constexpr int kQuadMaxBlocks = 256;  // one workgroup per CU; 6 tiles per wave at C3 (measured: 256 < 512 < 768 us)
 
 using rsrc_t = __amdgpu_buffer_rsrc_t;
@@ -437,49 +429,6 @@ __device__ __forceinline__ void store_piece(rsrc_t r, uint32_t off, const float 
 
 __device__ __forceinline__ float load_f32(rsrc_t r, uint32_t off) {
     return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
-}
-
-// Sum over the 4 lanes of a quad (DPP quad_perm [1,0,3,2] then [2,3,0,1]); every lane of the quad
-// gets the same bits ((v0 + v1) + (v2 + v3), fp addition being commutative).
-__device__ __forceinline__ float quad_sum(float v) {
-    const float a = __fadd_rn(v, __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xB1,
-                                                                                      0xF, 0xF, false)));
-    return __fadd_rn(a, __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, a), 0x4E, 0xF,
-                                                                             0xF, false)));
-}
-
-// Fixed-order fold of `n` (<= 64) partials per column (column c at src[c * ld + r]) into out[c]:
-// 16 lanes per column, each adding rows l16, l16+16, l16+32, l16+48 in that order, then a 16-lane
-// butterfly.  Every load is issued before the first add, so the fold costs one memory round trip.
-// Loads use sc1 (bypass the non-coherent per-CU cache); the caller has acquired.
-template <int kMaxC>
-__device__ __forceinline__ void fold_columns(const double* __restrict__ src, int ld, int n, int ncols,
-                                             double* __restrict__ out) {
-    constexpr int kPasses = (kMaxC + 15) / 16;
-    const int l16 = threadIdx.x & 15;
-    const int cc = threadIdx.x >> 4;
-    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<double*>(src), 0, static_cast<int>(sizeof(double) * ncols * ld), 0x00020000);
-    double v[kPasses][4];
-#pragma unroll
-    for (int ps = 0; ps < kPasses; ++ps) {
-        const int c = ps * 16 + cc;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int r = l16 + 16 * i;
-            // out-of-range offsets read 0 through the buffer resource
-            const int off = (c < ncols && r < n) ? (c * ld + r) * 8 : 0x7ffffff0;
-            v[ps][i] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rsrc, off, 0, 16 /* sc1 */));
-        }
-    }
-#pragma unroll
-    for (int ps = 0; ps < kPasses; ++ps) {
-        double t = ((v[ps][0] + v[ps][1]) + v[ps][2]) + v[ps][3];
-#pragma unroll
-        for (int off = 8; off >= 1; off >>= 1) t += __shfl_xor(t, off, kWave);
-        const int c = ps * 16 + cc;
-        if (l16 == 0 && c < ncols) out[c] = t;
-    }
 }
 
 // fold_columns for up to 256 partials per column: 16 lanes per column, each adding rows l16, l16 + 16, ..., l16 + 240

@@ -144,7 +144,7 @@ class ActorCritic(nn.Module):
         lin = [m for m in mlp if isinstance(m, nn.Linear)]
         return [m.weight for m in lin], [m.bias for m in lin]
 
-    def train_forward(self, obs, side_stream=None, value_head=None):
+    def train_forward(self, obs, side_stream=None, value_head=None, actor_head=None):
         """The update's forward (ppo.py:246-253) without an autograd graph: returns (mean [B, A], sigma, value
         [B, 1], tape) with sigma the shared [A] std (scalar / exp(log_std)) or the per-row [B, A] std of a
         state-dependent head (strided views of the actor output).  Call under torch.no_grad().
@@ -155,15 +155,26 @@ class ActorCritic(nn.Module):
 
         value_head: a fused_mlp.ValueHead of the mini-batch (target values, returns, value-loss settings): the critic's
         last launch then also computes d(value loss)/dV and the value head's backward (networks/fused_mlp.py
-        value_head_fwd_bwd; paired passes only) -- train_backward then takes the critic's gradient from the tape."""
+        value_head_fwd_bwd; paired passes only) -- train_backward then takes the critic's gradient from the tape.
+
+        actor_head: a fused_mlp.ActorHead of the mini-batch (with value_head; shared std only): the actor's last launch
+        then also runs the PPO loss and the output layer's backward (actor_head_fwd_bwd).  Its `sigma` is set here (the
+        std this call returns); actor_head.done tells whether it ran -- the loss statistics and d loss / d sigma are
+        then written and train_backward takes the actor's gradient from the tape (g_mean is not read)."""
         a_obs = self.actor_obs_normalizer(self.get_actor_obs(obs))
         c_obs = self.critic_obs_normalizer(self.get_critic_obs(obs))
         a_obs = a_obs if a_obs.is_contiguous() else a_obs.contiguous()
         c_obs = c_obs if c_obs.is_contiguous() else c_obs.contiguous()
         pair = None
+        if actor_head is not None:
+            if self.state_dependent_std or value_head is None or side_stream is not None:
+                actor_head = None
+            else:
+                std_now = self.std if self.noise_std_type == "scalar" else torch.exp(self.log_std)
+                actor_head.sigma = std_now.detach().contiguous()
         if side_stream is None:  # the actor's and the critic's same-shape layers batched into one launch each
             pair = fused_mlp.train_forward_pair(a_obs, *self._linears(self.actor), c_obs, *self._linears(self.critic),
-                                                value_head=value_head)
+                                                value_head=value_head, actor_head=actor_head)
         if pair is not None:
             y, tape_a, value, tape_c = pair
         elif side_stream is not None:

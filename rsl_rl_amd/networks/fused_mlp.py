@@ -331,6 +331,79 @@ def value_head_fwd_bwd(x, b, N: int, img, b_out, out_img, w_out, head: ValueHead
     return dz, y, wpart
 
 
+class ActorHead:
+    """What the actor's fused head (actor_head_fwd_bwd) needs for the PPO loss of the mini-batch (ppo.py:259-315): the
+    mini-batch fields, the shared std, the loss settings and the destinations of the loss statistics and of
+    d loss / d sigma.  `values` (the critic's output of this pass) is filled in by train_forward_pair."""
+
+    __slots__ = ("actions", "old_log_prob", "advantages", "target_values", "returns", "old_mu", "old_sigma", "sigma",
+                 "clip_param", "value_loss_coef", "entropy_coef", "use_clipped", "compute_kl", "grad_sigma", "stats",
+                 "grad_mu", "values", "done")
+
+    def __init__(self, actions, old_log_prob, advantages, target_values, returns, old_mu, old_sigma, sigma, *,
+                 clip_param, value_loss_coef, entropy_coef, use_clipped, compute_kl, grad_sigma, stats, grad_mu=None):
+        self.actions, self.old_log_prob, self.advantages = actions, old_log_prob, advantages
+        self.target_values, self.returns, self.old_mu, self.old_sigma = target_values, returns, old_mu, old_sigma
+        self.sigma = sigma
+        self.clip_param, self.value_loss_coef, self.entropy_coef = clip_param, value_loss_coef, entropy_coef
+        self.use_clipped, self.compute_kl = use_clipped, compute_kl
+        self.grad_sigma, self.stats, self.grad_mu = grad_sigma, stats, grad_mu
+        self.values = None
+        self.done = False  # set when the fused launch ran (the loss statistics and d sigma are then written)
+
+    def supported(self, M: int) -> bool:
+        A = _lib.ACTOR_HEAD_ACTIONS
+        flat = (self.old_log_prob, self.advantages, self.target_values, self.returns)
+        return (self.sigma.dim() == 1 and self.sigma.numel() == A and self.sigma.is_contiguous()
+                and all(t.is_contiguous() and tuple(t.shape) == (M, A) for t in (self.actions, self.old_mu,
+                                                                                   self.old_sigma))
+                and all(t.is_contiguous() and t.numel() == M for t in flat)
+                and self.grad_sigma.is_contiguous() and self.grad_sigma.numel() == A and self.stats.numel() >= 8
+                and (self.grad_mu is None or (self.grad_mu.is_contiguous() and tuple(self.grad_mu.shape) == (M, A))))
+
+
+_ACTOR_HEAD = os.environ.get("RSLRL_ACTOR_HEAD", "1") != "0"
+ACTOR_HEAD_ACTIONS = _lib.ACTOR_HEAD_ACTIONS
+
+
+def actor_head_fwd_bwd(x, b, N: int, img, b_out, out_img, w_t_img, head: ActorHead):
+    """The actor's last hidden layer, output layer, the PPO loss and the output layer's backward in one launch
+    (rslrl_actor_head_fwd_bwd): returns (dz [M, N], mu [M, A], wpart [tiles, A N + A]) -- dz the gradient at the last
+    hidden layer's pre-activation, mu the action means (the bits linear_fwd_out_ex gives), wpart the output layer's
+    [dW | db] partials for the fold; head.stats / head.grad_sigma receive what kernels.ppo_loss_fwd_bwd writes.  None
+    when the shape is not covered (nothing launched)."""
+    M, K = x.shape
+    A = _lib.ACTOR_HEAD_ACTIONS
+    if head.values is None or head.values.numel() != M or not head.values.is_contiguous() or not head.supported(M):
+        return None
+    L = _lib.lib()
+    tiles = L.rslrl_linear_tiles(M)
+    P = A * N + A
+    dz = torch.empty(M, N, device=x.device, dtype=torch.float32)
+    mu = torch.empty(M, A, device=x.device, dtype=torch.float32)
+    wpart = torch.empty(tiles, P, device=x.device, dtype=torch.float32)
+    args = _gemm_args(_lib.LINEAR_FWD_OUT, _lib.ARITH_X6, x, None, N, img, bias=b, c=dz, out_img=out_img,
+                      out_bias=b_out, y=mu, nout=A)
+    h = _lib.ActorHeadArgs(head.actions.data_ptr(), head.old_log_prob.data_ptr(), head.advantages.data_ptr(),
+                           head.values.data_ptr(), head.target_values.data_ptr(), head.returns.data_ptr(),
+                           head.old_mu.data_ptr(), head.old_sigma.data_ptr(), head.sigma.data_ptr(), A,
+                           float(head.clip_param), float(head.value_loss_coef), float(head.entropy_coef),
+                           int(bool(head.use_clipped)), int(bool(head.compute_kl)), w_t_img.data_ptr(),
+                           wpart.data_ptr(), head.grad_sigma.data_ptr(), head.stats.data_ptr(),
+                           head.grad_mu.data_ptr() if head.grad_mu is not None else None)
+    ws = _kernels_ws().get(x.device, "actor_head", L.rslrl_actor_head_workspace_bytes(M))  # zero-filled once
+    # algorithmic bytes: read x and the loss's row inputs (actions, old mu, old sigma, 5 scalars), write mu, dz and the
+    # per-tile partials
+    with timer.span(f"linear_actor_head[M={M},K={K},N={N}]", x.device,
+                    4 * M * (K + 3 * A + 5 + A + N) + 4 * tiles * P, 2 * M * N * (K + 3 * A)):
+        rc = L.rslrl_actor_head_fwd_bwd(ctypes.byref(args), ctypes.byref(h), ws.data_ptr(), ws.numel(), _stream(x))
+    if rc == _lib.E_UNSUPPORTED:
+        return None
+    _lib.check(rc, "rslrl_actor_head_fwd_bwd")
+    head.done = True
+    return dz, mu, wpart
+
+
 def _fuse_out_fwd(ws) -> bool:
     """The last hidden layer and the output layer run as one linear_fwd_out launch (split modes only)."""
     return _FUSE_OUT_FWD and _split() and len(ws) >= 2 and ws[-1].shape[0] <= MAX_OUT_WIDTH \
@@ -497,13 +570,14 @@ def linear_dgrad_elu_wgrad_deferred(dz, h, img, dwb_out, defer):
 
 
 def _head_result(tape, dwb_out, defer):
-    """(dz_prev, dw, db) of a critic tape whose head ran value_head_fwd_bwd: its dz, and the fold of its partials
-    queued on `defer`."""
-    dz, wpart = tape.head
+    """(dz_prev, dw, db) of a tape whose head ran fused (value_head_fwd_bwd: 1 output, actor_head_fwd_bwd: 12): its
+    dz, and the fold of its [dW | db] partials queued on `defer`."""
+    dz, wpart = tape.head[:2]
+    nred = tape.head[2] if len(tape.head) > 2 else 1
     K = dz.shape[1]
-    dwb = _out_or_empty(dwb_out, (K + 1,), dz.device)
-    defer.add(wpart, wpart.shape[0], wpart.shape[1], dwb, K + 1)
-    return dz, dwb[:K].view(1, K), dwb[K:]
+    dwb = _out_or_empty(dwb_out, (nred * K + nred,), dz.device)
+    defer.add(wpart, wpart.shape[0], wpart.shape[1], dwb, nred * K + nred)
+    return dz, dwb[:nred * K].view(nred, K), dwb[nred * K:]
 
 
 def linear_wgrad(dz, x, arith=_lib.ARITH_X6, dz_amax=None, x_amax=None, out=None, bias_side=0, dwb_out=None):
@@ -862,7 +936,8 @@ def _pairable(ws_a, ws_c, x_a, x_c) -> bool:
     return all(w.shape[0] <= 16 and w.shape[1] <= MAX_WIDTH for w in (ws_a[-1], ws_c[-1]))
 
 
-def train_forward_pair(x_a, ws_a, bs_a, x_c, ws_c, bs_c, value_head: ValueHead | None = None):
+def train_forward_pair(x_a, ws_a, bs_a, x_c, ws_c, bs_c, value_head: ValueHead | None = None,
+                       actor_head: ActorHead | None = None):
     """train_forward of the actor (x_a, ws_a, bs_a) and the critic (x_c, ...) with each same-shape hidden layer of the
     two in one launch (rslrl_linear_gemm_pair) and every B image of both passes in one launch; the output layers run
     as two fused launches.  Values identical to two train_forward calls.  Returns (y_a, tape_a, y_c, tape_c), or None
@@ -870,7 +945,10 @@ def train_forward_pair(x_a, ws_a, bs_a, x_c, ws_c, bs_c, value_head: ValueHead |
 
     value_head: the mini-batch's value-loss inputs -- the critic's last launch then also runs the value loss's gradient
     and the value head's backward (value_head_fwd_bwd): its tape carries the last hidden layer's dz instead of that
-    layer's activation, and train_backward_pair ignores the critic's dy (the same values the loss kernel writes)."""
+    layer's activation, and train_backward_pair ignores the critic's dy (the same values the loss kernel writes).
+    actor_head (with value_head): the PPO loss inputs -- the critic's launch then runs first and the actor's last
+    launch also runs the whole loss and the output layer's backward (actor_head_fwd_bwd; actor_head.done tells whether
+    it ran, in which case the loss statistics and d sigma are written and the actor's tape carries its head)."""
     if not _pairable(ws_a, ws_c, x_a, x_c):
         return None
     ws, bs, xs = (ws_a, ws_c), (bs_a, bs_c), (x_a, x_c)
@@ -888,18 +966,27 @@ def train_forward_pair(x_a, ws_a, bs_a, x_c, ws_c, bs_c, value_head: ValueHead |
     h = [x if x.is_contiguous() else x.contiguous() for x in xs]
     hs = [[h[0]], [h[1]]]
     y = [None, None]
-    head = None
+    head = head_a = None
     for l in range(nh):
         if l < nh - 1:
             h, _ = linear_fwd_pair(h, [bs[0][l], bs[1][l]], ws[0][l].shape[0], True, [fwd[0][l], fwd[1][l]],
                                    _lib.ARITH_X6, [None, None], [False, False])
         else:
-            for i in range(2):
+            # the critic first when the actor's head runs the loss (it reads the values)
+            fuse_actor = actor_head is not None and value_head is not None and _VALUE_HEAD and _ACTOR_HEAD
+            for i in ((1, 0) if fuse_actor else (0, 1)):
                 if i == 1 and value_head is not None and _VALUE_HEAD:
                     res = value_head_fwd_bwd(h[1], bs[1][l], ws[1][l].shape[0], fwd[1][l], bs[1][-1], out_img[1],
                                              ws[1][-1], value_head)
                     if res is not None:
                         head, y[1], h[1] = (res[0], res[2]), res[1], None
+                        continue
+                if i == 0 and fuse_actor and head is not None:
+                    actor_head.values = y[1]
+                    res = actor_head_fwd_bwd(h[0], bs[0][l], ws[0][l].shape[0], fwd[0][l], bs[0][-1], out_img[0],
+                                             dgr[0][nh], actor_head)
+                    if res is not None:
+                        head_a, y[0], h[0] = (res[0], res[2], _lib.ACTOR_HEAD_ACTIONS), res[1], None
                         continue
                 h[i], y[i] = linear_fwd_out_ex(h[i], bs[i][l], ws[i][l].shape[0], fwd[i][l], _lib.ARITH_X6, None,
                                                bs[i][-1], out_img[i], store_h=True)
@@ -907,6 +994,7 @@ def train_forward_pair(x_a, ws_a, bs_a, x_c, ws_c, bs_c, value_head: ValueHead |
             hs[i].append(h[i])
     tapes = [MLPTape(hs[i], list(ws[i]), dgr[i], [None] * (nh + 1), h3, True) for i in range(2)]
     tapes[1].head = head
+    tapes[0].head = head_a
     return y[0], tapes[0], y[1], tapes[1]
 
 
@@ -926,7 +1014,7 @@ def train_backward_pair(tape_a, dy_a, outs_a, tape_c, dy_c, outs_c):
         return False
     # output layers: dgrad + ELU' + their weight and bias gradients over one read of h, both in one launch
     ds = [d if d.is_contiguous() else d.contiguous() for d in dys]
-    K = tape_a.hs[L - 1].shape[1]
+    K = tape_a.ws[L - 1].shape[1]  # (hs[L - 1] is None behind a fused head)
     dwb_outs, adjacent = [], []
     for i in range(2):
         nred = ds[i].shape[1]
@@ -939,7 +1027,8 @@ def train_backward_pair(tape_a, dy_a, outs_a, tape_c, dy_c, outs_c):
     # are still in the Infinity Cache, instead of one batched fold after the pass (which reads them back from HBM)
     eager = os.environ.get("RSLRL_FOLD_EAGER", "0") == "1"
     if tape_c.head is not None:  # the critic's head ran its backward in the forward launch (value_head_fwd_bwd)
-        res = [linear_dgrad_elu_wgrad_deferred(ds[0], tape_a.hs[L - 1], tape_a.dgrad_imgs[L - 1], dwb_outs[0], folds),
+        res = [_head_result(tape_a, dwb_outs[0], folds) if tape_a.head is not None else  # actor_head_fwd_bwd
+               linear_dgrad_elu_wgrad_deferred(ds[0], tape_a.hs[L - 1], tape_a.dgrad_imgs[L - 1], dwb_outs[0], folds),
                _head_result(tape_c, dwb_outs[1], folds)]
     else:
         res = linear_dgrad_elu_wgrad_pair(ds, [t.hs[L - 1] for t in tapes], [t.dgrad_imgs[L - 1] for t in tapes],
