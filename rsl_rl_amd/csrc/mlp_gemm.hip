@@ -1188,19 +1188,20 @@ __device__ __forceinline__ void actor_head_epilogue(const GemmParams& p, const A
         s += __shfl_xor(s, 32, kWave);
         if (lane < kActA) wp[kActA * kBN + lane] = s;
     }
-    const int c = t & (kBN - 1), oh = t >> 8;  // dW columns c, actions 6 oh .. 6 oh + 5 (oh wave-uniform)
-    float wacc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    auto dw_pass = [&](int i) {
+    const int c = t & (kBN - 1), rh = t >> 8;  // dW column c over the 32 rows of buffer rh (wave-uniform)
+    float wacc[kActA];
 #pragma unroll
-        for (int b = 0; b < 2; ++b) {
-            const float* sb = reinterpret_cast<const float*>(b ? lds1 : lds0);
+    for (int o = 0; o < kActA; ++o) wacc[o] = 0.f;
+    auto dw_pass = [&](int i) {  // 3 broadcast d mu reads + 1 H read per 12 FMAs
+        const float* sb = reinterpret_cast<const float*>(rh ? lds1 : lds0);
 #pragma unroll 4
-            for (int l = 0; l < 32; ++l) {
-                const float hv = sb[act_stage_idx(l, c >> 2) + (c & 3)];
-                const float* dr = dmu + (b * 64 + i * 32 + l) * 16 + 6 * oh;
+        for (int l = 0; l < 32; ++l) {
+            const float hv = sb[act_stage_idx(l, c >> 2) + (c & 3)];
+            const float4* dr = reinterpret_cast<const float4*>(dmu + (rh * 64 + i * 32 + l) * 16);
+            const float4 d0 = dr[0], d1 = dr[1], d2 = dr[2];
+            const float dd[kActA] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w, d2.x, d2.y, d2.z, d2.w};
 #pragma unroll
-                for (int k = 0; k < 6; ++k) wacc[k] = fmaf(dr[k], hv, wacc[k]);
-            }
+            for (int o = 0; o < kActA; ++o) wacc[o] = fmaf(dd[o], hv, wacc[o]);
         }
     };
     bf16x8 wa[2][3];
@@ -1276,8 +1277,15 @@ __device__ __forceinline__ void actor_head_epilogue(const GemmParams& p, const A
         for (int j = 0; j < 2; ++j) dz_block(0, j, vb, acc[0][j]);
     }
     // ---- 4. per-tile partials: dW rows (coalesced over c), then the loss terms over the grid
+    __syncthreads();  // the stages are no longer read: the buffer-1 half of dW goes through LDS
+    float* dwx = reinterpret_cast<float*>(lds0);  // [12][256]
+    if (rh == 1)
 #pragma unroll
-    for (int k = 0; k < 6; ++k) wp[(6 * oh + k) * kBN + c] = wacc[k];
+        for (int o = 0; o < kActA; ++o) dwx[o * kBN + c] = wacc[o];
+    __syncthreads();
+    if (rh == 0)
+#pragma unroll
+        for (int o = 0; o < kActA; ++o) wp[o * kBN + c] = wacc[o] + dwx[o * kBN + c];
     double v = 0.0;
     if (t < kActCols) {
         v = wstat[t];

@@ -120,21 +120,30 @@ __global__ __launch_bounds__(kBlock) void rollout_record_kernel(rslrl_rollout_ar
             }
         }
         __syncthreads();
-        if (static_cast<int>(threadIdx.x) < rows) {
-            // log-prob of the action under Normal(mu, sigma), torch's expression (see the per-env part below)
+        {
+            // log-prob of the action under Normal(mu, sigma), torch's expression (see the per-env part below): the
+            // per-action terms (a division and a log each) on the row's four lanes (action j on lane j & 3), written
+            // over the action values they came from, then summed in action order by the row's first lane
+            const int r = threadIdx.x >> 2, q = threadIdx.x & 3;
             const float c = 0.918938533204672742f;
-            const float* xr = lds_w + threadIdx.x * A;
-            const float* mr = lds_w + (kRecRows + threadIdx.x) * A;
-            const float* sr = lds_w + (2 * kRecRows + threadIdx.x) * A;
-            float lp = 0.f;
-            for (int j = 0; j < A; ++j) {
-                const float sj = sr[j];
-                const float d = __fsub_rn(xr[j], mr[j]);
-                const float num = -__fmul_rn(d, d);
-                const float den = __fmul_rn(2.f, __fmul_rn(sj, sj));
-                lp = __fadd_rn(lp, __fsub_rn(__fsub_rn(__fdiv_rn(num, den), logf(sj)), c));
+            float* xr = lds_w + r * A;
+            const float* mr = lds_w + (kRecRows + r) * A;
+            const float* sr = lds_w + (2 * kRecRows + r) * A;
+            if (r < rows) {
+                for (int j = q; j < A; j += 4) {
+                    const float sj = sr[j];
+                    const float d = __fsub_rn(xr[j], mr[j]);
+                    const float num = -__fmul_rn(d, d);
+                    const float den = __fmul_rn(2.f, __fmul_rn(sj, sj));
+                    xr[j] = __fsub_rn(__fsub_rn(__fdiv_rn(num, den), logf(sj)), c);
+                }
             }
-            a.out_logp[n0 + threadIdx.x] = lp;
+            __syncthreads();
+            if (r < rows && q == 0) {
+                float lp = 0.f;
+                for (int j = 0; j < A; ++j) lp = __fadd_rn(lp, xr[j]);
+                a.out_logp[n0 + r] = lp;
+            }
         }
         return;
     }

@@ -364,6 +364,7 @@ class ActorHead:
 
 _ACTOR_HEAD = os.environ.get("RSLRL_ACTOR_HEAD", "1") != "0"
 ACTOR_HEAD_ACTIONS = _lib.ACTOR_HEAD_ACTIONS
+actor_head_launches = 0  # fused actor-head launches so far (tests check which path an update took)
 
 
 def actor_head_fwd_bwd(x, b, N: int, img, b_out, out_img, w_t_img, head: ActorHead):
@@ -401,6 +402,8 @@ def actor_head_fwd_bwd(x, b, N: int, img, b_out, out_img, w_t_img, head: ActorHe
         return None
     _lib.check(rc, "rslrl_actor_head_fwd_bwd")
     head.done = True
+    global actor_head_launches
+    actor_head_launches += 1
     return dz, mu, wpart
 
 

@@ -136,7 +136,8 @@ def test_runner_with_normalizers_and_rnd(cuda_device, reward_norm):
 def test_update_c2_width_matches_reference(golden_meta, cuda_device):
     """One full update() at config C2's shape (N4096 T24 O48 A12, actor/critic 3x256 ELU, E5 M4; mini-batch 24,576
     rows) against the reference's update on CPU (make_golden.make_update_c2), once through the default x6
-    split-bf16 GEMMs and once through the exact-fp32 MFMA GEMMs.
+    split-bf16 GEMMs (the actor's head with the loss fused: rslrl_actor_head_fwd_bwd) and once through the exact-fp32
+    MFMA GEMMs (separate loss kernel).
 
     * first mini-batch (no drift yet): every parameter's gradient within 1e-5 of its max |g|;
     * learning-rate trace (increase, then two decreases) exact; loss means rtol 1e-4;
@@ -160,7 +161,10 @@ def test_update_c2_width_matches_reference(golden_meta, cuda_device):
             head = torch.from_numpy(z["storage/returns_head"])
             torch.testing.assert_close(alg.storage.returns[:2].cpu(), head, rtol=1e-5, atol=1e-5)
             grads = [None]
+            launches = fused_mlp.actor_head_launches
             loss, lr_trace = run_recorded_update(alg, grads)
+            # x6: every mini-batch's actor head ran the loss and its backward fused (rslrl_actor_head_fwd_bwd)
+            assert fused_mlp.actor_head_launches - launches == (20 if mode == "x6" else 0), mode
         finally:
             fused_mlp.set_gemm_mode(prev)
         ref_g = torch.from_numpy(z["grad_mb0"]).double()
