@@ -23,6 +23,7 @@ SHORT = {
     "adv_normalize_kernel": "adv_normalize",
     "adv_normalize_slot_kernel": "adv_normalize_slot",
     "mlp_gemm_x6_value_head_kernel": "x6_value_head",
+    "mlp_gemm_x6_actor_head_kernel": "x6_actor_head",
     "out_bwd_valu_kernel": "out_bwd",
     "out_bwd_valu_pair_kernel": "out_bwd_pair",
     "moments_kernel": "moments",
