@@ -293,12 +293,14 @@ def main():
     kernels.timer.enabled = True
     if os.environ.get("RSLRL_BENCH_LAUNCH_EVENTS", "1") != "0":  # 0: A/B of the binding's cost
         kernels.timer.arm_launch_events(64 * args.steps * 20)  # ~20 loss launches per iteration at the default E x M
+    hist0 = len(runner.iteration_stats_history)
     t0 = time.perf_counter()
     runner.learn(args.steps)
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    timed_phases = runner.iteration_stats_history[hist0:]
     kernels.timer.enabled = False
     kernels.timer.disarm_launch_events()
     # one more iteration with the MLP GEMM launches timed (kept out of the headline timing: ~470 event
@@ -422,6 +424,10 @@ def main():
         "hot_path": {"kernels": hot, "ms_per_step": round(hot_ms, 4),
                      "env_steps_per_s": round(T * N / (hot_ms * 1e-3), 1) if hot_ms else None},
         "phases_last_iter": {k: round(v, 4) for k, v in runner.last_iteration_stats.items() if k != "loss_dict"},
+        # host-side phase times of every timed iteration (the runner's own split: collection = the rollout's host time up
+        # to compute_returns, learn = update() to its statistics read-back); phases_last_iter is the extra MLP-timed one
+        "phases_timed_ms": {"collection": [round(c * 1e3, 2) for c, _ in timed_phases],
+                            "learn": [round(l * 1e3, 2) for _, l in timed_phases]},
         # end-to-end (value), update phase and hot path (above) reported apart
         "update_env_steps_per_s": round(T * N * world / runner.last_iteration_stats["learn_time"], 1),
         "cpu_baseline": None,

@@ -69,6 +69,7 @@ class OnPolicyRunner:
         self.current_learning_iteration = 0
         self.git_status_repos = [rsl_rl_amd.__file__]
         self.last_iteration_stats: dict = {}
+        self.iteration_stats_history: list = []  # (collection_time, learn_time) of every iteration (benchmarking)
 
     # ------------------------------------------------------------------ training loop (:61-175)
     def learn(self, num_learning_iterations: int, init_at_random_ep_len: bool = False):  # noqa: C901
@@ -143,6 +144,7 @@ class OnPolicyRunner:
                 "total_fps": steps / (collection_time + learn_time),
                 "loss_dict": loss_dict,
             }
+            self.iteration_stats_history.append((collection_time, learn_time))
             if self.log_dir is not None and not self.disable_logs:
                 self.log(locals())
                 if it % self.save_interval == 0:
