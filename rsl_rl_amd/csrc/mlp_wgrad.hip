@@ -451,6 +451,10 @@ __global__ __launch_bounds__(kBlock) void fold_wide_kernel(const float* __restri
 // groups' fp64 sums go to the workspace and the last-arriving group of the column block adds them in group order.
 // Deterministic: the order depends on (S, G) alone.
 constexpr int kMaxFoldJobs = 16;
+#ifndef RSLRL_FOLD_UNROLL
+#define RSLRL_FOLD_UNROLL 8
+#endif
+constexpr int kFoldUnroll = RSLRL_FOLD_UNROLL;  // slices loaded per round per thread (fold_batch_kernel)
 constexpr int kFoldGroupSlices = 256;
 struct FoldJobs {
     const float* part[kMaxFoldJobs];
@@ -490,16 +494,19 @@ __global__ __launch_bounds__(kBlock) void fold_batch_kernel(FoldJobs jobs) {
     double a[4] = {0.0, 0.0, 0.0, 0.0};
     if (e0 < NK) {
         const float* src = jobs.part[j] + e0;
-        for (int s0 = s_lo + ph; s0 < s_hi; s0 += 16 * 16) {
-            float4 v[16];
+        // kFoldUnroll slices per round (the same slice order for any unroll: s_lo + ph, + 16, + 32, ...); 8 keeps the
+        // kernel at half the registers of 16, i.e. twice the blocks per CU in flight (the paired jobs have 128 slices:
+        // one round either way)
+        for (int s0 = s_lo + ph; s0 < s_hi; s0 += 16 * kFoldUnroll) {
+            float4 v[kFoldUnroll];
 #pragma unroll
-            for (int k = 0; k < 16; ++k) {
+            for (int k = 0; k < kFoldUnroll; ++k) {
                 const int s = s0 + 16 * k;
                 v[k] = s < s_hi ? *reinterpret_cast<const float4*>(src + static_cast<int64_t>(s) * NK)
                                 : make_float4(0.f, 0.f, 0.f, 0.f);
             }
 #pragma unroll
-            for (int k = 0; k < 16; ++k) {
+            for (int k = 0; k < kFoldUnroll; ++k) {
                 a[0] += v[k].x; a[1] += v[k].y; a[2] += v[k].z; a[3] += v[k].w;
             }
         }

@@ -17,6 +17,8 @@ from .vec_env import VecEnv
 
 
 class SyntheticVecEnv(VecEnv):
+    kRing = 3  # fused step: output buffer sets reused round-robin
+
     def __init__(self, num_envs: int, num_obs: int, num_actions: int, device="cpu", *, seed: int = 0,
                  num_privileged_obs: int = 0, done_prob: float = 0.02, timeout_prob: float = 0.0,
                  max_episode_length: int = 1000, step_dt: float = 0.02):
@@ -41,6 +43,7 @@ class SyntheticVecEnv(VecEnv):
                        and os.environ.get("RSLRL_SYNTH_ENV", "fused") != "torch")
         self._seed = int(seed)
         self._step_count = 0
+        self._ring = None  # the fused step's output buffer sets (allocated at the first step)
 
     @property
     def unwrapped(self):
@@ -81,15 +84,23 @@ class SyntheticVecEnv(VecEnv):
         from ..kernels import _stream
 
         n, dev = self.num_envs, self.device
-        obs = torch.empty(n, self.num_obs, device=dev)
-        rewards = torch.empty(n, device=dev)
-        dones = torch.empty(n, dtype=torch.long, device=dev)
-        time_outs = torch.empty(n, device=dev)
+        # outputs from a ring of kRing buffer sets: a step's tensors stay valid for the next kRing - 1 steps (the runner
+        # consumes them within one; a ring instead of four allocations and a TensorDict per step: ~10 us of host time
+        # on the launch-bound rollout of a small per-GPU share)
+        if self._ring is None:
+            self._ring = []
+            for _ in range(self.kRing):
+                obs = torch.empty(n, self.num_obs, device=dev)
+                bufs = (TensorDict({"policy": obs}, batch_size=[n], device=dev), obs, torch.empty(n, device=dev),
+                        torch.empty(n, dtype=torch.long, device=dev), torch.empty(n, device=dev))
+                ptrs = (bufs[1].data_ptr(), bufs[2].data_ptr(), bufs[3].data_ptr(), bufs[4].data_ptr())
+                self._ring.append((bufs, ptrs, {"time_outs": bufs[4]}))
         self._step_count += 1
+        bufs, ptrs, extras = self._ring[self._step_count % self.kRing]
         rc = _lib.lib().rslrl_synthetic_env_step(
-            obs.data_ptr(), self.num_obs, rewards.data_ptr(), dones.data_ptr(), time_outs.data_ptr(),
-            self.episode_length_buf.data_ptr(), n, self._seed, self._step_count & 0xFFFFFFFF, float(self.done_prob),
-            float(self.timeout_prob), int(self.max_episode_length), _stream(dev))
+            ptrs[0], self.num_obs, ptrs[1], ptrs[2], ptrs[3], self.episode_length_buf.data_ptr(), n, self._seed,
+            self._step_count & 0xFFFFFFFF, float(self.done_prob), float(self.timeout_prob), int(self.max_episode_length),
+            _stream(dev))
         _lib.check(rc, "rslrl_synthetic_env_step")
-        self._obs = TensorDict({"policy": obs}, batch_size=[n], device=dev)
-        return self._obs, rewards, dones, {"time_outs": time_outs}
+        self._obs = bufs[0]
+        return self._obs, bufs[2], bufs[3], dict(extras)

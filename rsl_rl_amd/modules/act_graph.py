@@ -47,6 +47,7 @@ class RolloutActGraph:
         self._imgs = None  # the image tensors both graphs use (written by the first one's replay)
         self._img_gen = None  # fused_mlp._frozen_gen of the last image build
         self._eps = None  # the sample's standard normals, drawn before each replay
+        self._dists = {}  # id(output tuple) -> the Normal over that graph's static mean / scale
 
     @staticmethod
     def enabled() -> bool:
@@ -68,13 +69,15 @@ class RolloutActGraph:
         """(actions, values) of the step, with policy.distribution set as act() sets it; None: run eagerly.
 
         actions is a fresh tensor; values and policy.distribution's mean / scale are the graph's static outputs and
-        stay valid only until the next call."""
+        stay valid only until the next call (policy.distribution is the same Normal object on every step of a graph:
+        the replay rewrites its loc / scale in place)."""
         key = self._config(obs)
         if key is None or key in self._failed:
             return None
         if key != self._key:
             self._key, self._seen, self._graph, self._static_in, self._out = key, 0, None, None, None
             self._graph_fwd, self._out_fwd, self._imgs, self._img_gen, self._eps = None, None, None, None, None
+            self._dists = {}
         if self._graph is None:
             self._seen += 1
             if self._seen < 2:  # the first call of a configuration runs eagerly (lazy initialisations happen there)
@@ -87,17 +90,23 @@ class RolloutActGraph:
         frozen = fused_mlp._frozen_depth > 0
         if frozen and self._graph_fwd is not None and self._img_gen == fused_mlp._frozen_gen:
             self._graph_fwd.replay()  # the images of this rollout's weights are current
-            actions, values, mean, scale = self._out_fwd
+            out = self._out_fwd
         else:
             self._graph.replay()
             self._img_gen = fused_mlp._frozen_gen if frozen else None
-            actions, values, mean, scale = self._out
+            out = self._out
+        actions, values = out[0], out[1]
         # Aliasing contract: actions are cloned; the returned values and the distribution's mean / scale ARE the
         # graph's static outputs, valid only until the next call (the next replay overwrites them; the eager path
         # allocates new tensors).  PPO.act keeps them in its transition only until process_env_step copies them into
         # the storage in the same env step.  (A clone of values would add one launch per env step to the
         # host-bound rollout at the 16384-env share.)
-        self.policy.distribution = Normal(mean, scale)
+        # one Normal per graph output set, built once: its loc / scale ARE the static outputs (a Normal per step cost
+        # ~8 us of host time in torch.distributions' broadcast_all on the launch-bound rollout)
+        dist = self._dists.get(id(out))
+        if dist is None or dist.loc is not out[2] or dist.scale is not out[3]:
+            dist = self._dists[id(out)] = Normal(out[2], out[3])
+        self.policy.distribution = dist
         return actions.clone(), values
 
     def _capture(self, obs, key) -> bool:

@@ -78,6 +78,7 @@ class RolloutStorage:
             return torch.zeros(*shape, dtype=dtype, device=device)
 
         self.records = None
+        self._rec_plan = None  # kernels.RolloutRecordPlan of the fused rollout step (add_transition_fused)
         self.record_layout = self._record_layout(training_type, obs, actions_shape, device)
         if self.record_layout is not None:
             R, offs = self.record_layout
@@ -188,6 +189,23 @@ class RolloutStorage:
         if self.step >= self.num_transitions_per_env:
             raise OverflowError("Rollout buffer overflow! You should call clear() before adding new transitions.")
         t = self.step
+        sigma = transition.action_sigma
+        if sigma.dim() == 2 and sigma.stride(0) == 0:  # Normal's expand of a shared [A] std
+            sigma = sigma[0]
+        if self.records is not None and rnd is None and extra_reward is None and intrinsic_out is None:
+            # the common step (record layout, no RND): a cached argument struct, only this step's pointers written
+            srcs = [transition.observations[k] for k in self.observations.keys()]
+            args = (transition.actions, transition.action_mean, sigma, transition.values, rewards, dones, time_outs, srcs,
+                    gamma)
+            plan = self._rec_plan
+            if plan is None or not plan.matches(*args):
+                plan = self._rec_plan = self._record_plan(*args)
+            if plan is not None:
+                plan.launch(t, *args[:-1])
+                self.step += 1
+                self._fills += 1
+                self._slot_key = None  # written through data_ptr (no _version bump): the slots are stale
+                return
         pairs, late = [], []
         for k, dst in self.observations.items():
             src = transition.observations[k]
@@ -198,9 +216,6 @@ class RolloutStorage:
                 pairs.append((src, dst[t]))
             else:
                 late.append((src, dst[t]))  # after the launch: with records it writes every record whole
-        sigma = transition.action_sigma
-        if sigma.dim() == 2 and sigma.stride(0) == 0:  # Normal's expand of a shared [A] std
-            sigma = sigma[0]
         kernels.rollout_record(
             t, obs_pairs=pairs, actions=transition.actions, mu=transition.action_mean, sigma=sigma,
             values=transition.values, rewards=rewards, dones=dones, time_outs=time_outs, gamma=gamma,
@@ -213,6 +228,22 @@ class RolloutStorage:
         self.step += 1
         self._fills += 1
         self._slot_key = None  # written through data_ptr (no _version bump): the slots are stale
+
+    def _record_plan(self, actions, mu, sigma, values, rewards, dones, time_outs, srcs, gamma):
+        """kernels.RolloutRecordPlan for steps shaped like this one, or None (the general path takes them)."""
+        codes = (torch.float32, torch.uint8, torch.bool, torch.int32, torch.int64)
+        if len(srcs) > 4 or dones.dtype not in codes or (time_outs is not None and time_outs.dtype not in codes):
+            return None
+        if not all(s.dtype == torch.float32 and s.is_cuda and s.dim() == 2 and s.shape[-1] % 4 == 0 for s in srcs):
+            return None
+        outs = {"out_actions": self.actions, "out_rewards": self.rewards, "out_dones": self.dones,
+                "out_values": self.values, "out_logp": self.actions_log_prob, "out_mu": self.mu,
+                "out_sigma": self.sigma, "out_records": self.records}
+        plan = kernels.RolloutRecordPlan(outs, [self.observations[k] for k in self.observations.keys()],
+                                         [s.shape[-1] for s in srcs], self.num_envs, self.actions.shape[-1], gamma,
+                                         dones.dtype, time_outs.dtype if time_outs is not None else None,
+                                         sigma.dim() == 1, self.device)
+        return plan if plan.matches(actions, mu, sigma, values, rewards, dones, time_outs, srcs, gamma) else None
 
     def _save_hidden_states(self, hidden_states):
         if hidden_states is None or hidden_states == (None, None):
