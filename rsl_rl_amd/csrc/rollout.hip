@@ -37,7 +37,10 @@ __device__ __forceinline__ float load_flag(const void* p, int dtype, int64_t i) 
 
 // Record-mode copy segments (obs groups, actions, mu, sigma) in 16-byte units of a destination record
 constexpr int kMaxSeg = RSLRL_ROLLOUT_MAX_OBS + 3;
-constexpr int kRecRows = 64;  // records per copy block
+#ifndef RSLRL_REC_ROWS
+#define RSLRL_REC_ROWS 64
+#endif
+constexpr int kRecRows = RSLRL_REC_ROWS;  // records per copy block (<= 64: four lanes per record in the log-prob)
 struct RecSegs {
     const float4* src[kMaxSeg];
     float4* dst0;                // record row 0 of step t (record start, 16-byte aligned)

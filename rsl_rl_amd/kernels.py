@@ -637,7 +637,7 @@ class RolloutRecordPlan:
         # [T, N, ...] buffers: row t of field f at base_f + t * stride_f (bytes)
         self.rows = [(k, outs[k].data_ptr(), outs[k].stride(0) * outs[k].element_size()) for k in self._OUTS]
         self.obs_rows = [(d.data_ptr(), d.stride(0) * d.element_size()) for d in obs_dsts]
-        self.a, self.N, self.A, self.device = a, N, A, device
+        self.a, self.N, self.A, self.device, self.gamma = a, N, A, device, float(gamma)  # (a.gamma reads back as fp32)
         self.dones_dtype, self.shared_sigma, self.obs_widths = dones_dtype, shared_sigma, tuple(obs_widths)
         obs_b = sum(8 * w for w in obs_widths)
         self.bytes = (obs_b + 4 * A * (5 + (0 if shared_sigma else 1)) + 4 + 4 + torch.tensor([], dtype=dones_dtype)
@@ -651,7 +651,7 @@ class RolloutRecordPlan:
         if (time_outs is None) != (self.time_outs_dtype is None) or (time_outs is not None and time_outs.dtype !=
                                                                        self.time_outs_dtype):
             return False
-        if float(gamma) != self.a.gamma or (sigma.dim() == 1) != self.shared_sigma:
+        if float(gamma) != self.gamma or (sigma.dim() == 1) != self.shared_sigma:
             return False
         for t, n in ((actions, N * A), (mu, N * A), (values, N), (rewards, N), (dones, N)):
             if t.numel() != n or not t.is_contiguous() or t.data_ptr() % 16 and n == N * A:
