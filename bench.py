@@ -50,7 +50,7 @@ C4_ENVS = 131072  # BASELINE.json configs[3]: the total partitioned over the ran
 # per-launch HBM traffic of the hot-path kernels from rocprofv3 FETCH_SIZE / WRITE_SIZE passes over this same
 # bench command (scripts/pmc_summary.py; raw counters next to it).  PMC passes serialise and slow the
 # run, so they are collected separately and the committed summary is reported here.
-PMC_TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r3_pmc_traffic.json")
+PMC_TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r4_pmc_traffic.json")
 # the MLP GEMM pairs' counters (scripts/mlp_pmc.sh + scripts/mlp_pmc_summary.py over scripts/mlp_pair_probe.py at C3's
 # 393,216-row mini-batch): FETCH_SIZE / WRITE_SIZE corrected by factors calibrated on the box in each kernel's own
 # access pattern (scripts/pmc_pattern_probe.hip), plus clock and MFMA-pipe utilisation from the SQ counters
@@ -292,7 +292,8 @@ def main():
     kernels.timer.reset()
     kernels.timer.enabled = True
     if os.environ.get("RSLRL_BENCH_LAUNCH_EVENTS", "1") != "0":  # 0: A/B of the binding's cost
-        kernels.timer.arm_launch_events(64 * args.steps * 20)  # ~20 loss launches per iteration at the default E x M
+        # ~20 loss + 24 rollout-record + 1 gather launches per iteration at the default T, E x M
+        kernels.timer.arm_launch_events(2 * args.steps * 50)
     hist0 = len(runner.iteration_stats_history)
     t0 = time.perf_counter()
     runner.learn(args.steps)
@@ -343,16 +344,18 @@ def main():
             mlp[name] = ent
     hot_ms = sum(h["ms_per_step"] for h in hot.values())
     dominant = max(hot, key=lambda k: hot[k]["ms_per_step"]) if hot else None
-    # the loss kernel's launches carry their own (start, stop) event pair (hipExtLaunchKernel, bound inside the
-    # library): the dispatch's begin-to-end duration, what rocprofv3 averages; the marker span around the C-ABI
-    # call (hot_path.ppo_loss.mean_us) adds the markers' dispatch latency and is kept beside it
-    ev_ms, ev_n = kernels.timer.launch_events()
+    # the timed hot-path kernels' launches (loss, rollout record, record gather) carry their own (start, stop) event
+    # pair (hipExtLaunchKernel, bound inside the library): the dispatch's begin-to-end duration, what rocprofv3
+    # averages; the marker span around the C-ABI call (hot_path.<kernel>.mean_us) adds the markers' dispatch latency
+    # and is kept beside it
     roofline = None
     if dominant:
         ach = hot[dominant]["achieved_GBps"]
         mean_us = hot[dominant]["mean_us"]
         timing = "HIP event span around the C-ABI call"
-        if dominant == "ppo_loss" and ev_n == hot[dominant]["launches_per_step"] * K:
+        ev_ms, ev_n = (kernels.timer.launch_events(dominant) if dominant in kernels.KernelTimer.LAUNCH_TAGS
+                       else (0.0, 0))
+        if ev_n == hot[dominant]["launches_per_step"] * K:
             mean_us = round(ev_ms / ev_n * 1e3, 2)
             ach = round(hot[dominant]["algorithmic_bytes_per_launch"] / (mean_us * 1e-6) / 1e9, 1)
             timing = ("HIP events bound to each launch (hipExtLaunchKernel start/stop: the dispatch's own duration, "

@@ -31,7 +31,7 @@ extern "C" {
 
 typedef struct ihipStream_t* rslrl_stream_t; /* == hipStream_t */
 
-#define RSLRL_ABI_VERSION 13
+#define RSLRL_ABI_VERSION 14
 
 enum {
     RSLRL_OK = 0,
@@ -673,6 +673,13 @@ int rslrl_synthetic_env_step(float* obs, int32_t num_obs, float* rewards, int64_
  * ----------------------------------------------------------------------------------------------*/
 int rslrl_launch_timing_enable(int32_t capacity);
 int rslrl_launch_timing_read(double* total_ms, int64_t* launches);
+/* ABI 14: the armed launches are those of the PPO loss kernel (tag 0), the rollout record (tag 1,
+ * rslrl_rollout_record) and the transition-record gather (tag 2, rslrl_gather_records[_side]); this reads one tag's
+ * summed duration and count (rslrl_launch_timing_read = tag 0). */
+#define RSLRL_LAUNCH_TAG_PPO_LOSS 0
+#define RSLRL_LAUNCH_TAG_ROLLOUT_RECORD 1
+#define RSLRL_LAUNCH_TAG_GATHER_RECORDS 2
+int rslrl_launch_timing_read_tag(int32_t tag, double* total_ms, int64_t* launches);
 
 #ifdef __cplusplus
 }

@@ -19,7 +19,7 @@ import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 # RSLRL_AMD_LIB: an alternative in-tree build of the same library (A/B kernel experiments)
 LIB_PATH = os.environ.get("RSLRL_AMD_LIB") or os.path.join(LIB_DIR, "librslrl_amd.so")
-ABI_VERSION = 13
+ABI_VERSION = 14
 
 # symbols declared in include/rslrl_amd.h (tests/test_capi.py checks the header against this list)
 EXPORTED_SYMBOLS = (
@@ -82,6 +82,7 @@ EXPORTED_SYMBOLS = (
     "rslrl_rnd_update",
     "rslrl_synthetic_env_step",
     "rslrl_launch_timing_enable",
+    "rslrl_launch_timing_read_tag",
     "rslrl_launch_timing_read",
 )
 
@@ -203,6 +204,7 @@ class ActorHeadArgs(ctypes.Structure):
     ]
 
 
+LAUNCH_TAG_PPO_LOSS, LAUNCH_TAG_ROLLOUT_RECORD, LAUNCH_TAG_GATHER_RECORDS = 0, 1, 2
 ACTOR_HEAD_ACTIONS = 12  # the fused actor head's output width (rslrl_actor_head_fwd_bwd)
 
 DTYPE_F32, DTYPE_U8, DTYPE_I32, DTYPE_I64 = 0, 1, 2, 3
@@ -477,6 +479,8 @@ def _declare(L):
     L.rslrl_launch_timing_enable.argtypes = [I32]
     L.rslrl_launch_timing_read.restype = ctypes.c_int
     L.rslrl_launch_timing_read.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)]
+    L.rslrl_launch_timing_read_tag.restype = ctypes.c_int
+    L.rslrl_launch_timing_read_tag.argtypes = [I32, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)]
 
 
 def lib():

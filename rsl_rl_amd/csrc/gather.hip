@@ -10,6 +10,7 @@
 #include <algorithm>
 
 #include "common.h"
+#include "launch_timing.h"
 
 namespace rslrl {
 namespace {
@@ -245,9 +246,8 @@ int gather_records_impl(const float* records, int64_t record_floats, const rslrl
     p.r4 = static_cast<int32_t>(record_floats / 4);
     const int64_t nb = ceil_div(num_rows, p.tile);
     if (nb > INT32_MAX) return RSLRL_E_INVALID_ARGUMENT;
-    hipLaunchKernelGGL(gather_records_kernel, dim3(static_cast<unsigned>(nb)), dim3(kBlock), 0,
-                       reinterpret_cast<hipStream_t>(stream), p, reinterpret_cast<const float4*>(records), indices,
-                       num_rows);
+    launch_timed(kTagGatherRecords, gather_records_kernel, dim3(static_cast<unsigned>(nb)), dim3(kBlock), 0,
+                 reinterpret_cast<hipStream_t>(stream), p, reinterpret_cast<const float4*>(records), indices, num_rows);
     return launch_status();
 }
 }  // namespace

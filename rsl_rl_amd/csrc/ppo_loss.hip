@@ -27,6 +27,7 @@
 
 #include "common.h"
 #include "ppo_loss_common.h"
+#include "launch_timing.h"
 
 namespace rslrl {
 namespace {
@@ -943,59 +944,19 @@ int loss_depth() {
     return (e && e[0] == '2') ? 2 : 1;
 }
 
-// Live launch timing (rslrl_launch_timing_*, bench.py's roofline): while armed, each quad-kernel launch is bound to
-// a (start, stop) event pair through hipExtLaunchKernelGGL, so the elapsed time is the dispatch's own begin / end --
-// the duration rocprofv3 reports -- rather than a marker-event span around the C-ABI call (which adds the dispatch
-// latency of the markers, ~3-5 us on a ~30 us kernel).  Never bound while the stream is being captured.
-struct LaunchTiming {
-    std::mutex mu;
-    std::vector<std::pair<hipEvent_t, hipEvent_t>> pool;
-    size_t used = 0, cap = 0;
-    std::atomic<bool> on{false};
-};
-
-LaunchTiming& launch_timing() {
-    static LaunchTiming t;
-    return t;
-}
-
-template <typename K, typename... Args>
-void launch_timed(K kernel, dim3 g, dim3 b, hipStream_t st, Args... args) {
-    LaunchTiming& t = launch_timing();
-    if (t.on.load(std::memory_order_relaxed)) {
-        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-        if (hipStreamIsCapturing(st, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone) {
-            hipEvent_t e0 = nullptr, e1 = nullptr;
-            {
-                std::lock_guard<std::mutex> lk(t.mu);
-                if (t.used < t.cap) {
-                    e0 = t.pool[t.used].first;
-                    e1 = t.pool[t.used].second;
-                    ++t.used;
-                }
-            }
-            if (e0) {
-                hipExtLaunchKernelGGL(kernel, g, b, 0, st, e0, e1, 0, args...);
-                return;
-            }
-        }
-    }
-    hipLaunchKernelGGL(kernel, g, b, 0, st, args...);
-}
-
 template <int APL>
 void launch_quad(const LossParams& p, int nb, double* part, unsigned* tickets, float cv, float ce, hipStream_t st) {
     const dim3 g(nb), b(kBlock);
     if (p.sigma_mode == 0 && p.compute_kl && loss_depth() == 2)
-        launch_timed(ppo_loss_quad_kernel<APL, true, true, 2>, g, b, st, p, part, tickets, cv, ce);
+        launch_timed(kTagPpoLoss, ppo_loss_quad_kernel<APL, true, true, 2>, g, b, 0, st, p, part, tickets, cv, ce);
     else if (p.sigma_mode == 0 && p.compute_kl)
-        launch_timed(ppo_loss_quad_kernel<APL, true, true>, g, b, st, p, part, tickets, cv, ce);
+        launch_timed(kTagPpoLoss, ppo_loss_quad_kernel<APL, true, true>, g, b, 0, st, p, part, tickets, cv, ce);
     else if (p.sigma_mode == 0)
-        launch_timed(ppo_loss_quad_kernel<APL, true, false>, g, b, st, p, part, tickets, cv, ce);
+        launch_timed(kTagPpoLoss, ppo_loss_quad_kernel<APL, true, false>, g, b, 0, st, p, part, tickets, cv, ce);
     else if (p.compute_kl)
-        launch_timed(ppo_loss_quad_kernel<APL, false, true>, g, b, st, p, part, tickets, cv, ce);
+        launch_timed(kTagPpoLoss, ppo_loss_quad_kernel<APL, false, true>, g, b, 0, st, p, part, tickets, cv, ce);
     else
-        launch_timed(ppo_loss_quad_kernel<APL, false, false>, g, b, st, p, part, tickets, cv, ce);
+        launch_timed(kTagPpoLoss, ppo_loss_quad_kernel<APL, false, false>, g, b, 0, st, p, part, tickets, cv, ce);
 }
 
 template <int MAXA, bool EXACT>
@@ -1182,6 +1143,13 @@ extern "C" int rslrl_ppo_update_tail(const float* stats, const float* kl, double
     return launch_status();
 }
 
+namespace rslrl {
+LaunchTiming& launch_timing() {
+    static LaunchTiming t;
+    return t;
+}
+}  // namespace rslrl
+
 extern "C" int rslrl_launch_timing_enable(int32_t capacity) {
     if (capacity < 0) return RSLRL_E_INVALID_ARGUMENT;
     LaunchTiming& t = launch_timing();
@@ -1199,7 +1167,7 @@ extern "C" int rslrl_launch_timing_enable(int32_t capacity) {
             if (e0) (void)hipEventDestroy(e0);
             return static_cast<int>(err);
         }
-        t.pool.emplace_back(e0, e1);
+        t.pool.push_back({e0, e1, 0});
     }
     t.used = 0;
     t.cap = static_cast<size_t>(capacity);
@@ -1207,25 +1175,32 @@ extern "C" int rslrl_launch_timing_enable(int32_t capacity) {
     return RSLRL_OK;
 }
 
-extern "C" int rslrl_launch_timing_read(double* total_ms, int64_t* launches) {
-    if (!total_ms || !launches) return RSLRL_E_INVALID_ARGUMENT;
+extern "C" int rslrl_launch_timing_read_tag(int32_t tag, double* total_ms, int64_t* launches) {
+    if (!total_ms || !launches || tag < 0 || tag >= kNumLaunchTags) return RSLRL_E_INVALID_ARGUMENT;
     LaunchTiming& t = launch_timing();
-    // the used event pairs are copied under the lock and synchronised after it is released: a loss launch on
+    // the used event pairs are copied under the lock and synchronised after it is released: a timed launch on
     // another thread (launch_timed takes the same lock) never waits for this read's event synchronisations
-    std::vector<std::pair<hipEvent_t, hipEvent_t>> pairs;
+    std::vector<LaunchTiming::Slot> slots;
     {
         std::lock_guard<std::mutex> lk(t.mu);
-        pairs.assign(t.pool.begin(), t.pool.begin() + static_cast<std::ptrdiff_t>(t.used));
+        slots.assign(t.pool.begin(), t.pool.begin() + static_cast<std::ptrdiff_t>(t.used));
     }
     double sum = 0.0;
-    for (const auto& pr : pairs) {
-        hipError_t err = hipEventSynchronize(pr.second);
+    int64_t n = 0;
+    for (const auto& sl : slots) {
+        if (sl.tag != tag) continue;
+        hipError_t err = hipEventSynchronize(sl.stop);
         float ms = 0.0f;
-        if (err == hipSuccess) err = hipEventElapsedTime(&ms, pr.first, pr.second);
+        if (err == hipSuccess) err = hipEventElapsedTime(&ms, sl.start, sl.stop);
         if (err != hipSuccess) return static_cast<int>(err);
         sum += static_cast<double>(ms);
+        ++n;
     }
     *total_ms = sum;
-    *launches = static_cast<int64_t>(pairs.size());
+    *launches = n;
     return RSLRL_OK;
+}
+
+extern "C" int rslrl_launch_timing_read(double* total_ms, int64_t* launches) {
+    return rslrl_launch_timing_read_tag(kTagPpoLoss, total_ms, launches);
 }

@@ -110,19 +110,25 @@ class KernelTimer:
         self.bytes[name].append(algorithmic_bytes)
         self.flops[name].append(flops)
 
-    # launches of the loss kernel bound to their own event pair inside the library (rslrl_launch_timing_*): the
-    # dispatch's begin-to-end time, the duration rocprofv3 reports, next to the marker span of the C-ABI call
+    # launches of the loss kernel, the rollout record and the record gather bound to their own event pair inside the
+    # library (rslrl_launch_timing_*, one tag per kernel): the dispatch's begin-to-end time, the duration rocprofv3
+    # reports, next to the marker span of the C-ABI call
     def arm_launch_events(self, capacity: int = 4096):
         _lib.check(_lib.lib().rslrl_launch_timing_enable(capacity), "rslrl_launch_timing_enable")
 
     def disarm_launch_events(self):
         _lib.check(_lib.lib().rslrl_launch_timing_enable(0), "rslrl_launch_timing_enable")
 
+    LAUNCH_TAGS = {"ppo_loss": _lib.LAUNCH_TAG_PPO_LOSS, "rollout_record": _lib.LAUNCH_TAG_ROLLOUT_RECORD,
+                   "gather_rows": _lib.LAUNCH_TAG_GATHER_RECORDS}
+
     @staticmethod
-    def launch_events():
-        """(total_ms, launches) of the launches bound to events since the last arm_launch_events()."""
+    def launch_events(kernel: str = "ppo_loss"):
+        """(total_ms, launches) of `kernel`'s launches bound to events since the last arm_launch_events()."""
         ms, n = ctypes.c_double(0.0), ctypes.c_int64(0)
-        _lib.check(_lib.lib().rslrl_launch_timing_read(ctypes.byref(ms), ctypes.byref(n)), "rslrl_launch_timing_read")
+        tag = KernelTimer.LAUNCH_TAGS[kernel]
+        _lib.check(_lib.lib().rslrl_launch_timing_read_tag(tag, ctypes.byref(ms), ctypes.byref(n)),
+                   "rslrl_launch_timing_read_tag")
         return ms.value, n.value
 
     def summary(self):

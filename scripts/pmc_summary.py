@@ -22,6 +22,7 @@ SHORT = {
     "gae_scan_kernel": "gae_scan",
     "adv_normalize_kernel": "adv_normalize",
     "adv_normalize_slot_kernel": "adv_normalize_slot",
+    "adv_normalize_slots_kernel": "adv_normalize_slots",
     "mlp_gemm_x6_value_head_kernel": "x6_value_head",
     "mlp_gemm_x6_actor_head_kernel": "x6_actor_head",
     "out_bwd_valu_kernel": "out_bwd",

@@ -59,3 +59,26 @@ def test_rollout_plan_matches_general_call(cuda_device, monkeypatch):
             assert torch.equal(a[k], b[k]), k
     for a, b in zip(p_general, p_planned):
         assert torch.equal(a, b)
+
+
+def test_rollout_and_gather_launches_bound_to_events(cuda_device):
+    """rslrl_launch_timing_* tags (ABI 14): while armed, every rollout-record launch of an iteration (8 env steps) and
+    the update's record gather carry their own event pair, read back per kernel with positive durations."""
+    torch.manual_seed(5)
+    env = SyntheticVecEnv(3000, 48, 12, device=cuda_device, seed=2)
+    with contextlib.redirect_stdout(io.StringIO()):
+        runner = OnPolicyRunner(env, _cfg(), log_dir=None, device=cuda_device)
+        runner.learn(1)
+        torch.cuda.synchronize()
+        kernels.timer.arm_launch_events(256)
+        try:
+            runner.learn(1)
+            torch.cuda.synchronize()
+        finally:
+            kernels.timer.disarm_launch_events()
+    ms_r, n_r = kernels.timer.launch_events("rollout_record")
+    ms_g, n_g = kernels.timer.launch_events("gather_rows")
+    ms_l, n_l = kernels.timer.launch_events("ppo_loss")
+    assert n_r == 8 and ms_r > 0.0
+    assert n_g == 1 and ms_g > 0.0
+    assert n_l == 4 and ms_l > 0.0  # 2 epochs x 2 mini-batches: the 2x64 actor is not the fused head's shape
