@@ -648,7 +648,6 @@ class RolloutRecordPlan:
         obs_b = sum(8 * w for w in obs_widths)
         self.bytes = (obs_b + 4 * A * (5 + (0 if shared_sigma else 1)) + 4 + 4 + torch.tensor([], dtype=dones_dtype)
                       .element_size() + 4 + (4 if time_outs_dtype is not None else 0) + 13) * N
-        self.stream = _stream(device)
 
     def matches(self, actions, mu, sigma, values, rewards, dones, time_outs, obs_srcs, gamma) -> bool:
         N, A = self.N, self.A
@@ -675,7 +674,7 @@ class RolloutRecordPlan:
         for i, (src, (base, st)) in enumerate(zip(obs_srcs, self.obs_rows)):
             a.obs[i].src, a.obs[i].dst = src.data_ptr(), base + t * st
         with timer.span("rollout_record", self.device, self.bytes):
-            rc = _lib.lib().rslrl_rollout_record(ctypes.byref(a), self.stream)
+            rc = _lib.lib().rslrl_rollout_record(ctypes.byref(a), _stream(self.device))  # the caller's current stream
         _lib.check(rc, "rslrl_rollout_record")
 
 
