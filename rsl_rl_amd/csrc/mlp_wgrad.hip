@@ -452,7 +452,7 @@ __global__ __launch_bounds__(kBlock) void fold_wide_kernel(const float* __restri
 // Deterministic: the order depends on (S, G) alone.
 constexpr int kMaxFoldJobs = 16;
 #ifndef RSLRL_FOLD_UNROLL
-#define RSLRL_FOLD_UNROLL 8
+#define RSLRL_FOLD_UNROLL 4
 #endif
 constexpr int kFoldUnroll = RSLRL_FOLD_UNROLL;  // slices loaded per round per thread (fold_batch_kernel)
 constexpr int kFoldGroupSlices = 256;
@@ -494,9 +494,9 @@ __global__ __launch_bounds__(kBlock) void fold_batch_kernel(FoldJobs jobs) {
     double a[4] = {0.0, 0.0, 0.0, 0.0};
     if (e0 < NK) {
         const float* src = jobs.part[j] + e0;
-        // kFoldUnroll slices per round (the same slice order for any unroll: s_lo + ph, + 16, + 32, ...); 8 keeps the
-        // kernel at half the registers of 16, i.e. twice the blocks per CU in flight (the paired jobs have 128 slices:
-        // one round either way)
+        // kFoldUnroll slices per round (the same slice order for any unroll: s_lo + ph, + 16, + 32, ...): 4 keeps the
+        // kernel at 52 VGPRs, 8 workgroups per CU (16: 148 VGPRs, 3 per CU, 49.7 us per fold at the 16384-env share;
+        // 8: 84 VGPRs, 36.2 us; 4: 35.1 us -- rocprof, profiles/r4_fold_unroll_ab.json)
         for (int s0 = s_lo + ph; s0 < s_hi; s0 += 16 * kFoldUnroll) {
             float4 v[kFoldUnroll];
 #pragma unroll
