@@ -41,6 +41,9 @@ constexpr int kMaxSeg = RSLRL_ROLLOUT_MAX_OBS + 3;
 #ifndef RSLRL_REC_ROWS
 #define RSLRL_REC_ROWS 64
 #endif
+#ifndef RSLRL_REC_NT
+#define RSLRL_REC_NT 1  // nontemporal record stores (0: plain stores, the round-4 form; an A/B knob)
+#endif
 constexpr int kRecRows = RSLRL_REC_ROWS;  // records per copy block (<= 64: four lanes per record in the log-prob)
 struct RecSegs {
     const float4* src[kMaxSeg];
@@ -114,7 +117,15 @@ __global__ __launch_bounds__(kBlock) void rollout_record_kernel(rslrl_rollout_ar
             for (int j = 0; j < kPass; ++j) {
                 const int k = k0 + j * kBlock;
                 if (k < total) {
+#if RSLRL_REC_NT
+                    // nontemporal: the records are read back only by the update's gather, T env steps later
+                    __builtin_nontemporal_store(v[j].x, &dst[k].x);
+                    __builtin_nontemporal_store(v[j].y, &dst[k].y);
+                    __builtin_nontemporal_store(v[j].z, &dst[k].z);
+                    __builtin_nontemporal_store(v[j].w, &dst[k].w);
+#else
                     dst[k] = v[j];
+#endif
                     const int r = static_cast<int>((static_cast<float>(k) + 0.5f) * rs.rcp_r4);
                     const int u = k - r * rs.r4;
                     const int sg = useg[u];
