@@ -44,6 +44,9 @@ constexpr int kMaxSeg = RSLRL_ROLLOUT_MAX_OBS + 3;
 #ifndef RSLRL_REC_NT
 #define RSLRL_REC_NT 1  // nontemporal record stores (0: plain stores, the round-4 form; an A/B knob)
 #endif
+#ifndef RSLRL_REC_DIAG
+#define RSLRL_REC_DIAG 0  // diagnostic builds only (wrong results): 1 skips the copy blocks' log-prob, 2 the per-env blocks
+#endif
 constexpr int kRecRows = RSLRL_REC_ROWS;  // records per copy block (<= 64: four lanes per record in the log-prob)
 struct RecSegs {
     const float4* src[kMaxSeg];
@@ -134,6 +137,7 @@ __global__ __launch_bounds__(kBlock) void rollout_record_kernel(rslrl_rollout_ar
                 }
             }
         }
+        if constexpr ((RSLRL_REC_DIAG & 1) != 0) return;
         __syncthreads();
         {
             // log-prob of the action under Normal(mu, sigma), torch's expression (see the per-env part below): the
@@ -198,6 +202,7 @@ __global__ __launch_bounds__(kBlock) void rollout_record_kernel(rslrl_rollout_ar
     }
 
     // ---- per-env work
+    if constexpr ((RSLRL_REC_DIAG & 2) != 0) return;
     using RS = RndShape<RNDK>;
     const int nw = rnd_net_floats(RS::INP, RS::HP, RNDK == 1 ? 1 : a.rnd_out);
     if constexpr (RNDK != 0) {

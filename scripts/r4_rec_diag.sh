@@ -1,5 +1,5 @@
-# rollout_record: where the time over a plain copy goes -- diagnostic builds (RSLRL_REC_DIAG: 1 no log-prob, 2 no
-# per-env blocks, 3 neither; wrong results, timing only) against the default, plus the plain-copy ceiling
+# rollout_record: where the time over a plain copy goes -- diagnostic builds (make HIPFLAGS+=-DRSLRL_REC_DIAG=v OUT=../lib/variants/recdiagv:
+# 1 no log-prob, 2 no per-env blocks, 3 neither; wrong results, timing only) against the default, plus the plain-copy ceiling
 set -e
 o=gpurun_out/r4/rec_diag
 mkdir -p $o
