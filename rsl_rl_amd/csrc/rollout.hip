@@ -141,28 +141,29 @@ __global__ __launch_bounds__(kBlock) void rollout_record_kernel(rslrl_rollout_ar
         __syncthreads();
         {
             // log-prob of the action under Normal(mu, sigma), torch's expression (see the per-env part below): the
-            // per-action terms (a division and a log each) on the row's four lanes (action j on lane j & 3), written
-            // over the action values they came from, then summed in action order by the row's first lane
+            // per-action terms (a division and a log each) on the row's four lanes (action j on lane j & 3), then
+            // summed in action order -- each group of four terms broadcast across the quad (DPP quad_perm, no LDS
+            // round trip or second barrier), so every lane of the quad adds t_0, t_1, ... in sequence and lane 0
+            // stores.  Quads past `rows` compute on stale LDS and store nothing (a whole quad is one row).
             const int r = threadIdx.x >> 2, q = threadIdx.x & 3;
             const float c = 0.918938533204672742f;
-            float* xr = lds_w + r * A;
+            const float* xr = lds_w + r * A;
             const float* mr = lds_w + (kRecRows + r) * A;
             const float* sr = lds_w + (2 * kRecRows + r) * A;
-            if (r < rows) {
-                for (int j = q; j < A; j += 4) {
-                    const float sj = sr[j];
-                    const float d = __fsub_rn(xr[j], mr[j]);
-                    const float num = -__fmul_rn(d, d);
-                    const float den = __fmul_rn(2.f, __fmul_rn(sj, sj));
-                    xr[j] = __fsub_rn(__fsub_rn(__fdiv_rn(num, den), logf(sj)), c);
-                }
+            float lp = 0.f;
+            for (int j0 = 0; j0 < A; j0 += 4) {  // A % 4 == 0 in record mode (checked on the host)
+                const int j = j0 + q;
+                const float sj = sr[j];
+                const float d = __fsub_rn(xr[j], mr[j]);
+                const float num = -__fmul_rn(d, d);
+                const float den = __fmul_rn(2.f, __fmul_rn(sj, sj));
+                const int t = __builtin_bit_cast(int, __fsub_rn(__fsub_rn(__fdiv_rn(num, den), logf(sj)), c));
+                lp = __fadd_rn(lp, __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(t, 0x00, 0xF, 0xF, false)));
+                lp = __fadd_rn(lp, __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(t, 0x55, 0xF, 0xF, false)));
+                lp = __fadd_rn(lp, __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(t, 0xAA, 0xF, 0xF, false)));
+                lp = __fadd_rn(lp, __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(t, 0xFF, 0xF, 0xF, false)));
             }
-            __syncthreads();
-            if (r < rows && q == 0) {
-                float lp = 0.f;
-                for (int j = 0; j < A; ++j) lp = __fadd_rn(lp, xr[j]);
-                a.out_logp[n0 + r] = lp;
-            }
+            if (r < rows && q == 0) a.out_logp[n0 + r] = lp;
         }
         return;
     }

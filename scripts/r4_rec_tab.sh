@@ -1,8 +1,8 @@
-# rollout_record: nontemporal record stores (default) vs plain stores (rec_old, the round-4 kernel)
+# rollout_record: log-prob sum through DPP quad broadcasts, one barrier (default) vs the LDS sum after a second barrier (rec_old)
 set -e
-o=gpurun_out/r4/rec_nt2
+o=gpurun_out/r4/rec_dpp
 mkdir -p $o
-timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_rollout.py tests/test_gpu_rollout_plan.py > $o/tests.log 2>&1 || { tail -30 $o/tests.log; exit 1; }
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_rollout.py tests/test_gpu_rollout_plan.py tests/test_gpu_update.py > $o/tests.log 2>&1 || { tail -30 $o/tests.log; exit 1; }
 tail -1 $o/tests.log
 for rep in 1 2 3 4; do
 for v in default rec_old; do

@@ -158,3 +158,18 @@ def test_rollout_record_kernel_record_mode(per_row, cuda_device):
     assert torch.equal(f("sigma", A), sigma.expand(N, A))
     assert (rec[:, 64:] == 0).all()  # past the fields: the record is written whole
     assert torch.equal(v, values) and torch.equal(d[:, 0], dones.to(torch.uint8))
+    # the copy blocks' log-prob (terms on a row's four lanes, summed in action order through quad broadcasts; the
+    # last block partial: 777 = 12 x 64 + 9) is the per-env form's bit for bit, and the oracle's within fp32
+    lp2 = torch.empty_like(lp)
+    scratch = {k: torch.empty(N, A, device=dev) for k in ("actions", "mu", "sigma")}
+    kernels.rollout_record(0, obs_pairs=[(obs1, torch.empty_like(obs1)), (obs2, torch.empty_like(obs2))],
+                           actions=actions, mu=mu, sigma=sigma, values=values, rewards=rewards, dones=dones,
+                           time_outs=None, gamma=0.97, out_actions=scratch["actions"], out_rewards=torch.empty_like(r),
+                           out_dones=torch.empty_like(d), out_values=torch.empty_like(v), out_logp=lp2,
+                           out_mu=scratch["mu"], out_sigma=scratch["sigma"])
+    torch.cuda.synchronize()
+    assert torch.equal(lp, lp2)
+    from oracle import ppo_oracle as po
+
+    c = lambda x: x.cpu().numpy()  # noqa: E731
+    np.testing.assert_allclose(c(lp[:, 0]), po.normal_log_prob_sum(c(actions), c(mu), c(sigma)), rtol=2e-6, atol=2e-6)
