@@ -371,6 +371,9 @@ extern "C" int rslrl_rollout_record(const rslrl_rollout_args_t* args, rslrl_stre
     if (row_blocks + copy_blocks > INT32_MAX) return RSLRL_E_INVALID_ARGUMENT;
     if (a.record_floats > 0)  // the copy blocks' [3][64][A] stage of actions / mu / sigma (log-prob)
         lds = std::max(lds, sizeof(float) * 3 * kRecRows * static_cast<size_t>(a.A));
+#ifdef RSLRL_REC_LDS_PAD
+    if (a.record_floats > 0) lds = std::max<size_t>(lds, RSLRL_REC_LDS_PAD);  // occupancy experiment
+#endif
     const dim3 grid(static_cast<unsigned>(copy_blocks + row_blocks));
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     // (launch_timed: bound to a timing event pair while bench.py's timed region has the library's timing armed)
