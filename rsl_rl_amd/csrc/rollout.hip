@@ -44,6 +44,9 @@ constexpr int kMaxSeg = RSLRL_ROLLOUT_MAX_OBS + 3;
 #ifndef RSLRL_REC_NT
 #define RSLRL_REC_NT 1  // nontemporal record stores (0: plain stores, the round-4 form; an A/B knob)
 #endif
+#ifndef RSLRL_REC_ENV_FIRST
+#define RSLRL_REC_ENV_FIRST 1  // the per-env blocks take the low block indices (dispatched first; 0: copy blocks first)
+#endif
 #ifndef RSLRL_REC_DIAG
 #define RSLRL_REC_DIAG 0  // diagnostic builds only (wrong results): 1 skips the copy blocks' log-prob, 2 the per-env blocks
 #endif
@@ -71,7 +74,15 @@ template <int RNDK>
 __global__ __launch_bounds__(kBlock) void rollout_record_kernel(rslrl_rollout_args_t a, int copy_blocks, RecSegs rs) {
     extern __shared__ __attribute__((aligned(16))) float lds_w[];  // RND target then predictor images (rnd_mlp.h)
     const int64_t N = a.N;
-    if (static_cast<int>(blockIdx.x) < copy_blocks && a.record_floats > 0) {
+    // block index in the copy-blocks-first numbering; RSLRL_REC_ENV_FIRST=1 dispatches the per-env blocks first
+#if RSLRL_REC_ENV_FIRST
+    const int row_blocks = static_cast<int>(gridDim.x) - copy_blocks;
+    const int bid = static_cast<int>(blockIdx.x) >= row_blocks ? static_cast<int>(blockIdx.x) - row_blocks
+                                                               : static_cast<int>(blockIdx.x) + copy_blocks;
+#else
+    const int bid = static_cast<int>(blockIdx.x);
+#endif
+    if (bid < copy_blocks && a.record_floats > 0) {
         // ---- record mode: block b writes records [64 b, 64 b + 64) unit by unit (contiguous stores); the unit ->
         // segment map and the segment table live in LDS
         __shared__ int8_t useg[RSLRL_MAX_RECORD_FLOATS / 4];
@@ -92,7 +103,7 @@ __global__ __launch_bounds__(kBlock) void rollout_record_kernel(rslrl_rollout_ar
             useg[u] = static_cast<int8_t>(sg);
         }
         __syncthreads();
-        const int64_t n0 = static_cast<int64_t>(blockIdx.x) * kRecRows;
+        const int64_t n0 = static_cast<int64_t>(bid) * kRecRows;
         const int rows = static_cast<int>(min<int64_t>(kRecRows, N - n0));
         const int total = rows * rs.r4;  // <= 64 * 64: exact float division below
         float4* dst = rs.dst0 + n0 * rs.r4;
@@ -167,9 +178,9 @@ __global__ __launch_bounds__(kBlock) void rollout_record_kernel(rslrl_rollout_ar
         }
         return;
     }
-    if (static_cast<int>(blockIdx.x) < copy_blocks) {
+    if (bid < copy_blocks) {
         // ---- slab copies: obs groups [N, d], actions / mu [N, A], sigma expanded [N, A]
-        const int64_t tid = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+        const int64_t tid = static_cast<int64_t>(bid) * kBlock + threadIdx.x;
         const int64_t stride = static_cast<int64_t>(copy_blocks) * kBlock;
         for (int g = 0; g < a.n_obs; ++g) {
             const int64_t n4 = N * a.obs[g].row_floats / 4;  // row_floats % 4 == 0 checked on the host
@@ -216,7 +227,7 @@ __global__ __launch_bounds__(kBlock) void rollout_record_kernel(rslrl_rollout_ar
                       a.rnd_predictor + H * in + H + Q * H, in, H, Q, RS::INP, RS::HP);
         __syncthreads();
     }
-    const int64_t n = static_cast<int64_t>(blockIdx.x - copy_blocks) * kBlock + threadIdx.x;
+    const int64_t n = static_cast<int64_t>(bid - copy_blocks) * kBlock + threadIdx.x;
     if (n >= N) return;
 
     // log-prob of the action under Normal(mu, sigma): torch's
