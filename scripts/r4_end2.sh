@@ -1,7 +1,7 @@
 # round-4 closing check after the rollout_record store / log-prob changes: whole GPU suite + smoke, the default bench
 # line, the 16384-env share, and the headline command's rocprofv3 kernel stats
 set -e
-o=gpurun_out/r4e2
+o=gpurun_out/r4e3
 mkdir -p $o
 timeout -k 10 1000 python -u -m pytest tests/ -m gpu -x -q --timeout 300 --timeout-method thread > $o/pytest_gpu.log 2>&1 || { tail -40 $o/pytest_gpu.log; exit 1; }
 tail -2 $o/pytest_gpu.log
@@ -16,7 +16,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $o/sta
 python - <<'P'
 import json
 for f in ("bench_default", "b16k", "bench_stats"):
-    d = json.loads(open(f"gpurun_out/r4e2/{f}.json").read().strip().splitlines()[-1])
+    d = json.loads(open(f"gpurun_out/r4e3/{f}.json").read().strip().splitlines()[-1])
     r = d.get("roofline", {})
     print(f, d["value"], d["ms_per_step"], r.get("kernel"), r.get("mean_launch_us"), r.get("frac"))
 P
