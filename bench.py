@@ -200,6 +200,28 @@ def cpu_baseline(args):
     }
 
 
+def hot_path_summary(hot, hot_ms, mlp, T, N):
+    """SURVEY.md §8(a)'s hot path per iteration: the stand-alone kernels (rollout record, compute_returns, record
+    gather; marker spans of the timed region) and, since round 4, the PPO loss, which runs inside the actor's fused head
+    launch (last hidden layer + output layer + loss + output-layer backward): that whole launch is counted
+    for it (its event time from the MLP-timed iteration), so the figure with it is an upper bound on the loss's share."""
+    out = {"kernels": hot, "ms_per_step": round(hot_ms, 4),
+           "env_steps_per_s": round(T * N / (hot_ms * 1e-3), 1) if hot_ms else None,
+           "ppo_loss": "inside linear_actor_head (not a stand-alone launch on the default path); see "
+                       "ms_per_step_with_actor_head"}
+    head = [k for k in mlp if k.startswith("linear_actor_head")]
+    if head:
+        h = mlp[head[0]]
+        out["actor_head_launch"] = {"kernel": head[0], "mean_us": h["mean_us"], "ms_per_step": h["ms_per_step"],
+                                    "launches_per_step": h["launches_per_step"]}
+        with_head = hot_ms + h["ms_per_step"]
+        out["ms_per_step_with_actor_head"] = round(with_head, 4)
+        out["env_steps_per_s_with_actor_head"] = round(T * N / (with_head * 1e-3), 1)
+    else:  # the loss runs as its own kernel (another shape / std type): it is one of `kernels`
+        out["ppo_loss"] = "stand-alone ppo_loss launches (in kernels)"
+    return out
+
+
 def _free_port():
     import socket
 
@@ -257,10 +279,13 @@ def main():
                                                          "MASTER_ADDR", "MASTER_PORT")}), flush=True)
         return
     visible = torch.cuda.device_count()  # does not initialise the GPU on this image
-    if local_rank >= visible:
+    # test-only (tests/test_bench_launch.py): every rank on cuda:0 over gloo, so the N > 1 line runs on one GPU
+    one_device = world > 1 and os.environ.get("RSLRL_TEST_ONE_DEVICE") == "1"
+    dev_index = 0 if one_device else local_rank
+    if dev_index >= visible:
         raise SystemExit(f"bench.py rank {rank}: --gpus {world} needs {world} GPUs on this node, {visible} visible")
-    torch.cuda.set_device(local_rank)
-    device = f"cuda:{local_rank}"
+    torch.cuda.set_device(dev_index)
+    device = f"cuda:{dev_index}"
     if args.num_envs is not None:
         if args.global_num_envs is not None:
             raise SystemExit("--num-envs (per GPU) and --global-num-envs (total) are exclusive")
@@ -285,7 +310,8 @@ def main():
         if world > 1:
             dist.barrier()
 
-    runner.learn(args.warmup)
+    with contextlib.redirect_stdout(sys.stderr):  # learn() prints (rank sync messages): stdout is the result line
+        runner.learn(args.warmup)
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
@@ -294,14 +320,14 @@ def main():
     if os.environ.get("RSLRL_BENCH_LAUNCH_EVENTS", "1") != "0":  # 0: A/B of the binding's cost
         # ~20 loss + 24 rollout-record + 1 gather launches per iteration at the default T, E x M
         kernels.timer.arm_launch_events(2 * args.steps * 50)
-    hist0 = len(runner.iteration_stats_history)
     t0 = time.perf_counter()
-    runner.learn(args.steps)
+    with contextlib.redirect_stdout(sys.stderr):
+        runner.learn(args.steps)
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    timed_phases = runner.iteration_stats_history[hist0:]
+    timed_phases = list(runner.iteration_stats_history)[-args.steps:]
     kernels.timer.enabled = False
     kernels.timer.disarm_launch_events()
     # one more iteration with the MLP GEMM launches timed (kept out of the headline timing: ~470 event
@@ -311,7 +337,8 @@ def main():
     kernels.timer.mlp_enabled = True
     two = os.environ.get("RSLRL_TWO_STREAMS")
     os.environ["RSLRL_TWO_STREAMS"] = "0"
-    runner.learn(1)
+    with contextlib.redirect_stdout(sys.stderr):
+        runner.learn(1)
     torch.cuda.synchronize()
     if two is None:
         os.environ.pop("RSLRL_TWO_STREAMS")
@@ -343,23 +370,33 @@ def main():
             ent["achieved_TFLOPs"] = round(s["flops_per_launch"] / (s["mean_ms"] * 1e-3) / 1e12, 1)
             mlp[name] = ent
     hot_ms = sum(h["ms_per_step"] for h in hot.values())
-    dominant = max(hot, key=lambda k: hot[k]["ms_per_step"]) if hot else None
     # the timed hot-path kernels' launches (loss, rollout record, record gather) carry their own (start, stop) event
     # pair (hipExtLaunchKernel, bound inside the library): the dispatch's begin-to-end duration, what rocprofv3
     # averages; the marker span around the C-ABI call (hot_path.<kernel>.mean_us) adds the markers' dispatch latency
-    # and is kept beside it
+    # and is kept beside it.  The dominant kernel is chosen by that launch-bound kernel time per step (the marker span
+    # of a 10 us kernel is ~2x its duration and would misrank it); kernels without bound events by their span.
+    kernel_ms = {}
+    for name, h in hot.items():
+        ev_ms, ev_n = (kernels.timer.launch_events(name) if name in kernels.KernelTimer.LAUNCH_TAGS else (0.0, 0))
+        if ev_n and ev_n == h["launches_per_step"] * K:
+            h["launch_bound_us"] = round(ev_ms / ev_n * 1e3, 2)
+            h["kernel_ms_per_step"] = round(ev_ms / K, 4)
+            kernel_ms[name] = (ev_ms / K, ev_ms / ev_n, ev_n)
+        else:
+            kernel_ms[name] = (h["ms_per_step"], None, 0)
+    dominant = max(kernel_ms, key=lambda k: kernel_ms[k][0]) if hot else None
     roofline = None
     if dominant:
         ach = hot[dominant]["achieved_GBps"]
         mean_us = hot[dominant]["mean_us"]
         timing = "HIP event span around the C-ABI call"
-        ev_ms, ev_n = (kernels.timer.launch_events(dominant) if dominant in kernels.KernelTimer.LAUNCH_TAGS
-                       else (0.0, 0))
-        if ev_n == hot[dominant]["launches_per_step"] * K:
-            mean_us = round(ev_ms / ev_n * 1e3, 2)
+        _, ev_launch_ms, ev_n = kernel_ms[dominant]
+        if ev_launch_ms is not None:
+            mean_us = round(ev_launch_ms * 1e3, 2)
             ach = round(hot[dominant]["algorithmic_bytes_per_launch"] / (mean_us * 1e-6) / 1e9, 1)
             timing = ("HIP events bound to each launch (hipExtLaunchKernel start/stop: the dispatch's own duration, "
-                      f"{ev_n} launches of the timed region)")
+                      f"{ev_n} launches of the timed region); chosen as the hot-path kernel with the most launch-bound "
+                      f"time per step: " + ", ".join(f"{k} {v[0] * 1e3:.1f} us" for k, v in kernel_ms.items()))
         traffic, traffic_src = pmc_traffic(dominant)
         roofline = {"kernel": dominant, "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                     "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": traffic, "traffic_source": traffic_src,
@@ -419,13 +456,14 @@ def main():
             "global_num_envs": N * world,
             "num_steps_per_env": T,
             "mini_batch_rows": N * T // 4,
-            "parallelism": f"dp{world} (env shards; one RCCL all-reduce of gradients + KL per mini-batch)",
+            "parallelism": (f"dp{world} (env shards; one "
+                            f"{'gloo (TEST: every rank on cuda:0)' if one_device else 'RCCL'} all-reduce of "
+                            f"gradients + KL per mini-batch)"),
         },
         "roofline": roofline,
         "roofline_mlp": roofline_mlp,
         "mlp_kernels": mlp,
-        "hot_path": {"kernels": hot, "ms_per_step": round(hot_ms, 4),
-                     "env_steps_per_s": round(T * N / (hot_ms * 1e-3), 1) if hot_ms else None},
+        "hot_path": hot_path_summary(hot, hot_ms, mlp, T, N),
         "phases_last_iter": {k: round(v, 4) for k, v in runner.last_iteration_stats.items() if k != "loss_dict"},
         # host-side phase times of every timed iteration (the runner's own split: collection = the rollout's host time up
         # to compute_returns, learn = update() to its statistics read-back); phases_last_iter is the extra MLP-timed one

@@ -645,23 +645,34 @@ class RolloutRecordPlan:
         self.obs_rows = [(d.data_ptr(), d.stride(0) * d.element_size()) for d in obs_dsts]
         self.a, self.N, self.A, self.device, self.gamma = a, N, A, device, float(gamma)  # (a.gamma reads back as fp32)
         self.dones_dtype, self.shared_sigma, self.obs_widths = dones_dtype, shared_sigma, tuple(obs_widths)
+        self.key = (self.obs_widths, dones_dtype, time_outs_dtype, self.gamma, shared_sigma)
         obs_b = sum(8 * w for w in obs_widths)
         self.bytes = (obs_b + 4 * A * (5 + (0 if shared_sigma else 1)) + 4 + 4 + torch.tensor([], dtype=dones_dtype)
                       .element_size() + 4 + (4 if time_outs_dtype is not None else 0) + 13) * N
 
-    def matches(self, actions, mu, sigma, values, rewards, dones, time_outs, obs_srcs, gamma) -> bool:
+    @staticmethod
+    def signature(sigma, dones, time_outs, obs_srcs, gamma):
+        """What a plan is built for (its static fields): steps with another signature need another plan."""
+        return (tuple(s.shape[-1] for s in obs_srcs), dones.dtype, None if time_outs is None else time_outs.dtype,
+                float(gamma), sigma.dim() == 1)
+
+    def fits(self, actions, mu, sigma, values, rewards, dones, time_outs, obs_srcs) -> bool:
+        """This step's inputs can be passed by pointer: every array dense with the element count the kernel reads
+        (the general path reshapes / copies what is not), the [N, A] rows and the observation rows 16-byte aligned."""
         N, A = self.N, self.A
-        if tuple(s.shape[-1] for s in obs_srcs) != self.obs_widths or dones.dtype != self.dones_dtype:
-            return False
-        if (time_outs is None) != (self.time_outs_dtype is None) or (time_outs is not None and time_outs.dtype !=
-                                                                       self.time_outs_dtype):
-            return False
-        if float(gamma) != self.gamma or (sigma.dim() == 1) != self.shared_sigma:
-            return False
         for t, n in ((actions, N * A), (mu, N * A), (values, N), (rewards, N), (dones, N)):
             if t.numel() != n or not t.is_contiguous() or t.data_ptr() % 16 and n == N * A:
                 return False
-        return all(s.is_contiguous() and s.data_ptr() % 16 == 0 for s in obs_srcs) and sigma.is_contiguous()
+        if time_outs is not None and (time_outs.numel() != N or not time_outs.is_contiguous()):
+            return False
+        if sigma.numel() != (A if self.shared_sigma else N * A) or not sigma.is_contiguous():
+            return False
+        return all(s.dtype == torch.float32 and s.dim() == 2 and s.shape[0] == N and s.is_contiguous()
+                   and s.data_ptr() % 16 == 0 for s in obs_srcs)
+
+    def matches(self, actions, mu, sigma, values, rewards, dones, time_outs, obs_srcs, gamma) -> bool:
+        return (self.signature(sigma, dones, time_outs, obs_srcs, gamma) == self.key
+                and self.fits(actions, mu, sigma, values, rewards, dones, time_outs, obs_srcs))
 
     def launch(self, t: int, actions, mu, sigma, values, rewards, dones, time_outs, obs_srcs):
         a = self.a

@@ -69,7 +69,8 @@ class OnPolicyRunner:
         self.current_learning_iteration = 0
         self.git_status_repos = [rsl_rl_amd.__file__]
         self.last_iteration_stats: dict = {}
-        self.iteration_stats_history: list = []  # (collection_time, learn_time) of every iteration (benchmarking)
+        # (collection_time, learn_time) of the latest iterations (benchmarking; bounded for long training runs)
+        self.iteration_stats_history: deque = deque(maxlen=1024)
 
     # ------------------------------------------------------------------ training loop (:61-175)
     def learn(self, num_learning_iterations: int, init_at_random_ep_len: bool = False):  # noqa: C901
@@ -290,7 +291,12 @@ class OnPolicyRunner:
 
     # ------------------------------------------------------------------ helpers (:353-460)
     def _configure_multi_gpu(self):
-        """One process per GPU: read WORLD_SIZE / LOCAL_RANK / RANK, validate, init RCCL ("nccl")."""
+        """One process per GPU: read WORLD_SIZE / LOCAL_RANK / RANK, validate, init RCCL ("nccl")
+        (on_policy_runner.py:353-395, same checks and error messages).
+
+        Test-only override: RSLRL_TEST_ONE_DEVICE=1 puts every rank on cuda:0 over a gloo group (RCCL refuses two
+        ranks on one device), so the world > 1 path -- this method, broadcast_parameters, the per-mini-batch
+        all-reduce, bench.py's max-over-ranks timing -- runs end to end on a one-GPU box (tests/test_bench_launch.py)."""
         self.gpu_world_size = int(os.getenv("WORLD_SIZE", "1"))
         self.is_distributed = self.gpu_world_size > 1
         if not self.is_distributed:
@@ -305,7 +311,8 @@ class OnPolicyRunner:
             "local_rank": self.gpu_local_rank,
             "world_size": self.gpu_world_size,
         }
-        if self.device != f"cuda:{self.gpu_local_rank}":
+        one_device = os.getenv("RSLRL_TEST_ONE_DEVICE") == "1"
+        if self.device != ("cuda:0" if one_device else f"cuda:{self.gpu_local_rank}"):
             raise ValueError(
                 f"Device '{self.device}' does not match expected device for local rank '{self.gpu_local_rank}'."
             )
@@ -318,9 +325,9 @@ class OnPolicyRunner:
                 f"Global rank '{self.gpu_global_rank}' is greater than or equal to world size '{self.gpu_world_size}'."
             )
         if not torch.distributed.is_initialized():
-            torch.distributed.init_process_group(backend="nccl", rank=self.gpu_global_rank,
+            torch.distributed.init_process_group(backend="gloo" if one_device else "nccl", rank=self.gpu_global_rank,
                                                  world_size=self.gpu_world_size)
-        torch.cuda.set_device(self.gpu_local_rank)
+        torch.cuda.set_device(0 if one_device else self.gpu_local_rank)
 
     def _construct_algorithm(self, obs) -> PPO:
         self.alg_cfg = resolve_rnd_config(self.alg_cfg, obs, self.cfg["obs_groups"], self.env)

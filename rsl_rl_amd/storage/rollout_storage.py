@@ -79,6 +79,7 @@ class RolloutStorage:
 
         self.records = None
         self._rec_plan = None  # kernels.RolloutRecordPlan of the fused rollout step (add_transition_fused)
+        self._rec_plan_key = None  # the step signature _rec_plan was built for (a None plan is remembered too)
         self.record_layout = self._record_layout(training_type, obs, actions_shape, device)
         if self.record_layout is not None:
             R, offs = self.record_layout
@@ -197,10 +198,11 @@ class RolloutStorage:
             srcs = [transition.observations[k] for k in self.observations.keys()]
             args = (transition.actions, transition.action_mean, sigma, transition.values, rewards, dones, time_outs, srcs,
                     gamma)
+            key = kernels.RolloutRecordPlan.signature(sigma, dones, time_outs, srcs, gamma)
+            if key != self._rec_plan_key:  # built once per signature (None: the signature has no plan)
+                self._rec_plan, self._rec_plan_key = self._record_plan(*args), key
             plan = self._rec_plan
-            if plan is None or not plan.matches(*args):
-                plan = self._rec_plan = self._record_plan(*args)
-            if plan is not None:
+            if plan is not None and plan.fits(*args[:-1]):
                 plan.launch(t, *args[:-1])
                 self.step += 1
                 self._fills += 1
@@ -230,7 +232,8 @@ class RolloutStorage:
         self._slot_key = None  # written through data_ptr (no _version bump): the slots are stale
 
     def _record_plan(self, actions, mu, sigma, values, rewards, dones, time_outs, srcs, gamma):
-        """kernels.RolloutRecordPlan for steps shaped like this one, or None (the general path takes them)."""
+        """kernels.RolloutRecordPlan for steps with this one's signature, or None (the general path takes them); each
+        step still checks that its own inputs fit the plan (RolloutRecordPlan.fits)."""
         codes = (torch.float32, torch.uint8, torch.bool, torch.int32, torch.int64)
         if len(srcs) > 4 or dones.dtype not in codes or (time_outs is not None and time_outs.dtype not in codes):
             return None
@@ -239,11 +242,10 @@ class RolloutStorage:
         outs = {"out_actions": self.actions, "out_rewards": self.rewards, "out_dones": self.dones,
                 "out_values": self.values, "out_logp": self.actions_log_prob, "out_mu": self.mu,
                 "out_sigma": self.sigma, "out_records": self.records}
-        plan = kernels.RolloutRecordPlan(outs, [self.observations[k] for k in self.observations.keys()],
+        return kernels.RolloutRecordPlan(outs, [self.observations[k] for k in self.observations.keys()],
                                          [s.shape[-1] for s in srcs], self.num_envs, self.actions.shape[-1], gamma,
                                          dones.dtype, time_outs.dtype if time_outs is not None else None,
                                          sigma.dim() == 1, self.device)
-        return plan if plan.matches(actions, mu, sigma, values, rewards, dones, time_outs, srcs, gamma) else None
 
     def _save_hidden_states(self, hidden_states):
         if hidden_states is None or hidden_states == (None, None):

@@ -18,7 +18,7 @@ pytestmark = pytest.mark.gpu
 A = 12
 
 
-def _problem(M, dev, seed):
+def _problem(M, dev, seed, old_sigma_per_row=False):
     g = torch.Generator(device=dev).manual_seed(seed)
     K = N = 256
     r = lambda *s: torch.randn(*s, device=dev, generator=g)  # noqa: E731
@@ -27,6 +27,8 @@ def _problem(M, dev, seed):
     wo, bo = r(A, N) / 16, r(A) * 0.1
     sigma = torch.rand(A, device=dev, generator=g) * 0.5 + 0.5
     old_sigma = (sigma * (1.0 + 0.1 * torch.rand(A, device=dev, generator=g))).expand(M, A).contiguous()
+    if old_sigma_per_row:  # every third row's sigma_old differs from row 0's bits: the per-element KL expression
+        old_sigma[1::3] *= 1.0 + 0.05 * torch.rand(old_sigma[1::3].shape, device=dev, generator=g)
     batch = dict(actions=r(M, A), old_log_prob=r(M, 1) - 8.0, advantages=r(M, 1), target_values=r(M, 1) * 0.3,
                  returns=r(M, 1), old_mu=r(M, A) * 0.1, old_sigma=old_sigma)
     values = r(M, 1) * 0.3
@@ -94,6 +96,27 @@ def test_actor_head_matches_separate_launches(M, clipped, kl, cuda_device):
         assert torch.equal(u, v)
 
 
+@pytest.mark.parametrize("case", ["old_sigma_per_row", "kl_fast_off"])
+def test_actor_head_kl_fallbacks_match_loss_kernel(case, cuda_device, monkeypatch):
+    """The fused head's KL on rows whose sigma_old is not sample 0's (the per-element fallback of the per-action-constant
+    fast path) and with the fast path switched off (RSLRL_KL_FAST=0, read per launch by both kernels): the KL
+    (stats[4]) and every other loss output as ppo_loss_fwd_bwd's on the same inputs."""
+    dev, M = cuda_device, 16384
+    if case == "kl_fast_off":
+        monkeypatch.setenv("RSLRL_KL_FAST", "0")
+    x, w, b, wo, bo, sigma, values, batch = _problem(M, dev, 77, old_sigma_per_row=case == "old_sigma_per_row")
+    img, out_img, img_t = fused_mlp.bimages([(w, False), (wo, False, _lib.BIMAGE_LAYOUT_OUT), (wo, True)])
+    mu_r, st_r, gmu_r, gs_r, dz_r, dw_r, db_r = _separate(x, w, b, wo, bo, sigma, values, batch, img, out_img, img_t,
+                                                          True, True)
+    mu, st, gmu, gs, dz, dw, db = _fused(x, w, b, wo, bo, sigma, values, batch, img, out_img, img_t, True, True)
+    torch.cuda.synchronize()
+    assert torch.equal(mu, mu_r) and torch.equal(gmu, gmu_r)
+    assert torch.allclose(st[:5], st_r[:5], rtol=2e-6, atol=1e-9), (st, st_r)
+    assert float(st[4]) > 0.0  # the KL of these inputs is not the rollout-consistent ~0
+    assert torch.allclose(gs, gs_r, rtol=1e-5, atol=1e-9)
+    assert _close(dz, dz_r, 1e-5) and _close(dw, dw_r, 1e-5) and _close(db, db_r, 1e-5)
+
+
 def test_actor_head_declines_unsupported(cuda_device):
     """Partial tiles or another action count: nothing launched, the caller keeps the separate launches."""
     dev = cuda_device
@@ -108,7 +131,8 @@ def test_actor_head_declines_unsupported(cuda_device):
     assert not head.done
 
 
-def test_update_with_actor_head_matches_separate_launches(cuda_device, monkeypatch):
+@pytest.mark.parametrize("noise_std_type", ["scalar", "log"])
+def test_update_with_actor_head_matches_separate_launches(noise_std_type, cuda_device, monkeypatch):
     """PPO.update() on one storage with the fused actor head and with the separate launches (RSLRL_ACTOR_HEAD off; the
     critic's fused head on in both): the same learning-rate trace and loss statistics, and parameters within fp32
     accumulation-order noise."""
@@ -130,7 +154,8 @@ def test_update_with_actor_head_matches_separate_launches(cuda_device, monkeypat
         real = fused_mlp.actor_head_fwd_bwd
         monkeypatch.setattr(fused_mlp, "actor_head_fwd_bwd", lambda *a, **k: calls.append(1) or real(*a, **k))
         torch.manual_seed(0)
-        pol = ActorCritic(obs0, groups, A, actor_hidden_dims=[256, 256, 256], critic_hidden_dims=[256, 256, 256])
+        pol = ActorCritic(obs0, groups, A, actor_hidden_dims=[256, 256, 256], critic_hidden_dims=[256, 256, 256],
+                          noise_std_type=noise_std_type)
         alg = PPO(pol, num_learning_epochs=2, num_mini_batches=4, device=dev, desired_kl=0.01)
         alg.init_storage("rl", N, T, obs0, [A])
         st = alg.storage

@@ -82,3 +82,58 @@ def test_rollout_and_gather_launches_bound_to_events(cuda_device):
     assert n_r == 8 and ms_r > 0.0
     assert n_g == 1 and ms_g > 0.0
     assert n_l == 4 and ms_l > 0.0  # 2 epochs x 2 mini-batches: the 2x64 actor is not the fused head's shape
+
+
+def _storage(dev, N, O, A, T=4):
+    from rsl_rl_amd.utils import TensorDict
+
+    obs = TensorDict({"policy": torch.zeros(N, O, device=dev)}, batch_size=[N], device=dev)
+    return rollout_storage.RolloutStorage("rl", N, T, obs, [A], device=dev)
+
+
+def test_rollout_plan_declines_strided_inputs(cuda_device, monkeypatch):
+    """A step whose time_outs arrive as a strided column (or whose observation source has the wrong row count) does not
+    fit the cached plan: it takes the general rollout_record path, and the rows written equal those of a storage that
+    never uses a plan, bit for bit.  Contiguous steps before and after keep using the one plan."""
+    from rsl_rl_amd.utils import TensorDict
+
+    dev, N, O, A = cuda_device, 1000, 48, 12
+    g = torch.Generator(device="cpu").manual_seed(3)
+    steps = []
+    for t in range(4):
+        r = lambda *s: torch.randn(*s, generator=g).to(dev)  # noqa: E731
+        to_wide = (torch.rand(N, 2, generator=g) < 0.3).to(dev)
+        steps.append(dict(obs=r(N, O), actions=r(N, A), mu=r(N, A), sigma=r(A).abs() + 0.5, values=r(N, 1),
+                          rewards=r(N), dones=(torch.rand(N, generator=g) < 0.1).to(dev),
+                          time_outs=to_wide[:, 0] if t in (1, 3) else to_wide[:, 0].contiguous()))
+    built = []
+    real = kernels.RolloutRecordPlan.__init__
+
+    def counting(self, *a, **k):
+        built.append(1)
+        real(self, *a, **k)
+
+    monkeypatch.setattr(kernels.RolloutRecordPlan, "__init__", counting)
+    planned, general = _storage(dev, N, O, A), _storage(dev, N, O, A)
+    for st, use_plan in ((planned, True), (general, False)):
+        if not use_plan:
+            monkeypatch.setattr(st, "_record_plan", lambda *a: None)
+        for s in steps:
+            tr = rollout_storage.RolloutStorage.Transition()
+            tr.observations = TensorDict({"policy": s["obs"]}, batch_size=[N], device=dev)
+            tr.actions, tr.action_mean, tr.values = s["actions"], s["mu"], s["values"]
+            tr.action_sigma = s["sigma"].expand(N, A)
+            st.add_transition_fused(tr, s["rewards"], s["dones"], s["time_outs"], 0.99)
+    torch.cuda.synchronize()
+    assert not steps[1]["time_outs"].is_contiguous()
+    assert len(built) == 1  # one plan for the planned storage; the strided steps did not rebuild it
+    for k in ("records", "rewards", "dones", "values", "actions_log_prob"):
+        assert torch.equal(getattr(planned, k), getattr(general, k)), k
+    plan = planned._rec_plan
+    s = steps[0]
+    obs_short = s["obs"][: N - 1]
+    assert not plan.fits(s["actions"], s["mu"], s["sigma"], s["values"], s["rewards"], s["dones"], steps[1]["time_outs"],
+                         [s["obs"]])
+    assert not plan.fits(s["actions"], s["mu"], s["sigma"], s["values"], s["rewards"], s["dones"], s["time_outs"],
+                         [obs_short])
+    assert plan.fits(s["actions"], s["mu"], s["sigma"], s["values"], s["rewards"], s["dones"], s["time_outs"], [s["obs"]])
