@@ -31,7 +31,7 @@ extern "C" {
 
 typedef struct ihipStream_t* rslrl_stream_t; /* == hipStream_t */
 
-#define RSLRL_ABI_VERSION 14
+#define RSLRL_ABI_VERSION 15
 
 enum {
     RSLRL_OK = 0,
@@ -513,6 +513,27 @@ int64_t rslrl_linear_wgrad_bias_pair_slices(int64_t M, int32_t N);
 int rslrl_linear_wgrad_bias_pair(const rslrl_wgrad_problem_t* p0, const rslrl_wgrad_problem_t* p1, int64_t M,
                                  int32_t N, int32_t K, int32_t arith, int32_t bias_side, int32_t flags,
                                  rslrl_stream_t stream);
+
+/* Backward of a square hidden layer (Linear(256, 256) + ELU; rsl_rl/networks/mlp.py:106-114 via ppo.py:367) in one
+ * pass over the rows (ABI 15): the input gradient dz_prev = (dz W) * ELU'(h) -- the bits rslrl_linear_gemm
+ * (RSLRL_LINEAR_DGRAD_ELU, x6) gives -- and the slice partials of the weight and bias gradients, [S][256 * 256 + 256]
+ * rows [sum dz^T h | sum dz] (rslrl_linear_wgrad_bias bias_side 1's partial layout: rslrl_fold_partials* folds them
+ * into [dW | db]), reading dz and h from HBM once instead of once per GEMM.  Replaces, for this shape, the pair
+ * rslrl_linear_wgrad_bias_pair(bias_side 1) + rslrl_linear_gemm_pair(RSLRL_LINEAR_DGRAD_ELU).  M a multiple of 64
+ * (else RSLRL_E_UNSUPPORTED, nothing launched); S = rslrl_hidden_bwd_slices(M) slices per problem (<= 128: a pair
+ * fills 256 CUs with one workgroup each).  bimage: the x6 image of W^T (rslrl_linear_prepare_bimage(W, 256, 256, 1)).
+ * p1 may be NULL (one problem).  All pointers 16-byte aligned. */
+typedef struct {
+    const float* dz;      /* [M, 256] gradient at this layer's pre-activation */
+    const float* h;       /* [M, 256] this layer's input (the previous layer's ELU output) */
+    const void* bimage;   /* x6 image of W^T */
+    float* dz_prev;       /* [M, 256] */
+    float* partials;      /* [S][256 * 256 + 256] */
+} rslrl_hidden_bwd_problem_t;
+int64_t rslrl_hidden_bwd_slices(int64_t M);
+size_t rslrl_hidden_bwd_partial_floats(void);
+int rslrl_hidden_bwd_pair(const rslrl_hidden_bwd_problem_t* p0, const rslrl_hidden_bwd_problem_t* p1, int64_t M,
+                          int32_t width, rslrl_stream_t stream);
 
 /* ------------------------------------------------------------------------------------------------
  * Rollout-side record: for environment step t, in one launch,

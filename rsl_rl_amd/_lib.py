@@ -19,7 +19,7 @@ import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 # RSLRL_AMD_LIB: an alternative in-tree build of the same library (A/B kernel experiments)
 LIB_PATH = os.environ.get("RSLRL_AMD_LIB") or os.path.join(LIB_DIR, "librslrl_amd.so")
-ABI_VERSION = 14
+ABI_VERSION = 15
 
 # symbols declared in include/rslrl_amd.h (tests/test_capi.py checks the header against this list)
 EXPORTED_SYMBOLS = (
@@ -84,6 +84,9 @@ EXPORTED_SYMBOLS = (
     "rslrl_launch_timing_enable",
     "rslrl_launch_timing_read_tag",
     "rslrl_launch_timing_read",
+    "rslrl_hidden_bwd_slices",
+    "rslrl_hidden_bwd_partial_floats",
+    "rslrl_hidden_bwd_pair",
 )
 
 MAX_GATHER_FIELDS = 16
@@ -349,6 +352,17 @@ class WgradProblem(ctypes.Structure):
     ]
 
 
+class HiddenBwdProblem(ctypes.Structure):
+    """include/rslrl_amd.h rslrl_hidden_bwd_problem_t"""
+    _fields_ = [
+        ("dz", ctypes.c_void_p),
+        ("h", ctypes.c_void_p),
+        ("bimage", ctypes.c_void_p),
+        ("dz_prev", ctypes.c_void_p),
+        ("partials", ctypes.c_void_p),
+    ]
+
+
 RND_MAX_IN, RND_MAX_HIDDEN, RND_MAX_OUT = 64, 64, 8
 
 _lib = None
@@ -460,6 +474,12 @@ def _declare(L):
     L.rslrl_linear_wgrad_bias.argtypes = [P, P, P, P, I64, I32, I32, I32, I32, P, P, SZ, P]
     L.rslrl_linear_wgrad_bias_pair_workspace_bytes.restype = SZ
     L.rslrl_linear_wgrad_bias_pair_workspace_bytes.argtypes = [I64, I32, I32, I32]
+    L.rslrl_hidden_bwd_slices.restype = I64
+    L.rslrl_hidden_bwd_slices.argtypes = [I64]
+    L.rslrl_hidden_bwd_partial_floats.restype = SZ
+    L.rslrl_hidden_bwd_partial_floats.argtypes = []
+    L.rslrl_hidden_bwd_pair.restype = ctypes.c_int
+    L.rslrl_hidden_bwd_pair.argtypes = [ctypes.POINTER(HiddenBwdProblem), ctypes.POINTER(HiddenBwdProblem), I64, I32, P]
     L.rslrl_linear_wgrad_bias_pair.restype = ctypes.c_int
     L.rslrl_linear_wgrad_bias_pair.argtypes = [ctypes.POINTER(WgradProblem), ctypes.POINTER(WgradProblem), I64, I32,
                                                I32, I32, I32, I32, P]

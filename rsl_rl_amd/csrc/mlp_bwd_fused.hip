@@ -1,0 +1,386 @@
+// Backward of a square hidden layer (Linear(256, 256) + ELU of rsl_rl/networks/mlp.py:106-114, reached from
+// ppo.py:367's loss.backward()) in ONE pass over the mini-batch rows, on the x6 split-bf16 MFMA path:
+//   input gradient   dZp = (dZ W) * ELU'(H)            (rslrl_linear_gemm RSLRL_LINEAR_DGRAD_ELU: the same bits)
+//   weight gradient  dW  = dZ^T H,  bias gradient db = sum_m dZ[m]   (rslrl_linear_wgrad_bias, bias_side 1)
+// where dZ [M, 256] is the gradient at this layer's pre-activation and H [M, 256] this layer's input (the previous
+// layer's ELU output).  The separate kernels read dZ and H twice (input gradient, then weight gradient: 1.6 GB per
+// actor + critic pair at 393,216 rows); here every 64-row tile of dZ and H is read from HBM once and feeds both GEMMs.
+//
+// One workgroup per CU (8 waves, 256 registers per lane, all 160 KiB of LDS) runs a slice of consecutive 64-row
+// tiles and keeps the slice's whole 256 x 256 weight gradient in registers (wave w: columns k in [32w, 32w + 32),
+// 8 MFMA blocks of 32 x 32 = 128 accumulator registers); the slice's [dW | db] partial row is folded in fp64 in a
+// fixed order afterwards (rslrl_fold_partials_batch, as the weight-gradient kernel's).  Per tile:
+//  1. the dZ tile sits in LDS as three bf16 planes (96 KiB, split once) for the whole tile;
+//  2. input gradient: wave w computes the output columns [32w, 32w + 32) of all 64 rows (2 MFMA blocks) over the
+//     16 k-chunks -- A fragments (dZ rows) from the resident planes, B fragments (the W^T image, L2-resident) straight
+//     from global memory two chunks ahead: no LDS writes and no barrier inside the main loop;
+//  3. epilogue: H (DMA'd into a 64 KiB LDS stage during the main loop) read in the accumulator layout, ELU', dZp
+//     stored (nontemporal);
+//  4. weight gradient: dW[n][k] += sum over the tile's rows of dZ[m][n] H[m][k] -- A = dZ^T from the resident planes
+//     by ds_read_b64_tr_b16, B = H straight from the epilogue's registers: the accumulator layout holds, per lane,
+//     column k at rows (r & 3) + 8 (r >> 2) + 4 (lane >> 5), so each 16-deep MFMA step takes the reduction rows in
+//     the permuted order pi(8 h + t) = 16 s + 4 h + (t & 3) + 8 (t >> 2) -- the same order for the dZ^T fragments
+//     (the transposed reads address exactly those rows), i.e. the same sum over the tile's rows;
+//  5. meanwhile the next tile's dZ is loaded into registers and its H DMA'd into the (then free) stage.
+// The column sums of dZ (db) accumulate in fp32 from the staged registers (every thread owns four fixed columns) and
+// fold over the 8 waves in wave order at the end.  Deterministic: the summation order depends on M alone.
+//
+// LDS image of a dZ plane: [16 chunks of 16 columns][64 row slots][32 bytes] (the input gradient's 16-deep k-chunks),
+// row m of chunk c in slot m ^ f(c), f(c) = (c & 3) | 4 (c & 1), its two 16-byte halves swapped when (m >> 3) & 1.
+// Bank-conflict free for all three accesses: the input gradient's ds_read_b128 row fragments (one chunk per
+// instruction: the half swap separates the rows that share a bank quad), the weight gradient's transposed reads
+// (4 rows of two adjacent chunks per 32-lane group: bit 2 of f puts the odd chunk's rows on the other 32 banks) and
+// the staging stores (ds_write_b64, 16 lanes = one row of 4 chunks: f's low bits give each chunk its own 8 banks).
+// Every chunk offset (and the 8-row / 32-row steps) lands in the instructions' immediate offsets: a handful of
+// address registers for the whole tile.
+#include <algorithm>
+
+#include "common.h"
+#include "x6_split.h"
+
+namespace rslrl {
+namespace {
+
+constexpr int kHbT = 64;                        // rows per tile
+constexpr int kHbW = 256;                       // the layer's width (N = K = 256)
+constexpr int kHbThreads = 512;                 // 8 waves
+constexpr int kHbPlane = kHbT * kHbW * 2;       // one bf16 plane of the dZ tile: 32 KiB
+constexpr int kHbDzBytes = 3 * kHbPlane;        // 96 KiB
+constexpr int kHbHBytes = kHbT * kHbW * 4;      // the H stage: 64 KiB
+constexpr int kHbLds = kHbDzBytes + kHbHBytes;  // 160 KiB: the whole LDS of a CU
+constexpr int kHbChunks = kHbW / 16;            // k-chunks of the input gradient
+constexpr int kHbImgPlaneU = kHbW * 32 / 16;    // 16-byte units of one plane of one image chunk (bimage layout 0)
+constexpr int kHbImgChunkU = 3 * kHbImgPlaneU;
+constexpr int kHbPartFloats = kHbW * kHbW + kHbW;  // a slice's partial row: [dW (256 x 256) | db (256)]
+constexpr int kHbMaxSlices = 128;               // per problem: a pair fills the 256 CUs with one workgroup each
+#ifndef RSLRL_HB_BDEPTH
+#define RSLRL_HB_BDEPTH 2
+#endif
+constexpr int kHbBDepth = RSLRL_HB_BDEPTH;      // image chunks loaded ahead of the input gradient's MFMAs
+
+using s16x4 = __attribute__((ext_vector_type(4))) short;
+
+struct HbProblem {
+    const float* dz;   // [M, 256]
+    const float* h;    // [M, 256]
+    const uint4* img;  // x6 image of W^T (layout 0, 16 chunks)
+    float* dz_prev;    // [M, 256]
+    float* part;       // [S][kHbPartFloats]
+};
+
+struct HbArgs {
+    HbProblem p[2];
+    int tiles;      // M / 64
+    int tiles_per;  // tiles per slice
+};
+
+constexpr int kHbChunkB = kHbT * 32;  // one chunk of one plane: 2 KiB
+
+__host__ __device__ constexpr int hb_f(int c) { return (c & 3) | ((c & 1) << 2); }
+
+// byte offset of (row m, column col % 4 == 0) in a plane
+__device__ __forceinline__ int hb_dz_off(int m, int col) {
+    const int c = col >> 4;
+    return c * kHbChunkB + (m ^ hb_f(c)) * 32 + 16 * (((col >> 3) & 1) ^ ((m >> 3) & 1)) + 8 * ((col >> 2) & 1);
+}
+
+constexpr uint32_t kHbRsrcFlags = 0x00020000;
+constexpr uint32_t kHbTileBytes = kHbT * kHbW * 4;  // 64 KiB: one tile of dZ or H
+
+// a buffer resource over the tile's rows of an [M, 256] fp32 array: wave-uniform base, every offset in the
+// instructions' voffset / soffset / immediate fields (no 64-bit address registers)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t hb_tile_rsrc(const float* base, int64_t row0) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base + row0 * kHbW), 0, kHbTileBytes, kHbRsrcFlags);
+}
+
+// the tile's dZ (8 float4 per thread: row (t >> 6) + 8 i, columns 4 (t & 63) .. + 3)
+__device__ __forceinline__ void hb_load_dz(__amdgpu_buffer_rsrc_t r, float4 (&v)[8]) {
+    const int off = ((threadIdx.x >> 6) * kHbW + 4 * (threadIdx.x & 63)) * 4;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+        v[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, off, i * 8 * kHbW * 4, 0));
+}
+
+__device__ __forceinline__ void hb_store_dz(const float4 (&v)[8], char* __restrict__ lds, float4& csum) {
+    const int col = 4 * (threadIdx.x & 63);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int m = (threadIdx.x >> 6) + 8 * i;
+        csum.x += v[i].x;
+        csum.y += v[i].y;
+        csum.z += v[i].z;
+        csum.w += v[i].w;
+        uint2 w[3];
+        split4(v[i], w[0], w[1], w[2]);
+        const int off = hb_dz_off(m, col);
+#pragma unroll
+        for (int q = 0; q < 3; ++q) *reinterpret_cast<uint2*>(lds + q * kHbPlane + off) = w[q];
+    }
+}
+
+// the tile's H rows into the stage: wave w DMAs rows w + 8 i (1 KiB each, 16 bytes per lane)
+__device__ __forceinline__ void hb_dma_h(__amdgpu_buffer_rsrc_t r, char* stage) {
+    const int wave = threadIdx.x >> 6;
+    const int off = (wave * kHbW + 4 * (threadIdx.x & 63)) * 4;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)(stage + (wave + 8 * i) * (kHbW * 4)),
+                                                 16, off, i * 8 * kHbW * 4, 0, 0);
+}
+
+// one 4-row transposed read (ds_read_b64_tr_b16) at byte address addr of the LDS
+__device__ __forceinline__ s16x4 hb_tr(int addr) {
+    typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16(reinterpret_cast<lds_s16x4*>(addr));
+}
+
+__device__ __forceinline__ bf16x8 hb_cat(s16x4 lo, s16x4 hi) {
+    const __attribute__((ext_vector_type(8))) short v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, v);
+}
+
+__device__ __forceinline__ bf16x8 hb_read16(int addr) {
+    typedef __attribute__((address_space(3))) uint4 lds_u4;
+    return __builtin_bit_cast(bf16x8, *reinterpret_cast<const lds_u4*>(addr));
+}
+
+__global__ __launch_bounds__(kHbThreads, 2) void hidden_bwd_kernel(HbArgs args) {
+    __shared__ __attribute__((aligned(16))) char lds[kHbLds];
+    char* const dzl = lds;
+    char* const stage = lds + kHbDzBytes;
+    const HbProblem& P = args.p[blockIdx.y];
+    const int s = blockIdx.x;
+    const int t_begin = s * args.tiles_per;
+    const int t_end = min(args.tiles, t_begin + args.tiles_per);
+
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int h = lane >> 5;
+    const int l32 = lane & 31;
+    const int g1 = (lane >> 4) & 1;  // transposed reads: which 16 of a block's 32 columns
+    const int tq = (lane >> 2) & 3;  //   row within the 4-row group
+    const int tp = lane & 3;         //   column quad
+
+    // LDS lane address parts (the dZ planes start at LDS address 0): la[c & 3] = hb_dz_off(l32, 16 c + 8 h) - c * 2 KiB
+    // for the input gradient's row fragments; lt[nb & 1][hi] = hb_dz_off(4 h + tq + 8 hi, 32 nb + 16 g1 + 4 tp) -
+    // 2 (nb >> 1) * 4 KiB for the weight gradient's transposed reads; la2 / lt2: the same + two planes
+    const int lbase = static_cast<int>(reinterpret_cast<uintptr_t>(dzl));
+    int la[4], la2[4], lt[2][2], lt2[2][2];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        la[c] = lbase + hb_dz_off(l32, 16 * c + 8 * h) - c * kHbChunkB;
+        la2[c] = la[c] + 2 * kHbPlane;
+    }
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+        for (int hi = 0; hi < 2; ++hi) {
+            lt[nb][hi] = lbase + hb_dz_off(4 * h + tq + 8 * hi, 32 * nb + 16 * g1 + 4 * tp);
+            lt2[nb][hi] = lt[nb][hi] + 2 * kHbPlane;
+        }
+
+    f32x16 dw[8];
+#pragma unroll
+    for (int nb = 0; nb < 8; ++nb) dw[nb] = f32x16{};
+    float4 csum = make_float4(0.f, 0.f, 0.f, 0.f);
+
+    // this wave's B fragments: image row 32 w + l32 (output column), half h, swizzled as the image stores it; the
+    // chunk and plane offsets ride in soffset
+    const int brow = 32 * wave + l32;
+    const int boff = (brow * 2 + (h ^ ((brow >> 3) & 1))) * 16;
+    const __amdgpu_buffer_rsrc_t rimg = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint4*>(P.img), 0, static_cast<uint32_t>(kHbChunks * kHbImgChunkU * 16), kHbRsrcFlags);
+    auto bload = [&](int c, int q) {
+        return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rimg, boff, (c * kHbImgChunkU + q * kHbImgPlaneU) * 16, 0));
+    };
+
+    // prologue: the first tile's H stage and dZ planes
+    {
+        const int64_t row0 = static_cast<int64_t>(t_begin) * kHbT;
+        hb_dma_h(hb_tile_rsrc(P.h, row0), stage);
+        float4 v[8];
+        hb_load_dz(hb_tile_rsrc(P.dz, row0), v);
+        hb_store_dz(v, dzl, csum);
+    }
+    __syncthreads();
+
+    for (int t = t_begin; t < t_end; ++t) {
+        const int64_t row0 = static_cast<int64_t>(t) * kHbT;
+        const bool has_next = t + 1 < t_end;
+        // ---- input gradient main loop: dZ rows (LDS, resident) x W^T columns (global, two chunks ahead)
+        f32x16 acc[2] = {f32x16{}, f32x16{}};
+        uint4 bq[kHbBDepth + 1][3];  // ring of image chunks in flight (kHbBDepth ahead)
+#pragma unroll
+        for (int c = 0; c < kHbBDepth; ++c)
+#pragma unroll
+            for (int q = 0; q < 3; ++q) bq[c][q] = bload(c, q);
+#pragma unroll
+        for (int c = 0; c < kHbChunks; ++c) {
+            if (c + kHbBDepth < kHbChunks) {
+#pragma unroll
+                for (int q = 0; q < 3; ++q)
+                    bq[(c + kHbBDepth) % (kHbBDepth + 1)][q] = bload(c + kHbBDepth, q);
+            }
+            bf16x8 b[3];
+#pragma unroll
+            for (int q = 0; q < 3; ++q) b[q] = __builtin_bit_cast(bf16x8, bq[c % (kHbBDepth + 1)][q]);
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                // hb_dz_off(32 i + l32, 16 c + 8 h) = lane part (by c & 3) + c * 2 KiB + i * 1 KiB: the constant in the
+                // immediate offset (plane 2 from a second base: the field holds 16 bits)
+                const int ci = c * kHbChunkB + i * 1024;
+                bf16x8 a[3];
+                a[0] = hb_read16(la[c & 3] + ci);
+                a[1] = hb_read16(la[c & 3] + ci + kHbPlane);
+                a[2] = hb_read16(la2[c & 3] + ci);
+                acc[i] = mfma_x6(a, b, acc[i]);
+            }
+            __builtin_amdgcn_sched_barrier(0);  // one chunk's fragments live at a time (the 128 dW registers stay)
+        }
+        // ---- epilogue: H from the stage (this wave's DMA landed, then every wave's), ELU', dZp out
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        float hr[2][16];
+        {
+            const float* hs = reinterpret_cast<const float*>(stage) + 32 * wave + l32;
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) hr[i][r] = hs[(32 * i + 4 * h + (r & 3) + 8 * (r >> 2)) * kHbW];
+        }
+        {
+            // buffer resource over the tile's rows of this wave's columns: the 8-row group step in soffset, the row in
+            // the immediate (no per-store address arithmetic)
+            const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
+                P.dz_prev + row0 * kHbW + 32 * wave, 0, static_cast<uint32_t>(kHbT * kHbW * 4), 0x00020000);
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const float v = acc[i][r];
+                    const float hv = hr[i][r];
+                    const float g = v * (hv + 1.f);  // ELU'(z) = 1 if z > 0 else h + 1 (epilogue_tiles_impl's bits)
+                    const float o = hv > 0.f ? v : g;
+                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, o), rc,
+                                                          ((4 * h + (r & 3)) * kHbW + l32) * 4,
+                                                          (32 * i + 8 * (r >> 2)) * kHbW * 4, 2 /* nt */);
+                }
+        }
+        __syncthreads();  // every wave has read the stage
+        if (has_next) hb_dma_h(hb_tile_rsrc(P.h, row0 + kHbT), stage);
+        float4 vn[8];
+        // ---- weight gradient of the tile: dW[n][32 w + l32] += sum over rows of dZ[m][n] H[m][32 w + l32]
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int st = 0; st < 2; ++st) {
+                if (i == 1 && st == 0) {
+                    // the next tile's dZ into registers behind the first half (H block 0 is dead by now: 32 registers
+                    // for the loads instead of 32 + 16), ~4 us before its use
+                    __builtin_amdgcn_sched_barrier(0);
+                    if (has_next) hb_load_dz(hb_tile_rsrc(P.dz, row0 + kHbT), vn);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+                // B = H rows pi(8 h + t) of column 32 w + l32: accumulator entries r = 8 st + t of block i
+                bf16x8 hb[3];
+                {
+                    uint32_t p0[4], p1[4], p2[4];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        float x = hr[i][8 * st + 2 * j], y = hr[i][8 * st + 2 * j + 1];
+                        p0[j] = split_pair(x, y);
+                        p1[j] = split_pair(x, y);
+                        p2[j] = pack_pair(x, y);
+                    }
+                    hb[0] = __builtin_bit_cast(bf16x8, make_uint4(p0[0], p0[1], p0[2], p0[3]));
+                    hb[1] = __builtin_bit_cast(bf16x8, make_uint4(p1[0], p1[1], p1[2], p1[3]));
+                    hb[2] = __builtin_bit_cast(bf16x8, make_uint4(p2[0], p2[1], p2[2], p2[3]));
+                }
+#pragma unroll
+                for (int nb = 0; nb < 8; ++nb) {
+                    // rows 32 i + 16 st + 4 h + tq (lo) and + 8 (hi), columns 32 nb + 16 g1 + 4 tp: lane part by
+                    // (nb & 1, lo / hi), the rest constant
+                    const int ci = 2 * (nb >> 1) * 2 * kHbChunkB + (32 * i + 16 * st) * 32;
+                    const int b0 = lt[nb & 1][0] + ci, b1 = lt[nb & 1][1] + ci;
+                    const int c0 = lt2[nb & 1][0] + ci, c1 = lt2[nb & 1][1] + ci;
+                    bf16x8 a[3];
+                    a[0] = hb_cat(hb_tr(b0), hb_tr(b1));
+                    a[1] = hb_cat(hb_tr(b0 + kHbPlane), hb_tr(b1 + kHbPlane));
+                    a[2] = hb_cat(hb_tr(c0), hb_tr(c1));
+                    dw[nb] = mfma_x6(a, hb, dw[nb]);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+        __syncthreads();  // every wave has read the dZ planes
+        if (has_next) {
+            hb_store_dz(vn, dzl, csum);
+            __syncthreads();
+        }
+    }
+
+    // ---- the slice's partial row: dW (lane: column 32 w + l32 of rows 32 nb + (r & 3) + 8 (r >> 2) + 4 h), then db
+    float* out = P.part + static_cast<int64_t>(s) * kHbPartFloats;
+#pragma unroll
+    for (int nb = 0; nb < 8; ++nb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+            out[(32 * nb + (r & 3) + 8 * (r >> 2) + 4 * h) * kHbW + 32 * wave + l32] = dw[nb][r];
+    float4* red = reinterpret_cast<float4*>(stage);  // free: the last tile's H was read before the last barrier
+    red[threadIdx.x] = csum;
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        float4 a = red[threadIdx.x];
+#pragma unroll
+        for (int g = 1; g < 8; ++g) {
+            const float4 b = red[64 * g + threadIdx.x];
+            a.x += b.x;
+            a.y += b.y;
+            a.z += b.z;
+            a.w += b.w;
+        }
+        reinterpret_cast<float4*>(out + kHbW * kHbW)[threadIdx.x] = a;
+    }
+}
+
+int64_t hb_tiles_per(int64_t tiles) {
+    const int64_t s = std::min<int64_t>(kHbMaxSlices, tiles);
+    return ceil_div(tiles, s);
+}
+
+}  // namespace
+}  // namespace rslrl
+
+using namespace rslrl;
+
+extern "C" int64_t rslrl_hidden_bwd_slices(int64_t M) {
+    if (M < kHbT || M % kHbT || M / kHbT > INT32_MAX) return 0;
+    const int64_t tiles = M / kHbT;
+    return ceil_div(tiles, hb_tiles_per(tiles));
+}
+
+extern "C" size_t rslrl_hidden_bwd_partial_floats(void) { return kHbPartFloats; }
+
+extern "C" int rslrl_hidden_bwd_pair(const rslrl_hidden_bwd_problem_t* p0, const rslrl_hidden_bwd_problem_t* p1,
+                                     int64_t M, int32_t width, rslrl_stream_t stream) {
+    if (!p0 || width != kHbW) return RSLRL_E_INVALID_ARGUMENT;
+    if (M < kHbT || M % kHbT || M / kHbT > INT32_MAX) return M == 0 ? RSLRL_OK : RSLRL_E_UNSUPPORTED;
+    const rslrl_hidden_bwd_problem_t* a[2] = {p0, p1};
+    const int n = p1 ? 2 : 1;
+    HbArgs args{};
+    for (int i = 0; i < n; ++i) {
+        const rslrl_hidden_bwd_problem_t* q = a[i];
+        if (!q->dz || !q->h || !q->bimage || !q->dz_prev || !q->partials) return RSLRL_E_INVALID_ARGUMENT;
+        const uintptr_t bits = reinterpret_cast<uintptr_t>(q->dz) | reinterpret_cast<uintptr_t>(q->h) |
+                               reinterpret_cast<uintptr_t>(q->bimage) | reinterpret_cast<uintptr_t>(q->dz_prev) |
+                               reinterpret_cast<uintptr_t>(q->partials);
+        if (bits & 15) return RSLRL_E_MISALIGNED;
+        args.p[i] = HbProblem{q->dz, q->h, static_cast<const uint4*>(q->bimage), q->dz_prev, q->partials};
+    }
+    const int64_t tiles = M / kHbT;
+    const int64_t per = hb_tiles_per(tiles);
+    args.tiles = static_cast<int>(tiles);
+    args.tiles_per = static_cast<int>(per);
+    const dim3 grid(static_cast<unsigned>(ceil_div(tiles, per)), static_cast<unsigned>(n));
+    hipLaunchKernelGGL(hidden_bwd_kernel, grid, dim3(kHbThreads), 0, reinterpret_cast<hipStream_t>(stream), args);
+    return launch_status();
+}

@@ -650,6 +650,59 @@ def linear_wgrad_pair(dzs, xs, arith=_lib.ARITH_X6, bias_side=0, dwb_outs=(None,
     return [(d[: N * K].view(*shape), d[N * K:]) for d in dwbs]
 
 
+# RSLRL_HIDDEN_BWD=0 keeps the square hidden layers' input and weight gradients in separate launches (A/B)
+_HIDDEN_BWD = os.environ.get("RSLRL_HIDDEN_BWD", "1") != "0"
+HIDDEN_BWD_WIDTH = 256
+
+
+def hidden_bwd_ok(dzs, hs) -> bool:
+    """hidden_bwd_pair covers the problems: x6, a 256 x 256 hidden layer, M a multiple of 64, contiguous operands."""
+    M, N = dzs[0].shape
+    return (N == HIDDEN_BWD_WIDTH and hs[0].shape[1] == HIDDEN_BWD_WIDTH and M % 64 == 0 and M >= 64
+            and all(t.is_contiguous() and t.shape == (M, HIDDEN_BWD_WIDTH) and t.data_ptr() % 16 == 0
+                    for t in list(dzs) + list(hs)))
+
+
+def hidden_bwd_pair(dzs, hs, imgs, dwb_outs=(None, None), defer=None):
+    """The backward of a square hidden layer (Linear(256, 256) + ELU) of one or two problems over the same rows in one
+    launch (rslrl_hidden_bwd_pair, csrc/mlp_bwd_fused.hip): per problem dz_prev = (dz W) * ELU'(h) -- the bits of
+    linear_dgrad_elu_pair -- and [dW | db] = [dz^T h | sum dz] from the same read of dz and h (the weight gradient of
+    linear_wgrad_pair(bias_side=1), summed in another order: fp32-close).  imgs: the x6 images of W^T (the tapes'
+    dgrad images).  dwb_outs: optional [256 * 256 + 256] destinations (adjacent arena slots); defer: a _FoldBatch --
+    the folds are queued there (dW, db valid after its run()).  Returns per problem (dz_prev, dw, db)."""
+    n = len(dzs)
+    M = dzs[0].shape[0]
+    W = HIDDEN_BWD_WIDTH
+    L = _lib.lib()
+    S = L.rslrl_hidden_bwd_slices(M)
+    NK = L.rslrl_hidden_bwd_partial_floats()
+    dev = dzs[0].device
+    outs, parts, dwbs, probs = [], [], [], []
+    for i in range(n):
+        outs.append(torch.empty(M, W, device=dev, dtype=torch.float32))
+        parts.append(torch.empty(S, NK, device=dev, dtype=torch.float32))
+        dwbs.append(_out_or_empty(dwb_outs[i] if i < len(dwb_outs) else None, (NK,), dev))
+        probs.append(_lib.HiddenBwdProblem(dzs[i].data_ptr(), hs[i].data_ptr(), imgs[i].data_ptr(),
+                                           outs[i].data_ptr(), parts[i].data_ptr()))
+    with timer.span(f"linear_hidden_bwd{'_pair' if n == 2 else ''}[M={M},N={W},K={W}]", dev, n * 4 * M * 3 * W,
+                    n * 4 * M * W * W):
+        rc = L.rslrl_hidden_bwd_pair(ctypes.byref(probs[0]), ctypes.byref(probs[1]) if n == 2 else None, M, W,
+                                     _stream(dzs[0]))
+    _lib.check(rc, "rslrl_hidden_bwd_pair")
+    res = []
+    for i in range(n):
+        if defer is not None:
+            defer.add(parts[i], S, NK, dwbs[i], NK)
+        else:
+            nbytes = L.rslrl_fold_partials_workspace_bytes(S, NK)
+            ws = torch.empty(max(nbytes, 16) // 8, dtype=torch.float64, device=dev)
+            rc = L.rslrl_fold_partials_ex(parts[i].data_ptr(), S, NK, dwbs[i].data_ptr(), NK, 0, 0, ws.data_ptr(),
+                                          nbytes, _stream(dzs[i]))
+            _lib.check(rc, "rslrl_fold_partials_ex")
+        res.append((outs[i], dwbs[i][: W * W].view(W, W), dwbs[i][W * W:]))
+    return res
+
+
 def _weight_grad(dz, x, x6: bool, h3=False, dz_amax=None, x_amax=None, out=None, want_bias=False, db_out=None):
     # the split weight-gradient kernel computes TN x 256 tiles (TN = 32, 64 or 256 rows of its first operand):
     # the square hidden layers run it as dz^T x (h3 when both operands come from h3-layer producers); the first
@@ -1051,13 +1104,23 @@ def train_backward_pair(tape_a, dy_a, outs_a, tape_c, dy_c, outs_c):
                 wo, bo = outs[i][l]
                 adj = wo.is_contiguous() and bo.data_ptr() == wo.data_ptr() + 4 * wo.numel()
                 dwb_outs.append(torch.as_strided(wo, (N * K + N,), (1,)) if adj else None)
-            res = linear_wgrad_pair(dz, h_in, bias_side=1, dwb_outs=dwb_outs, defer=folds)
+            if _HIDDEN_BWD and hidden_bwd_ok(dz, h_in):
+                # input and weight gradients of the layer from one read of dz and h (csrc/mlp_bwd_fused.hip)
+                both = hidden_bwd_pair(dz, h_in, [t.dgrad_imgs[l] for t in tapes], dwb_outs, defer=folds)
+                res = [(r[1], r[2]) for r in both]
+                dz_next = [r[0] for r in both]
+            else:
+                res = linear_wgrad_pair(dz, h_in, bias_side=1, dwb_outs=dwb_outs, defer=folds)
+                dz_next = None
             for i in range(2):
                 if dwb_outs[i] is None:
                     folds.after.append(lambda o=outs[i][l], r=res[i]: torch._foreach_copy_(list(o), list(r)))
             if eager:
                 folds.run(dz[0].device)
-            dz, _ = linear_dgrad_elu_pair(dz, h_in, [t.dgrad_imgs[l] for t in tapes], _lib.ARITH_X6)
+            if dz_next is None:
+                dz, _ = linear_dgrad_elu_pair(dz, h_in, [t.dgrad_imgs[l] for t in tapes], _lib.ARITH_X6)
+            else:
+                dz = dz_next
         else:  # first layer: (x^T dz)^T on the 64-row tiles, the bias from dz (the kernel's K side)
             pad = (-K) % 4
             xp = [F.pad(x, (0, pad)) if pad else x for x in h_in]

@@ -21,6 +21,7 @@ from collections import defaultdict
 
 CAL_BYTES = 512 << 20
 SHORT = [
+    (r"hidden_bwd_kernel", "x6_hidden_bwd_pair"),
     (r"mlp_gemm_x6_w4_pair_kernel<2>", "x6_dgrad_pair_w4"),
     (r"mlp_gemm_x6_w4s_pair_kernel<2>", "x6_dgrad_pair_w4s"),
     (r"mlp_gemm_x6_pair_kernel<1,", "x6_fwd_elu_pair"),
@@ -40,14 +41,18 @@ ALGO = {
     "x6_dgrad_pair_w4s": lambda M: 2 * (M * 256 * 4 * 3),
     "x6_dgrad_pair": lambda M: 2 * (M * 256 * 4 * 3),
     "x6_wgrad_pair": lambda M: 2 * (M * 256 * 4 * 2),             # dZ, H read (+ partials)
+    # fused input + weight gradient (csrc/mlp_bwd_fused.hip): dZ, H read once, dZ_prev written, + 128 slice partial rows
+    "x6_hidden_bwd_pair": lambda M: 2 * (M * 256 * 4 * 3 + min(128, M // 64) * 65792 * 4),
 }
 FLOPS = {k: (lambda M: 2 * 2 * M * 256 * 256) for k in ALGO}
+FLOPS["x6_hidden_bwd_pair"] = lambda M: 2 * 2 * 2 * M * 256 * 256  # two GEMMs per problem
 # which calibration pattern each kernel's traffic follows: (reads, writes)
 PATTERN = {
     "x6_fwd_elu_pair": ("cal_read_gemm_a", "cal_write_c_b32_nt"),
     "x6_dgrad_pair_w4": ("cal_read_gemm_a+cal_read_c_b32", "cal_write_c_b32_nt"),
     "x6_dgrad_pair": ("cal_read_gemm_a+cal_read_c_b32", "cal_write_c_b32_nt"),
     "x6_wgrad_pair": ("cal_read_v4", "cal_write_v4"),
+    "x6_hidden_bwd_pair": ("cal_read_v4", "cal_write_c_b32_nt"),
 }
 
 

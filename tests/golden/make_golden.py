@@ -778,6 +778,78 @@ def make_update_c2(PPO, ActorCritic, RolloutStorage):
 
 
 # --------------------------------------------------------------------------------------------------
+# one reference update at config C3's full size (N 65536, T 24, O 48, A 12, 3x256; 393,216-row mini-batches):
+# the first mini-batch's pre-clip gradient, the loss means and the lr trace.  The whole storage is regenerated from
+# one numpy seed on the test side (policy-independent: 1.57 M transitions cannot travel as a fixture), so the stored
+# mean / values / log-probs are seeded draws, not the policy's outputs -- the rollout policy's std (1.0) is stored as
+# sigma, as a rollout with a shared std records it.  The fixture holds the initial weights, the gradient and the
+# generator state (~2.3 MB).
+# --------------------------------------------------------------------------------------------------
+def storage_c3(seed, T, N, O, A):
+    """Every storage input of the C3 fixture from one PCG64 stream (tests/test_gpu_update_c3.py draws the same)."""
+    rng = np.random.default_rng(seed)
+    nz = {
+        "obs": rng.standard_normal((T, N, O), dtype=np.float32),
+        "rewards": rng.standard_normal((T, N, 1), dtype=np.float32),
+        "dones": (rng.random((T, N, 1)) < 0.02).astype(np.uint8),
+        "noise": rng.standard_normal((T, N, A), dtype=np.float32),
+        "last_obs": rng.standard_normal((N, O), dtype=np.float32),
+        "mu": rng.standard_normal((T, N, A), dtype=np.float32),
+        "values": rng.standard_normal((T, N, 1), dtype=np.float32),
+    }
+    nz["mu"] *= np.float32(0.3)
+    # the stored log-prob of the actions mu + 1.0 * noise under N(mu, 1): -0.5 sum_a noise_a^2 - A/2 log(2 pi), by
+    # elementwise fp32 operations in action order (correctly rounded on any CPU: bit-reproducible)
+    s = np.zeros((T, N), dtype=np.float32)
+    for a in range(A):
+        s = s + nz["noise"][..., a] * nz["noise"][..., a]
+    nz["logp"] = (np.float32(-0.5) * s - np.float32(A * 0.9189385332046727))[..., None]
+    return nz
+
+
+def make_update_c3(PPO, ActorCritic, RolloutStorage):
+    T, N, O, A, hidden, seed = 24, 65536, 48, 12, [256, 256, 256], 113
+    torch.manual_seed(seed)
+    obs0 = {"policy": torch.zeros(N, O)}
+    groups = {"policy": ["policy"], "critic": ["policy"]}
+    pol = ActorCritic(obs0, groups, A, actor_hidden_dims=hidden, critic_hidden_dims=hidden)
+    alg = PPO(pol, num_learning_epochs=5, num_mini_batches=4, device="cpu")
+    init_state = {k: f32(v) for k, v in pol.state_dict().items()}
+    alg.init_storage("rl", N, T, obs0, [A])
+    nz = storage_c3(seed * 100, T, N, O, A)
+    st = alg.storage
+    std = pol.std.detach().clone()  # noise_std_type "scalar": the distribution's std is this parameter
+    st.observations["policy"].copy_(torch.from_numpy(nz["obs"]))
+    st.rewards.copy_(torch.from_numpy(nz["rewards"]))
+    st.dones.copy_(torch.from_numpy(nz["dones"]))
+    mu = torch.from_numpy(nz["mu"])
+    sig = std.reshape(1, 1, A).expand(T, N, A)
+    st.mu.copy_(mu)
+    st.sigma.copy_(sig)
+    st.actions.copy_(mu + sig * torch.from_numpy(nz["noise"]))
+    st.values.copy_(torch.from_numpy(nz["values"]))
+    st.actions_log_prob.copy_(torch.from_numpy(nz["logp"]))
+    st.step = T
+    with torch.inference_mode():
+        alg.compute_returns({"policy": torch.from_numpy(nz["last_obs"])})
+    torch.manual_seed(5000)
+    gen_state = torch.default_generator.get_state().numpy().copy()
+    loss_dict, lr_trace, grads, _ = _run_recorded_update(alg, grad_batches=1)
+    arrays = {f"init/{k}": v for k, v in init_state.items()}
+    arrays["grad_mb0"] = f32(grads[0])
+    arrays["std"] = f32(std)
+    arrays["gen_state"] = gen_state
+    arrays["returns_head"] = f32(st.returns[:2, :256])
+    arrays["advantages_head"] = f32(st.advantages[:2, :256])
+    arrays["obs_sha256"] = np.frombuffer(hashlib.sha256(nz["obs"].tobytes()).digest(), dtype=np.uint8)
+    arrays["logp_sha256"] = np.frombuffer(hashlib.sha256(nz["logp"].tobytes()).digest(), dtype=np.uint8)
+    np.savez_compressed(os.path.join(HERE, "update_c3.npz"), **arrays)
+    print("update_c3 lr", lr_trace[:4], "...", alg.learning_rate, loss_dict, flush=True)
+    return {"T": T, "N": N, "O": O, "A": A, "hidden": hidden, "M": 4, "E": 5, "seed": seed, "noise_seed": seed * 100,
+            "loss_dict": loss_dict, "lr_trace": lr_trace, "final_lr": alg.learning_rate}
+
+
+# --------------------------------------------------------------------------------------------------
 # rollout side: act + process_env_step + add_transitions + RND (ppo.py:129-169, rollout_storage.py:77-103,
 # rnd.py:113-135) -- the inputs of each step, the transition act() produced, and the storage after T steps
 # --------------------------------------------------------------------------------------------------
@@ -879,7 +951,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reference", default=os.environ.get("RSL_RL_REFERENCE", "/root/reference"))
     ap.add_argument("--only", choices=["rollout", "normalizer", "multirank", "update_c2", "update_rnd",
-                                           "update_std"],
+                                           "update_std", "update_c3"],
                     help="regenerate one fixture family, keep the rest")
     ap.add_argument("--cases", default=None, help="with --only multirank: comma-separated case names to (re)generate")
     args = ap.parse_args()
@@ -899,6 +971,9 @@ def main():
             meta["update_std"] = make_update_std(args.reference)
         elif args.only == "update_c2":
             meta["update_c2"] = make_update_c2(PPO, ActorCritic, RolloutStorage)
+        elif args.only == "update_c3":
+            torch.set_num_threads(8)
+            meta["update_c3"] = make_update_c3(PPO, ActorCritic, RolloutStorage)
         else:
             meta["normalizer"] = make_normalizer(args.reference)
         with open(os.path.join(HERE, "golden.json"), "w") as f:
@@ -920,6 +995,7 @@ def main():
         "update_c2": make_update_c2(PPO, ActorCritic, RolloutStorage),
         "update_rnd": make_update_rnd(args.reference),
         "update_std": make_update_std(args.reference),
+        "update_c3": make_update_c3(PPO, ActorCritic, RolloutStorage),
     }
     with open(os.path.join(HERE, "golden.json"), "w") as f:
         json.dump(meta, f, indent=1, sort_keys=True)

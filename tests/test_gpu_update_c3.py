@@ -1,0 +1,114 @@
+"""One PPO.update() at config C3's full size (N 65536, T 24, O 48, A 12, actor/critic 3x256 ELU, E 5 x M 4: 393,216-row
+mini-batches) against the reference's own update on the same inputs (tests/golden/make_golden.py make_update_c3,
+rsl_rl/algorithms/ppo.py:245-368).  The storage is regenerated here from the fixture's numpy seed (every input of it is
+a seeded draw: 1.57 M transitions do not travel as a fixture); the fixture holds the initial weights, the generator
+state and what the reference produced.  This is the mini-batch size the bench measures: the first mini-batch runs
+through the fused critic and actor heads (the whole PPO loss inside the actor's last GEMM launch), the fused hidden-layer
+backward (input + weight gradients in one pass) and the x6 GEMMs, and its pre-clip gradient must match the reference's
+within 1e-5 of each parameter tensor's max; the learning-rate trace exactly, the loss means within rtol 1e-4."""
+
+import hashlib
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+
+def storage_c3(seed, T, N, O, A):
+    # make_golden.storage_c3: the same PCG64 draws in the same order, the log-prob by the same fp32 elementwise ops
+    rng = np.random.default_rng(seed)
+    nz = {
+        "obs": rng.standard_normal((T, N, O), dtype=np.float32),
+        "rewards": rng.standard_normal((T, N, 1), dtype=np.float32),
+        "dones": (rng.random((T, N, 1)) < 0.02).astype(np.uint8),
+        "noise": rng.standard_normal((T, N, A), dtype=np.float32),
+        "last_obs": rng.standard_normal((N, O), dtype=np.float32),
+        "mu": rng.standard_normal((T, N, A), dtype=np.float32),
+        "values": rng.standard_normal((T, N, 1), dtype=np.float32),
+    }
+    nz["mu"] *= np.float32(0.3)
+    s = np.zeros((T, N), dtype=np.float32)
+    for a in range(A):
+        s = s + nz["noise"][..., a] * nz["noise"][..., a]
+    nz["logp"] = (np.float32(-0.5) * s - np.float32(A * 0.9189385332046727))[..., None]
+    return nz
+
+
+@pytest.mark.timeout(600)
+def test_update_c3_matches_reference(golden_meta, cuda_device, monkeypatch):
+    from rsl_rl_amd.algorithms import PPO
+    from rsl_rl_amd.modules import ActorCritic
+    from rsl_rl_amd.networks import fused_mlp
+    from update_fixtures import run_recorded_update
+
+    meta = golden_meta["update_c3"]
+    z = np.load(os.path.join(GOLDEN, "update_c3.npz"))
+    T, N, O, A = meta["T"], meta["N"], meta["O"], meta["A"]
+    nz = storage_c3(meta["noise_seed"], T, N, O, A)
+    assert hashlib.sha256(nz["obs"].tobytes()).digest() == z["obs_sha256"].tobytes(), "numpy stream differs"
+    assert hashlib.sha256(nz["logp"].tobytes()).digest() == z["logp_sha256"].tobytes(), "log-prob bits differ"
+    dev = cuda_device
+    obs0 = {"policy": torch.zeros(N, O)}
+    groups = {"policy": ["policy"], "critic": ["policy"]}
+    pol = ActorCritic(obs0, groups, A, actor_hidden_dims=meta["hidden"], critic_hidden_dims=meta["hidden"])
+    pol.load_state_dict({k[5:]: torch.from_numpy(z[k]) for k in z.files if k.startswith("init/")})
+    alg = PPO(pol, num_learning_epochs=meta["E"], num_mini_batches=meta["M"], device=dev)
+    alg.init_storage("rl", N, T, obs0, [A])
+    st = alg.storage
+    std = torch.from_numpy(z["std"])
+    mu = torch.from_numpy(nz["mu"])
+    sig = std.reshape(1, 1, A).expand(T, N, A)
+    st.observations["policy"].copy_(torch.from_numpy(nz["obs"]))
+    st.rewards.copy_(torch.from_numpy(nz["rewards"]))
+    st.dones.copy_(torch.from_numpy(nz["dones"]))
+    st.mu.copy_(mu)
+    st.sigma.copy_(sig)
+    st.actions.copy_(mu + sig * torch.from_numpy(nz["noise"]))  # the fixture's fp32 mul then add (CPU, IEEE)
+    st.values.copy_(torch.from_numpy(nz["values"]))
+    st.actions_log_prob.copy_(torch.from_numpy(nz["logp"]))
+    st.step = T
+    last_obs = nz["last_obs"]
+    del nz
+    with torch.inference_mode():
+        alg.compute_returns({"policy": torch.from_numpy(last_obs).to(dev)})
+    # GAE is bit-exact with the reference; the normalised advantages within fp32 rounding of its statistics
+    assert torch.equal(st.returns[:2, :256].cpu(), torch.from_numpy(z["returns_head"]))
+    assert torch.allclose(st.advantages[:2, :256].cpu(), torch.from_numpy(z["advantages_head"]), rtol=1e-5, atol=1e-6)
+    torch.default_generator.set_state(torch.from_numpy(z["gen_state"].copy()))
+
+    counts = {"actor_head": 0, "hidden_bwd": 0}
+    for name, key in (("actor_head_fwd_bwd", "actor_head"), ("hidden_bwd_pair", "hidden_bwd")):
+        real = getattr(fused_mlp, name)
+
+        def spy(*a, _real=real, _key=key, **k):
+            counts[_key] += 1
+            return _real(*a, **k)
+
+        monkeypatch.setattr(fused_mlp, name, spy)
+    grads = [None]
+    loss, lr_trace = run_recorded_update(alg, grads)
+    # the measured path ran: the loss inside the actor's head launch, the square hidden layers' fused backward
+    assert counts["actor_head"] == 20 and counts["hidden_bwd"] == 40, counts
+    assert lr_trace == meta["lr_trace"], (lr_trace[:5], meta["lr_trace"][:5])
+    assert alg.learning_rate == meta["final_lr"]
+    for k, v in meta["loss_dict"].items():
+        assert abs(loss[k] - v) <= 1e-4 * abs(v) + 1e-6, (k, loss[k], v)
+    ref = torch.from_numpy(z["grad_mb0"]).double()
+    ours = grads[0].double()
+    assert ours.shape == ref.shape
+    off = 0
+    worst = {}
+    for name, p in pol.named_parameters():
+        n = p.numel()
+        r, o = ref[off:off + n], ours[off:off + n]
+        err = (o - r).abs().max().item() / max(r.abs().max().item(), 1e-30)
+        worst[name] = err
+        off += n
+    print("grad_mb0 max error / max |ref| per tensor:", {k: f"{v:.1e}" for k, v in worst.items()})
+    assert all(v <= 1e-5 for v in worst.values()), worst
+
