@@ -26,6 +26,7 @@ same learning rates on every rank, no broadcast.
 
 from __future__ import annotations
 
+import os
 from itertools import chain
 
 import torch
@@ -63,19 +64,26 @@ def adapt_learning_rate_device(lr: torch.Tensor, kl_mean: torch.Tensor, desired_
 
 
 class GradArena:
-    """One contiguous fp32 buffer behind every trainable parameter's gradient, in the concatenation order of the
-    reference's reduce_parameters (policy.parameters(), then the RND predictor's; ppo.py:447-450), followed by
-    `extra` scalar slots (the mini-batch KL) that travel in the same all-reduce."""
+    """One contiguous fp32 buffer behind every trainable parameter's gradient, followed by `extra` scalar slots (the
+    mini-batch KL) that travel in the same all-reduce.  The reference concatenates the gradients in parameters() order
+    (policy.parameters(), then the RND predictor's; ppo.py:447-450); here `early` parameters (those whose gradients are
+    complete before the rest of the backward, see PPO._early_params) come first, so that the all-reduce can start on
+    that prefix while the backward still runs (`early_numel`).  The order of a SUM all-reduce's elements does not change
+    any element's sum; every other parameter keeps its relative order (the RND predictor's span stays contiguous)."""
 
-    def __init__(self, params, extra: int, device):
+    def __init__(self, params, extra: int, device, early=()):
         self.params = list(params)
+        ids = {id(p) for p in early}
+        order = [p for p in self.params if id(p) in ids] + [p for p in self.params if id(p) not in ids]
         self.numel = sum(p.numel() for p in self.params)
+        self.early_numel = sum(p.numel() for p in order if id(p) in ids)
         self.flat = torch.zeros(self.numel + extra, dtype=torch.float32, device=device)
-        self.views, off = [], 0
-        for p in self.params:
-            self.views.append(self.flat[off:off + p.numel()].view_as(p))
+        slots, off = {}, 0
+        for p in order:
+            slots[id(p)] = self.flat[off:off + p.numel()].view_as(p)
             off += p.numel()
-        self._slot = {id(p): v for p, v in zip(self.params, self.views)}
+        self.views = [slots[id(p)] for p in self.params]
+        self._slot = slots
         self.extra = self.flat[self.numel:]
 
     def matches(self, params) -> bool:
@@ -308,8 +316,23 @@ class PPO:
         the parameter list changes."""
         params = self._trainable_params()
         if self._arena is None or not self._arena.matches(params) or self._arena.flat.device != params[0].device:
-            self._arena = GradArena(params, extra=1, device=params[0].device)
+            early = self._early_params() if self.is_multi_gpu else ()
+            self._arena = GradArena(params, extra=1, device=params[0].device, early=early)
         return self._arena
+
+    def _early_params(self):
+        """Parameters whose gradients the manual backward completes before its last layer: every Linear of the actor
+        and the critic but the first (the paired backward runs the output layers, then the hidden layers from the top;
+        the first layers' weight gradients come last).  Their arena prefix is all-reduced while the first layers'
+        backward runs (RSLRL_OVERLAP_ALLREDUCE=0: one all-reduce after the backward, as before)."""
+        if os.environ.get("RSLRL_OVERLAP_ALLREDUCE", "1") == "0" or not isinstance(self.policy, ActorCritic):
+            return ()
+        out = []
+        for net in (self.policy.actor, self.policy.critic):
+            lins = [m for m in net.modules() if isinstance(m, nn.Linear)]
+            for m in lins[1:]:
+                out += [m.weight, m.bias]
+        return out
 
     def _sync_kl_and_lr(self, kl_mean: torch.Tensor):
         """KL all-reduce + adaptive lr + fp32 lr rounding under multi-GPU (ppo.py:271-294), host version
@@ -418,7 +441,17 @@ class PPO:
                             mean, sigma, value_batch, actions_batch, old_actions_log_prob_batch, advantages_batch,
                             target_values_batch, returns_batch, old_mu_batch, old_sigma_batch, grad_mu=g_mean,
                             grad_sigma=g_sigma, **loss_kw)
-                    self.policy.train_backward(tape, g_mean, g_sigma, g_value, sigma, arena.slot, side_stream=side)
+                    early_work = []
+                    if self.is_multi_gpu and arena.early_numel:
+                        def on_early(buf=arena.flat[:arena.early_numel]):
+                            # the early prefix's gradients are enqueued: its all-reduce starts now and overlaps the
+                            # first layers' backward (the collective's stream waits for this point of ours)
+                            early_work.append(torch.distributed.all_reduce(buf, op=torch.distributed.ReduceOp.SUM,
+                                                                           async_op=True))
+                    else:
+                        on_early = None
+                    self.policy.train_backward(tape, g_mean, g_sigma, g_value, sigma, arena.slot, side_stream=side,
+                                               on_early=on_early)
                     del tape
             else:
                 # autograd path for any other policy (ppo.py:246-253, :367-372)
@@ -469,7 +502,8 @@ class PPO:
                 if manual:
                     if adaptive:
                         arena.extra[:1].copy_(kl_src)
-                    self._all_reduce_arena(arena, with_kl=adaptive)
+                    self._all_reduce_arena(arena, with_kl=adaptive, skip=arena.early_numel if early_work else 0,
+                                           pending=early_work)
                     kl_src = arena.extra[:1]
                 else:
                     kl_src = kl_src.clone() if adaptive else None
@@ -595,11 +629,16 @@ class PPO:
         if self.rnd:
             self.rnd.predictor.load_state_dict(model_params[1])
 
-    def _all_reduce_arena(self, arena: GradArena, with_kl: bool):
-        """The one collective per mini-batch: SUM all-reduce of the arena's gradients (+ its KL slot), then
-        / world size (ppo.py:453-454 for the gradients, :273-274 for the KL)."""
+    def _all_reduce_arena(self, arena: GradArena, with_kl: bool, skip: int = 0, pending=()):
+        """The gradient collective per mini-batch: SUM all-reduce of the arena's gradients (+ its KL slot), then
+        / world size (ppo.py:453-454 for the gradients, :273-274 for the KL).  skip / pending: the first `skip`
+        elements were already handed to the asynchronous all-reduce(s) `pending` during the backward (the early
+        prefix); the rest is reduced here, then the current stream waits for them before the division."""
         buf = arena.flat[:arena.numel + (1 if with_kl else 0)]
-        torch.distributed.all_reduce(buf, op=torch.distributed.ReduceOp.SUM)
+        if skip < buf.numel():
+            torch.distributed.all_reduce(buf[skip:], op=torch.distributed.ReduceOp.SUM)
+        for w in pending:
+            w.wait()
         buf /= self.gpu_world_size
 
     def reduce_parameters(self, kl_mean: torch.Tensor | None = None):

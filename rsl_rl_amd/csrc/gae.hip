@@ -7,7 +7,11 @@
 //                     independent across envs).  All T (value, reward, done) loads of a lane are issued
 //                     before the recurrence (TMAX-unrolled register arrays), so the wave has 3*T
 //                     coalesced loads in flight; writes returns and raw advantages and emits one fp64
-//                     (sum, sum of squares) partial per block for the normalisation.
+//                     (count, mean, M2) partial per block for the normalisation: each lane keeps its T
+//                     advantages in registers and takes their mean and centred sum of squares exactly as a
+//                     two-pass variance would, lanes and waves merge by Chan's pairwise formula in a fixed tree
+//                     (round 5: this replaced round 3's separate centring pass -- one launch and a re-read of
+//                     the advantages fewer, and still no sum(a^2) - n mean^2 cancellation).
 //   adv_normalize     every block folds the <= kMaxPartials partials in one fixed order (so all blocks
 //                     agree bitwise), then rescales the advantages with 16-byte accesses.
 // Bytes per element (T*N of them): read 4 (V) + 4 (R) + 1 (done), write 4 (returns) + 4 (adv) = 17 in
@@ -36,19 +40,56 @@ struct GaeStep {
     }
 };
 
+// Chan et al.'s pairwise update of (count, mean, M2 = sum of squared deviations): exact in real arithmetic, and in
+// fp64 free of the sum(a^2) - n mean^2 cancellation.  Either side may be empty.
+struct Moments {
+    double n, mean, m2;
+};
+
+__device__ __forceinline__ Moments chan(const Moments& a, const Moments& b) {
+    const double n = a.n + b.n;
+    if (n == 0.0) return a;
+    const double delta = b.mean - a.mean;
+    const double fb = b.n / n;
+    return {n, a.mean + delta * fb, a.m2 + b.m2 + delta * delta * a.n * fb};
+}
+
+// block-wide merge in a fixed tree (wave: lane i takes lane i + off for off = 32 .. 1; then the waves in order);
+// the result is valid in thread 0
+__device__ __forceinline__ Moments block_chan(Moments m, double (*scratch)[3]) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const Moments o{__shfl_down(m.n, off, kWave), __shfl_down(m.mean, off, kWave), __shfl_down(m.m2, off, kWave)};
+        if ((threadIdx.x & (kWave - 1)) < off) m = chan(m, o);
+    }
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wid = threadIdx.x / kWave;
+    __syncthreads();
+    if (lane == 0) {
+        scratch[wid][0] = m.n;
+        scratch[wid][1] = m.mean;
+        scratch[wid][2] = m.m2;
+    }
+    __syncthreads();
+    Moments r{scratch[0][0], scratch[0][1], scratch[0][2]};
+#pragma unroll
+    for (int w = 1; w < kBlock / kWave; ++w) r = chan(r, Moments{scratch[w][0], scratch[w][1], scratch[w][2]});
+    return r;
+}
+
 // EXACT: T == TMAX, the `t < T` guards fold away and all 3*T loads issue back to back.
 template <int TMAX, bool EXACT>
 __global__ __launch_bounds__(kBlock) void gae_scan_kernel(
     const float* __restrict__ values, const float* __restrict__ rewards, const uint8_t* __restrict__ dones,
     const float* __restrict__ last_values, float gamma, float lam, int T_, int64_t N,
-    float* __restrict__ returns, float* __restrict__ advantages, double2* __restrict__ partials) {
+    float* __restrict__ returns, float* __restrict__ advantages, double4* __restrict__ partials) {
     const int T = EXACT ? TMAX : T_;
-    __shared__ double scratch[2][kBlock / kWave];
-    double s = 0.0, ss = 0.0;
+    __shared__ double scratch[kBlock / kWave][3];
+    Moments m{0.0, 0.0, 0.0};
     const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
     for (int64_t n = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; n < N; n += stride) {
         if constexpr (TMAX > 0) {
-            float v[TMAX], r[TMAX];
+            float v[TMAX], r[TMAX], av[TMAX];
             unsigned d[TMAX];
 #pragma unroll
             for (int t = 0; t < TMAX; ++t) {
@@ -61,6 +102,7 @@ __global__ __launch_bounds__(kBlock) void gae_scan_kernel(
             }
             float next_v = last_values[n];
             float adv = 0.0f;
+            double s = 0.0;
 #pragma unroll
             for (int t = TMAX - 1; t >= 0; --t) {
                 if (t < T) {
@@ -70,12 +112,24 @@ __global__ __launch_bounds__(kBlock) void gae_scan_kernel(
                     const float a = __fsub_rn(ret, v[t]);    // :145
                     returns[i] = ret;
                     advantages[i] = a;
+                    av[t] = a;
                     s += static_cast<double>(a);
-                    ss += static_cast<double>(a) * static_cast<double>(a);
                     next_v = v[t];
                 }
             }
-        } else {  // long rollouts: streaming loop
+            if (partials != nullptr) {  // this environment's T advantages: mean, then the centred sum of squares
+                const double mean = s / static_cast<double>(T);
+                double m2 = 0.0;
+#pragma unroll
+                for (int t = 0; t < TMAX; ++t) {
+                    if (t < T) {
+                        const double dlt = static_cast<double>(av[t]) - mean;
+                        m2 += dlt * dlt;
+                    }
+                }
+                m = chan(m, Moments{static_cast<double>(T), mean, m2});
+            }
+        } else {  // long rollouts: streaming loop (Welford's update per element)
             float next_v = last_values[n];
             float adv = 0.0f;
             for (int t = T - 1; t >= 0; --t) {
@@ -86,83 +140,56 @@ __global__ __launch_bounds__(kBlock) void gae_scan_kernel(
                 const float a = __fsub_rn(ret, v);
                 returns[i] = ret;
                 advantages[i] = a;
-                s += static_cast<double>(a);
-                ss += static_cast<double>(a) * static_cast<double>(a);
+                m.n += 1.0;
+                const double dlt = static_cast<double>(a) - m.mean;
+                m.mean += dlt / m.n;
+                m.m2 += dlt * (static_cast<double>(a) - m.mean);
                 next_v = v;
             }
         }
     }
     if (partials != nullptr) {
-        s = block_sum(s, scratch[0]);
-        ss = block_sum(ss, scratch[1]);
-        if (threadIdx.x == 0) partials[blockIdx.x] = make_double2(s, ss);
+        m = block_chan(m, scratch);
+        if (threadIdx.x == 0) partials[blockIdx.x] = make_double4(m.n, m.mean, m.m2, 0.0);
     }
 }
 
-// (sum, sum of squares) partials of an arbitrary vector (standalone normaliser).
+// (count, mean, M2) partials of an arbitrary vector (standalone normaliser): Welford per lane over its grid-stride
+// elements, then the block tree.
 __global__ __launch_bounds__(kBlock) void moments_kernel(const float* __restrict__ x, int64_t n,
-                                                         double2* __restrict__ partials) {
-    __shared__ double scratch[2][kBlock / kWave];
-    double s = 0.0, ss = 0.0;
+                                                         double4* __restrict__ partials) {
+    __shared__ double scratch[kBlock / kWave][3];
+    Moments m{0.0, 0.0, 0.0};
     const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
     for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < n; i += stride) {
         const double a = x[i];
-        s += a;
-        ss += a * a;
+        m.n += 1.0;
+        const double dlt = a - m.mean;
+        m.mean += dlt / m.n;
+        m.m2 += dlt * (a - m.mean);
     }
-    s = block_sum(s, scratch[0]);
-    ss = block_sum(ss, scratch[1]);
-    if (threadIdx.x == 0) partials[blockIdx.x] = make_double2(s, ss);
+    m = block_chan(m, scratch);
+    if (threadIdx.x == 0) partials[blockIdx.x] = make_double4(m.n, m.mean, m.m2, 0.0);
 }
 
-// fp64 mean of the vector from the partials' sums (.x), folded in a fixed order (every block gets the same bits).
-__device__ __forceinline__ double fold_mean(const double2* __restrict__ partials, int np, int64_t n) {
-    __shared__ double scratch[kBlock / kWave];
-    double s = 0.0;
-    for (int i = threadIdx.x; i < np; i += kBlock) s += partials[i].x;
-    s = block_sum(s, scratch);
-    return s / static_cast<double>(n);
-}
-
-// Second pass of the two-pass variance: block b (of the np blocks that wrote the sums) replaces partials[b].y with
-// sum over its grid-stride slice of (a - mean)^2 in fp64 (the first pass's sum of squares is not used: no
-// cancellation between sum(a^2) and n mean^2).
-__global__ __launch_bounds__(kBlock) void centered_sq_kernel(const float* __restrict__ x, int64_t n,
-                                                             double2* __restrict__ partials) {
-    __shared__ double scratch[kBlock / kWave];
-    const double mean = fold_mean(partials, gridDim.x, n);
-    double ss = 0.0;
-    const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
-    for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < n; i += stride) {
-        const double d = static_cast<double>(x[i]) - mean;
-        ss += d * d;
-    }
-    ss = block_sum(ss, scratch);
-    __syncthreads();  // every wave of this block has read partials[*].x (fold_mean) before .y is replaced
-    if (threadIdx.x == 0) partials[blockIdx.x].y = ss;
-}
-
-// Mean and unbiased std (torch.Tensor.std default, correction = 1) from the partials (.x sums, .y centred sums of
-// squares from centered_sq_kernel), in a fixed order.
-__device__ __forceinline__ void fold_moments(const double2* __restrict__ partials, int np, int64_t n,
+// Mean and unbiased std (torch.Tensor.std default, correction = 1) from the (count, mean, M2) partials, merged in a
+// fixed order (thread t takes partials t, t + 256; then the block tree): every block gets the same bits.
+__device__ __forceinline__ void fold_moments(const double4* __restrict__ partials, int np, int64_t n,
                                              float* mean_out, float* std_out) {
-    __shared__ double scratch[2][kBlock / kWave];
-    double s = 0.0, ss = 0.0;
+    __shared__ double scratch[kBlock / kWave][3];
+    Moments m{0.0, 0.0, 0.0};
     for (int i = threadIdx.x; i < np; i += kBlock) {
-        const double2 p = partials[i];
-        s += p.x;
-        ss += p.y;
+        const double4 p = partials[i];
+        m = chan(m, Moments{p.x, p.y, p.z});
     }
-    s = block_sum(s, scratch[0]);
-    ss = block_sum(ss, scratch[1]);
-    const double mean = s / static_cast<double>(n);
-    const double var = n > 1 ? ss / static_cast<double>(n - 1) : __builtin_nan("");  // torch: NaN std for one element
-    *mean_out = static_cast<float>(mean);
+    m = block_chan(m, scratch);
+    const double var = n > 1 ? m.m2 / static_cast<double>(n - 1) : __builtin_nan("");  // torch: NaN std for one element
+    *mean_out = static_cast<float>(m.mean);
     *std_out = static_cast<float>(sqrt(var));
 }
 
 __global__ __launch_bounds__(kBlock) void adv_normalize_kernel(float* __restrict__ adv, int64_t n,
-                                                               const double2* __restrict__ partials, int np,
+                                                               const double4* __restrict__ partials, int np,
                                                                float eps) {
     float mean, std;
     fold_moments(partials, np, n, &mean, &std);
@@ -188,7 +215,7 @@ __global__ __launch_bounds__(kBlock) void adv_normalize_kernel(float* __restrict
 // produces the final advantages is the one that places them, so no separate slot copy runs per update.  Two
 // consecutive lanes write one 32-byte slot (unit 0 the four scalars, unit 1 zeros): each slot leaves the store whole.
 __global__ __launch_bounds__(kBlock) void adv_normalize_slot_kernel(float* __restrict__ adv, int64_t n,
-                                                                    const double2* __restrict__ partials, int np,
+                                                                    const double4* __restrict__ partials, int np,
                                                                     float eps, const float* __restrict__ values,
                                                                     const float* __restrict__ logp,
                                                                     const float* __restrict__ returns,
@@ -214,7 +241,7 @@ __global__ __launch_bounds__(kBlock) void adv_normalize_slot_kernel(float* __res
 // are 32-byte pieces at the record stride (~1.6 TB/s: 49 us of the 72 us compute_returns at C3, profiles/r3_*).  The
 // mini-batch gather takes each row's slot from this array beside the record (rslrl_gather_records_side).
 __global__ __launch_bounds__(kBlock) void adv_normalize_slots_kernel(float* __restrict__ adv, int64_t n,
-                                                                     const double2* __restrict__ partials, int np,
+                                                                     const double4* __restrict__ partials, int np,
                                                                      float eps, const float* __restrict__ values,
                                                                      const float* __restrict__ logp,
                                                                      const float* __restrict__ returns,
@@ -238,7 +265,7 @@ int elementwise_blocks(int64_t n) {
 
 template <int TMAX>
 void launch_scan(int nb, hipStream_t st, const float* v, const float* r, const uint8_t* d, const float* lv,
-                 float g, float l, int T, int64_t N, float* ret, float* adv, double2* part) {
+                 float g, float l, int T, int64_t N, float* ret, float* adv, double4* part) {
     if (T == TMAX)
         hipLaunchKernelGGL((gae_scan_kernel<TMAX, true>), dim3(nb), dim3(kBlock), 0, st, v, r, d, lv, g, l, T, N, ret,
                            adv, part);
@@ -255,12 +282,12 @@ using namespace rslrl;
 extern "C" size_t rslrl_compute_returns_workspace_bytes(int64_t T, int64_t N) {
     (void)T;
     (void)N;
-    return sizeof(double2) * kMaxPartials;
+    return sizeof(double4) * kMaxPartials;
 }
 
 extern "C" size_t rslrl_normalize_workspace_bytes(int64_t n) {
     (void)n;
-    return sizeof(double2) * kMaxPartials;
+    return sizeof(double4) * kMaxPartials;
 }
 
 namespace {
@@ -279,12 +306,12 @@ int compute_returns_impl(const float* values, const float* rewards, const uint8_
     if (T < 0 || N < 0 || T > INT32_MAX) return RSLRL_E_INVALID_ARGUMENT;
     if (T == 0 || N == 0) return RSLRL_OK;
     if (!values || !rewards || !dones || !last_values || !returns || !advantages) return RSLRL_E_INVALID_ARGUMENT;
-    double2* part = nullptr;
+    double4* part = nullptr;
     if (normalize_advantage) {
         if (!workspace) return RSLRL_E_INVALID_ARGUMENT;
         if (workspace_bytes < rslrl_compute_returns_workspace_bytes(T, N)) return RSLRL_E_WORKSPACE_TOO_SMALL;
         if (reinterpret_cast<uintptr_t>(workspace) & 15) return RSLRL_E_MISALIGNED;
-        part = static_cast<double2*>(workspace);
+        part = static_cast<double4*>(workspace);
     }
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     const int nb = scan_blocks(N);
@@ -302,9 +329,6 @@ int compute_returns_impl(const float* values, const float* rewards, const uint8_
     int rc = launch_status();
     if (rc != RSLRL_OK || !normalize_advantage) return rc;
     const int64_t n = T * N;
-    hipLaunchKernelGGL(centered_sq_kernel, dim3(nb), dim3(kBlock), 0, st, advantages, n, part);
-    rc = launch_status();
-    if (rc != RSLRL_OK) return rc;
     if (slot && slot->record_floats == 0) {
         const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, kBlock), 4096));
         hipLaunchKernelGGL(adv_normalize_slots_kernel, dim3(static_cast<unsigned>(blocks)), dim3(kBlock), 0, st,
@@ -364,13 +388,10 @@ extern "C" int rslrl_normalize_advantages(float* advantages, int64_t n, float ep
     if (workspace_bytes < rslrl_normalize_workspace_bytes(n)) return RSLRL_E_WORKSPACE_TOO_SMALL;
     if (reinterpret_cast<uintptr_t>(workspace) & 15) return RSLRL_E_MISALIGNED;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    double2* part = static_cast<double2*>(workspace);
+    double4* part = static_cast<double4*>(workspace);
     const int nb = static_cast<int>(std::min<int64_t>(ceil_div(n, kBlock), kMaxPartials));
     hipLaunchKernelGGL(moments_kernel, dim3(nb), dim3(kBlock), 0, st, advantages, n, part);
     int rc = launch_status();
-    if (rc != RSLRL_OK) return rc;
-    hipLaunchKernelGGL(centered_sq_kernel, dim3(nb), dim3(kBlock), 0, st, advantages, n, part);
-    rc = launch_status();
     if (rc != RSLRL_OK) return rc;
     hipLaunchKernelGGL(adv_normalize_kernel, dim3(elementwise_blocks(n)), dim3(kBlock), 0, st, advantages, n, part,
                        nb, eps);

@@ -13,7 +13,7 @@
 //  1. the dZ tile sits in LDS as three bf16 planes (96 KiB, split once) for the whole tile;
 //  2. input gradient: wave w computes the output columns [32w, 32w + 32) of all 64 rows (2 MFMA blocks) over the
 //     16 k-chunks -- A fragments (dZ rows) from the resident planes, B fragments (the W^T image, L2-resident) straight
-//     from global memory two chunks ahead: no LDS writes and no barrier inside the main loop;
+//     from global memory one chunk ahead: no LDS writes and no barrier inside the main loop;
 //  3. epilogue: H (DMA'd into a 64 KiB LDS stage during the main loop) read in the accumulator layout, ELU', dZp
 //     stored (nontemporal);
 //  4. weight gradient: dW[n][k] += sum over the tile's rows of dZ[m][n] H[m][k] -- A = dZ^T from the resident planes
@@ -34,6 +34,8 @@
 // Every chunk offset (and the 8-row / 32-row steps) lands in the instructions' immediate offsets: a handful of
 // address registers for the whole tile.
 #include <algorithm>
+#include <cstdlib>
+#include <cstring>
 
 #include "common.h"
 #include "x6_split.h"
@@ -54,7 +56,7 @@ constexpr int kHbImgChunkU = 3 * kHbImgPlaneU;
 constexpr int kHbPartFloats = kHbW * kHbW + kHbW;  // a slice's partial row: [dW (256 x 256) | db (256)]
 constexpr int kHbMaxSlices = 128;               // per problem: a pair fills the 256 CUs with one workgroup each
 #ifndef RSLRL_HB_BDEPTH
-#define RSLRL_HB_BDEPTH 2
+#define RSLRL_HB_BDEPTH 1
 #endif
 constexpr int kHbBDepth = RSLRL_HB_BDEPTH;      // image chunks loaded ahead of the input gradient's MFMAs
 
@@ -94,10 +96,11 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t hb_tile_rsrc(const float* base
 }
 
 // the tile's dZ (8 float4 per thread: row (t >> 6) + 8 i, columns 4 (t & 63) .. + 3)
+template <int I0 = 0, int I1 = 8>
 __device__ __forceinline__ void hb_load_dz(__amdgpu_buffer_rsrc_t r, float4 (&v)[8]) {
     const int off = ((threadIdx.x >> 6) * kHbW + 4 * (threadIdx.x & 63)) * 4;
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+    for (int i = I0; i < I1; ++i)
         v[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, off, i * 8 * kHbW * 4, 0));
 }
 
@@ -120,7 +123,7 @@ __device__ __forceinline__ void hb_store_dz(const float4 (&v)[8], char* __restri
 
 // the tile's H rows into the stage: wave w DMAs rows w + 8 i (1 KiB each, 16 bytes per lane)
 __device__ __forceinline__ void hb_dma_h(__amdgpu_buffer_rsrc_t r, char* stage) {
-    const int wave = threadIdx.x >> 6;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int off = (wave * kHbW + 4 * (threadIdx.x & 63)) * 4;
 #pragma unroll
     for (int i = 0; i < 8; ++i)
@@ -144,6 +147,10 @@ __device__ __forceinline__ bf16x8 hb_read16(int addr) {
     return __builtin_bit_cast(bf16x8, *reinterpret_cast<const lds_u4*>(addr));
 }
 
+// BD: image chunks loaded ahead of the input gradient's MFMAs; LA: the LDS fragments of the next MFMA block read
+// ahead of the current block's MFMAs (1) or just before their own (0).  RSLRL_HB_VARIANT="BD,LA" picks an instance
+// per call (A/B in one process); default kHbBDepth, 1.
+template <int BD, int LA>
 __global__ __launch_bounds__(kHbThreads, 2) void hidden_bwd_kernel(HbArgs args) {
     __shared__ __attribute__((aligned(16))) char lds[kHbLds];
     char* const dzl = lds;
@@ -207,35 +214,38 @@ __global__ __launch_bounds__(kHbThreads, 2) void hidden_bwd_kernel(HbArgs args) 
     for (int t = t_begin; t < t_end; ++t) {
         const int64_t row0 = static_cast<int64_t>(t) * kHbT;
         const bool has_next = t + 1 < t_end;
-        // ---- input gradient main loop: dZ rows (LDS, resident) x W^T columns (global, two chunks ahead)
+        // ---- input gradient main loop: dZ rows (LDS, resident) x W^T columns (global, two chunks ahead).  Block
+        // b = 2 c + i is chunk c of row block i; the A fragments of block b + 1 are read while block b's MFMAs run.
         f32x16 acc[2] = {f32x16{}, f32x16{}};
-        uint4 bq[kHbBDepth + 1][3];  // ring of image chunks in flight (kHbBDepth ahead)
+        uint4 bq[BD + 1][3];  // ring of image chunks in flight (BD ahead)
 #pragma unroll
-        for (int c = 0; c < kHbBDepth; ++c)
+        for (int c = 0; c < BD; ++c)
 #pragma unroll
             for (int q = 0; q < 3; ++q) bq[c][q] = bload(c, q);
+        auto read_a = [&](int b, bf16x8 (&a)[3]) {
+            // hb_dz_off(32 i + l32, 16 c + 8 h) = lane part (by c & 3) + c * 2 KiB + i * 1 KiB: the constant in the
+            // immediate offset (plane 2 from a second base: the field holds 16 bits)
+            const int c = b >> 1, ci = c * kHbChunkB + (b & 1) * 1024;
+            a[0] = hb_read16(la[c & 3] + ci);
+            a[1] = hb_read16(la[c & 3] + ci + kHbPlane);
+            a[2] = hb_read16(la2[c & 3] + ci);
+        };
+        bf16x8 af[2][3];
+        if (LA) read_a(0, af[0]);
 #pragma unroll
-        for (int c = 0; c < kHbChunks; ++c) {
-            if (c + kHbBDepth < kHbChunks) {
+        for (int b = 0; b < 2 * kHbChunks; ++b) {
+            const int c = b >> 1;
+            if ((b & 1) == 0 && c + BD < kHbChunks) {
 #pragma unroll
-                for (int q = 0; q < 3; ++q)
-                    bq[(c + kHbBDepth) % (kHbBDepth + 1)][q] = bload(c + kHbBDepth, q);
+                for (int q = 0; q < 3; ++q) bq[(c + BD) % (BD + 1)][q] = bload(c + BD, q);
             }
-            bf16x8 b[3];
+            if (LA && b + 1 < 2 * kHbChunks) read_a(b + 1, af[(b + 1) & 1]);
+            if (!LA) read_a(b, af[b & 1]);
+            bf16x8 bf[3];
 #pragma unroll
-            for (int q = 0; q < 3; ++q) b[q] = __builtin_bit_cast(bf16x8, bq[c % (kHbBDepth + 1)][q]);
-#pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                // hb_dz_off(32 i + l32, 16 c + 8 h) = lane part (by c & 3) + c * 2 KiB + i * 1 KiB: the constant in the
-                // immediate offset (plane 2 from a second base: the field holds 16 bits)
-                const int ci = c * kHbChunkB + i * 1024;
-                bf16x8 a[3];
-                a[0] = hb_read16(la[c & 3] + ci);
-                a[1] = hb_read16(la[c & 3] + ci + kHbPlane);
-                a[2] = hb_read16(la2[c & 3] + ci);
-                acc[i] = mfma_x6(a, b, acc[i]);
-            }
-            __builtin_amdgcn_sched_barrier(0);  // one chunk's fragments live at a time (the 128 dW registers stay)
+            for (int q = 0; q < 3; ++q) bf[q] = __builtin_bit_cast(bf16x8, bq[c % (BD + 1)][q]);
+            acc[b & 1] = mfma_x6(af[b & 1], bf, acc[b & 1]);
+            __builtin_amdgcn_sched_barrier(0);  // two blocks' fragments live at a time (the 128 dW registers stay)
         }
         // ---- epilogue: H from the stage (this wave's DMA landed, then every wave's), ELU', dZp out
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -266,53 +276,53 @@ __global__ __launch_bounds__(kHbThreads, 2) void hidden_bwd_kernel(HbArgs args) 
                                                           (32 * i + 8 * (r >> 2)) * kHbW * 4, 2 /* nt */);
                 }
         }
-        __syncthreads();  // every wave has read the stage
-        if (has_next) hb_dma_h(hb_tile_rsrc(P.h, row0 + kHbT), stage);
         float4 vn[8];
-        // ---- weight gradient of the tile: dW[n][32 w + l32] += sum over rows of dZ[m][n] H[m][32 w + l32]
+        // ---- weight gradient of the tile: dW[n][32 w + l32] += sum over rows of dZ[m][n] H[m][32 w + l32].  Block
+        // k = 8 (2 i + st) + nb: row step (i, st), column block nb; the dZ^T fragments of block k + 1 are read while
+        // block k's MFMAs run.
+        auto read_t = [&](int k, bf16x8 (&a)[3]) {
+            // rows 32 i + 16 st + 4 h + tq (lo) and + 8 (hi), columns 32 nb + 16 g1 + 4 tp: lane part by (nb & 1,
+            // lo / hi), the rest constant
+            const int nb = k & 7, i = k >> 4, st = (k >> 3) & 1;
+            const int ci = 2 * (nb >> 1) * 2 * kHbChunkB + (32 * i + 16 * st) * 32;
+            const int b0 = lt[nb & 1][0] + ci, b1 = lt[nb & 1][1] + ci;
+            const int c0 = lt2[nb & 1][0] + ci, c1 = lt2[nb & 1][1] + ci;
+            a[0] = hb_cat(hb_tr(b0), hb_tr(b1));
+            a[1] = hb_cat(hb_tr(b0 + kHbPlane), hb_tr(b1 + kHbPlane));
+            a[2] = hb_cat(hb_tr(c0), hb_tr(c1));
+        };
+        bf16x8 tf[2][3];
+        bf16x8 hb[3];
+        if (LA) read_t(0, tf[0]);
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int st = 0; st < 2; ++st) {
-                if (i == 1 && st == 0) {
-                    // the next tile's dZ into registers behind the first half (H block 0 is dead by now: 32 registers
-                    // for the loads instead of 32 + 16), ~4 us before its use
-                    __builtin_amdgcn_sched_barrier(0);
-                    if (has_next) hb_load_dz(hb_tile_rsrc(P.dz, row0 + kHbT), vn);
-                    __builtin_amdgcn_sched_barrier(0);
-                }
+        for (int k = 0; k < 32; ++k) {
+            const int nb = k & 7, i = k >> 4, st = (k >> 3) & 1;
+            if (nb == 0) {
+                // the next tile's dZ into registers behind the first half, in two parts as the H rows die (block 0 of H
+                // is dead at k = 16, the first half of block 1 at k = 24): ~2-4 us before its use
+                if (k == 16 && has_next) hb_load_dz<0, 4>(hb_tile_rsrc(P.dz, row0 + kHbT), vn);
+                if (k == 24 && has_next) hb_load_dz<4, 8>(hb_tile_rsrc(P.dz, row0 + kHbT), vn);
                 // B = H rows pi(8 h + t) of column 32 w + l32: accumulator entries r = 8 st + t of block i
-                bf16x8 hb[3];
-                {
-                    uint32_t p0[4], p1[4], p2[4];
+                uint32_t p0[4], p1[4], p2[4];
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        float x = hr[i][8 * st + 2 * j], y = hr[i][8 * st + 2 * j + 1];
-                        p0[j] = split_pair(x, y);
-                        p1[j] = split_pair(x, y);
-                        p2[j] = pack_pair(x, y);
-                    }
-                    hb[0] = __builtin_bit_cast(bf16x8, make_uint4(p0[0], p0[1], p0[2], p0[3]));
-                    hb[1] = __builtin_bit_cast(bf16x8, make_uint4(p1[0], p1[1], p1[2], p1[3]));
-                    hb[2] = __builtin_bit_cast(bf16x8, make_uint4(p2[0], p2[1], p2[2], p2[3]));
+                for (int j = 0; j < 4; ++j) {
+                    float x = hr[i][8 * st + 2 * j], y = hr[i][8 * st + 2 * j + 1];
+                    p0[j] = split_pair(x, y);
+                    p1[j] = split_pair(x, y);
+                    p2[j] = pack_pair(x, y);
                 }
-#pragma unroll
-                for (int nb = 0; nb < 8; ++nb) {
-                    // rows 32 i + 16 st + 4 h + tq (lo) and + 8 (hi), columns 32 nb + 16 g1 + 4 tp: lane part by
-                    // (nb & 1, lo / hi), the rest constant
-                    const int ci = 2 * (nb >> 1) * 2 * kHbChunkB + (32 * i + 16 * st) * 32;
-                    const int b0 = lt[nb & 1][0] + ci, b1 = lt[nb & 1][1] + ci;
-                    const int c0 = lt2[nb & 1][0] + ci, c1 = lt2[nb & 1][1] + ci;
-                    bf16x8 a[3];
-                    a[0] = hb_cat(hb_tr(b0), hb_tr(b1));
-                    a[1] = hb_cat(hb_tr(b0 + kHbPlane), hb_tr(b1 + kHbPlane));
-                    a[2] = hb_cat(hb_tr(c0), hb_tr(c1));
-                    dw[nb] = mfma_x6(a, hb, dw[nb]);
-                    __builtin_amdgcn_sched_barrier(0);
-                }
+                hb[0] = __builtin_bit_cast(bf16x8, make_uint4(p0[0], p0[1], p0[2], p0[3]));
+                hb[1] = __builtin_bit_cast(bf16x8, make_uint4(p1[0], p1[1], p1[2], p1[3]));
+                hb[2] = __builtin_bit_cast(bf16x8, make_uint4(p2[0], p2[1], p2[2], p2[3]));
             }
-        __syncthreads();  // every wave has read the dZ planes
+            if (LA && k + 1 < 32) read_t(k + 1, tf[(k + 1) & 1]);
+            if (!LA) read_t(k, tf[k & 1]);
+            dw[nb] = mfma_x6(tf[k & 1], hb, dw[nb]);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        __syncthreads();  // every wave has read the dZ planes (and, in the epilogue, the H stage)
         if (has_next) {
+            hb_dma_h(hb_tile_rsrc(P.h, row0 + kHbT), stage);  // lands during the split and the next main loop
             hb_store_dz(vn, dzl, csum);
             __syncthreads();
         }
@@ -381,6 +391,19 @@ extern "C" int rslrl_hidden_bwd_pair(const rslrl_hidden_bwd_problem_t* p0, const
     args.tiles = static_cast<int>(tiles);
     args.tiles_per = static_cast<int>(per);
     const dim3 grid(static_cast<unsigned>(ceil_div(tiles, per)), static_cast<unsigned>(n));
-    hipLaunchKernelGGL(hidden_bwd_kernel, grid, dim3(kHbThreads), 0, reinterpret_cast<hipStream_t>(stream), args);
+    int bd = kHbBDepth, la = 0;
+    if (const char* e = std::getenv("RSLRL_HB_VARIANT")) {  // "BD,LA" (A/B builds in one process)
+        bd = std::atoi(e);
+        const char* c = std::strchr(e, ',');
+        la = c ? std::atoi(c + 1) : 0;
+    }
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const dim3 blk(kHbThreads);
+    // measured at 393,216 rows (scripts/hidden_bwd_probe.py --variants, one process): BD,LA = 1,0 1067 us, 1,1 1094,
+    // 2,0 1110, 2,1 1127, 3,1 1216 -- the fewer registers live, the faster (3,1 spills 37 VGPRs)
+    if (bd == 2 && la == 0) hipLaunchKernelGGL((hidden_bwd_kernel<2, 0>), grid, blk, 0, st, args);
+    else if (bd == 2) hipLaunchKernelGGL((hidden_bwd_kernel<2, 1>), grid, blk, 0, st, args);
+    else if (la == 1) hipLaunchKernelGGL((hidden_bwd_kernel<1, 1>), grid, blk, 0, st, args);
+    else hipLaunchKernelGGL((hidden_bwd_kernel<1, 0>), grid, blk, 0, st, args);
     return launch_status();
 }

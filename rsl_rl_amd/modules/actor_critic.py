@@ -209,13 +209,16 @@ class ActorCritic(nn.Module):
             return dy[:, :A], dy[:, A:]
         return torch.empty(B, A, device=mean.device, dtype=torch.float32), None
 
-    def train_backward(self, tape, g_mean, g_sigma, g_value, std, slot, side_stream=None, g_value_padded=None):
+    def train_backward(self, tape, g_mean, g_sigma, g_value, std, slot, side_stream=None, g_value_padded=None,
+                       on_early=None):
         """Backward of train_forward given the loss gradients w.r.t. (mean, sigma, value), written into the
         gradient slots `slot(param)` (a gradient arena).  g_sigma: for the shared std the [A] gradient w.r.t.
         sigma (for log_std it is chained through exp here); for a state-dependent head the half of the actor-output
         gradient buffer (train_grad_buffers) the loss kernel wrote.  side_stream: as in train_forward (the
         critic's backward runs there; the current stream waits for it before returning).  g_value_padded: a zero-padded
-        [B, 4] buffer whose column 0 is g_value (the loss kernel wrote it there), or None."""
+        [B, 4] buffer whose column 0 is g_value (the loss kernel wrote it there), or None.  on_early: called once the
+        gradients of every layer but the first of both networks are enqueued (PPO starts their all-reduce there); on
+        the paths that do not split the backward it is called at the end."""
         tape_a, tape_c, y_shape, paired = tape
         if self.state_dependent_std:
             dy = torch.as_strided(g_mean, y_shape, (y_shape[1], 1))  # the [B, 2A] buffer behind both halves
@@ -234,13 +237,16 @@ class ActorCritic(nn.Module):
         if side_stream is None:
             if paired and g_value_padded is None:
                 outs = [[(slot(w), slot(b)) for w, b in zip(*self._linears(m))] for m in (self.actor, self.critic)]
-                if fused_mlp.train_backward_pair(tape_a, dy, outs[0], tape_c, g_value.reshape(-1, 1), outs[1]):
+                if fused_mlp.train_backward_pair(tape_a, dy, outs[0], tape_c, g_value.reshape(-1, 1), outs[1],
+                                                 on_early=on_early):
                     return
             if tape_c.head is not None:
                 raise RuntimeError("train_backward: the critic's head ran fused (value_head) but the paired backward "
                                    "does not apply to these gradient destinations")
             run(self.actor, tape_a, dy)
             run(self.critic, tape_c, g_value.reshape(-1, 1), g_value_padded)
+            if on_early is not None:
+                on_early()
             return
         main = torch.cuda.current_stream(dy.device)
         side_stream.wait_stream(main)
@@ -249,6 +255,8 @@ class ActorCritic(nn.Module):
             run(self.critic, tape_c, g_value.reshape(-1, 1), g_value_padded)
         run(self.actor, tape_a, dy)
         main.wait_stream(side_stream)
+        if on_early is not None:
+            on_early()
 
     def act(self, obs, **kwargs):
         obs = self.actor_obs_normalizer(self.get_actor_obs(obs))

@@ -1054,13 +1054,14 @@ def train_forward_pair(x_a, ws_a, bs_a, x_c, ws_c, bs_c, value_head: ValueHead |
     return y[0], tapes[0], y[1], tapes[1]
 
 
-def train_backward_pair(tape_a, dy_a, outs_a, tape_c, dy_c, outs_c):
+def train_backward_pair(tape_a, dy_a, outs_a, tape_c, dy_c, outs_c, on_early=None):
     """train_backward of two passes of train_forward_pair, gradients into outs_* (per layer (dW, db) destinations,
     as train_backward's outs): the output layers as two fused launches, then per hidden layer the two weight
     gradients (rslrl_linear_wgrad_bias_pair) and the two input gradients (rslrl_linear_gemm_pair) in one launch each.
     Input gradients are bit-identical to two train_backward calls; a weight gradient's fp32 slice partials cover
     twice the rows (half the slices), so its rounding differs within fp32 accumulation error.  Returns False (nothing
-    done) when the tapes do not qualify."""
+    done) when the tapes do not qualify.  on_early: called after every layer's gradient but the first layers' is
+    enqueued (their folds run first, in a launch of their own) -- a multi-GPU update starts its all-reduce there."""
     tapes, dys, outs = (tape_a, tape_c), (dy_a, dy_c), (outs_a, outs_c)
     L = len(tape_a.ws)
     if not (tape_a.x6 and tape_c.x6 and not any(tape_a.h3) and not any(tape_c.h3) and len(tape_c.ws) == L
@@ -1122,6 +1123,10 @@ def train_backward_pair(tape_a, dy_a, outs_a, tape_c, dy_c, outs_c):
             else:
                 dz = dz_next
         else:  # first layer: (x^T dz)^T on the 64-row tiles, the bias from dz (the kernel's K side)
+            if on_early is not None:
+                folds.run(dz[0].device)  # every other layer's gradient complete in the arena
+                on_early()
+                on_early = None
             pad = (-K) % 4
             xp = [F.pad(x, (0, pad)) if pad else x for x in h_in]
             dwb_outs = []
@@ -1137,6 +1142,8 @@ def train_backward_pair(tape_a, dy_a, outs_a, tape_c, dy_c, outs_c):
                         torch._foreach_copy_(list(o), [dwt[:, :K] if not pad else dwt[:K].t(), db])
                     folds.after.append(copy)
     folds.run(dz[0].device)
+    if on_early is not None:
+        on_early()
     return True
 
 

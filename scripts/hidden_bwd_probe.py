@@ -37,6 +37,7 @@ def main():
     ap.add_argument("--only", choices=["fused", "separate"], help="launch only this form --iters times (profiling)")
     ap.add_argument("--iters", type=int, default=6)
     ap.add_argument("--M", type=int, default=0)
+    ap.add_argument("--variants", default="", help="comma-separated RSLRL_HB_VARIANT values 'BD:LA' timed in turn")
     args = ap.parse_args()
     out = {}
     rounds = int(os.environ.get("PROBE_ROUNDS", "3"))
@@ -69,10 +70,17 @@ def main():
             torch.cuda.synchronize()
             continue
         res = {"fused": [], "separate": [], "fused_kernel_only": []}
+        variants = [v.replace(":", ",") for v in args.variants.split(",") if v]
+        for v in variants:
+            res["variant " + v] = []
         for _ in range(rounds):
             res["fused"] += timed(fused, 10)
             res["separate"] += timed(separate, 10)
             res["fused_kernel_only"] += timed(kern_fused, 10)
+            for v in variants:
+                os.environ["RSLRL_HB_VARIANT"] = v
+                res["variant " + v] += timed(kern_fused, 10)
+                os.environ.pop("RSLRL_HB_VARIANT")
         out[M] = {k: {"median_us": round(sorted(v)[len(v) // 2], 1), "min_us": round(min(v), 1)} for k, v in res.items()}
         del p, dzs, hs, imgs
         torch.cuda.empty_cache()

@@ -76,8 +76,9 @@ def test_update_c3_matches_reference(golden_meta, cuda_device, monkeypatch):
     del nz
     with torch.inference_mode():
         alg.compute_returns({"policy": torch.from_numpy(last_obs).to(dev)})
-    # GAE is bit-exact with the reference; the normalised advantages within fp32 rounding of its statistics
-    assert torch.equal(st.returns[:2, :256].cpu(), torch.from_numpy(z["returns_head"]))
+    # the bootstrap values of the last step come from our critic's forward (x6, fp32-faithful, not the CPU GEMM's
+    # bits), so the returns agree within fp32 rounding (GAE itself is bit-exact: tests/test_gpu_gae.py)
+    assert torch.allclose(st.returns[:2, :256].cpu(), torch.from_numpy(z["returns_head"]), rtol=1e-5, atol=1e-6)
     assert torch.allclose(st.advantages[:2, :256].cpu(), torch.from_numpy(z["advantages_head"]), rtol=1e-5, atol=1e-6)
     torch.default_generator.set_state(torch.from_numpy(z["gen_state"].copy()))
 

@@ -62,6 +62,25 @@ def _worker(rank, port, out_dir):
         ppo.reduce_parameters()
         res["arena_grads2"] = [p.grad.clone() for p in ppo.policy.parameters()]
 
+        # the overlapped form of update(): the early prefix (every Linear but the first of actor and critic) handed
+        # to an asynchronous all-reduce during the backward, the rest (+ the KL) reduced after it
+        for i, p in enumerate(ppo.policy.parameters()):
+            p.grad.copy_(torch.full_like(p, float(rank + 1) * (i + 3)))
+        arena.extra[:1].fill_(0.005 if rank == 0 else 0.001)
+        work = dist.all_reduce(arena.flat[:arena.early_numel], op=dist.ReduceOp.SUM, async_op=True)
+        ppo._all_reduce_arena(arena, with_kl=True, skip=arena.early_numel, pending=[work])
+        res["split_grads"] = [p.grad.clone() for p in ppo.policy.parameters()]
+        res["split_kl"] = arena.extra[0].item()
+        early = {id(p) for p in ppo._early_params()}
+        res["early_numel"] = arena.early_numel
+        res["early_in_prefix"] = all(
+            (arena.slot(p).data_ptr() - arena.flat.data_ptr()) // 4 + p.numel() <= arena.early_numel
+            for p in ppo.policy.parameters() if id(p) in early)
+        res["late_after_prefix"] = all(
+            (arena.slot(p).data_ptr() - arena.flat.data_ptr()) // 4 >= arena.early_numel
+            for p in ppo.policy.parameters() if id(p) not in early)
+        res["early_count"] = len(early)
+
         # reference cat path (grads not backed by the arena), with the KL appended to the concatenation
         for i, p in enumerate(ppo.policy.parameters()):
             p.grad = torch.full_like(p, float(rank + 1) * (i + 2))
@@ -103,6 +122,20 @@ def test_arena_allreduce(results):
             assert torch.all(g == (1 + 2) * (i + 1) / WORLD)  # identical inputs on both ranks: unchanged
         assert r["arena_kl"] == torch.tensor((0.003 + 0.001) / WORLD, dtype=torch.float32).item()
     for a, b in zip(results[0]["arena_grads"], results[1]["arena_grads"]):
+        assert torch.equal(a, b)
+
+
+def test_overlapped_arena_allreduce(results):
+    """The early-prefix all-reduce (overlapping the first layers' backward in update()) + the rest: the same averaged
+    gradients and KL as one all-reduce of the whole arena, identical on every rank; the prefix holds exactly the
+    early parameters (4 per network here: the second Linear's weight and bias of actor and critic)."""
+    for r in results:
+        assert r["early_count"] == 4 and r["early_numel"] > 0
+        assert r["early_in_prefix"] and r["late_after_prefix"]
+        for i, g in enumerate(r["split_grads"]):
+            assert torch.all(g == (1 + 2) * (i + 3) / WORLD)
+        assert r["split_kl"] == torch.tensor((0.005 + 0.001) / WORLD, dtype=torch.float32).item()
+    for a, b in zip(results[0]["split_grads"], results[1]["split_grads"]):
         assert torch.equal(a, b)
 
 
