@@ -61,6 +61,7 @@ constexpr int kHbMaxSlices = 128;               // per problem: a pair fills the
 constexpr int kHbBDepth = RSLRL_HB_BDEPTH;      // image chunks loaded ahead of the input gradient's MFMAs
 
 using s16x4 = __attribute__((ext_vector_type(4))) short;
+using u32x4 = __attribute__((ext_vector_type(4))) unsigned int;
 
 struct HbProblem {
     const float* dz;   // [M, 256]
@@ -147,10 +148,26 @@ __device__ __forceinline__ bf16x8 hb_read16(int addr) {
     return __builtin_bit_cast(bf16x8, *reinterpret_cast<const lds_u4*>(addr));
 }
 
+#ifdef RSLRL_HB_STAMPS
+// diagnostic build only (never the shipped library): per workgroup, tile and wave, s_memtime at 7 phase points ->
+// g_hb_stamps[((wg * tiles_per + tile) * 8 + wave) * 8 + k]; the values go to this buffer alone (scripts/hb_stamps.py)
+__device__ uint64_t* g_hb_stamps;
+#define HB_STAMP(k)                                                                                          \
+    do {                                                                                                     \
+        if (g_hb_stamps && (threadIdx.x & 63) == 0)                                                          \
+            g_hb_stamps[((static_cast<int64_t>(blockIdx.y * gridDim.x + blockIdx.x) * args.tiles_per + (t - t_begin)) * 8 + \
+                         (threadIdx.x >> 6)) * 8 + (k)] = __builtin_amdgcn_s_memtime();                     \
+    } while (0)
+#else
+#define HB_STAMP(k) \
+    do {            \
+    } while (0)
+#endif
+
 // BD: image chunks loaded ahead of the input gradient's MFMAs; LA: the LDS fragments of the next MFMA block read
 // ahead of the current block's MFMAs (1) or just before their own (0).  RSLRL_HB_VARIANT="BD,LA" picks an instance
 // per call (A/B in one process); default kHbBDepth, 1.
-template <int BD, int LA>
+template <int BD, int LA, int PRIO = 0>
 __global__ __launch_bounds__(kHbThreads, 2) void hidden_bwd_kernel(HbArgs args) {
     __shared__ __attribute__((aligned(16))) char lds[kHbLds];
     char* const dzl = lds;
@@ -162,6 +179,9 @@ __global__ __launch_bounds__(kHbThreads, 2) void hidden_bwd_kernel(HbArgs args) 
 
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if constexpr (PRIO) {  // static priority for the second-dispatched half (MI355X_MICROARCH.md, two waves per SIMD)
+        if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+    }
     const int h = lane >> 5;
     const int l32 = lane & 31;
     const int g1 = (lane >> 4) & 1;  // transposed reads: which 16 of a block's 32 columns
@@ -214,6 +234,7 @@ __global__ __launch_bounds__(kHbThreads, 2) void hidden_bwd_kernel(HbArgs args) 
     for (int t = t_begin; t < t_end; ++t) {
         const int64_t row0 = static_cast<int64_t>(t) * kHbT;
         const bool has_next = t + 1 < t_end;
+        HB_STAMP(0);
         // ---- input gradient main loop: dZ rows (LDS, resident) x W^T columns (global, two chunks ahead).  Block
         // b = 2 c + i is chunk c of row block i; the A fragments of block b + 1 are read while block b's MFMAs run.
         f32x16 acc[2] = {f32x16{}, f32x16{}};
@@ -248,35 +269,49 @@ __global__ __launch_bounds__(kHbThreads, 2) void hidden_bwd_kernel(HbArgs args) 
             __builtin_amdgcn_sched_barrier(0);  // two blocks' fragments live at a time (the 128 dW registers stay)
         }
         // ---- epilogue: H from the stage (this wave's DMA landed, then every wave's), ELU', dZp out
+        HB_STAMP(1);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
+        HB_STAMP(2);
         float hr[2][16];
         {
-            const float* hs = reinterpret_cast<const float*>(stage) + 32 * wave + l32;
+            // H in the accumulator layout from this wave's columns of the stage; dZp = acc * ELU'(H)
+            // (epilogue_tiles_impl's bits) written back over the same stage words (only this wave reads them), then
+            // read row-contiguous and stored as 16-byte units: 8 stores per lane instead of 32 4-byte ones (the
+            // epilogue runs while no wave of the CU issues MFMAs)
+            float* hs = reinterpret_cast<float*>(stage) + 32 * wave + l32;
 #pragma unroll
             for (int i = 0; i < 2; ++i)
 #pragma unroll
                 for (int r = 0; r < 16; ++r) hr[i][r] = hs[(32 * i + 4 * h + (r & 3) + 8 * (r >> 2)) * kHbW];
-        }
-        {
-            // buffer resource over the tile's rows of this wave's columns: the 8-row group step in soffset, the row in
-            // the immediate (no per-store address arithmetic)
-            const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
-                P.dz_prev + row0 * kHbW + 32 * wave, 0, static_cast<uint32_t>(kHbT * kHbW * 4), 0x00020000);
 #pragma unroll
             for (int i = 0; i < 2; ++i)
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     const float v = acc[i][r];
                     const float hv = hr[i][r];
-                    const float g = v * (hv + 1.f);  // ELU'(z) = 1 if z > 0 else h + 1 (epilogue_tiles_impl's bits)
-                    const float o = hv > 0.f ? v : g;
-                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, o), rc,
-                                                          ((4 * h + (r & 3)) * kHbW + l32) * 4,
-                                                          (32 * i + 8 * (r >> 2)) * kHbW * 4, 2 /* nt */);
+                    const float g = v * (hv + 1.f);  // ELU'(z) = 1 if z > 0 else h + 1
+                    hs[(32 * i + 4 * h + (r & 3) + 8 * (r >> 2)) * kHbW] = hv > 0.f ? v : g;
                 }
+            // the dword writes retire before the 16-byte reads (the LDS does not keep that order by itself)
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
+                P.dz_prev + row0 * kHbW + 32 * wave, 0, static_cast<uint32_t>(kHbT * kHbW * 4), kHbRsrcFlags);
+            const float* rs = reinterpret_cast<const float*>(stage) + 32 * wave + 4 * (lane & 7);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int row = 8 * j + (lane >> 3);
+                const u32x4 sv = *reinterpret_cast<const u32x4*>(rs + row * kHbW);
+                __builtin_amdgcn_raw_buffer_store_b128(sv, rc, ((lane >> 3) * kHbW + 4 * (lane & 7)) * 4,
+                                                       8 * j * kHbW * 4, 2 /* nt */);
+                // VMEM store-data hazard (mlp_gemm.hip epilogue_tiles_staged): keep the data registers live past wait
+                // states of their own after the 16-byte store
+                asm volatile("s_nop 3" ::"v"(sv) : "memory");
+            }
         }
         float4 vn[8];
+        uint2 pl[8][3];  // the next tile's dZ units as bf16 planes
+        HB_STAMP(3);
         // ---- weight gradient of the tile: dW[n][32 w + l32] += sum over rows of dZ[m][n] H[m][32 w + l32].  Block
         // k = 8 (2 i + st) + nb: row step (i, st), column block nb; the dZ^T fragments of block k + 1 are read while
         // block k's MFMAs run.
@@ -298,10 +333,6 @@ __global__ __launch_bounds__(kHbThreads, 2) void hidden_bwd_kernel(HbArgs args) 
         for (int k = 0; k < 32; ++k) {
             const int nb = k & 7, i = k >> 4, st = (k >> 3) & 1;
             if (nb == 0) {
-                // the next tile's dZ into registers behind the first half, in two parts as the H rows die (block 0 of H
-                // is dead at k = 16, the first half of block 1 at k = 24): ~2-4 us before its use
-                if (k == 16 && has_next) hb_load_dz<0, 4>(hb_tile_rsrc(P.dz, row0 + kHbT), vn);
-                if (k == 24 && has_next) hb_load_dz<4, 8>(hb_tile_rsrc(P.dz, row0 + kHbT), vn);
                 // B = H rows pi(8 h + t) of column 32 w + l32: accumulator entries r = 8 st + t of block i
                 uint32_t p0[4], p1[4], p2[4];
 #pragma unroll
@@ -314,18 +345,32 @@ __global__ __launch_bounds__(kHbThreads, 2) void hidden_bwd_kernel(HbArgs args) 
                 hb[0] = __builtin_bit_cast(bf16x8, make_uint4(p0[0], p0[1], p0[2], p0[3]));
                 hb[1] = __builtin_bit_cast(bf16x8, make_uint4(p1[0], p1[1], p1[2], p1[3]));
                 hb[2] = __builtin_bit_cast(bf16x8, make_uint4(p2[0], p2[1], p2[2], p2[3]));
+                // the next tile's dZ into registers once H block 0 is dead (~8 blocks of MFMAs before its split into
+                // bf16 planes at k = 16 .. 23, beside the MFMAs: the phase after the loop only writes them to LDS)
+                if (k == 8 && has_next) hb_load_dz(hb_tile_rsrc(P.dz, row0 + kHbT), vn);
             }
             if (LA && k + 1 < 32) read_t(k + 1, tf[(k + 1) & 1]);
             if (!LA) read_t(k, tf[k & 1]);
             dw[nb] = mfma_x6(tf[k & 1], hb, dw[nb]);
+            if (false) {
+                const int u = k - 16;
+                csum.x += vn[u].x;
+                csum.y += vn[u].y;
+                csum.z += vn[u].z;
+                csum.w += vn[u].w;
+                split4(vn[u], pl[u][0], pl[u][1], pl[u][2]);
+            }
             __builtin_amdgcn_sched_barrier(0);
         }
+        HB_STAMP(4);
         __syncthreads();  // every wave has read the dZ planes (and, in the epilogue, the H stage)
+        HB_STAMP(5);
         if (has_next) {
-            hb_dma_h(hb_tile_rsrc(P.h, row0 + kHbT), stage);  // lands during the split and the next main loop
+            hb_dma_h(hb_tile_rsrc(P.h, row0 + kHbT), stage);  // lands during the next main loop
             hb_store_dz(vn, dzl, csum);
             __syncthreads();
         }
+        HB_STAMP(6);
     }
 
     // ---- the slice's partial row: dW (lane: column 32 w + l32 of rows 32 nb + (r & 3) + 8 (r >> 2) + 4 h), then db
@@ -361,6 +406,13 @@ int64_t hb_tiles_per(int64_t tiles) {
 }  // namespace rslrl
 
 using namespace rslrl;
+
+#ifdef RSLRL_HB_STAMPS
+extern "C" int rslrl_hb_debug_stamps(void* buf) {  // diagnostic build only
+    uint64_t* p = static_cast<uint64_t*>(buf);
+    return static_cast<int>(hipMemcpyToSymbol(HIP_SYMBOL(g_hb_stamps), &p, sizeof(p)));
+}
+#endif
 
 extern "C" int64_t rslrl_hidden_bwd_slices(int64_t M) {
     if (M < kHbT || M % kHbT || M / kHbT > INT32_MAX) return 0;
@@ -404,6 +456,8 @@ extern "C" int rslrl_hidden_bwd_pair(const rslrl_hidden_bwd_problem_t* p0, const
     if (bd == 2 && la == 0) hipLaunchKernelGGL((hidden_bwd_kernel<2, 0>), grid, blk, 0, st, args);
     else if (bd == 2) hipLaunchKernelGGL((hidden_bwd_kernel<2, 1>), grid, blk, 0, st, args);
     else if (la == 1) hipLaunchKernelGGL((hidden_bwd_kernel<1, 1>), grid, blk, 0, st, args);
+    else if (la == 2) hipLaunchKernelGGL((hidden_bwd_kernel<1, 0, 1>), grid, blk, 0, st, args);  // LA 2: prio
+    else if (la == 3) hipLaunchKernelGGL((hidden_bwd_kernel<1, 1, 1>), grid, blk, 0, st, args);
     else hipLaunchKernelGGL((hidden_bwd_kernel<1, 0>), grid, blk, 0, st, args);
     return launch_status();
 }
