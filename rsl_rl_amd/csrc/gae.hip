@@ -250,7 +250,31 @@ __global__ __launch_bounds__(kBlock) void adv_normalize_slots_kernel(float* __re
     fold_moments(partials, np, n, &mean, &std);
     const float denom = __fadd_rn(std, eps);  // rollout_storage.py:149  (std + 1e-8)
     const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
-    for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < n; i += stride) {
+    const int64_t tid = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    // four env-steps per thread and iteration (16-byte loads of the four sources, 64 contiguous bytes of slots), so a
+    // grid of a few blocks per CU covers the rollout and the partial fold above runs once per block, not per 256
+    // elements; the scalar loop takes the tail (and every element when a source is not 16-byte aligned)
+    const bool vec = ((reinterpret_cast<uintptr_t>(adv) | reinterpret_cast<uintptr_t>(values) |
+                       reinterpret_cast<uintptr_t>(logp) | reinterpret_cast<uintptr_t>(returns)) & 15) == 0;
+    const int64_t nvec = vec ? n / 4 : 0;
+    for (int64_t i = tid; i < nvec; i += stride) {
+        const float4 a4 = reinterpret_cast<const float4*>(adv)[i];
+        const float4 v4 = reinterpret_cast<const float4*>(values)[i];
+        const float4 l4 = reinterpret_cast<const float4*>(logp)[i];
+        const float4 r4 = reinterpret_cast<const float4*>(returns)[i];
+        float4 o;
+        o.x = __fdiv_rn(__fsub_rn(a4.x, mean), denom);
+        o.y = __fdiv_rn(__fsub_rn(a4.y, mean), denom);
+        o.z = __fdiv_rn(__fsub_rn(a4.z, mean), denom);
+        o.w = __fdiv_rn(__fsub_rn(a4.w, mean), denom);
+        reinterpret_cast<float4*>(adv)[i] = o;
+        float4* s = slots + 4 * i;
+        s[0] = make_float4(v4.x, l4.x, r4.x, o.x);
+        s[1] = make_float4(v4.y, l4.y, r4.y, o.y);
+        s[2] = make_float4(v4.z, l4.z, r4.z, o.z);
+        s[3] = make_float4(v4.w, l4.w, r4.w, o.w);
+    }
+    for (int64_t i = nvec * 4 + tid; i < n; i += stride) {
         const float a = __fdiv_rn(__fsub_rn(adv[i], mean), denom);
         adv[i] = a;
         slots[i] = make_float4(values[i], logp[i], returns[i], a);
@@ -330,7 +354,7 @@ int compute_returns_impl(const float* values, const float* rewards, const uint8_
     if (rc != RSLRL_OK || !normalize_advantage) return rc;
     const int64_t n = T * N;
     if (slot && slot->record_floats == 0) {
-        const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, kBlock), 4096));
+        const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, 4 * kBlock), 1024));
         hipLaunchKernelGGL(adv_normalize_slots_kernel, dim3(static_cast<unsigned>(blocks)), dim3(kBlock), 0, st,
                            advantages, n, part, nb, 1e-8f, values, slot->log_prob, returns,
                            reinterpret_cast<float4*>(slot->records));

@@ -14,14 +14,16 @@
 //  2. input gradient: wave w computes the output columns [32w, 32w + 32) of all 64 rows (2 MFMA blocks) over the
 //     16 k-chunks -- A fragments (dZ rows) from the resident planes, B fragments (the W^T image, L2-resident) straight
 //     from global memory one chunk ahead: no LDS writes and no barrier inside the main loop;
-//  3. epilogue: H (DMA'd into a 64 KiB LDS stage during the main loop) read in the accumulator layout, ELU', dZp
-//     stored (nontemporal);
+//  3. epilogue: H read in the accumulator layout from the wave's own 8 KiB region of a 64 KiB LDS stage (each wave
+//     DMAs exactly the H columns it needs, so the epilogue waits for its own loads only: no workgroup barrier between
+//     the two GEMMs, and waves that finish the main loop early run their epilogue beside the others' MFMAs), ELU',
+//     dZp stored (nontemporal); the next tile's H is DMA'd into the region right after;
 //  4. weight gradient: dW[n][k] += sum over the tile's rows of dZ[m][n] H[m][k] -- A = dZ^T from the resident planes
 //     by ds_read_b64_tr_b16, B = H straight from the epilogue's registers: the accumulator layout holds, per lane,
 //     column k at rows (r & 3) + 8 (r >> 2) + 4 (lane >> 5), so each 16-deep MFMA step takes the reduction rows in
 //     the permuted order pi(8 h + t) = 16 s + 4 h + (t & 3) + 8 (t >> 2) -- the same order for the dZ^T fragments
 //     (the transposed reads address exactly those rows), i.e. the same sum over the tile's rows;
-//  5. meanwhile the next tile's dZ is loaded into registers and its H DMA'd into the (then free) stage.
+//  5. meanwhile the next tile's dZ is loaded into registers (split into the planes after a barrier: 2 per tile).
 // The column sums of dZ (db) accumulate in fp32 from the staged registers (every thread owns four fixed columns) and
 // fold over the 8 waves in wave order at the end.  Deterministic: the summation order depends on M alone.
 //
@@ -122,14 +124,23 @@ __device__ __forceinline__ void hb_store_dz(const float4 (&v)[8], char* __restri
     }
 }
 
-// the tile's H rows into the stage: wave w DMAs rows w + 8 i (1 KiB each, 16 bytes per lane)
+// H stage: wave w owns the 8 KiB region [64 row slots][32 columns] of its columns [32 w, 32 w + 32) -- the only H
+// the wave's epilogue reads, so no other wave's DMA is waited for.  Row r sits in slot r ^ ((r >> 2) & 1): rows r and
+// r + 4 (the two lane halves of one accumulator-layout read) land on opposite 32-bank halves.
+constexpr int kHbHRegion = kHbT * 32 * 4;  // 8 KiB
+__device__ __forceinline__ int hb_hslot(int r) { return r ^ ((r >> 2) & 1); }
+
+// the tile's H columns of this wave into its region: instruction i fills slots 8 i .. 8 i + 7 (lane l: slot 8 i + l / 8,
+// 16 bytes of column quad l % 8)
 __device__ __forceinline__ void hb_dma_h(__amdgpu_buffer_rsrc_t r, char* stage) {
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int off = (wave * kHbW + 4 * (threadIdx.x & 63)) * 4;
+    const int lane = threadIdx.x & 63;
+    const int off = (hb_hslot(lane >> 3) * kHbW + 32 * wave + 4 * (lane & 7)) * 4;  // slot ^ row differ in bit 0 only
 #pragma unroll
     for (int i = 0; i < 8; ++i)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)(stage + (wave + 8 * i) * (kHbW * 4)),
-                                                 16, off, i * 8 * kHbW * 4, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            r, (__attribute__((address_space(3))) void*)(stage + wave * kHbHRegion + i * 1024), 16, off,
+            i * 8 * kHbW * 4, 0, 0);
 }
 
 // one 4-row transposed read (ds_read_b64_tr_b16) at byte address addr of the LDS
@@ -268,22 +279,24 @@ __global__ __launch_bounds__(kHbThreads, 2) void hidden_bwd_kernel(HbArgs args) 
             acc[b & 1] = mfma_x6(af[b & 1], bf, acc[b & 1]);
             __builtin_amdgcn_sched_barrier(0);  // two blocks' fragments live at a time (the 128 dW registers stay)
         }
-        // ---- epilogue: H from the stage (this wave's DMA landed, then every wave's), ELU', dZp out
+        // ---- epilogue: H from this wave's stage region (its own DMA: no workgroup barrier), ELU', dZp out
         HB_STAMP(1);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
+        __builtin_amdgcn_sched_barrier(0);  // the main loop's registers die here (nothing of the epilogue moves up)
         HB_STAMP(2);
         float hr[2][16];
         {
-            // H in the accumulator layout from this wave's columns of the stage; dZp = acc * ELU'(H)
-            // (epilogue_tiles_impl's bits) written back over the same stage words (only this wave reads them), then
-            // read row-contiguous and stored as 16-byte units: 8 stores per lane instead of 32 4-byte ones (the
-            // epilogue runs while no wave of the CU issues MFMAs)
-            float* hs = reinterpret_cast<float*>(stage) + 32 * wave + l32;
+            // H in the accumulator layout; dZp = acc * ELU'(H) (epilogue_tiles_impl's bits) written back over the
+            // same region words, then read row-contiguous and stored as 16-byte units: 8 stores per lane instead of
+            // 32 4-byte ones
+            // row 32 i + 4 h + rr (rr = (r & 3) + 8 (r >> 2), bit 2 clear) sits in slot 32 i + rr + 5 h (rr even) or
+            // 32 i + rr + 3 h (rr odd): two lane bases, the rest in the immediate offsets
+            float* const reg = reinterpret_cast<float*>(stage + wave * kHbHRegion) + l32;
+            float* const hs[2] = {reg + 5 * h * 32, reg + 3 * h * 32};
 #pragma unroll
             for (int i = 0; i < 2; ++i)
 #pragma unroll
-                for (int r = 0; r < 16; ++r) hr[i][r] = hs[(32 * i + 4 * h + (r & 3) + 8 * (r >> 2)) * kHbW];
+                for (int r = 0; r < 16; ++r) hr[i][r] = hs[r & 1][(32 * i + (r & 3) + 8 * (r >> 2)) * 32];
 #pragma unroll
             for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -291,23 +304,26 @@ __global__ __launch_bounds__(kHbThreads, 2) void hidden_bwd_kernel(HbArgs args) 
                     const float v = acc[i][r];
                     const float hv = hr[i][r];
                     const float g = v * (hv + 1.f);  // ELU'(z) = 1 if z > 0 else h + 1
-                    hs[(32 * i + 4 * h + (r & 3) + 8 * (r >> 2)) * kHbW] = hv > 0.f ? v : g;
+                    hs[r & 1][(32 * i + (r & 3) + 8 * (r >> 2)) * 32] = hv > 0.f ? v : g;
                 }
             // the dword writes retire before the 16-byte reads (the LDS does not keep that order by itself)
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
                 P.dz_prev + row0 * kHbW + 32 * wave, 0, static_cast<uint32_t>(kHbT * kHbW * 4), kHbRsrcFlags);
-            const float* rs = reinterpret_cast<const float*>(stage) + 32 * wave + 4 * (lane & 7);
+            const float* rs = reinterpret_cast<const float*>(stage + wave * kHbHRegion) + hb_hslot(lane >> 3) * 32 +
+                              4 * (lane & 7);
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                const int row = 8 * j + (lane >> 3);
-                const u32x4 sv = *reinterpret_cast<const u32x4*>(rs + row * kHbW);
+                const u32x4 sv = *reinterpret_cast<const u32x4*>(rs + 8 * j * 32);  // row 8 j + lane / 8
                 __builtin_amdgcn_raw_buffer_store_b128(sv, rc, ((lane >> 3) * kHbW + 4 * (lane & 7)) * 4,
                                                        8 * j * kHbW * 4, 2 /* nt */);
                 // VMEM store-data hazard (mlp_gemm.hip epilogue_tiles_staged): keep the data registers live past wait
                 // states of their own after the 16-byte store
                 asm volatile("s_nop 3" ::"v"(sv) : "memory");
             }
+            // the next tile's H into the (now read) region: it lands during this tile's weight gradient
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (has_next) hb_dma_h(hb_tile_rsrc(P.h, row0 + kHbT), stage);
         }
         float4 vn[8];
         uint2 pl[8][3];  // the next tile's dZ units as bf16 planes
@@ -366,7 +382,6 @@ __global__ __launch_bounds__(kHbThreads, 2) void hidden_bwd_kernel(HbArgs args) 
         __syncthreads();  // every wave has read the dZ planes (and, in the epilogue, the H stage)
         HB_STAMP(5);
         if (has_next) {
-            hb_dma_h(hb_tile_rsrc(P.h, row0 + kHbT), stage);  // lands during the next main loop
             hb_store_dz(vn, dzl, csum);
             __syncthreads();
         }
