@@ -31,7 +31,7 @@ extern "C" {
 
 typedef struct ihipStream_t* rslrl_stream_t; /* == hipStream_t */
 
-#define RSLRL_ABI_VERSION 15
+#define RSLRL_ABI_VERSION 16
 
 enum {
     RSLRL_OK = 0,
@@ -77,7 +77,11 @@ int rslrl_compute_returns_records(const float* values, const float* rewards, con
  * 16-byte unit per env-step (slots: [T*N, 4] fp32, 16-byte aligned) -- coalesced stores where the in-record slots
  * of rslrl_compute_returns_records are 32-byte pieces at the record stride.  The mini-batch gather reads each drawn
  * row's slot beside its record (rslrl_gather_records_side).  Replaces rollout_storage.py:127-149 like
- * rslrl_compute_returns. */
+ * rslrl_compute_returns.
+ * ABI 16: for T in {8, 16, 24, 32} and N <= 131072 whose blocks the device holds at once, the scan, the statistics and
+ * the normalisation run as ONE launch (a grid barrier between the scan and the normalisation; same bits as the
+ * two-launch form, RSLRL_GAE_FUSED=0 forces that).  The barrier words sit after the partials in the workspace:
+ * a workspace must be zero-filled before its first use with this entry point (the library leaves it so). */
 int rslrl_compute_returns_slots(const float* values, const float* rewards, const uint8_t* dones,
                                 const float* last_values, float gamma, float lam, int64_t T, int64_t N,
                                 float* returns, float* advantages, const float* log_prob, float* slots,

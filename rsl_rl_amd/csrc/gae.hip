@@ -16,6 +16,8 @@
 //                     agree bitwise), then rescales the advantages with 16-byte accesses.
 // Bytes per element (T*N of them): read 4 (V) + 4 (R) + 1 (done), write 4 (returns) + 4 (adv) = 17 in
 // the scan; read 4 + write 4 = 8 in the normaliser.
+//   gae_fused_slots   (round 5, rslrl_compute_returns_slots) both in one launch with a grid barrier between them:
+//                     read V, R, done, log-prob (13 B), write returns, advantages, slot (24 B) per element.
 //
 // Bit-exactness: every fp32 operation of the reference expression is issued separately with
 // round-to-nearest intrinsics in the reference's evaluation order (Python left-to-right:
@@ -246,22 +248,32 @@ __global__ __launch_bounds__(kBlock) void adv_normalize_slots_kernel(float* __re
                                                                      const float* __restrict__ logp,
                                                                      const float* __restrict__ returns,
                                                                      float4* __restrict__ slots) {
-    float mean, std;
-    fold_moments(partials, np, n, &mean, &std);
-    const float denom = __fadd_rn(std, eps);  // rollout_storage.py:149  (std + 1e-8)
     const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
     const int64_t tid = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
     // four env-steps per thread and iteration (16-byte loads of the four sources, 64 contiguous bytes of slots), so a
-    // grid of a few blocks per CU covers the rollout and the partial fold above runs once per block, not per 256
-    // elements; the scalar loop takes the tail (and every element when a source is not 16-byte aligned)
+    // grid of a few blocks per CU covers the rollout and the partial fold runs once per block, not per 256 elements;
+    // the first iteration's loads are issued before the fold (they do not depend on it: the fold's latency hides
+    // under them).  The scalar loop takes the tail (and every element when a source is not 16-byte aligned).
     const bool vec = ((reinterpret_cast<uintptr_t>(adv) | reinterpret_cast<uintptr_t>(values) |
                        reinterpret_cast<uintptr_t>(logp) | reinterpret_cast<uintptr_t>(returns)) & 15) == 0;
     const int64_t nvec = vec ? n / 4 : 0;
+    float4 a4 = {}, v4 = {}, l4 = {}, r4 = {};
+    if (tid < nvec) {
+        a4 = reinterpret_cast<const float4*>(adv)[tid];
+        v4 = reinterpret_cast<const float4*>(values)[tid];
+        l4 = reinterpret_cast<const float4*>(logp)[tid];
+        r4 = reinterpret_cast<const float4*>(returns)[tid];
+    }
+    float mean, std;
+    fold_moments(partials, np, n, &mean, &std);
+    const float denom = __fadd_rn(std, eps);  // rollout_storage.py:149  (std + 1e-8)
     for (int64_t i = tid; i < nvec; i += stride) {
-        const float4 a4 = reinterpret_cast<const float4*>(adv)[i];
-        const float4 v4 = reinterpret_cast<const float4*>(values)[i];
-        const float4 l4 = reinterpret_cast<const float4*>(logp)[i];
-        const float4 r4 = reinterpret_cast<const float4*>(returns)[i];
+        if (i != tid) {
+            a4 = reinterpret_cast<const float4*>(adv)[i];
+            v4 = reinterpret_cast<const float4*>(values)[i];
+            l4 = reinterpret_cast<const float4*>(logp)[i];
+            r4 = reinterpret_cast<const float4*>(returns)[i];
+        }
         float4 o;
         o.x = __fdiv_rn(__fsub_rn(a4.x, mean), denom);
         o.y = __fdiv_rn(__fsub_rn(a4.y, mean), denom);
@@ -287,6 +299,148 @@ int elementwise_blocks(int64_t n) {
     return static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, 4 * kBlock), 2048)));
 }
 
+// ---- compute_returns_slots in ONE launch (round 5): scan, grid barrier, normalisation from registers ----------------
+// One env per lane (nb = N / 256 blocks, every block resident at once -- checked against the occupancy on the host):
+// the lane keeps its T values and returns in registers through the whole kernel, so the normalisation reads neither
+// the advantages nor the values back, and the raw advantages are never written.  The block partials are the scan's
+// (same partition, same Chan tree) and every block folds them in fold_moments' order after the barrier: mean / std,
+// returns, advantages and slots are bit-identical to gae_scan_kernel + adv_normalize_slots_kernel.
+//
+// Grid barrier: the partials go out as agent-scope atomic stores; thread 0 of each block reads the generation word,
+// takes a ticket, and the last arrival re-arms the ticket (0) and bumps the generation; the others spin on
+// the generation with s_sleep (bounded: after ~2^22 polls a block gives up and raises the error word instead of
+// hanging -- it cannot happen with every block resident).  Workspace: [kMaxPartials double4][ticket][generation]
+// [error]; the ticket must be zero before the first call (zero-filled allocation) and is left zero.
+constexpr int kBarOffset = sizeof(double4) * kMaxPartials;
+
+__device__ __forceinline__ void gae_grid_barrier(unsigned* bar, unsigned nb) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned* ticket = bar;
+        unsigned* gen = bar + 1;
+        // no release / acquire fences (on gfx950 they write back / invalidate the whole L2 of the XCD -- the
+        // scan's returns are in it): the partials went out as agent-scope atomic stores, which complete at the
+        // coherence point before the ticket is taken (vmcnt), and are read back by agent-scope atomic loads
+        const unsigned g0 = __hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (t == nb - 1) {
+            __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(gen, g0 + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            unsigned polls = 0;
+            while (__hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g0) {
+                __builtin_amdgcn_s_sleep(2);
+                if (++polls == (1u << 22)) {
+                    __hip_atomic_store(bar + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    break;
+                }
+            }
+        }
+    }
+    __syncthreads();
+}
+
+template <int T>
+__global__ __launch_bounds__(kBlock) void gae_fused_slots_kernel(
+    const float* __restrict__ values, const float* __restrict__ rewards, const uint8_t* __restrict__ dones,
+    const float* __restrict__ last_values, float gamma, float lam, int64_t N, float eps, float* __restrict__ returns,
+    float* __restrict__ advantages, const float* __restrict__ logp, float4* __restrict__ slots,
+    double4* __restrict__ partials, unsigned* __restrict__ bar) {
+    __shared__ double scratch[kBlock / kWave][3];
+    const int64_t n = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    const bool ok = n < N;
+    float v[T], ret[T];
+    Moments m{0.0, 0.0, 0.0};
+    if (ok) {
+        float r[T];
+        unsigned d[T];
+#pragma unroll
+        for (int t = 0; t < T; ++t) {
+            const int64_t i = static_cast<int64_t>(t) * N + n;
+            v[t] = values[i];
+            r[t] = rewards[i];
+            d[t] = dones[i];
+        }
+        float next_v = last_values[n];
+        float adv = 0.0f;
+        double s = 0.0;
+#pragma unroll
+        for (int t = T - 1; t >= 0; --t) {
+            adv = GaeStep::step(v[t], r[t], d[t], next_v, adv, gamma, lam);
+            ret[t] = __fadd_rn(adv, v[t]);  // :142
+            returns[static_cast<int64_t>(t) * N + n] = ret[t];
+            s += static_cast<double>(__fsub_rn(ret[t], v[t]));  // :145
+            next_v = v[t];
+        }
+        const double mean = s / static_cast<double>(T);
+        double m2 = 0.0;
+#pragma unroll
+        for (int t = 0; t < T; ++t) {
+            const double dlt = static_cast<double>(__fsub_rn(ret[t], v[t])) - mean;
+            m2 += dlt * dlt;
+        }
+        m = chan(m, Moments{static_cast<double>(T), mean, m2});
+    }
+    m = block_chan(m, scratch);
+    if (threadIdx.x == 0) {
+        unsigned long long* p = reinterpret_cast<unsigned long long*>(partials + blockIdx.x);
+        __hip_atomic_store(p, __double_as_longlong(m.n), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(p + 1, __double_as_longlong(m.mean), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(p + 2, __double_as_longlong(m.m2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    float lp[T];  // the log-probs load while the grid gathers
+    if (ok) {
+#pragma unroll
+        for (int t = 0; t < T; ++t) lp[t] = logp[static_cast<int64_t>(t) * N + n];
+    }
+    gae_grid_barrier(bar, gridDim.x);
+    // fold_moments' order over the partials (atomic loads: another XCD's L2 wrote them)
+    Moments f{0.0, 0.0, 0.0};
+    for (int i = threadIdx.x; i < static_cast<int>(gridDim.x); i += kBlock) {
+        const unsigned long long* p = reinterpret_cast<const unsigned long long*>(partials + i);
+        const Moments q{__longlong_as_double(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)),
+                        __longlong_as_double(__hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)),
+                        __longlong_as_double(__hip_atomic_load(p + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))};
+        f = chan(f, q);
+    }
+    f = block_chan(f, scratch);
+    const int64_t total = static_cast<int64_t>(T) * N;
+    const double var = total > 1 ? f.m2 / static_cast<double>(total - 1) : __builtin_nan("");
+    const float mean = static_cast<float>(f.mean);
+    const float denom = __fadd_rn(static_cast<float>(sqrt(var)), eps);  // rollout_storage.py:149
+    if (ok) {
+#pragma unroll
+        for (int t = 0; t < T; ++t) {
+            const int64_t i = static_cast<int64_t>(t) * N + n;
+            const float a = __fdiv_rn(__fsub_rn(__fsub_rn(ret[t], v[t]), mean), denom);
+            advantages[i] = a;
+            slots[i] = make_float4(v[t], lp[t], ret[t], a);
+        }
+    }
+}
+
+// blocks of gae_fused_slots_kernel<T> the device holds at once (0: no fused instance for T)
+int gae_fused_capacity(int T) {
+    static int cap[4] = {-1, -1, -1, -1};
+    const int k = T == 8 ? 0 : T == 16 ? 1 : T == 24 ? 2 : T == 32 ? 3 : -1;
+    if (k < 0) return 0;
+    if (cap[k] < 0) {
+        int dev = 0, cus = 0, per = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            cus = 0;
+        const void* f = k == 0 ? reinterpret_cast<const void*>(&gae_fused_slots_kernel<8>)
+                        : k == 1 ? reinterpret_cast<const void*>(&gae_fused_slots_kernel<16>)
+                        : k == 2 ? reinterpret_cast<const void*>(&gae_fused_slots_kernel<24>)
+                                 : reinterpret_cast<const void*>(&gae_fused_slots_kernel<32>);
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, f, kBlock, 0) != hipSuccess) per = 0;
+        cap[k] = per * cus;
+    }
+    return cap[k];
+}
+
 template <int TMAX>
 void launch_scan(int nb, hipStream_t st, const float* v, const float* r, const uint8_t* d, const float* lv,
                  float g, float l, int T, int64_t N, float* ret, float* adv, double4* part) {
@@ -306,7 +460,7 @@ using namespace rslrl;
 extern "C" size_t rslrl_compute_returns_workspace_bytes(int64_t T, int64_t N) {
     (void)T;
     (void)N;
-    return sizeof(double4) * kMaxPartials;
+    return kBarOffset + 64;  // the partials, then the one-launch form's barrier words
 }
 
 extern "C" size_t rslrl_normalize_workspace_bytes(int64_t n) {
@@ -340,6 +494,24 @@ int compute_returns_impl(const float* values, const float* rewards, const uint8_
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     const int nb = scan_blocks(N);
     const int t = static_cast<int>(T);
+    static const bool fused_on = [] {
+        const char* e = std::getenv("RSLRL_GAE_FUSED");
+        return !(e && e[0] == '0');
+    }();
+    if (slot && slot->record_floats == 0 && fused_on && nb == ceil_div(N, kBlock) && nb <= gae_fused_capacity(t)) {
+        // one launch: scan + grid barrier + normalisation + slots (bit-identical to the two-launch path below)
+        unsigned* bar = reinterpret_cast<unsigned*>(static_cast<char*>(workspace) + kBarOffset);
+        float4* sl = reinterpret_cast<float4*>(slot->records);
+#define RSLRL_GAE_FUSED_LAUNCH(TT)                                                                                    \
+    hipLaunchKernelGGL((gae_fused_slots_kernel<TT>), dim3(nb), dim3(kBlock), 0, st, values, rewards, dones,           \
+                       last_values, gamma, lam, N, 1e-8f, returns, advantages, slot->log_prob, sl, part, bar)
+        if (t == 8) RSLRL_GAE_FUSED_LAUNCH(8);
+        else if (t == 16) RSLRL_GAE_FUSED_LAUNCH(16);
+        else if (t == 24) RSLRL_GAE_FUSED_LAUNCH(24);
+        else RSLRL_GAE_FUSED_LAUNCH(32);
+#undef RSLRL_GAE_FUSED_LAUNCH
+        return launch_status();
+    }
     if (t <= 8)
         launch_scan<8>(nb, st, values, rewards, dones, last_values, gamma, lam, t, N, returns, advantages, part);
     else if (t <= 16)

@@ -98,13 +98,14 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t hb_tile_rsrc(const float* base
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base + row0 * kHbW), 0, kHbTileBytes, kHbRsrcFlags);
 }
 
-// the tile's dZ (8 float4 per thread: row (t >> 6) + 8 i, columns 4 (t & 63) .. + 3)
+// the tile's dZ (8 float4 per thread: row (t >> 6) + 8 i, columns 4 (t & 63) .. + 3); nontemporal like the H DMA:
+// dZ and H are read once, so they should not push the W^T image out of L2 (PMC: reads 1.14x -> 1.00x algorithmic)
 template <int I0 = 0, int I1 = 8>
 __device__ __forceinline__ void hb_load_dz(__amdgpu_buffer_rsrc_t r, float4 (&v)[8]) {
     const int off = ((threadIdx.x >> 6) * kHbW + 4 * (threadIdx.x & 63)) * 4;
 #pragma unroll
     for (int i = I0; i < I1; ++i)
-        v[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, off, i * 8 * kHbW * 4, 0));
+        v[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, off, i * 8 * kHbW * 4, 2));
 }
 
 __device__ __forceinline__ void hb_store_dz(const float4 (&v)[8], char* __restrict__ lds, float4& csum) {
@@ -140,7 +141,7 @@ __device__ __forceinline__ void hb_dma_h(__amdgpu_buffer_rsrc_t r, char* stage) 
     for (int i = 0; i < 8; ++i)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(
             r, (__attribute__((address_space(3))) void*)(stage + wave * kHbHRegion + i * 1024), 16, off,
-            i * 8 * kHbW * 4, 0, 0);
+            i * 8 * kHbW * 4, 0, 2);
 }
 
 // one 4-row transposed read (ds_read_b64_tr_b16) at byte address addr of the LDS

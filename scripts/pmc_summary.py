@@ -25,6 +25,7 @@ SHORT = {
     "adv_normalize_slots_kernel": "adv_normalize_slots",
     "mlp_gemm_x6_value_head_kernel": "x6_value_head",
     "mlp_gemm_x6_actor_head_kernel": "x6_actor_head",
+    "hidden_bwd_kernel": "x6_hidden_bwd_pair",
     "out_bwd_valu_kernel": "out_bwd",
     "out_bwd_valu_pair_kernel": "out_bwd_pair",
     "moments_kernel": "moments",

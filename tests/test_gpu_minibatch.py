@@ -201,10 +201,13 @@ def test_compute_returns_records_matches_scan_plus_slot_copy(T, N, cuda_device):
     assert torch.equal(rec_a, rec_b)
 
 
-@pytest.mark.parametrize("T,N", [(24, 4096), (5, 1031), (1, 3)])
+@pytest.mark.parametrize("T,N", [(24, 4096), (5, 1031), (1, 3), (24, 65536), (8, 1031), (16, 300), (32, 131072),
+                                 (24, 300000)])
 def test_compute_returns_slots_matches_scan_plus_stack(T, N, cuda_device):
     """rslrl_compute_returns_slots == rslrl_compute_returns (normalised) followed by stacking {value, log-prob, return,
-    advantage} per env-step, bit for bit (returns, advantages and the whole slot array)."""
+    advantage} per env-step, bit for bit (returns, advantages and the whole slot array).  T in {8, 16, 24, 32} with
+    every block resident takes the one-launch form (scan + grid barrier + normalisation, round 5); T = 5, T = 1 and
+    N = 300000 (more blocks than the partial array holds) the scan + normaliser pair: both must equal the plain path."""
     rng = np.random.default_rng(T * N + 1)
     f = lambda *s: torch.from_numpy(rng.standard_normal(s, dtype=np.float32)).to(cuda_device)  # noqa: E731
     values, rewards, logp, last = f(T, N, 1), f(T, N, 1), f(T, N, 1), f(N, 1)
@@ -216,6 +219,32 @@ def test_compute_returns_slots_matches_scan_plus_stack(T, N, cuda_device):
     kernels.compute_returns_slots(values, rewards, dones, last, 0.99, 0.95, ret_b, adv_b, logp, slots)
     assert torch.equal(ret_a, ret_b) and torch.equal(adv_a, adv_b)
     assert torch.equal(slots, torch.cat([values, logp, ret_a, adv_a], dim=-1))
+
+
+def test_compute_returns_slots_one_launch_rearms(cuda_device):
+    """The one-launch form's grid barrier leaves its ticket at zero and raises no error word, so back-to-back calls
+    (and a call after the two-launch path used the same workspace) give the same bits."""
+    T, N = 24, 65536
+    rng = np.random.default_rng(7)
+    f = lambda *s: torch.from_numpy(rng.standard_normal(s, dtype=np.float32)).to(cuda_device)  # noqa: E731
+    values, rewards, logp, last = f(T, N, 1), f(T, N, 1), f(T, N, 1), f(N, 1)
+    dones = torch.from_numpy((rng.random((T, N, 1)) < 0.05).astype(np.uint8)).to(cuda_device)
+    outs = []
+    for _ in range(3):
+        ret, adv = torch.empty_like(values), torch.empty_like(values)
+        slots = torch.full((T, N, 4), float("nan"), device=cuda_device)
+        kernels.compute_returns_slots(values, rewards, dones, last, 0.99, 0.95, ret, adv, logp, slots)
+        kernels.compute_returns(values, rewards, dones, last, 0.99, 0.95, True, torch.empty_like(values),
+                                torch.empty_like(values))
+        outs.append((ret, adv, slots))
+    torch.cuda.synchronize()
+    for o in outs[1:]:
+        assert all(torch.equal(a, b) for a, b in zip(outs[0], o))
+    L = kernels._lib.lib()
+    ws = kernels._ws.get(values.device, "gae", L.rslrl_compute_returns_workspace_bytes(T, N))
+    words = ws[16384:16384 + 12].view(torch.int32).cpu().tolist()
+    assert words[0] == 0 and words[2] == 0, words  # ticket re-armed, no barrier time-out
+    assert words[1] >= 3  # the generation advanced once per one-launch call
 
 
 @pytest.mark.parametrize("R,used", [(96, 84), (64, 56), (256, 252)])
