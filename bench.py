@@ -50,12 +50,13 @@ C4_ENVS = 131072  # BASELINE.json configs[3]: the total partitioned over the ran
 # per-launch HBM traffic of the hot-path kernels from rocprofv3 FETCH_SIZE / WRITE_SIZE passes over this same
 # bench command (scripts/pmc_summary.py; raw counters next to it).  PMC passes serialise and slow the
 # run, so they are collected separately and the committed summary is reported here.
-PMC_TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r4_pmc_traffic.json")
+PMC_TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r5_pmc_traffic.json")
 # the MLP GEMM pairs' counters (scripts/mlp_pmc.sh + scripts/mlp_pmc_summary.py over scripts/mlp_pair_probe.py at C3's
 # 393,216-row mini-batch): FETCH_SIZE / WRITE_SIZE corrected by factors calibrated on the box in each kernel's own
 # access pattern (scripts/pmc_pattern_probe.hip), plus clock and MFMA-pipe utilisation from the SQ counters
-MLP_PMC_FILE = os.path.join(ROOT, "profiles", "r4_mlp_pmc.json")
-MLP_PMC_NAMES = {"linear_dgrad_pair[M=393216,Nred=256,K=256]": "x6_dgrad_pair_w4",
+MLP_PMC_FILE = os.path.join(ROOT, "profiles", "r5_mlp_pmc.json")
+MLP_PMC_NAMES = {"linear_hidden_bwd_pair[M=393216,N=256,K=256]": "x6_hidden_bwd_pair",
+                 "linear_dgrad_pair[M=393216,Nred=256,K=256]": "x6_dgrad_pair_w4",
                  "linear_fwd_pair[M=393216,K=256,N=256]": "x6_fwd_elu_pair",
                  "linear_wgrad_pair[M=393216,N=256,K=256]": "x6_wgrad_pair"}
 
