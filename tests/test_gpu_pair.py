@@ -34,6 +34,30 @@ def test_pair_matches_two_launches(M, K, arith, cuda_device):
         assert float(amaxes[i]) == float(ys[i].abs().max())
 
 
+@pytest.mark.parametrize("M", [393216, 65536, 16384 + 128, 4096, 128, 1000])
+def test_stream_forward_pair_matches_tiled_kernel(M, cuda_device):
+    """The square hidden layers' x6 forward pair without amax (the update's and the rollout's path) runs on the
+    streaming kernel (mlp_fwd_stream.hip) whenever M is a multiple of 128: its H must equal the tiled kernel's
+    (the single-problem launch) bit for bit -- slices of 1 to 24 tiles, the last slice shorter, and a ragged M that
+    stays on the tiled pair kernel."""
+    dev = cuda_device
+    g = torch.Generator(device=dev).manual_seed(M)
+    N = K = 256
+    xs = [torch.nn.functional.elu(torch.randn(M, K, device=dev, generator=g)) * s for s in (1.0, 9.0)]
+    ws = [torch.randn(N, K, device=dev, generator=g) / K ** 0.5 for _ in range(2)]
+    bs = [torch.randn(N, device=dev, generator=g) * 0.1 for _ in range(2)]
+    imgs = fused_mlp.bimages([(w, False, _lib.BIMAGE_LAYOUT_GEMM) for w in ws])
+    ref = [fused_mlp.linear_fwd_ex(xs[i], bs[i], N, True, imgs[i], _lib.ARITH_X6, None, want_amax=False)[0]
+           for i in range(2)]
+    ys, _ = fused_mlp.linear_fwd_pair(xs, bs, N, True, imgs, _lib.ARITH_X6, [None, None], [False, False])
+    torch.cuda.synchronize()
+    for i in range(2):
+        assert torch.equal(ys[i], ref[i]), (i, float((ys[i] - ref[i]).abs().max()))
+    # fp32 sanity against torch (x6 is fp32-faithful)
+    y64 = torch.nn.functional.elu(xs[1].double() @ ws[1].double().t() + bs[1].double())
+    assert float((ys[1].double() - y64).abs().max()) <= 1e-5 * float(y64.abs().max())
+
+
 def test_pair_rejects_mismatched_shapes(cuda_device):
     x = torch.randn(128, 48, device=cuda_device)
     w = torch.randn(256, 48, device=cuda_device)
