@@ -468,12 +468,14 @@ extern "C" int rslrl_hidden_bwd_pair(const rslrl_hidden_bwd_problem_t* p0, const
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     const dim3 blk(kHbThreads);
     // measured at 393,216 rows (scripts/hidden_bwd_probe.py --variants, one process): BD,LA = 1,0 1067 us, 1,1 1094,
-    // 2,0 1110, 2,1 1127, 3,1 1216 -- the fewer registers live, the faster (3,1 spills 37 VGPRs)
+    // 2,0 1110, 2,1 1127, 3,1 1216 -- the fewer registers live, the faster (3,1 spills 37 VGPRs); the default adds
+    // s_setprio 1 for waves 4-7 (1048 vs 1055 and 1043 vs 1047 us in two runs, profiles/r5_hb_variants.json)
     if (bd == 2 && la == 0) hipLaunchKernelGGL((hidden_bwd_kernel<2, 0>), grid, blk, 0, st, args);
     else if (bd == 2) hipLaunchKernelGGL((hidden_bwd_kernel<2, 1>), grid, blk, 0, st, args);
     else if (la == 1) hipLaunchKernelGGL((hidden_bwd_kernel<1, 1>), grid, blk, 0, st, args);
     else if (la == 2) hipLaunchKernelGGL((hidden_bwd_kernel<1, 0, 1>), grid, blk, 0, st, args);  // LA 2: prio
     else if (la == 3) hipLaunchKernelGGL((hidden_bwd_kernel<1, 1, 1>), grid, blk, 0, st, args);
-    else hipLaunchKernelGGL((hidden_bwd_kernel<1, 0>), grid, blk, 0, st, args);
+    else if (la == 4) hipLaunchKernelGGL((hidden_bwd_kernel<1, 0, 0>), grid, blk, 0, st, args);  // LA 4: no prio
+    else hipLaunchKernelGGL((hidden_bwd_kernel<1, 0, 1>), grid, blk, 0, st, args);
     return launch_status();
 }

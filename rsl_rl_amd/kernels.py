@@ -7,6 +7,7 @@ torch stream and never synchronises.  CPU tensors are rejected: there is no CPU 
 from __future__ import annotations
 
 import contextlib
+import os
 import ctypes
 from collections import defaultdict
 
@@ -245,9 +246,13 @@ def compute_returns_slots(values, rewards, dones, last_values, gamma, lam, retur
     L = _lib.lib()
     dev = values.device
     ws = _ws.get(dev, "gae", L.rslrl_compute_returns_workspace_bytes(T, N))
-    # scan (17 B + 4 B per env) + centred squares (4 B) + normalisation reading adv / value / log-prob / return and
-    # writing adv + the 16-byte slot
-    moved = 17 * T * N + 4 * N + 4 * T * N + (4 * 4 + 4 + 16) * T * N
+    if T in (8, 16, 24, 32) and N <= 131072 and os.environ.get("RSLRL_GAE_FUSED", "1") != "0":
+        # the one-launch form (ABI 16): read value, reward, done, log-prob (13 B) + last value per env, write return,
+        # advantage and the 16-byte slot (24 B)
+        moved = 37 * T * N + 4 * N
+    else:
+        # scan (17 B + 4 B per env) + normalisation reading adv / value / log-prob / return, writing adv + the slot
+        moved = 17 * T * N + 4 * N + (4 * 4 + 4 + 16) * T * N
     with timer.span("compute_returns", dev, moved):
         rc = L.rslrl_compute_returns_slots(
             _ptr(values), _ptr(rewards), _ptr(dones), _ptr(last_values), ctypes.c_float(gamma), ctypes.c_float(lam),
