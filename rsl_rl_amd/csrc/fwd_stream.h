@@ -1,5 +1,5 @@
 // Internal interface of the streaming hidden-layer forward (mlp_fwd_stream.hip), called by rslrl_linear_gemm_pair for
-// RSLRL_LINEAR_FWD_ELU on x6 with K = N = 256 and M a multiple of 128 (no C ABI of its own: same entry point, same
+// RSLRL_LINEAR_FWD_ELU on x6 with N = 256, K = 256 or 48 and M a multiple of 128 (no C ABI of its own: same entry point, same
 // bits as the tiled kernel).
 #pragma once
 
@@ -11,13 +11,14 @@
 namespace rslrl {
 
 struct FwdStreamProblem {
-    const float* x;     // [M, 256] layer input
+    const float* x;     // [M, K] layer input
     const void* img;    // x6 image of W (layout 0)
     const float* bias;  // [256]
     float* h;           // [M, 256] output ELU(x W^T + b)
 };
 
 bool fwd_stream_enabled();  // RSLRL_FWD_STREAM=0 keeps the tiled kernel (A/B)
-int fwd_stream_pair(const FwdStreamProblem* p, int n, int64_t M, hipStream_t st);
+bool fwd_stream48();        // RSLRL_FWD_STREAM=48: the 48-wide first layer too (opt-in: slower, see the call site)
+int fwd_stream_pair(const FwdStreamProblem* p, int n, int64_t M, int K, hipStream_t st);  // K = 256 or 48
 
 }  // namespace rslrl

@@ -21,6 +21,8 @@
 // LDS image of a quarter buffer plane: [4 chunks][128 row slots][32 bytes], row m of chunk c in slot m ^ f(c),
 // f(c) = (c & 3) | 4 (c & 1), 16-byte halves swapped when (m >> 3) & 1 (mlp_bwd_fused.hip's plane layout with 128
 // rows): conflict-free for the ds_read_b128 row fragments and the split's ds_write_b64 (16 lanes = one row of 4 chunks).
+#include <cstring>
+
 #include "common.h"
 #include "fwd_stream.h"
 #include "x6_split.h"
@@ -29,14 +31,11 @@ namespace rslrl {
 namespace {
 
 constexpr int kFsT = 128;                  // rows per tile
-constexpr int kFsW = 256;                  // K = N = 256
+constexpr int kFsN = 256;                  // output width
 constexpr int kFsThreads = 512;            // 8 waves
-constexpr int kFsQChunks = 4;              // chunks per K quarter
-constexpr int kFsChunkB = kFsT * 32;       // one chunk of one plane: 4 KiB
-constexpr int kFsPlaneB = kFsQChunks * kFsChunkB;  // 16 KiB
-constexpr int kFsBufB = 3 * kFsPlaneB;     // 48 KiB per quarter buffer
+constexpr int kFsChunkB = kFsT * 32;       // one chunk of one plane of a stage buffer: 4 KiB
 constexpr int kFsMaxSlices = 128;          // per problem: a pair fills the 256 CUs with one workgroup each
-constexpr int kFsImgPlaneU = kFsW * 32 / 16;  // 16-byte units of one plane of one image chunk (bimage layout 0)
+constexpr int kFsImgPlaneU = kFsN * 32 / 16;  // 16-byte units of one plane of one image chunk (bimage layout 0)
 constexpr int kFsImgChunkU = 3 * kFsImgPlaneU;
 constexpr uint32_t kFsRsrcFlags = 0x00020000;
 #ifndef RSLRL_FS_LA
@@ -44,9 +43,24 @@ constexpr uint32_t kFsRsrcFlags = 0x00020000;
 #endif
 constexpr bool kFsLA = RSLRL_FS_LA != 0;  // A fragments one MFMA block ahead (A/B: 688-693 vs 697-721 us, r5_fs_ab.json)
 
+// K = 256: four stages (K quarters) of 4 chunks per tile; K = 48 (the first layer): one stage of 3 chunks per tile
+template <int K>
+struct FsCfg {
+    static constexpr int kChunks = K / 16;                   // chunks of the tile
+    static constexpr int kStages = K == 256 ? 4 : 1;         // stages per tile
+    static constexpr int kNch = kChunks / kStages;           // chunks per stage
+    static constexpr int kCols = 16 * kNch;                  // columns of X per stage
+    static constexpr int kPlaneB = kNch * kFsChunkB;         // one plane of a stage buffer
+    static constexpr int kBufB = 3 * kPlaneB;                // 48 KiB (K = 256) / 36 KiB (K = 48)
+    static constexpr int kUnitsRow = kCols / 4;              // 16-byte units of a row's stage columns
+    static constexpr int kUpt = kFsT * kUnitsRow / kFsThreads;  // units per thread per stage: 4 / 3
+    static_assert(K == 256 || K == 48, "streaming forward: K = 256 or 48");
+    static_assert(kNch >= 2 && kUpt <= 4 && kFsT * kUnitsRow % kFsThreads == 0, "stage shape");
+};
+
 struct FsProblem {
-    const float* x;     // [M, 256]
-    const uint4* img;   // x6 image of W (layout 0, 16 chunks)
+    const float* x;     // [M, K]
+    const uint4* img;   // x6 image of W (layout 0, K / 16 chunks)
     const float* bias;  // [256]
     float* h;           // [M, 256]
 };
@@ -59,7 +73,7 @@ struct FsArgs {
 
 __host__ __device__ constexpr int fs_f(int c) { return (c & 3) | ((c & 1) << 2); }
 
-// byte offset of (row m, column col % 4 == 0 of the quarter) in a plane of a quarter buffer
+// byte offset of (row m, column col % 4 == 0 of the stage) in a plane of a stage buffer
 __device__ __forceinline__ int fs_off(int m, int col) {
     const int c = col >> 4;
     return c * kFsChunkB + (m ^ fs_f(c)) * 32 + 16 * (((col >> 3) & 1) ^ ((m >> 3) & 1)) + 8 * ((col >> 2) & 1);
@@ -70,26 +84,28 @@ __device__ __forceinline__ bf16x8 fs_read16(int addr) {
     return __builtin_bit_cast(bf16x8, *reinterpret_cast<const lds_u4*>(addr));
 }
 
-// the tile's X columns [64 q, 64 q + 64): 4 float4 per thread, row (t >> 4) + 32 j, columns 64 q + 4 (t & 15) .. + 3
+// stage q of the tile's X: unit u = t + 512 j (j < kUpt) is row u / kUnitsRow, columns kCols q + 4 (u % kUnitsRow)
+template <int K>
 __device__ __forceinline__ void fs_load_x(__amdgpu_buffer_rsrc_t r, int q, float4 (&v)[4]) {
-    const int off = ((threadIdx.x >> 4) * kFsW + 4 * (threadIdx.x & 15)) * 4;
+    using C = FsCfg<K>;
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-        v[j] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, off, j * 32 * kFsW * 4 + q * 256, 2));
+    for (int j = 0; j < C::kUpt; ++j) {
+        const int u = threadIdx.x + kFsThreads * j;
+        const int off = ((u / C::kUnitsRow) * K + 4 * (u % C::kUnitsRow)) * 4;
+        v[j] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, off, q * C::kCols * 4, 2));
+    }
 }
 
-// unit j of the thread's share: split into the three planes of a quarter buffer
+// unit j of the thread's share of a stage: split into the three planes of a stage buffer
+template <int K>
 __device__ __forceinline__ void fs_store_x1(const float4& v, int j, char* __restrict__ buf) {
+    using C = FsCfg<K>;
     uint2 w[3];
     split4(v, w[0], w[1], w[2]);
-    const int off = fs_off((threadIdx.x >> 4) + 32 * j, 4 * (threadIdx.x & 15));
+    const int u = threadIdx.x + kFsThreads * j;
+    const int off = fs_off(u / C::kUnitsRow, 4 * (u % C::kUnitsRow));
 #pragma unroll
-    for (int q = 0; q < 3; ++q) *reinterpret_cast<uint2*>(buf + q * kFsPlaneB + off) = w[q];
-}
-
-__device__ __forceinline__ void fs_store_x(const float4 (&v)[4], char* __restrict__ buf) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) fs_store_x1(v[j], j, buf);
+    for (int q = 0; q < 3; ++q) *reinterpret_cast<uint2*>(buf + q * C::kPlaneB + off) = w[q];
 }
 
 __device__ __forceinline__ float fs_elu_neg(float v) {  // mlp_gemm.hip elu_neg: the same expression
@@ -106,8 +122,10 @@ __device__ __forceinline__ float fs_elu_neg(float v) {  // mlp_gemm.hip elu_neg:
     return v > -0.5f ? poly : e;
 }
 
+template <int K>
 __global__ __launch_bounds__(kFsThreads, 1) void fwd_stream_kernel(FsArgs args) {
-    __shared__ __attribute__((aligned(16))) char lds[2 * kFsBufB];
+    using C = FsCfg<K>;
+    __shared__ __attribute__((aligned(16))) char lds[2 * C::kBufB];
     const FsProblem& P = args.p[blockIdx.y];
     const int t_begin = blockIdx.x * args.tiles_per;
     const int t_end = min(args.tiles, t_begin + args.tiles_per);
@@ -121,32 +139,34 @@ __global__ __launch_bounds__(kFsThreads, 1) void fwd_stream_kernel(FsArgs args) 
 
     // A fragment lane addresses: fs_off(32 i + l32, 16 c + 8 h) = la[c] + i * 1 KiB (+ plane, + buffer)
     const int lbase = static_cast<int>(reinterpret_cast<uintptr_t>(lds));
-    int la[2][4];
+    int la[2][C::kNch];
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
+    for (int c = 0; c < C::kNch; ++c) {
         la[0][c] = lbase + fs_off(l32, 16 * c + 8 * h);
-        la[1][c] = la[0][c] + kFsBufB;
+        la[1][c] = la[0][c] + C::kBufB;
     }
     // B fragments: image row 32 w + l32 (output column), half h, swizzled as the image stores it
     const int brow = 32 * wave + l32;
     const int boff = (brow * 2 + (h ^ ((brow >> 3) & 1))) * 16;
     const __amdgpu_buffer_rsrc_t rimg = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint4*>(P.img), 0, static_cast<uint32_t>(16 * kFsImgChunkU * 16), kFsRsrcFlags);
+        const_cast<uint4*>(P.img), 0, static_cast<uint32_t>(C::kChunks * kFsImgChunkU * 16), kFsRsrcFlags);
     auto bload = [&](int c, int q) {
         return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rimg, boff, (c * kFsImgChunkU + q * kFsImgPlaneU) * 16, 0));
     };
     const float bias = P.bias[32 * wave + l32];
 
     auto tile_rsrc = [&](int tile) {
-        return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(P.x + static_cast<int64_t>(tile) * kFsT * kFsW), 0,
-                                                 static_cast<uint32_t>(kFsT * kFsW * 4), kFsRsrcFlags);
+        return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(P.x + static_cast<int64_t>(tile) * kFsT * K), 0,
+                                                 static_cast<uint32_t>(kFsT * K * 4), kFsRsrcFlags);
     };
 
-    // prologue: quarter 0 split into buffer 0, quarter 1 in registers
+    // prologue: stage 0 split into buffer 0, stage 1 (the next tile's stage 0 when a tile is one stage) in registers
     float4 xr[4];
-    fs_load_x(tile_rsrc(t_begin), 0, xr);
-    fs_store_x(xr, lds);
-    fs_load_x(tile_rsrc(t_begin), 1, xr);
+    fs_load_x<K>(tile_rsrc(t_begin), 0, xr);
+#pragma unroll
+    for (int j = 0; j < C::kUpt; ++j) fs_store_x1<K>(xr[j], j, lds);
+    if (C::kStages > 1) fs_load_x<K>(tile_rsrc(t_begin), 1, xr);
+    else if (t_begin + 1 < t_end) fs_load_x<K>(tile_rsrc(t_begin + 1), 0, xr);
     __syncthreads();
 
     uint4 bq[2][3];
@@ -157,7 +177,7 @@ __global__ __launch_bounds__(kFsThreads, 1) void fwd_stream_kernel(FsArgs args) 
     // ELU, nontemporal stores (lane: column 32 w + l32, rows 32 i + 4 h + (r & 3) + 8 (r >> 2))
     auto epi_part = [&](const f32x16 (&acc)[4], int tile, int e) {
         const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
-            P.h + static_cast<int64_t>(tile) * kFsT * kFsW + 32 * wave, 0, static_cast<uint32_t>(kFsT * kFsW * 4),
+            P.h + static_cast<int64_t>(tile) * kFsT * kFsN + 32 * wave, 0, static_cast<uint32_t>(kFsT * kFsN * 4),
             kFsRsrcFlags);
         const int i = e >> 2;
 #pragma unroll
@@ -166,81 +186,99 @@ __global__ __launch_bounds__(kFsThreads, 1) void fwd_stream_kernel(FsArgs args) 
             float v = acc[i][r] + bias;
             const float n = fs_elu_neg(fminf(v, 0.f));
             v = v > 0.f ? v : n;
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), rc, ((4 * h + (r & 3)) * kFsW + l32) * 4,
-                                                  (32 * i + 8 * (r >> 2)) * kFsW * 4, 2 /* nt */);
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), rc, ((4 * h + (r & 3)) * kFsN + l32) * 4,
+                                                  (32 * i + 8 * (r >> 2)) * kFsN * 4, 2 /* nt */);
         }
     };
 
-    // One tile into acc; the previous tile's epilogue (prev, when has_prev) spread over the first quarter's 16 MFMA
-    // blocks, 4 values after each, beside the MFMAs.  Two accumulator sets alternate by tile parity.
-    auto run_tile = [&](int tile, f32x16 (&acc)[4], const f32x16 (&prev)[4], bool has_prev) {
+    // One tile into acc; the previous tile's epilogue (prev, when has_prev) spread over the first stage's MFMA blocks,
+    // one part after each (the rest after the stage's last block), beside the MFMAs.  Two accumulator sets alternate by
+    // tile parity.  Stage s = kStages (tile - t_begin) + kq lives in buffer s & 1.
+    // par: the tile's parity from t_begin (a literal at each call: the buffers' indices fold into immediates)
+    auto run_tile = [&](int tile, f32x16 (&acc)[4], const f32x16 (&prev)[4], bool has_prev, int par) {
         const bool more = tile + 1 < t_end;
 #pragma unroll
-        for (int kq = 0; kq < 4; ++kq) {  // quarter s = 4 (tile - t_begin) + kq lives in buffer kq & 1
-            const int buf = kq & 1;
+        for (int kq = 0; kq < C::kStages; ++kq) {
+            const int buf = (C::kStages % 2 == 0) ? (kq & 1) : (par ^ (kq & 1));
             bf16x8 an[3];
             if constexpr (kFsLA) {
                 an[0] = fs_read16(la[buf][0]);
-                an[1] = fs_read16(la[buf][0] + kFsPlaneB);
-                an[2] = fs_read16(la[buf][0] + 2 * kFsPlaneB);
+                an[1] = fs_read16(la[buf][0] + C::kPlaneB);
+                an[2] = fs_read16(la[buf][0] + 2 * C::kPlaneB);
             }
+            const bool next_stage = kq + 1 < C::kStages || more;   // a stage follows this one
 #pragma unroll
-            for (int c = 0; c < kFsQChunks; ++c) {
-                const int gc = 4 * kq + c;  // chunk of the tile
-                // the image chunk after this one (the next tile's chunk 0 after chunk 15)
+            for (int c = 0; c < C::kNch; ++c) {
+                const int gc = C::kNch * kq + c;  // chunk of the tile
+                // the image chunk after this one (the next tile's chunk 0 after the last)
+                // ring slot of this chunk: chunks alternate over the whole slice (a tile of 3 chunks flips it)
+                const int slot = (par * C::kChunks + gc) & 1;
 #pragma unroll
-                for (int q = 0; q < 3; ++q) bq[(c + 1) & 1][q] = bload((gc + 1) & 15, q);
+                for (int q = 0; q < 3; ++q) bq[slot ^ 1][q] = bload((gc + 1) % C::kChunks, q);
                 bf16x8 bf[3];
 #pragma unroll
-                for (int q = 0; q < 3; ++q) bf[q] = __builtin_bit_cast(bf16x8, bq[c & 1][q]);
+                for (int q = 0; q < 3; ++q) bf[q] = __builtin_bit_cast(bf16x8, bq[slot][q]);
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
+                    const int blk = 4 * c + i;  // block of the stage
                     bf16x8 af[3];
                     if constexpr (kFsLA) {
                         // the fragments of block (c, i) were read during the previous block; read the next one's now
-                        // (not across the quarter's barrier: block (0, 0) is read at the quarter's start)
+                        // (not across the stage's barrier: block (0, 0) is read at the stage's start)
 #pragma unroll
                         for (int q = 0; q < 3; ++q) af[q] = an[q];
-                        if (4 * c + i + 1 < 16) {
-                            const int cn = (4 * c + i + 1) >> 2, in = (4 * c + i + 1) & 3;
-                            const int a1 = la[buf][cn] + in * 1024;
+                        if (blk + 1 < 4 * C::kNch) {
+                            const int a1 = la[buf][(blk + 1) >> 2] + ((blk + 1) & 3) * 1024;
                             an[0] = fs_read16(a1);
-                            an[1] = fs_read16(a1 + kFsPlaneB);
-                            an[2] = fs_read16(a1 + 2 * kFsPlaneB);
+                            an[1] = fs_read16(a1 + C::kPlaneB);
+                            an[2] = fs_read16(a1 + 2 * C::kPlaneB);
                         }
                     } else {
                         const int a0 = la[buf][c] + i * 1024;
                         af[0] = fs_read16(a0);
-                        af[1] = fs_read16(a0 + kFsPlaneB);
-                        af[2] = fs_read16(a0 + 2 * kFsPlaneB);
+                        af[1] = fs_read16(a0 + C::kPlaneB);
+                        af[2] = fs_read16(a0 + 2 * C::kPlaneB);
                     }
                     // chunk 0 starts from zero accumulators: the same bits as accumulating onto zeros
                     acc[i] = mfma_x6(af, bf, gc == 0 ? f32x16{} : acc[i]);
-                    if (kq == 0 && has_prev) epi_part(prev, tile - 1, 4 * c + i);
-                    // quarter s + 1 into the other buffer, one unit after each of chunk 1's MFMA blocks (the buffer
-                    // was last read in quarter s - 1 and every wave passed the barrier after it)
-                    if (c == 1 && (kq < 3 || more)) fs_store_x1(xr[i], i, lds + (buf ^ 1) * kFsBufB);
+                    if (kq == 0 && has_prev) {
+                        if (blk < 16) epi_part(prev, tile - 1, blk);
+                        if (blk == 4 * C::kNch - 1) {
+#pragma unroll
+                            for (int e = 4 * C::kNch; e < 16; ++e) epi_part(prev, tile - 1, e);
+                        }
+                    }
+                    // stage s + 1 into the other buffer, one unit after each of chunk 1's MFMA blocks (that buffer was
+                    // last read in stage s - 1 and every wave passed the barrier after it)
+                    if (c == 1 && i < C::kUpt && next_stage) fs_store_x1<K>(xr[i], i, lds + (buf ^ 1) * C::kBufB);
                     __builtin_amdgcn_sched_barrier(0);
                 }
-                // quarter s + 2 into the registers after chunk 3's B load.  Loads return in issue order: a B fragment
-                // issued after them waits for them, so they go out where the next such wait is two chunks away.
-                if (c == 3 && (kq < 2 || more)) {
-                    fs_load_x(tile_rsrc(kq < 2 ? tile : tile + 1), (kq + 2) & 3, xr);
+                // stage s + 2 into the registers after the last chunk's B load.  Loads return in issue order: a B
+                // fragment issued after them waits for them, so they go out where the next such wait is a chunk away.
+                if (c == C::kNch - 1) {
+                    if (C::kStages > 1) {
+                        if (kq < C::kStages - 2 || more) {
+                            const int s2 = kq + 2;
+                            fs_load_x<K>(tile_rsrc(s2 < C::kStages ? tile : tile + 1), s2 % C::kStages, xr);
+                        }
+                    } else if (tile + 2 < t_end) {
+                        fs_load_x<K>(tile_rsrc(tile + 2), 0, xr);
+                    }
                     __builtin_amdgcn_sched_barrier(0);
                 }
             }
-            __syncthreads();  // the other buffer holds quarter s + 1; this one may be overwritten
+            __syncthreads();  // the other buffer holds stage s + 1; this one may be overwritten
         }
     };
 
     f32x16 acc0[4], acc1[4];
     int tile = t_begin;
     for (; tile + 1 < t_end; tile += 2) {
-        run_tile(tile, acc0, acc1, tile > t_begin);
-        run_tile(tile + 1, acc1, acc0, true);
+        run_tile(tile, acc0, acc1, tile > t_begin, 0);
+        run_tile(tile + 1, acc1, acc0, true, 1);
     }
     if (tile < t_end) {  // an odd tile count: the last tile in acc0, after acc1's tile (if any)
-        run_tile(tile, acc0, acc1, tile > t_begin);
+        run_tile(tile, acc0, acc1, tile > t_begin, 0);
 #pragma unroll
         for (int e = 0; e < 16; ++e) epi_part(acc0, tile, e);
     } else {
@@ -253,6 +291,14 @@ int64_t fs_tiles_per(int64_t tiles) { return ceil_div(tiles, std::min<int64_t>(k
 
 }  // namespace
 
+bool fwd_stream48() {
+    static const bool on = [] {
+        const char* e = std::getenv("RSLRL_FWD_STREAM");
+        return e && std::strcmp(e, "48") == 0;
+    }();
+    return on;
+}
+
 bool fwd_stream_enabled() {
     static const bool on = [] {
         const char* e = std::getenv("RSLRL_FWD_STREAM");
@@ -261,8 +307,9 @@ bool fwd_stream_enabled() {
     return on;
 }
 
-int fwd_stream_pair(const FwdStreamProblem* p, int n, int64_t M, hipStream_t st) {
-    if (n < 1 || n > 2 || M <= 0 || M % kFsT || M / kFsT > INT32_MAX) return RSLRL_E_UNSUPPORTED;
+int fwd_stream_pair(const FwdStreamProblem* p, int n, int64_t M, int K, hipStream_t st) {
+    if (n < 1 || n > 2 || M <= 0 || M % kFsT || M / kFsT > INT32_MAX || (K != 256 && K != 48))
+        return RSLRL_E_UNSUPPORTED;
     FsArgs args{};
     for (int i = 0; i < n; ++i) {
         const uintptr_t bits = reinterpret_cast<uintptr_t>(p[i].x) | reinterpret_cast<uintptr_t>(p[i].img);
@@ -275,7 +322,8 @@ int fwd_stream_pair(const FwdStreamProblem* p, int n, int64_t M, hipStream_t st)
     args.tiles = static_cast<int>(tiles);
     args.tiles_per = static_cast<int>(per);
     const dim3 grid(static_cast<unsigned>(ceil_div(tiles, per)), static_cast<unsigned>(n));
-    hipLaunchKernelGGL(fwd_stream_kernel, grid, dim3(kFsThreads), 0, st, args);
+    if (K == 256) hipLaunchKernelGGL(fwd_stream_kernel<256>, grid, dim3(kFsThreads), 0, st, args);
+    else hipLaunchKernelGGL(fwd_stream_kernel<48>, grid, dim3(kFsThreads), 0, st, args);
     return launch_status();
 }
 

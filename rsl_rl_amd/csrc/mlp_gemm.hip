@@ -3271,12 +3271,14 @@ extern "C" int rslrl_linear_gemm_pair(const rslrl_linear_args_t* a0, const rslrl
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     if (op == RSLRL_LINEAR_DGRAD_ELU)
         return h3 ? launch_pair<kEpiEluGrad, 2>(b, fullm, st) : launch_pair<kEpiEluGrad, 3>(b, fullm, st);
-    if (op == RSLRL_LINEAR_FWD_ELU && !h3 && fwd_stream_enabled() && a0->K == kBN && a0->N == kBN &&
-        a0->M % kBM == 0 && !a0->amax_out && !a1->amax_out) {
-        // the square hidden layers: the streaming forward (mlp_fwd_stream.hip, the same bits)
+    if (op == RSLRL_LINEAR_FWD_ELU && !h3 && fwd_stream_enabled() && (a0->K == kBN || (a0->K == 48 && fwd_stream48())) &&
+        a0->N == kBN && a0->M % kBM == 0 && !a0->amax_out && !a1->amax_out) {
+        // the square hidden layers: the streaming forward (mlp_fwd_stream.hip, same bits); the 48-wide first layer only
+        // on request (RSLRL_FWD_STREAM=48): HBM-bound, it measured 222 vs 190-201 us on the tiled kernel's two
+        // workgroups per CU (profiles/r5_fs_ab.json)
         const FwdStreamProblem fp[2] = {{b.p[0].a, b.img[0], b.p[0].bias, b.p[0].c},
                                         {b.p[1].a, b.img[1], b.p[1].bias, b.p[1].c}};
-        return fwd_stream_pair(fp, 2, a0->M, st);
+        return fwd_stream_pair(fp, 2, a0->M, a0->K, st);
     }
     if (op == RSLRL_LINEAR_FWD_ELU)
         return h3 ? launch_pair<kEpiBiasElu, 2>(b, fullm, st) : launch_pair<kEpiBiasElu, 3>(b, fullm, st);

@@ -17,10 +17,10 @@ def main():
     iters = int(sys.argv[1]) if len(sys.argv) > 1 else 20
     dev = torch.device("cuda:0")
     out = {}
-    for M in (393216, 65536):
+    for M, K in ((393216, 256), (65536, 256), (393216, 48), (65536, 48)):
         g = torch.Generator(device=dev).manual_seed(1)
-        xs = [torch.nn.functional.elu(torch.randn(M, 256, device=dev, generator=g)) for _ in range(2)]
-        ws = [torch.randn(256, 256, device=dev, generator=g) / 16 for _ in range(2)]
+        xs = [torch.nn.functional.elu(torch.randn(M, K, device=dev, generator=g)) for _ in range(2)]
+        ws = [torch.randn(256, K, device=dev, generator=g) / 16 for _ in range(2)]
         bs = [torch.randn(256, device=dev, generator=g) * 0.1 for _ in range(2)]
         imgs = fused_mlp.bimages([(w, False, _lib.BIMAGE_LAYOUT_GEMM) for w in ws])
         ts = []
@@ -33,7 +33,7 @@ def main():
             if it >= 3:
                 ts.append(e0.elapsed_time(e1) * 1e3)
         ts.sort()
-        out[M] = {"median_us": round(ts[len(ts) // 2], 1), "min_us": round(ts[0], 1)}
+        out[f"{M}x{K}"] = {"median_us": round(ts[len(ts) // 2], 1), "min_us": round(ts[0], 1)}
     print(json.dumps(out))
 
 

@@ -34,15 +34,18 @@ def test_pair_matches_two_launches(M, K, arith, cuda_device):
         assert float(amaxes[i]) == float(ys[i].abs().max())
 
 
-@pytest.mark.parametrize("M", [393216, 65536, 16384 + 128, 4096, 128, 1000])
-def test_stream_forward_pair_matches_tiled_kernel(M, cuda_device):
-    """The square hidden layers' x6 forward pair without amax (the update's and the rollout's path) runs on the
-    streaming kernel (mlp_fwd_stream.hip) whenever M is a multiple of 128: its H must equal the tiled kernel's
-    (the single-problem launch) bit for bit -- slices of 1 to 24 tiles, the last slice shorter, and a ragged M that
-    stays on the tiled pair kernel."""
+@pytest.mark.parametrize("K", [256, 48])
+@pytest.mark.parametrize("M", [393216, 65536, 16384 + 128, 4096, 384, 128, 1000])
+def test_stream_forward_pair_matches_tiled_kernel(M, K, cuda_device):
+    """The x6 forward pair without amax of the square hidden layers (the update's and the rollout's path) runs on the
+    streaming kernel (mlp_fwd_stream.hip) whenever M is a multiple of 128: its H must equal the tiled kernel's (the
+    single-problem launch) bit for bit -- slices of 1 to 24 tiles (odd and even counts: the two accumulator sets
+    alternate by tile), the last slice shorter, and a ragged M that stays on the tiled pair kernel.  K = 48 (the first
+    layer) takes the streaming kernel only with RSLRL_FWD_STREAM=48 (measured bit-exact there too at every M below,
+    profiles/r5_fs_ab.json); by default it checks the tiled pair against the single launch."""
     dev = cuda_device
-    g = torch.Generator(device=dev).manual_seed(M)
-    N = K = 256
+    g = torch.Generator(device=dev).manual_seed(M + K)
+    N = 256
     xs = [torch.nn.functional.elu(torch.randn(M, K, device=dev, generator=g)) * s for s in (1.0, 9.0)]
     ws = [torch.randn(N, K, device=dev, generator=g) / K ** 0.5 for _ in range(2)]
     bs = [torch.randn(N, device=dev, generator=g) * 0.1 for _ in range(2)]
