@@ -18,6 +18,7 @@ struct FwdStreamProblem {
 };
 
 bool fwd_stream_enabled();  // RSLRL_FWD_STREAM=0 keeps the tiled kernel (A/B)
+bool fwd_stream_forced();   // RSLRL_FWD_STREAM=1 (or 48): every M, not only the sizes where it measured faster
 bool fwd_stream48();        // RSLRL_FWD_STREAM=48: the 48-wide first layer too (opt-in: slower, see the call site)
 int fwd_stream_pair(const FwdStreamProblem* p, int n, int64_t M, int K, hipStream_t st);  // K = 256 or 48
 

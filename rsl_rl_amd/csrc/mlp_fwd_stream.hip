@@ -291,6 +291,14 @@ int64_t fs_tiles_per(int64_t tiles) { return ceil_div(tiles, std::min<int64_t>(k
 
 }  // namespace
 
+bool fwd_stream_forced() {  // RSLRL_FWD_STREAM=1 or 48: every eligible M (tests, A/B)
+    static const bool on = [] {
+        const char* e = std::getenv("RSLRL_FWD_STREAM");
+        return e && (std::strcmp(e, "1") == 0 || std::strcmp(e, "48") == 0);
+    }();
+    return on;
+}
+
 bool fwd_stream48() {
     static const bool on = [] {
         const char* e = std::getenv("RSLRL_FWD_STREAM");

@@ -3271,8 +3271,14 @@ extern "C" int rslrl_linear_gemm_pair(const rslrl_linear_args_t* a0, const rslrl
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     if (op == RSLRL_LINEAR_DGRAD_ELU)
         return h3 ? launch_pair<kEpiEluGrad, 2>(b, fullm, st) : launch_pair<kEpiEluGrad, 3>(b, fullm, st);
-    if (op == RSLRL_LINEAR_FWD_ELU && !h3 && fwd_stream_enabled() && (a0->K == kBN || (a0->K == 48 && fwd_stream48())) &&
-        a0->N == kBN && a0->M % kBM == 0 && !a0->amax_out && !a1->amax_out) {
+    // streaming only where it measured faster (profiles/r5_fs_ab.json, medians of two processes each): M >= 196,608
+    // (393,216: 688-695 vs 706-708 us; 196,608: 307 vs 325-327) and M <= 16,384 (37 vs 40 us; one tile per
+    // workgroup); 65,536 and 98,304 rows stay tiled (106-108 vs 105-106, 155-157 vs 151-152)
+    const int64_t ftiles = a0->M / kBM;
+    const bool stream_m = ftiles >= 1536 || ftiles <= 128 || fwd_stream_forced();
+    if (op == RSLRL_LINEAR_FWD_ELU && !h3 && fwd_stream_enabled() && stream_m &&
+        (a0->K == kBN || (a0->K == 48 && fwd_stream48())) && a0->N == kBN && a0->M % kBM == 0 && !a0->amax_out &&
+        !a1->amax_out) {
         // the square hidden layers: the streaming forward (mlp_fwd_stream.hip, same bits); the 48-wide first layer only
         // on request (RSLRL_FWD_STREAM=48): HBM-bound, it measured 222 vs 190-201 us on the tiled kernel's two
         // workgroups per CU (profiles/r5_fs_ab.json)

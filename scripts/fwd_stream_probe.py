@@ -17,7 +17,8 @@ def main():
     iters = int(sys.argv[1]) if len(sys.argv) > 1 else 20
     dev = torch.device("cuda:0")
     out = {}
-    for M, K in ((393216, 256), (65536, 256), (393216, 48), (65536, 48)):
+    shapes = [(393216, 256), (196608, 256), (98304, 256), (65536, 256), (16384, 256)]
+    for M, K in shapes:
         g = torch.Generator(device=dev).manual_seed(1)
         xs = [torch.nn.functional.elu(torch.randn(M, K, device=dev, generator=g)) for _ in range(2)]
         ws = [torch.randn(256, K, device=dev, generator=g) / 16 for _ in range(2)]

@@ -35,12 +35,13 @@ def test_pair_matches_two_launches(M, K, arith, cuda_device):
 
 
 @pytest.mark.parametrize("K", [256, 48])
-@pytest.mark.parametrize("M", [393216, 65536, 16384 + 128, 4096, 384, 128, 1000])
+@pytest.mark.parametrize("M", [393216, 212992, 65536, 16384 + 128, 4096, 384, 128, 1000])
 def test_stream_forward_pair_matches_tiled_kernel(M, K, cuda_device):
     """The x6 forward pair without amax of the square hidden layers (the update's and the rollout's path) runs on the
-    streaming kernel (mlp_fwd_stream.hip) whenever M is a multiple of 128: its H must equal the tiled kernel's (the
-    single-problem launch) bit for bit -- slices of 1 to 24 tiles (odd and even counts: the two accumulator sets
-    alternate by tile), the last slice shorter, and a ragged M that stays on the tiled pair kernel.  K = 48 (the first
+    streaming kernel (mlp_fwd_stream.hip) when M is a multiple of 128 of >= 1536 or <= 128 tiles (65,536 and 16,512
+    rows stay on the tiled pair): its H must equal the tiled kernel's (the single-problem launch) bit for bit --
+    slices of 1, 13 and 24 tiles (odd and even counts: the two accumulator sets alternate by tile), the last slice
+    shorter, and a ragged M that stays on the tiled pair kernel.  K = 48 (the first
     layer) takes the streaming kernel only with RSLRL_FWD_STREAM=48 (measured bit-exact there too at every M below,
     profiles/r5_fs_ab.json); by default it checks the tiled pair against the single launch."""
     dev = cuda_device
