@@ -57,7 +57,7 @@ PMC_TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r5_pmc_traffic.json")
 MLP_PMC_FILE = os.path.join(ROOT, "profiles", "r5_mlp_pmc.json")
 MLP_PMC_NAMES = {"linear_hidden_bwd_pair[M=393216,N=256,K=256]": "x6_hidden_bwd_pair",
                  "linear_dgrad_pair[M=393216,Nred=256,K=256]": "x6_dgrad_pair_w4",
-                 "linear_fwd_pair[M=393216,K=256,N=256]": "x6_fwd_elu_pair",
+                 "linear_fwd_pair[M=393216,K=256,N=256]": "x6_fwd_stream_pair",
                  "linear_wgrad_pair[M=393216,N=256,K=256]": "x6_wgrad_pair"}
 
 

@@ -22,6 +22,7 @@ from collections import defaultdict
 CAL_BYTES = 512 << 20
 SHORT = [
     (r"hidden_bwd_kernel", "x6_hidden_bwd_pair"),
+    (r"fwd_stream_kernel", "x6_fwd_stream_pair"),
     (r"mlp_gemm_x6_w4_pair_kernel<2>", "x6_dgrad_pair_w4"),
     (r"mlp_gemm_x6_w4s_pair_kernel<2>", "x6_dgrad_pair_w4s"),
     (r"mlp_gemm_x6_pair_kernel<1,", "x6_fwd_elu_pair"),
@@ -37,6 +38,7 @@ SHORT = [
 # algorithmic HBM bytes per launch at M rows (both problems of a pair): what each kernel must move at least
 ALGO = {
     "x6_fwd_elu_pair": lambda M: 2 * (M * 256 * 4 * 2),           # X read, H written
+    "x6_fwd_stream_pair": lambda M: 2 * (M * 256 * 4 * 2),
     "x6_dgrad_pair_w4": lambda M: 2 * (M * 256 * 4 * 3),          # dZ, H read, dZ_prev written
     "x6_dgrad_pair_w4s": lambda M: 2 * (M * 256 * 4 * 3),
     "x6_dgrad_pair": lambda M: 2 * (M * 256 * 4 * 3),
@@ -49,6 +51,7 @@ FLOPS["x6_hidden_bwd_pair"] = lambda M: 2 * 2 * 2 * M * 256 * 256  # two GEMMs p
 # which calibration pattern each kernel's traffic follows: (reads, writes)
 PATTERN = {
     "x6_fwd_elu_pair": ("cal_read_gemm_a", "cal_write_c_b32_nt"),
+    "x6_fwd_stream_pair": ("cal_read_v4", "cal_write_c_b32_nt"),
     "x6_dgrad_pair_w4": ("cal_read_gemm_a+cal_read_c_b32", "cal_write_c_b32_nt"),
     "x6_dgrad_pair": ("cal_read_gemm_a+cal_read_c_b32", "cal_write_c_b32_nt"),
     "x6_wgrad_pair": ("cal_read_v4", "cal_write_v4"),
