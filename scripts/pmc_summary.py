@@ -20,6 +20,7 @@ SHORT = {
     "ppo_loss_kernel": "ppo_loss",
     "ppo_loss_quad_kernel": "ppo_loss",
     "gae_scan_kernel": "gae_scan",
+    "gae_fused_slots_kernel": "compute_returns_one_launch",
     "adv_normalize_kernel": "adv_normalize",
     "adv_normalize_slot_kernel": "adv_normalize_slot",
     "adv_normalize_slots_kernel": "adv_normalize_slots",
