@@ -23,6 +23,10 @@
 // round-to-nearest intrinsics in the reference's evaluation order (Python left-to-right:
 // (nnt*gamma)*next_v, ((nnt*gamma)*lam)*adv), and advantages = returns - values exactly as :145.
 
+#include <atomic>
+#include <cstdlib>
+#include <mutex>
+
 #include "common.h"
 
 namespace rslrl {
@@ -423,22 +427,30 @@ __global__ __launch_bounds__(kBlock) void gae_fused_slots_kernel(
 
 // blocks of gae_fused_slots_kernel<T> the device holds at once (0: no fused instance for T)
 int gae_fused_capacity(int T) {
-    static int cap[4] = {-1, -1, -1, -1};
+    // per device (the current one) and T, computed once; concurrent first calls compute the same value
+    constexpr int kMaxDev = 64;
+    static std::atomic<int> cap[kMaxDev][4];
+    static std::once_flag init;
+    std::call_once(init, [] {
+        for (auto& d : cap)
+            for (auto& c : d) c.store(-1, std::memory_order_relaxed);
+    });
     const int k = T == 8 ? 0 : T == 16 ? 1 : T == 24 ? 2 : T == 32 ? 3 : -1;
-    if (k < 0) return 0;
-    if (cap[k] < 0) {
-        int dev = 0, cus = 0, per = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-            cus = 0;
+    int dev = 0;
+    if (k < 0 || hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return 0;
+    int c = cap[dev][k].load(std::memory_order_relaxed);
+    if (c < 0) {
+        int cus = 0, per = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 0;
         const void* f = k == 0 ? reinterpret_cast<const void*>(&gae_fused_slots_kernel<8>)
                         : k == 1 ? reinterpret_cast<const void*>(&gae_fused_slots_kernel<16>)
                         : k == 2 ? reinterpret_cast<const void*>(&gae_fused_slots_kernel<24>)
                                  : reinterpret_cast<const void*>(&gae_fused_slots_kernel<32>);
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, f, kBlock, 0) != hipSuccess) per = 0;
-        cap[k] = per * cus;
+        c = per * cus;
+        cap[dev][k].store(c, std::memory_order_relaxed);
     }
-    return cap[k];
+    return c;
 }
 
 template <int TMAX>
