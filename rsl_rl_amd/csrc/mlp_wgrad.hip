@@ -28,7 +28,10 @@ namespace {
 constexpr int kThreadsW = 512;
 constexpr int kMC = 16;  // rows of m per chunk (one MFMA k step)
 constexpr int kTK = 256;
-constexpr int kWgradDepth = 2;  // chunks of look-ahead in registers (full tiles)
+#ifndef RSLRL_WGRAD_DEPTH
+#define RSLRL_WGRAD_DEPTH 2
+#endif
+constexpr int kWgradDepth = RSLRL_WGRAD_DEPTH;  // chunks of look-ahead in registers (full tiles): 2 or 4
 
 using s16x4 = __attribute__((ext_vector_type(4))) short;
 
@@ -229,13 +232,21 @@ __device__ __forceinline__ void wgrad_x6_body(const WgradParams& p) {
             // only the LDS writes must retire before the barrier (not the look-ahead loads)
             asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
         };
-        static_assert(D == 2, "the host guarantees an even chunk count >= 2 for full tiles");
+        static_assert(D == 2 || D == 4, "the host guarantees a chunk count that is a multiple of D >= 2");
         int c0 = 0;
         for (; c0 + D < nchunks; c0 += D) {
             step(std::integral_constant<int, 0>{}, c0);
             step(std::integral_constant<int, 1>{}, c0 + 1);
+            if constexpr (D == 4) {
+                step(std::integral_constant<int, 2>{}, c0 + 2);
+                step(std::integral_constant<int, 3>{}, c0 + 3);
+            }
         }
         step(std::integral_constant<int, 0>{}, c0);
+        if constexpr (D == 4) {
+            step(std::integral_constant<int, 1>{}, c0 + 1);
+            step(std::integral_constant<int, 2>{}, c0 + 2);
+        }
         compute(lds[1]);
     } else {
     float4 va[perA], vb[perB];
