@@ -19,7 +19,7 @@ import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 # RSLRL_AMD_LIB: an alternative in-tree build of the same library (A/B kernel experiments)
 LIB_PATH = os.environ.get("RSLRL_AMD_LIB") or os.path.join(LIB_DIR, "librslrl_amd.so")
-ABI_VERSION = 16
+ABI_VERSION = 17
 
 # symbols declared in include/rslrl_amd.h (tests/test_capi.py checks the header against this list)
 EXPORTED_SYMBOLS = (
@@ -63,6 +63,7 @@ EXPORTED_SYMBOLS = (
     "rslrl_linear_gemm",
     "rslrl_linear_gemm_pair",
     "rslrl_value_head_fwd_bwd",
+    "rslrl_value_head_partial_rows",
     "rslrl_actor_head_workspace_bytes",
     "rslrl_actor_head_fwd_bwd",
     "rslrl_linear_wgrad_ex",
@@ -456,6 +457,8 @@ def _declare(L):
     L.rslrl_linear_gemm_pair.argtypes = [ctypes.POINTER(LinearArgs), ctypes.POINTER(LinearArgs), P]
     L.rslrl_value_head_fwd_bwd.restype = ctypes.c_int
     L.rslrl_value_head_fwd_bwd.argtypes = [ctypes.POINTER(LinearArgs), ctypes.POINTER(ValueHeadArgs), P]
+    L.rslrl_value_head_partial_rows.restype = ctypes.c_int64
+    L.rslrl_value_head_partial_rows.argtypes = [ctypes.c_int64]
     L.rslrl_actor_head_workspace_bytes.restype = ctypes.c_size_t
     L.rslrl_actor_head_workspace_bytes.argtypes = [I64]
     L.rslrl_actor_head_fwd_bwd.restype = ctypes.c_int

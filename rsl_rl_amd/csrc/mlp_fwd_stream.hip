@@ -25,6 +25,7 @@
 
 #include "common.h"
 #include "fwd_stream.h"
+#include "ppo_loss_common.h"
 #include "x6_split.h"
 
 namespace rslrl {
@@ -287,6 +288,222 @@ __global__ __launch_bounds__(kFsThreads, 1) void fwd_stream_kernel(FsArgs args) 
     }
 }
 
+
+// ---- The critic's head on the streaming main loop (round 5, opt-in: RSLRL_VALUE_HEAD_STREAM=1) ----------------------
+// rslrl_value_head_fwd_bwd's computation -- H = ELU(X W^T + b) of the last hidden layer, V = H w_v + b_v, dV = d(value
+// loss)/dV (value_loss_grad: the loss kernel's expression), dZ = (dV w_v) * ELU'(H) and the head's [dW | db] -- with
+// the main loop of fwd_stream_kernel<256> on C^T accumulators (lane: row 32 i + l32, columns 8 g + 4 h + k of the
+// wave's 32; the tiled value head's orientation and MFMA order, so H has its bits).  V sums each wave's 32 columns
+// (16 per lane in one fma chain, then the other lane half) and the 8 waves in order: a different association than the
+// tiled head's 4 x 64 columns (fp32 reassociation; V, dV and dZ agree to rounding).  The [dW | db] partials are one
+// row per slice (rows = rslrl_value_head_stream_rows(M)), accumulated in registers across the slice's tiles.
+struct VhArgs {
+    const float* x;      // [M, 256] the critic's last hidden input
+    const uint4* img;    // x6 image of W (layout 0)
+    const float* bias;   // [256]
+    const float* wv;     // [256] value weights
+    float bv;            // value bias (read by the host from nothing: passed as a device pointer below)
+    const float* bvp;    // [1] value bias (device)
+    const float* tv;     // [M] target values
+    const float* ret;    // [M] returns
+    float* dz;           // [M, 256]
+    float* y;            // [M] values
+    float* wpart;        // [slices][kVhP]
+    float clip, g;
+    int clipped;
+    int tiles, tiles_per;
+};
+constexpr int kVhP = 260;  // [dW (256) | db | pad 3]
+
+__global__ __launch_bounds__(kFsThreads, 1) void value_head_stream_kernel(VhArgs a) {
+    using C = FsCfg<256>;
+    __shared__ __attribute__((aligned(16))) char lds[2 * C::kBufB];
+    __shared__ float red[8 * kFsT];   // per wave: its 32 columns' share of V, per row
+    __shared__ float dvl[kFsT];       // dV per row
+    __shared__ float dbred[kFsT / 64];
+    const int t_begin = blockIdx.x * a.tiles_per;
+    const int t_end = min(a.tiles, t_begin + a.tiles_per);
+    if (t_begin >= t_end) return;
+
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+    const int h = lane >> 5;
+    const int l32 = lane & 31;
+
+    const int lbase = static_cast<int>(reinterpret_cast<uintptr_t>(lds));
+    int la[2][C::kNch];
+#pragma unroll
+    for (int c = 0; c < C::kNch; ++c) {
+        la[0][c] = lbase + fs_off(l32, 16 * c + 8 * h);
+        la[1][c] = la[0][c] + C::kBufB;
+    }
+    const int brow = 32 * wave + l32;
+    const int boff = (brow * 2 + (h ^ ((brow >> 3) & 1))) * 16;
+    const __amdgpu_buffer_rsrc_t rimg = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint4*>(a.img), 0, static_cast<uint32_t>(C::kChunks * kFsImgChunkU * 16), kFsRsrcFlags);
+    auto bload = [&](int c, int q) {
+        return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rimg, boff, (c * kFsImgChunkU + q * kFsImgPlaneU) * 16, 0));
+    };
+    // this lane's 16 columns 32 w + 8 g + 4 h + k (r = 4 g + k): bias and value weights, fixed for the slice
+    float bcol[16], wcol[16];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        const float4 b4 = *reinterpret_cast<const float4*>(a.bias + 32 * wave + 8 * g + 4 * h);
+        const float4 w4 = *reinterpret_cast<const float4*>(a.wv + 32 * wave + 8 * g + 4 * h);
+        bcol[4 * g] = b4.x; bcol[4 * g + 1] = b4.y; bcol[4 * g + 2] = b4.z; bcol[4 * g + 3] = b4.w;
+        wcol[4 * g] = w4.x; wcol[4 * g + 1] = w4.y; wcol[4 * g + 2] = w4.z; wcol[4 * g + 3] = w4.w;
+    }
+    const float bv = *a.bvp;
+    auto tile_rsrc = [&](int tile) {
+        return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.x + static_cast<int64_t>(tile) * kFsT * 256), 0,
+                                                 static_cast<uint32_t>(kFsT * 256 * 4), kFsRsrcFlags);
+    };
+
+    float4 xr[4];
+    fs_load_x<256>(tile_rsrc(t_begin), 0, xr);
+#pragma unroll
+    for (int j = 0; j < C::kUpt; ++j) fs_store_x1<256>(xr[j], j, lds);
+    fs_load_x<256>(tile_rsrc(t_begin), 1, xr);
+    __syncthreads();
+
+    uint4 bq[2][3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) bq[0][q] = bload(0, q);
+
+    float wacc[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) wacc[r] = 0.f;
+    float dbacc = 0.f;  // threads < 128: this row position's dV over the slice's tiles
+
+    for (int tile = t_begin; tile < t_end; ++tile) {
+        const bool more = tile + 1 < t_end;
+        const int64_t row0 = static_cast<int64_t>(tile) * kFsT;
+        f32x16 acc[4];
+#pragma unroll
+        for (int kq = 0; kq < 4; ++kq) {
+            const int buf = kq & 1;
+            bf16x8 an[3];
+            an[0] = fs_read16(la[buf][0]);
+            an[1] = fs_read16(la[buf][0] + C::kPlaneB);
+            an[2] = fs_read16(la[buf][0] + 2 * C::kPlaneB);
+#pragma unroll
+            for (int c = 0; c < C::kNch; ++c) {
+                const int gc = C::kNch * kq + c;
+                const int slot = gc & 1;
+#pragma unroll
+                for (int q = 0; q < 3; ++q) bq[slot ^ 1][q] = bload((gc + 1) % C::kChunks, q);
+                bf16x8 bf[3];
+#pragma unroll
+                for (int q = 0; q < 3; ++q) bf[q] = __builtin_bit_cast(bf16x8, bq[slot][q]);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int blk = 4 * c + i;
+                    bf16x8 af[3];
+#pragma unroll
+                    for (int q = 0; q < 3; ++q) af[q] = an[q];
+                    if (blk + 1 < 4 * C::kNch) {
+                        const int a1 = la[buf][(blk + 1) >> 2] + ((blk + 1) & 3) * 1024;
+                        an[0] = fs_read16(a1);
+                        an[1] = fs_read16(a1 + C::kPlaneB);
+                        an[2] = fs_read16(a1 + 2 * C::kPlaneB);
+                    }
+                    // C^T: the weight fragment is the A operand (rows = output columns)
+                    acc[i] = mfma_x6(bf, af, gc == 0 ? f32x16{} : acc[i]);
+                    if (c == 1 && i < C::kUpt && (kq < 3 || more)) fs_store_x1<256>(xr[i], i, lds + (buf ^ 1) * C::kBufB);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+                if (c == C::kNch - 1) {
+                    if (kq < 2 || more) fs_load_x<256>(tile_rsrc(kq < 2 ? tile : tile + 1), (kq + 2) & 3, xr);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+            __syncthreads();
+        }
+        // ---- the head's epilogue (the next tile's first quarter is in buffer 0 already)
+        float tvr = 0.f, retr = 0.f;
+        if (threadIdx.x < kFsT) {
+            tvr = a.tv[row0 + threadIdx.x];
+            retr = a.ret[row0 + threadIdx.x];
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            float oval = 0.f;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float tt = acc[i][r] + bcol[r];
+                const float n = fs_elu_neg(fminf(tt, 0.f));
+                const float hv = tt > 0.f ? tt : n;
+                acc[i][r] = hv;
+                oval = fmaf(hv, wcol[r], oval);
+            }
+            const float tsum = oval + __shfl_xor(oval, 32, 64);
+            if (h == 0) red[wave * kFsT + 32 * i + l32] = tsum;
+        }
+        __syncthreads();
+        if (threadIdx.x < kFsT) {
+            const int rl = threadIdx.x;
+            float V = red[rl];
+#pragma unroll
+            for (int w = 1; w < 8; ++w) V += red[w * kFsT + rl];
+            V += bv;
+            a.y[row0 + rl] = V;
+            const float dV = value_loss_grad(V, tvr, retr, a.clipped, a.clip, a.g);
+            dvl[rl] = dV;
+            dbacc += dV;
+        }
+        __syncthreads();
+        float* dzt = a.dz + row0 * 256 + 32 * wave + 4 * h;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const float dv = dvl[32 * i + l32];
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                float o[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const int r = 4 * g + k;
+                    const float hh = acc[i][r];
+                    const float z = __fmaf_rn(dv, wcol[r], 0.f);  // out_bwd_valu_body's fma chain of one term
+                    o[k] = hh > 0.f ? z : z * (hh + 1.f);          // ELU'(x) = 1 if h > 0 else h + 1
+                    wacc[r] = fmaf(dv, hh, wacc[r]);
+                }
+                const f32x4 ov = {o[0], o[1], o[2], o[3]};
+                __builtin_nontemporal_store(ov, reinterpret_cast<f32x4*>(dzt + (32 * i + l32) * 256 + 8 * g));
+            }
+        }
+        // dvl / red are rewritten only after the next tile's four quarter barriers
+    }
+    // ---- the slice's partial row: dW over the 32 row lanes (fixed butterfly), db over the 128 row positions
+    float* wp = a.wpart + static_cast<int64_t>(blockIdx.x) * kVhP;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        float v = wacc[r];
+#pragma unroll
+        for (int off = 1; off < 32; off <<= 1) v += __shfl_xor(v, off, 64);
+        wacc[r] = v;
+    }
+    if (l32 == 0) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+            *reinterpret_cast<float4*>(wp + 32 * wave + 8 * g + 4 * h) =
+                make_float4(wacc[4 * g], wacc[4 * g + 1], wacc[4 * g + 2], wacc[4 * g + 3]);
+    }
+    if (threadIdx.x < kFsT) {
+        float v = dbacc;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) v += __shfl_xor(v, off, 64);
+        if (lane == 0) dbred[wave] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        wp[256] = dbred[0] + dbred[1];
+        wp[257] = 0.f;
+        wp[258] = 0.f;
+        wp[259] = 0.f;
+    }
+}
+
 int64_t fs_tiles_per(int64_t tiles) { return ceil_div(tiles, std::min<int64_t>(kFsMaxSlices, tiles)); }
 
 }  // namespace
@@ -335,4 +552,48 @@ int fwd_stream_pair(const FwdStreamProblem* p, int n, int64_t M, int K, hipStrea
     return launch_status();
 }
 
+
+int value_head_stream(const ValueHeadStreamArgs& v, hipStream_t st) {
+    if (v.M <= 0 || v.M % kFsT || v.M / kFsT > INT32_MAX) return RSLRL_E_UNSUPPORTED;
+    const uintptr_t bits = reinterpret_cast<uintptr_t>(v.x) | reinterpret_cast<uintptr_t>(v.img) |
+                           reinterpret_cast<uintptr_t>(v.bias) | reinterpret_cast<uintptr_t>(v.wv) |
+                           reinterpret_cast<uintptr_t>(v.dz) | reinterpret_cast<uintptr_t>(v.wpart);
+    if (bits & 15) return RSLRL_E_MISALIGNED;
+    const int64_t tiles = v.M / kFsT;
+    const int64_t per = ceil_div(tiles, std::min<int64_t>(2 * kFsMaxSlices, tiles));
+    VhArgs a{};
+    a.x = v.x;
+    a.img = static_cast<const uint4*>(v.img);
+    a.bias = v.bias;
+    a.wv = v.wv;
+    a.bvp = v.bv;
+    a.tv = v.tv;
+    a.ret = v.ret;
+    a.dz = v.dz;
+    a.y = v.y;
+    a.wpart = v.wpart;
+    a.clip = v.clip;
+    a.g = v.g;
+    a.clipped = v.clipped;
+    a.tiles = static_cast<int>(tiles);
+    a.tiles_per = static_cast<int>(per);
+    hipLaunchKernelGGL(value_head_stream_kernel, dim3(static_cast<unsigned>(ceil_div(tiles, per))), dim3(kFsThreads), 0,
+                       st, a);
+    return launch_status();
+}
+
+int64_t value_head_stream_rows(int64_t M) {
+    if (M <= 0 || M % kFsT) return 0;
+    const int64_t tiles = M / kFsT;
+    const int64_t per = ceil_div(tiles, std::min<int64_t>(2 * kFsMaxSlices, tiles));
+    return ceil_div(tiles, per);
+}
+
+bool value_head_stream_enabled() {
+    static const bool on = [] {
+        const char* e = std::getenv("RSLRL_VALUE_HEAD_STREAM");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
 }  // namespace rslrl

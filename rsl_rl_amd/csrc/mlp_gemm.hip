@@ -106,27 +106,6 @@ struct ActorParams {
     int clipped_value, compute_kl, kl_fast;
 };
 
-// d(loss)/dV of one sample (ppo.py:305-313, :367 backward): the loss kernel's expression and operation order
-// (ppo_loss.hip, ppo_loss_quad_kernel; both compiled with -ffp-contract=off), so both produce the same bits.
-__device__ __forceinline__ float value_loss_grad(float V, float tv, float R, int clipped, float clip, float g_value) {
-    if (clipped) {
-        const float dv = V - tv;
-        const float vc = tv + fminf(fmaxf(dv, -clip), clip);
-        const float e1 = V - R;
-        const float e2 = vc - R;
-        const float vl = e1 * e1;
-        const float vlc = e2 * e2;
-        const float half = __fmul_rn(g_value, 0.5f);  // max(): ties split the gradient 1/2 : 1/2
-        const float g1 = (vl > vlc) ? g_value : ((vl == vlc) ? half : 0.0f);
-        const float g2 = (vlc > vl) ? g_value : ((vl == vlc) ? half : 0.0f);
-        float dV = 2.0f * g1 * e1;
-        if (dv >= -clip && dv <= clip) dV += 2.0f * g2 * e2;
-        return dV;
-    }
-    const float e = R - V;
-    return -2.0f * g_value * e;
-}
-
 // global -> registers for one K chunk: A: 128 x 16 floats = 512 float4 (1 per thread); B: 256 x 16 = 1024
 // float4 (2 per thread, only the first N rows real).  Rows >= M / N and k >= K read as zero.
 struct Stage {
@@ -3125,9 +3104,19 @@ extern "C" int rslrl_value_head_fwd_bwd(const rslrl_linear_args_t* a, const rslr
     if (a->M == 0) return RSLRL_OK;
     const int64_t tiles = ceil_div(a->M, kBM);
     if (tiles > INT32_MAX) return RSLRL_E_INVALID_ARGUMENT;
+    if (value_head_stream_enabled() && !v->colsum_partials) {  // opt-in: the streaming main loop (mlp_fwd_stream.hip)
+        const ValueHeadStreamArgs s{p.a, a->bimage, p.bias, v->out_weight, p.obias, v->target_values, v->returns,
+                                    a->c, p.y, v->wgrad_partials, p.vh_clip, p.vh_g, p.vh_clipped, a->M};
+        return value_head_stream(s, reinterpret_cast<hipStream_t>(stream));
+    }
     hipLaunchKernelGGL(mlp_gemm_x6_value_head_kernel, dim3(static_cast<unsigned>(tiles)), dim3(kThreads), 0,
                        reinterpret_cast<hipStream_t>(stream), p, static_cast<const uint4*>(a->bimage));
     return launch_status();
+}
+
+extern "C" int64_t rslrl_value_head_partial_rows(int64_t M) {
+    if (M <= 0) return 0;
+    return value_head_stream_enabled() ? value_head_stream_rows(M) : ceil_div(M, kBM);
 }
 
 // The actor's last hidden layer, output layer, the PPO loss and the output layer's backward in one launch

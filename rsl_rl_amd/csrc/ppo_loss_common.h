@@ -122,5 +122,26 @@ __device__ __forceinline__ bool fold_grid_partials(double* __restrict__ partials
     return true;
 }
 
+// d(loss)/dV of one sample (ppo.py:305-313, :367 backward): the loss kernel's expression and operation order
+// (ppo_loss.hip, ppo_loss_quad_kernel; both compiled with -ffp-contract=off), so both produce the same bits.
+__device__ __forceinline__ float value_loss_grad(float V, float tv, float R, int clipped, float clip, float g_value) {
+    if (clipped) {
+        const float dv = V - tv;
+        const float vc = tv + fminf(fmaxf(dv, -clip), clip);
+        const float e1 = V - R;
+        const float e2 = vc - R;
+        const float vl = e1 * e1;
+        const float vlc = e2 * e2;
+        const float half = __fmul_rn(g_value, 0.5f);  // max(): ties split the gradient 1/2 : 1/2
+        const float g1 = (vl > vlc) ? g_value : ((vl == vlc) ? half : 0.0f);
+        const float g2 = (vlc > vl) ? g_value : ((vl == vlc) ? half : 0.0f);
+        float dV = 2.0f * g1 * e1;
+        if (dv >= -clip && dv <= clip) dV += 2.0f * g2 * e2;
+        return dV;
+    }
+    const float e = R - V;
+    return -2.0f * g_value * e;
+}
+
 }  // namespace
 }  // namespace rslrl

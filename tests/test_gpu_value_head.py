@@ -4,6 +4,10 @@ head's backward in one launch) against the separate launches it replaces: the fu
 (linear_dgrad_elu_wgrad).  Values and the last hidden layer's dz are bit-identical; the head's weight and bias
 gradients are sums over the rows in another order (fp32-close).  Then a whole PPO.update() with and without it."""
 
+import os
+import subprocess
+import sys
+
 import numpy as np
 import pytest
 import torch
@@ -12,6 +16,10 @@ from rsl_rl_amd import _lib, kernels
 from rsl_rl_amd.networks import fused_mlp
 
 pytestmark = pytest.mark.gpu
+
+
+def L_rows(M):
+    return _lib.lib().rslrl_value_head_partial_rows(M)
 
 
 def _loss_dv(values, tv, ret, clipped, clip, coef, dev, g):
@@ -54,8 +62,14 @@ def test_value_head_matches_separate_launches(M, clipped, cuda_device):
     folds.add(wpart, wpart.shape[0], wpart.shape[1], dwb, N + 1)
     folds.run(dev)
     torch.cuda.synchronize()
-    assert torch.equal(y, y_ref)
-    assert torch.equal(dz, dz_ref)
+    if os.environ.get("RSLRL_VALUE_HEAD_STREAM") == "1":
+        # the streaming form sums V over 8 waves x 32 columns (fp32 reassociation): V, dV and dz to rounding
+        assert wpart.shape[0] == L_rows(M) and wpart.shape[0] < M // 128
+        assert torch.allclose(y, y_ref, rtol=1e-5, atol=1e-6 * float(y_ref.abs().max()))
+        assert torch.allclose(dz, dz_ref, rtol=1e-4, atol=1e-5 * float(dz_ref.abs().max()))
+    else:
+        assert torch.equal(y, y_ref)
+        assert torch.equal(dz, dz_ref)
     scale = float(dw_ref.abs().max()) + 1e-30
     assert torch.allclose(dwb[:N].view(1, N), dw_ref, rtol=1e-5, atol=1e-6 * scale)
     assert torch.allclose(dwb[N:], db_ref, rtol=1e-5, atol=1e-6 * float(db_ref.abs().max() + 1e-30))
@@ -116,3 +130,15 @@ def test_update_with_value_head_matches_separate_launches(cuda_device, monkeypat
         assert np.isclose(l1[k], l0[k], rtol=1e-4, atol=1e-7), k
     for k in p0:
         assert torch.allclose(p1[k], p0[k], rtol=1e-4, atol=2e-6), k
+
+
+def test_value_head_stream_form_in_a_child(cuda_device):
+    """The opt-in streaming form (RSLRL_VALUE_HEAD_STREAM=1, read once per process) against the same separate launches,
+    in a child process: V / dz to rounding, the per-slice partial rows fold to the head's dW / db."""
+    if os.environ.get("RSLRL_VALUE_HEAD_STREAM") == "1":
+        pytest.skip("this process already runs the streaming form")
+    env = dict(os.environ, RSLRL_VALUE_HEAD_STREAM="1")
+    r = subprocess.run([sys.executable, "-m", "pytest", "-x", "-q", "-p", "no:cacheprovider", __file__,
+                        "-k", "test_value_head_matches_separate_launches"],
+                       env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
