@@ -62,9 +62,10 @@ def test_value_head_matches_separate_launches(M, clipped, cuda_device):
     folds.add(wpart, wpart.shape[0], wpart.shape[1], dwb, N + 1)
     folds.run(dev)
     torch.cuda.synchronize()
-    if os.environ.get("RSLRL_VALUE_HEAD_STREAM") == "1":
-        # the streaming form sums V over 8 waves x 32 columns (fp32 reassociation): V, dV and dz to rounding
-        assert wpart.shape[0] == L_rows(M) and wpart.shape[0] < M // 128
+    if L_rows(M) < M // 128:
+        # the streaming form (one partial row per slice) sums V over 8 waves x 32 columns (fp32 reassociation): V, dV
+        # and dz to rounding
+        assert wpart.shape[0] == L_rows(M)
         assert torch.allclose(y, y_ref, rtol=1e-5, atol=1e-6 * float(y_ref.abs().max()))
         assert torch.allclose(dz, dz_ref, rtol=1e-4, atol=1e-5 * float(dz_ref.abs().max()))
     else:
@@ -132,12 +133,12 @@ def test_update_with_value_head_matches_separate_launches(cuda_device, monkeypat
         assert torch.allclose(p1[k], p0[k], rtol=1e-4, atol=2e-6), k
 
 
-def test_value_head_stream_form_in_a_child(cuda_device):
-    """The opt-in streaming form (RSLRL_VALUE_HEAD_STREAM=1, read once per process) against the same separate launches,
-    in a child process: V / dz to rounding, the per-slice partial rows fold to the head's dW / db."""
-    if os.environ.get("RSLRL_VALUE_HEAD_STREAM") == "1":
-        pytest.skip("this process already runs the streaming form")
-    env = dict(os.environ, RSLRL_VALUE_HEAD_STREAM="1")
+def test_value_head_other_form_in_a_child(cuda_device):
+    """The head's other form (RSLRL_VALUE_HEAD_STREAM, read once per process: the tiled kernel or the streaming main
+    loop) against the same separate launches, in a child process: the tiled form bit-exact, the streaming form's V / dz
+    to rounding and its per-slice partial rows folded to the head's dW / db."""
+    stream_here = L_rows(4096) < 4096 // 128
+    env = dict(os.environ, RSLRL_VALUE_HEAD_STREAM="0" if stream_here else "1")
     r = subprocess.run([sys.executable, "-m", "pytest", "-x", "-q", "-p", "no:cacheprovider", __file__,
                         "-k", "test_value_head_matches_separate_launches"],
                        env=env, capture_output=True, text=True, timeout=240)
