@@ -22,6 +22,11 @@ def L_rows(M):
     return _lib.lib().rslrl_value_head_partial_rows(M)
 
 
+def _stream_form():
+    """True when this process runs the head's streaming form: one partial row per slice (256 at C3, not 3072)."""
+    return L_rows(393216) < 393216 // 128
+
+
 def _loss_dv(values, tv, ret, clipped, clip, coef, dev, g):
     """The loss kernel's d loss / dV for these values (random actor-side inputs: they do not enter d/dV)."""
     B, A = values.shape[0], 12
@@ -62,7 +67,7 @@ def test_value_head_matches_separate_launches(M, clipped, cuda_device):
     folds.add(wpart, wpart.shape[0], wpart.shape[1], dwb, N + 1)
     folds.run(dev)
     torch.cuda.synchronize()
-    if L_rows(M) < M // 128:
+    if _stream_form():
         # the streaming form (one partial row per slice) sums V over 8 waves x 32 columns (fp32 reassociation): V, dV
         # and dz to rounding
         assert wpart.shape[0] == L_rows(M)
@@ -137,7 +142,7 @@ def test_value_head_other_form_in_a_child(cuda_device):
     """The head's other form (RSLRL_VALUE_HEAD_STREAM, read once per process: the tiled kernel or the streaming main
     loop) against the same separate launches, in a child process: the tiled form bit-exact, the streaming form's V / dz
     to rounding and its per-slice partial rows folded to the head's dW / db."""
-    stream_here = L_rows(4096) < 4096 // 128
+    stream_here = _stream_form()
     env = dict(os.environ, RSLRL_VALUE_HEAD_STREAM="0" if stream_here else "1")
     r = subprocess.run([sys.executable, "-m", "pytest", "-x", "-q", "-p", "no:cacheprovider", __file__,
                         "-k", "test_value_head_matches_separate_launches"],
