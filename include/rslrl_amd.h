@@ -437,8 +437,8 @@ typedef struct {
     float* colsum_partials; /* [M / 128][256] or NULL */
 } rslrl_value_head_args_t;
 int rslrl_value_head_fwd_bwd(const rslrl_linear_args_t* a, const rslrl_value_head_args_t* v, rslrl_stream_t stream);
-/* ABI 17: how many rows of wgrad_partials the call above fills (M / 128 for the tiled kernel; with the opt-in streaming
- * form, RSLRL_VALUE_HEAD_STREAM=1, one row per workgroup slice) -- the fold's row count. */
+/* ABI 17: how many rows of wgrad_partials the call above fills: one row per workgroup slice of the streaming form (the
+ * default since round 5; at most 256), M / 128 for the tiled kernel (RSLRL_VALUE_HEAD_STREAM=0) -- the fold's row count. */
 int64_t rslrl_value_head_partial_rows(int64_t M);
 
 /* The actor's last hidden layer, its 12-wide output layer (the action mean), the whole PPO loss of the mini-batch and

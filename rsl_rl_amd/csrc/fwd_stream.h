@@ -23,7 +23,7 @@ bool fwd_stream48();        // RSLRL_FWD_STREAM=48: the 48-wide first layer too 
 int fwd_stream_pair(const FwdStreamProblem* p, int n, int64_t M, int K, hipStream_t st);  // K = 256 or 48
 
 
-// the critic's fused head on the streaming main loop (opt-in: RSLRL_VALUE_HEAD_STREAM=1); rslrl_value_head_fwd_bwd's
+// the critic's fused head on the streaming main loop (default; RSLRL_VALUE_HEAD_STREAM=0: the tiled head); rslrl_value_head_fwd_bwd's
 // inputs and outputs, the [dW | db] partials one 260-float row per slice (value_head_stream_rows(M) rows)
 struct ValueHeadStreamArgs {
     const float* x;

@@ -289,7 +289,7 @@ __global__ __launch_bounds__(kFsThreads, 1) void fwd_stream_kernel(FsArgs args) 
 }
 
 
-// ---- The critic's head on the streaming main loop (round 5, opt-in: RSLRL_VALUE_HEAD_STREAM=1) ----------------------
+// ---- The critic's head on the streaming main loop (round 5; RSLRL_VALUE_HEAD_STREAM=0 keeps the tiled head) --------
 // rslrl_value_head_fwd_bwd's computation -- H = ELU(X W^T + b) of the last hidden layer, V = H w_v + b_v, dV = d(value
 // loss)/dV (value_loss_grad: the loss kernel's expression), dZ = (dV w_v) * ELU'(H) and the head's [dW | db] -- with
 // the main loop of fwd_stream_kernel<256> on C^T accumulators (lane: row 32 i + l32, columns 8 g + 4 h + k of the
@@ -468,11 +468,14 @@ __global__ __launch_bounds__(kFsThreads, 1) void value_head_stream_kernel(VhArgs
                     o[k] = hh > 0.f ? z : z * (hh + 1.f);          // ELU'(x) = 1 if h > 0 else h + 1
                     wacc[r] = fmaf(dv, hh, wacc[r]);
                 }
+                // plain (write-back) stores: the four 32-byte pieces of a row's line from this wave's 4 g steps merge
+                // in L2 (nontemporal ones reach HBM as partial-line writes: 571 vs 418 us measured)
                 const f32x4 ov = {o[0], o[1], o[2], o[3]};
-                __builtin_nontemporal_store(ov, reinterpret_cast<f32x4*>(dzt + (32 * i + l32) * 256 + 8 * g));
+                *reinterpret_cast<f32x4*>(dzt + (32 * i + l32) * 256 + 8 * g) = ov;
             }
         }
-        // dvl / red are rewritten only after the next tile's four quarter barriers
+        // dvl / red are rewritten only after the next tile's four quarter barriers (a one-barrier form in which every
+        // lane finishes V / dV of its own rows measured slower: 347-353 vs 340-342 us, the 16-fold redundant tail)
     }
     // ---- the slice's partial row: dW over the 32 row lanes (fixed butterfly), db over the 128 row positions
     float* wp = a.wpart + static_cast<int64_t>(blockIdx.x) * kVhP;
@@ -589,10 +592,10 @@ int64_t value_head_stream_rows(int64_t M) {
     return ceil_div(tiles, per);
 }
 
-bool value_head_stream_enabled() {
+bool value_head_stream_enabled() {  // default since round 5's bench A/B; RSLRL_VALUE_HEAD_STREAM=0 keeps the tiled head
     static const bool on = [] {
         const char* e = std::getenv("RSLRL_VALUE_HEAD_STREAM");
-        return e && e[0] == '1';
+        return !(e && e[0] == '0');
     }();
     return on;
 }
