@@ -364,11 +364,13 @@ class PPO:
         stats_buf = torch.empty(8, dtype=torch.float32, device=dev)
         # device-resident lr (needs an optimizer that takes a tensor lr: fused / capturable Adam)
         device_lr = adaptive and dev.type == "cuda" and self._optimizer_takes_tensor_lr()
-        lr_dev = torch.tensor(self.learning_rate, dtype=torch.float64, device=dev) if device_lr else None
+        # torch.full, not torch.tensor: a fill launch instead of a pageable host-to-device copy, which would block the
+        # host until the rollout's kernels have drained (the GPU then idles through the update's host prologue)
+        lr_dev = torch.full((), self.learning_rate, dtype=torch.float64, device=dev) if device_lr else None
         self.learning_rate_device = lr_dev  # the reference's self.learning_rate during update() (fp64, device)
         lr32 = None
         if device_lr:  # the optimizer reads the lr as this fp32 device tensor (written by ppo_update_tail)
-            lr32 = torch.tensor(self.learning_rate, dtype=torch.float32, device=dev)
+            lr32 = torch.full((), self.learning_rate, dtype=torch.float32, device=dev)
             for param_group in self.optimizer.param_groups:
                 param_group["lr"] = lr32
         manual = None  # decided at the first mini-batch (needs the observation batch)
@@ -541,9 +543,11 @@ class PPO:
                 sums[3] += rnd_loss.detach().double()
 
         num_updates = self.num_learning_epochs * self.num_mini_batches
-        host = (sums / num_updates).tolist()
-        if device_lr:  # back to a Python float, as the reference keeps it (logging, checkpoints)
-            self.learning_rate = lr_dev.item()
+        # one read-back for the loss means and the device lr (back to a Python float, as the reference keeps it:
+        # logging, checkpoints)
+        host = torch.cat([sums / num_updates, lr_dev.reshape(1)]).tolist() if device_lr else (sums / num_updates).tolist()
+        if device_lr:
+            self.learning_rate = host[4]
             self.learning_rate_device = None
             for param_group in self.optimizer.param_groups:
                 param_group["lr"] = self.learning_rate
