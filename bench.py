@@ -27,6 +27,7 @@ import argparse
 import contextlib
 import json
 import os
+import statistics
 import sys
 import time
 
@@ -50,7 +51,10 @@ C4_ENVS = 131072  # BASELINE.json configs[3]: the total partitioned over the ran
 # per-launch HBM traffic of the hot-path kernels from rocprofv3 FETCH_SIZE / WRITE_SIZE passes over this same
 # bench command (scripts/pmc_summary.py; raw counters next to it).  PMC passes serialise and slow the
 # run, so they are collected separately and the committed summary is reported here.
-PMC_TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r5_pmc_traffic.json")
+# One summary per profiled workload (scripts/pmc_summary.py --num-envs): bench.py reports `traffic` only from the file
+# whose recorded workload (envs per GPU, T) is the run's own, else null -- per-launch traffic does not carry over
+# between workloads (round 5 quoted C3's for every workload).
+PMC_TRAFFIC_GLOB = os.path.join(ROOT, "profiles", "r6_pmc_traffic*.json")
 # the MLP GEMM pairs' counters (scripts/mlp_pmc.sh + scripts/mlp_pmc_summary.py over scripts/mlp_pair_probe.py at C3's
 # 393,216-row mini-batch): FETCH_SIZE / WRITE_SIZE corrected by factors calibrated on the box in each kernel's own
 # access pattern (scripts/pmc_pattern_probe.hip), plus clock and MFMA-pipe utilisation from the SQ counters
@@ -59,6 +63,10 @@ MLP_PMC_NAMES = {"linear_hidden_bwd_pair[M=393216,N=256,K=256]": "x6_hidden_bwd_
                  "linear_dgrad_pair[M=393216,Nred=256,K=256]": "x6_dgrad_pair_w4",
                  "linear_fwd_pair[M=393216,K=256,N=256]": "x6_fwd_stream_pair",
                  "linear_wgrad_pair[M=393216,N=256,K=256]": "x6_wgrad_pair"}
+
+
+# hot-path timer names -> PMC summary names (scripts/pmc_summary.py SHORT)
+PMC_NAMES = {"compute_returns": "compute_returns_one_launch"}
 
 
 def mlp_pmc(kernel):
@@ -74,13 +82,21 @@ def mlp_pmc(kernel):
             "source": os.path.relpath(MLP_PMC_FILE, ROOT)}
 
 
-def pmc_traffic(kernel):
-    try:
-        with open(PMC_TRAFFIC_FILE) as f:
-            k = json.load(f)["kernels"].get(kernel)
-        return (k["traffic_bytes"], os.path.relpath(PMC_TRAFFIC_FILE, ROOT)) if k else (None, None)
-    except (OSError, ValueError, KeyError):
-        return None, None
+def pmc_traffic(kernel, num_envs, T):
+    """(traffic bytes per launch, source) of `kernel` from the PMC summary of this workload, or (None, reason)."""
+    import glob
+    for path in sorted(glob.glob(PMC_TRAFFIC_GLOB)):
+        try:
+            with open(path) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            continue
+        w = d.get("workload") or {}
+        if w.get("num_envs_per_gpu") == num_envs and w.get("num_steps_per_env") == T:
+            k = d.get("kernels", {}).get(kernel)
+            src = os.path.relpath(path, ROOT)
+            return (k["traffic_bytes"], src) if k else (None, f"{src} has no {kernel} entry")
+    return None, f"no PMC summary for {num_envs} envs x T={T} (profiles/r6_pmc_traffic*.json)"
 
 
 def train_cfg(args, rnd=False):
@@ -398,7 +414,8 @@ def main():
             timing = ("HIP events bound to each launch (hipExtLaunchKernel start/stop: the dispatch's own duration, "
                       f"{ev_n} launches of the timed region); chosen as the hot-path kernel with the most launch-bound "
                       f"time per step: " + ", ".join(f"{k} {v[0] * 1e3:.1f} us" for k, v in kernel_ms.items()))
-        traffic, traffic_src = pmc_traffic(dominant)
+        traffic, traffic_src = pmc_traffic(PMC_NAMES.get(dominant, dominant), args.num_envs_local,
+                                           args.num_steps_per_env)
         roofline = {"kernel": dominant, "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                     "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": traffic, "traffic_source": traffic_src,
                     "algorithmic_bytes_per_launch": hot[dominant]["algorithmic_bytes_per_launch"],
@@ -471,7 +488,9 @@ def main():
         "phases_timed_ms": {"collection": [round(c * 1e3, 2) for c, _ in timed_phases],
                             "learn": [round(l * 1e3, 2) for _, l in timed_phases]},
         # end-to-end (value), update phase and hot path (above) reported apart
-        "update_env_steps_per_s": round(T * N * world / runner.last_iteration_stats["learn_time"], 1),
+        # from the median host learn time of the timed iterations (update() to its statistics read-back; the rollout's
+        # queued GPU work that drains during it is counted there too)
+        "update_env_steps_per_s": round(T * N * world / statistics.median(l for _, l in timed_phases), 1),
         "cpu_baseline": None,
     }
     if world == 1 and not args.no_extra:

@@ -31,7 +31,7 @@ extern "C" {
 
 typedef struct ihipStream_t* rslrl_stream_t; /* == hipStream_t */
 
-#define RSLRL_ABI_VERSION 17
+#define RSLRL_ABI_VERSION 18
 
 enum {
     RSLRL_OK = 0,
@@ -81,11 +81,32 @@ int rslrl_compute_returns_records(const float* values, const float* rewards, con
  * ABI 16: for T in {8, 16, 24, 32} and N <= 131072 whose blocks the device holds at once, the scan, the statistics and
  * the normalisation run as ONE launch (a grid barrier between the scan and the normalisation; same bits as the
  * two-launch form, RSLRL_GAE_FUSED=0 forces that).  The barrier words sit after the partials in the workspace:
- * a workspace must be zero-filled before its first use with this entry point (the library leaves it so). */
+ * a workspace must be zero-filled before its first use with this entry point (the library leaves it so).
+ * ABI 18: for N a multiple of 64 (16-byte aligned pointers) the one launch is the LDS-staged form (64 envs per block,
+ * N / 64 blocks; the same bits).  The one-launch forms run as a cooperative launch where the device supports it (a
+ * refused launch runs the two-launch form).  A workspace serves one stream at a time (the barrier's ticket).  If the
+ * grid barrier ever times out (blocks not co-resident) the call writes NaN advantages and sets the uint32 status word
+ * at rslrl_compute_returns_status_offset() in the workspace to nonzero; the caller reads it at its next
+ * synchronisation and clears it (PPO.update raises on it). */
 int rslrl_compute_returns_slots(const float* values, const float* rewards, const uint8_t* dones,
                                 const float* last_values, float gamma, float lam, int64_t T, int64_t N,
                                 float* returns, float* advantages, const float* log_prob, float* slots,
                                 void* workspace, size_t workspace_bytes, rslrl_stream_t stream);
+
+/* ABI 18: byte offset of the uint32 barrier status word in a compute_returns workspace (0 = ok). */
+size_t rslrl_compute_returns_status_offset(void);
+/* ABI 18: which form rslrl_compute_returns_slots takes for these arguments on the current device: 0 = scan + normaliser
+ * (two launches), 1 = one launch, one env per lane, 2 = one launch, LDS-staged tiles of 64 envs (the algorithmic bytes
+ * of forms 1 and 2: read 13 B + write 24 B per env-step, + 4 B per env; form 0 also writes and re-reads the raw
+ * advantages). */
+int rslrl_compute_returns_slots_form(int64_t T, int64_t N, const float* values, const float* rewards,
+                                     const uint8_t* dones, const float* log_prob, const float* returns,
+                                     const float* advantages);
+/* ABI 18: test / diagnostic knobs (not a reference interface).  "gae_form": -1 auto, else the highest
+ * rslrl_compute_returns_slots form allowed (0 forces the two-launch path); "gae_coop": -1 auto, 0 plain launch, 1
+ * cooperative launch; "gae_spin_limit": polls before a grid-barrier wait gives up (default 2^22).  Writes the old
+ * value into *previous (may be NULL). */
+int rslrl_debug_knob(const char* name, int64_t value, int64_t* previous);
 
 /* Advantage statistics + in-place normalisation of an arbitrary fp32 vector (the normalisation half
  * of rollout_storage.py:148-149; ppo.py:221-223 uses the same expression per mini-batch).          */
@@ -438,8 +459,10 @@ typedef struct {
 } rslrl_value_head_args_t;
 int rslrl_value_head_fwd_bwd(const rslrl_linear_args_t* a, const rslrl_value_head_args_t* v, rslrl_stream_t stream);
 /* ABI 17: how many rows of wgrad_partials the call above fills: one row per workgroup slice of the streaming form (the
- * default since round 5; at most 256), M / 128 for the tiled kernel (RSLRL_VALUE_HEAD_STREAM=0) -- the fold's row count. */
-int64_t rslrl_value_head_partial_rows(int64_t M);
+ * default since round 5; at most 256), M / 128 for the tiled kernel (RSLRL_VALUE_HEAD_STREAM=0, or any call with
+ * colsum_partials, which only the tiled kernel writes) -- the fold's row count.  ABI 18: with_colsum says whether the
+ * call passes colsum_partials, so the count follows the same dispatch as rslrl_value_head_fwd_bwd. */
+int64_t rslrl_value_head_partial_rows(int64_t M, int32_t with_colsum);
 
 /* The actor's last hidden layer, its 12-wide output layer (the action mean), the whole PPO loss of the mini-batch and
  * the backward through the output layer in one launch (ABI 13): rsl_rl/networks/mlp.py:106-114 (the actor's last

@@ -19,7 +19,7 @@ import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 # RSLRL_AMD_LIB: an alternative in-tree build of the same library (A/B kernel experiments)
 LIB_PATH = os.environ.get("RSLRL_AMD_LIB") or os.path.join(LIB_DIR, "librslrl_amd.so")
-ABI_VERSION = 17
+ABI_VERSION = 18
 
 # symbols declared in include/rslrl_amd.h (tests/test_capi.py checks the header against this list)
 EXPORTED_SYMBOLS = (
@@ -29,6 +29,9 @@ EXPORTED_SYMBOLS = (
     "rslrl_compute_returns",
     "rslrl_compute_returns_records",
     "rslrl_compute_returns_slots",
+    "rslrl_compute_returns_status_offset",
+    "rslrl_compute_returns_slots_form",
+    "rslrl_debug_knob",
     "rslrl_normalize_workspace_bytes",
     "rslrl_normalize_advantages",
     "rslrl_randperm_mt19937",
@@ -397,6 +400,12 @@ def _declare(L):
                                             I32, P, I64, P]
     L.rslrl_compute_returns_slots.restype = ctypes.c_int
     L.rslrl_compute_returns_slots.argtypes = [P, P, P, P, F, F, I64, I64, P, P, P, P, P, SZ, P]
+    L.rslrl_compute_returns_status_offset.restype = SZ
+    L.rslrl_compute_returns_status_offset.argtypes = []
+    L.rslrl_compute_returns_slots_form.restype = ctypes.c_int
+    L.rslrl_compute_returns_slots_form.argtypes = [I64, I64, P, P, P, P, P, P]
+    L.rslrl_debug_knob.restype = ctypes.c_int
+    L.rslrl_debug_knob.argtypes = [ctypes.c_char_p, I64, ctypes.POINTER(I64)]
     L.rslrl_record_fill_slot.restype = ctypes.c_int
     L.rslrl_record_fill_slot.argtypes = [P, I64, I64, I32, P, I32, ctypes.POINTER(ctypes.c_void_p), I32, I64, P]
     L.rslrl_ppo_loss_workspace_bytes.restype = SZ
@@ -458,7 +467,7 @@ def _declare(L):
     L.rslrl_value_head_fwd_bwd.restype = ctypes.c_int
     L.rslrl_value_head_fwd_bwd.argtypes = [ctypes.POINTER(LinearArgs), ctypes.POINTER(ValueHeadArgs), P]
     L.rslrl_value_head_partial_rows.restype = ctypes.c_int64
-    L.rslrl_value_head_partial_rows.argtypes = [ctypes.c_int64]
+    L.rslrl_value_head_partial_rows.argtypes = [ctypes.c_int64, ctypes.c_int32]
     L.rslrl_actor_head_workspace_bytes.restype = ctypes.c_size_t
     L.rslrl_actor_head_workspace_bytes.argtypes = [I64]
     L.rslrl_actor_head_fwd_bwd.restype = ctypes.c_int

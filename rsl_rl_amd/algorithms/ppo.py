@@ -545,13 +545,22 @@ class PPO:
         num_updates = self.num_learning_epochs * self.num_mini_batches
         # one read-back for the loss means and the device lr (back to a Python float, as the reference keeps it:
         # logging, checkpoints)
-        host = torch.cat([sums / num_updates, lr_dev.reshape(1)]).tolist() if device_lr else (sums / num_updates).tolist()
+        # (+ compute_returns' grid-barrier status word, if its one-launch form ran: nonzero = NaN advantages, raise)
+        gae_status = getattr(self.storage, "gae_status", None)
+        parts = [sums / num_updates] + ([lr_dev.reshape(1)] if device_lr else [])
+        if gae_status is not None:
+            parts.append(gae_status.to(sums.dtype))
+        host = torch.cat(parts).tolist()
         if device_lr:
             self.learning_rate = host[4]
             self.learning_rate_device = None
             for param_group in self.optimizer.param_groups:
                 param_group["lr"] = self.learning_rate
         self.storage.clear()
+        if gae_status is not None:
+            # the rollout's advantages were NaN, and so are this update's parameters: stop loudly
+            self.storage.gae_status = None
+            kernels.raise_on_gae_status(gae_status, host[-1])
         loss_dict = {"value_function": host[0], "surrogate": host[1], "entropy": host[2]}
         if self.rnd:
             loss_dict["rnd"] = host[3]

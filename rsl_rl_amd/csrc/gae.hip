@@ -26,6 +26,7 @@
 #include <atomic>
 #include <cstdlib>
 #include <mutex>
+#include <string>
 
 #include "common.h"
 
@@ -303,47 +304,153 @@ int elementwise_blocks(int64_t n) {
     return static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, 4 * kBlock), 2048)));
 }
 
-// ---- compute_returns_slots in ONE launch (round 5): scan, grid barrier, normalisation from registers ----------------
-// One env per lane (nb = N / 256 blocks, every block resident at once -- checked against the occupancy on the host):
-// the lane keeps its T values and returns in registers through the whole kernel, so the normalisation reads neither
-// the advantages nor the values back, and the raw advantages are never written.  The block partials are the scan's
-// (same partition, same Chan tree) and every block folds them in fold_moments' order after the barrier: mean / std,
-// returns, advantages and slots are bit-identical to gae_scan_kernel + adv_normalize_slots_kernel.
+// ---- compute_returns_slots in ONE launch: scan, grid barrier, normalisation --------------------------------------
+// Two kernels take this form; both keep the values and returns of their envs on chip through the whole launch, so the
+// normalisation reads neither the advantages nor the values back and the raw advantages are never written:
+//   gae_staged_slots_kernel (round 6, default; N % 64 == 0): a 256-thread block owns 64 envs.  All four waves stage
+//       the block's [T][64] values, rewards and dones tiles into LDS with 16-byte loads (every thread has ~5 loads in
+//       flight, and N / 64 blocks fill the chip where one lane per env left the 16,384-env share on 64 CUs), wave 0
+//       runs the serial reverse recurrence out of LDS (one lane per env, the reference's fp32 operation order), and
+//       after the barrier all four waves write advantages and slots from the tiles as 16-byte units.
+//   gae_fused_slots_kernel (round 5; any N): one env per lane, 256 envs per block, the tiles in registers.
+// The block partials reproduce the two-launch scan's partition exactly: a staged block's partial is the Chan tree of
+// ONE wave of a scan block, and the fold chains each group of four in the scan's wave order before fold_moments'
+// order over the groups -- mean / std, returns, advantages and slots are bit-identical to gae_scan_kernel +
+// adv_normalize_slots_kernel.
 //
-// Grid barrier: the partials go out as agent-scope atomic stores; thread 0 of each block reads the generation word,
-// takes a ticket, and the last arrival re-arms the ticket (0) and bumps the generation; the others spin on
-// the generation with s_sleep (bounded: after ~2^22 polls a block gives up and raises the error word instead of
-// hanging -- it cannot happen with every block resident).  Workspace: [kMaxPartials double4][ticket][generation]
-// [error]; the ticket must be zero before the first call (zero-filled allocation) and is left zero.
-constexpr int kBarOffset = sizeof(double4) * kMaxPartials;
+// Grid barrier + statistics (grid_stats): thread 0 of each block stores its partial as agent-scope atomic stores, reads
+// the generation word and takes a ticket; the LAST arrival folds every partial (one block: no all-to-all partial
+// reads), publishes (mean, std + eps), re-arms the ticket (0) and bumps the generation; the others spin on the
+// generation with s_sleep.  No release / acquire fences: on gfx950 they write back / invalidate the XCD's whole L2 (the
+// returns just written are in it); agent-scope atomics complete at the coherence point (vmcnt) and are read back by
+// agent-scope atomic loads.
+// Co-residency: the grid is sized to what the device holds at once (occupancy x CUs, checked on the host).  That is
+// not a guarantee when another kernel or process holds CUs, so a waiting block gives up after `spin_limit` polls
+// (seconds): it raises the workspace's status word and normalises with NaN statistics -- a barrier that could not
+// complete shows as NaN advantages AND a status word that PPO.update reads with its loss statistics and raises on,
+// never as silently wrong numbers.  A late block still arrives, folds and re-arms, so the words are consistent for the
+// next call.  RSLRL_GAE_COOP=1 launches cooperatively instead (hipLaunchCooperativeKernel: the runtime refuses a grid
+// it cannot hold, and the call falls back to the two-launch path) -- opt-in, since it costs more than the barrier.
+// Workspace: [kMaxWaveParts double4 partials][ticket][-][status][-][mean][denom] then one generation word per group of
+// 64 blocks, 256 bytes apart; zero-filled before its first use, ticket left zero by every call.  One workspace per
+// stream (two concurrent calls must not share a ticket).
+constexpr int kStagedEnvs = 64;                 // envs per block of the staged kernel (one wave of the scan's blocks)
+constexpr int kMaxWaveParts = 4 * kMaxPartials; // partials of the staged kernel: N / 64 <= 2048
+constexpr int kBarOffset = sizeof(double4) * kMaxWaveParts;
+constexpr int kStatusWord = 2;                  // index of the status word among the barrier words
+constexpr unsigned kDefaultSpinLimit = 1u << 22;
 
-__device__ __forceinline__ void gae_grid_barrier(unsigned* bar, unsigned nb) {
+__device__ __forceinline__ void store_partial(double4* partials, int i, const Moments& m) {
+    unsigned long long* p = reinterpret_cast<unsigned long long*>(partials + i);
+    __hip_atomic_store(p, __double_as_longlong(m.n), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(p + 1, __double_as_longlong(m.mean), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(p + 2, __double_as_longlong(m.m2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ Moments load_partial(const double4* partials, int i) {
+    const unsigned long long* p = reinterpret_cast<const unsigned long long*>(partials + i);
+    return {__longlong_as_double(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)),
+            __longlong_as_double(__hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)),
+            __longlong_as_double(__hip_atomic_load(p + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))};
+}
+
+// The barrier's generation words: one per group of kGenGroup blocks, each in its own 256-byte piece (a different
+// memory channel), so ~64 pollers share a word instead of every block of the grid hammering one address -- with 1,024
+// pollers on one word the arrival of the last block and its fold waited behind their loads.
+constexpr int kGenGroup = 64;
+constexpr int kGenStride = 64;  // words (256 bytes)
+constexpr int kGenOffset = 64;  // words after the barrier base
+constexpr int kMaxGenGroups = kMaxWaveParts / kGenGroup;
+
+// Every block calls this after thread 0 stored its partial (partials[blockIdx.x]).  G partials make one scan-block
+// partial (chained in index order, as block_chan chains a scan block's waves); those are folded in fold_moments'
+// order.  Returns (mean, std + eps) in every thread; (NaN, NaN) after a barrier time-out.
+template <int G>
+__device__ float2 grid_stats(const double4* partials, int64_t total, float eps, unsigned* bar, unsigned spin_limit,
+                             unsigned sleep_units, double (*scratch)[3]) {
+    __shared__ float2 s_res;
+    __shared__ int s_last;
+    __shared__ unsigned s_gen;
+    unsigned* ticket = bar;
+    unsigned* res = bar + 4;
+    const unsigned nb = gridDim.x;
+    unsigned* gen = bar + kGenOffset + kGenStride * (blockIdx.x / kGenGroup);
     __syncthreads();
     if (threadIdx.x == 0) {
-        unsigned* ticket = bar;
-        unsigned* gen = bar + 1;
-        // no release / acquire fences (on gfx950 they write back / invalidate the whole L2 of the XCD -- the
-        // scan's returns are in it): the partials went out as agent-scope atomic stores, which complete at the
-        // coherence point before the ticket is taken (vmcnt), and are read back by agent-scope atomic loads
         const unsigned g0 = __hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this block's partial (and the generation read) complete
         const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (t == nb - 1) {
-            __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __hip_atomic_store(gen, g0 + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            unsigned polls = 0;
-            while (__hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g0) {
-                __builtin_amdgcn_s_sleep(2);
-                if (++polls == (1u << 22)) {
-                    __hip_atomic_store(bar + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    break;
-                }
+        s_last = t == nb - 1;
+        s_gen = g0;
+    }
+    __syncthreads();
+    const unsigned g0 = s_gen;
+    if (s_last) {
+        // every partial this thread folds is loaded before the first chan (one memory round trip; sc1: read at the
+        // coherence point, where the other XCDs' atomic stores went)
+        constexpr int kPer = G * (kMaxPartials / kBlock);  // partials per thread at most (<= 512 groups of G)
+        const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<double4*>(partials), 0, static_cast<int>(sizeof(double4) * nb), 0x00020000);
+        double3 q[kPer];
+#pragma unroll
+        for (int i = 0; i < kPer; ++i) {
+            const int idx = (threadIdx.x + kBlock * (i / G)) * G + (i % G);  // group gi = tid + 256 (i / G), member i % G
+            const int off = idx < static_cast<int>(nb) ? idx * 32 : 0x7ffffff0;  // out of range reads 0
+            const auto lo = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, 16 /* sc1 */);
+            const auto hi = __builtin_amdgcn_raw_buffer_load_b64(rsrc, off + 16, 0, 16 /* sc1 */);
+            q[i] = make_double3(__builtin_bit_cast(double, make_uint2(lo[0], lo[1])),
+                                __builtin_bit_cast(double, make_uint2(lo[2], lo[3])), __builtin_bit_cast(double, hi));
+        }
+        const int ngroups = static_cast<int>((nb + G - 1) / G);
+        Moments m{0.0, 0.0, 0.0};
+#pragma unroll
+        for (int j = 0; j < kPer / G; ++j) {
+            const int gi = threadIdx.x + kBlock * j;
+            if (gi < ngroups) {
+                Moments p{q[j * G].x, q[j * G].y, q[j * G].z};
+#pragma unroll
+                for (int k = 1; k < G; ++k)
+                    if (gi * G + k < static_cast<int>(nb)) p = chan(p, Moments{q[j * G + k].x, q[j * G + k].y, q[j * G + k].z});
+                m = chan(m, p);
             }
+        }
+        m = block_chan(m, scratch);
+        if (threadIdx.x == 0) {
+            const double var = total > 1 ? m.m2 / static_cast<double>(total - 1) : __builtin_nan("");
+            const float mean = static_cast<float>(m.mean);
+            const float denom = __fadd_rn(static_cast<float>(sqrt(var)), eps);  // rollout_storage.py:149
+            __hip_atomic_store(res, __float_as_uint(mean), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(res + 1, __float_as_uint(denom), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // results and re-armed ticket complete ...
+            s_res = make_float2(mean, denom);
+        }
+        __syncthreads();
+        const unsigned ngen = (nb + kGenGroup - 1) / kGenGroup;
+        if (threadIdx.x < ngen) {  // ... before any group's generation moves
+            __hip_atomic_store(bar + kGenOffset + kGenStride * threadIdx.x, g0 + 1u, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+    } else if (threadIdx.x == 0) {
+        unsigned polls = 0;
+        bool ok = true;
+        while (__hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g0) {
+            if (polls++ >= spin_limit) {
+                ok = false;
+                break;
+            }
+            for (unsigned z = 0; z < sleep_units; ++z) __builtin_amdgcn_s_sleep(2);
+        }
+        if (ok) {
+            s_res = make_float2(__uint_as_float(__hip_atomic_load(res, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)),
+                                __uint_as_float(__hip_atomic_load(res + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
+        } else {
+            __hip_atomic_store(bar + kStatusWord, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_res = make_float2(__builtin_nanf(""), __builtin_nanf(""));
         }
     }
     __syncthreads();
+    return s_res;
 }
 
 template <int T>
@@ -351,7 +458,8 @@ __global__ __launch_bounds__(kBlock) void gae_fused_slots_kernel(
     const float* __restrict__ values, const float* __restrict__ rewards, const uint8_t* __restrict__ dones,
     const float* __restrict__ last_values, float gamma, float lam, int64_t N, float eps, float* __restrict__ returns,
     float* __restrict__ advantages, const float* __restrict__ logp, float4* __restrict__ slots,
-    double4* __restrict__ partials, unsigned* __restrict__ bar) {
+    double4* __restrict__ partials, unsigned* __restrict__ bar, unsigned spin_limit,
+    unsigned sleep_units) {
     __shared__ double scratch[kBlock / kWave][3];
     const int64_t n = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
     const bool ok = n < N;
@@ -388,69 +496,246 @@ __global__ __launch_bounds__(kBlock) void gae_fused_slots_kernel(
         m = chan(m, Moments{static_cast<double>(T), mean, m2});
     }
     m = block_chan(m, scratch);
-    if (threadIdx.x == 0) {
-        unsigned long long* p = reinterpret_cast<unsigned long long*>(partials + blockIdx.x);
-        __hip_atomic_store(p, __double_as_longlong(m.n), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(p + 1, __double_as_longlong(m.mean), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(p + 2, __double_as_longlong(m.m2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    if (threadIdx.x == 0) store_partial(partials, blockIdx.x, m);
     float lp[T];  // the log-probs load while the grid gathers
     if (ok) {
 #pragma unroll
         for (int t = 0; t < T; ++t) lp[t] = logp[static_cast<int64_t>(t) * N + n];
     }
-    gae_grid_barrier(bar, gridDim.x);
-    // fold_moments' order over the partials (atomic loads: another XCD's L2 wrote them)
-    Moments f{0.0, 0.0, 0.0};
-    for (int i = threadIdx.x; i < static_cast<int>(gridDim.x); i += kBlock) {
-        const unsigned long long* p = reinterpret_cast<const unsigned long long*>(partials + i);
-        const Moments q{__longlong_as_double(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)),
-                        __longlong_as_double(__hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)),
-                        __longlong_as_double(__hip_atomic_load(p + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))};
-        f = chan(f, q);
-    }
-    f = block_chan(f, scratch);
-    const int64_t total = static_cast<int64_t>(T) * N;
-    const double var = total > 1 ? f.m2 / static_cast<double>(total - 1) : __builtin_nan("");
-    const float mean = static_cast<float>(f.mean);
-    const float denom = __fadd_rn(static_cast<float>(sqrt(var)), eps);  // rollout_storage.py:149
+    const float2 st = grid_stats<1>(partials, static_cast<int64_t>(T) * N, eps, bar, spin_limit, sleep_units, scratch);
     if (ok) {
 #pragma unroll
         for (int t = 0; t < T; ++t) {
             const int64_t i = static_cast<int64_t>(t) * N + n;
-            const float a = __fdiv_rn(__fsub_rn(__fsub_rn(ret[t], v[t]), mean), denom);
+            const float a = __fdiv_rn(__fsub_rn(__fsub_rn(ret[t], v[t]), st.x), st.y);
             advantages[i] = a;
             slots[i] = make_float4(v[t], lp[t], ret[t], a);
         }
     }
 }
 
-// blocks of gae_fused_slots_kernel<T> the device holds at once (0: no fused instance for T)
-int gae_fused_capacity(int T) {
-    // per device (the current one) and T, computed once; concurrent first calls compute the same value
+template <int T>
+__global__ __launch_bounds__(kBlock) void gae_staged_slots_kernel(
+    const float* __restrict__ values, const float* __restrict__ rewards, const uint8_t* __restrict__ dones,
+    const float* __restrict__ last_values, float gamma, float lam, int64_t N, float eps, float* __restrict__ returns,
+    float* __restrict__ advantages, const float* __restrict__ logp, float4* __restrict__ slots,
+    double4* __restrict__ partials, unsigned* __restrict__ bar, unsigned spin_limit,
+    unsigned sleep_units) {
+    constexpr int E = kStagedEnvs;
+    constexpr int U = T * E / 4;                    // 16-byte units of a [T][64] fp32 tile (16 per row)
+    constexpr int UD = T * E / 16;                  // 16-byte units of the [T][64] uint8 dones tile (4 per row)
+    constexpr int J = (U + kBlock - 1) / kBlock;    // fp32 units per thread
+    constexpr int JD = (UD + kBlock - 1) / kBlock;  // dones units per thread
+    __shared__ float4 s_v[U];
+    __shared__ float4 s_r[U];  // rewards, overwritten by the returns as the scan consumes them
+    __shared__ uint4 s_d[UD];
+    __shared__ double scratch[kBlock / kWave][3];
+    const int tid = threadIdx.x;
+    const int64_t n0 = static_cast<int64_t>(blockIdx.x) * E;
+    // ---- stage: every load of the block in flight at once (rows of 64 envs = 256 contiguous bytes) ----
+    float4 v4[J], r4[J], l4[J];
+    uint4 d4[JD];
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        const int u = tid + j * kBlock;
+        if (U % kBlock == 0 || u < U) {
+            const int64_t g = static_cast<int64_t>(u >> 4) * N + n0 + 4 * (u & 15);
+            v4[j] = *reinterpret_cast<const float4*>(values + g);
+            r4[j] = *reinterpret_cast<const float4*>(rewards + g);
+            l4[j] = *reinterpret_cast<const float4*>(logp + g);  // for this thread's slots after the barrier
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < JD; ++j) {
+        const int u = tid + j * kBlock;
+        if (UD % kBlock == 0 || u < UD)
+            d4[j] = *reinterpret_cast<const uint4*>(dones + static_cast<int64_t>(u >> 2) * N + n0 + 16 * (u & 3));
+    }
+    const float lv = tid < E ? last_values[n0 + tid] : 0.0f;
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        const int u = tid + j * kBlock;
+        if (U % kBlock == 0 || u < U) {
+            s_v[u] = v4[j];
+            s_r[u] = r4[j];
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < JD; ++j) {
+        const int u = tid + j * kBlock;
+        if (UD % kBlock == 0 || u < UD) s_d[u] = d4[j];
+    }
+    __syncthreads();
+    // ---- wave 0: the reverse recurrence of rollout_storage.py:128-145, one lane per env ----
+    if (tid < E) {
+        const float* sv = reinterpret_cast<const float*>(s_v);
+        float* sr = reinterpret_cast<float*>(s_r);
+        const uint8_t* sd = reinterpret_cast<const uint8_t*>(s_d);
+        float next_v = lv;
+        float adv = 0.0f;
+        double s = 0.0;
+#pragma unroll
+        for (int t = T - 1; t >= 0; --t) {
+            const float v = sv[t * E + tid];
+            adv = GaeStep::step(v, sr[t * E + tid], sd[t * E + tid], next_v, adv, gamma, lam);
+            const float ret = __fadd_rn(adv, v);  // :142
+            sr[t * E + tid] = ret;
+            returns[static_cast<int64_t>(t) * N + n0 + tid] = ret;
+            s += static_cast<double>(__fsub_rn(ret, v));  // :145
+            next_v = v;
+        }
+        const double mean = s / static_cast<double>(T);
+        double m2 = 0.0;
+#pragma unroll
+        for (int t = 0; t < T; ++t) {
+            const double dlt = static_cast<double>(__fsub_rn(sr[t * E + tid], sv[t * E + tid])) - mean;
+            m2 += dlt * dlt;
+        }
+        Moments m = chan(Moments{0.0, 0.0, 0.0}, Moments{static_cast<double>(T), mean, m2});
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {  // block_chan's wave tree
+            const Moments o{__shfl_down(m.n, off, kWave), __shfl_down(m.mean, off, kWave),
+                            __shfl_down(m.m2, off, kWave)};
+            if (tid < off) m = chan(m, o);
+        }
+        if (tid == 0) store_partial(partials, blockIdx.x, m);
+    }
+    // ---- statistics over the grid (4 staged blocks = one scan block) ----
+    const float2 st = grid_stats<4>(partials, static_cast<int64_t>(T) * N, eps, bar, spin_limit, sleep_units, scratch);
+    // ---- normalise and write: per thread its units of the tiles (the barrier's __syncthreads published s_r) ----
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        const int u = tid + j * kBlock;
+        if (U % kBlock == 0 || u < U) {
+            const int64_t g = static_cast<int64_t>(u >> 4) * N + n0 + 4 * (u & 15);
+            const float4 v = s_v[u];
+            const float4 rt = s_r[u];
+            float4 a;
+            a.x = __fdiv_rn(__fsub_rn(__fsub_rn(rt.x, v.x), st.x), st.y);
+            a.y = __fdiv_rn(__fsub_rn(__fsub_rn(rt.y, v.y), st.x), st.y);
+            a.z = __fdiv_rn(__fsub_rn(__fsub_rn(rt.z, v.z), st.x), st.y);
+            a.w = __fdiv_rn(__fsub_rn(__fsub_rn(rt.w, v.w), st.x), st.y);
+            *reinterpret_cast<float4*>(advantages + g) = a;
+            float4* sl = slots + g;
+            sl[0] = make_float4(v.x, l4[j].x, rt.x, a.x);
+            sl[1] = make_float4(v.y, l4[j].y, rt.y, a.y);
+            sl[2] = make_float4(v.z, l4[j].z, rt.z, a.z);
+            sl[3] = make_float4(v.w, l4[j].w, rt.w, a.w);
+        }
+    }
+}
+
+// ---- host side: which form a call takes, device capacities, the debug knobs ----
+enum GaeForm { kFormTwoLaunch = 0, kFormOneLaunch = 1, kFormStaged = 2 };
+
+std::atomic<int64_t> g_knob_form{-1};       // -1 auto; 0 / 1 / 2 cap the form (tests: force a decline)
+std::atomic<int64_t> g_knob_coop{-1};       // -1 RSLRL_GAE_COOP (default 0), 0 plain launch, 1 cooperative
+std::atomic<int64_t> g_knob_spin{kDefaultSpinLimit};
+std::atomic<int64_t> g_knob_sleep{1};       // s_sleep 2 rounds between two polls of a waiting block
+
+template <int T>
+const void* fused_fn(int form) {
+    return form == kFormStaged ? reinterpret_cast<const void*>(&gae_staged_slots_kernel<T>)
+                               : reinterpret_cast<const void*>(&gae_fused_slots_kernel<T>);
+}
+
+const void* fused_fn_t(int T, int form) {
+    return T == 8 ? fused_fn<8>(form) : T == 16 ? fused_fn<16>(form) : T == 24 ? fused_fn<24>(form) : fused_fn<32>(form);
+}
+
+// blocks of the form's kernel for T the current device holds at once (0: no such instance), computed once per
+// (device, T, form); concurrent first calls compute the same value
+int gae_fused_capacity(int T, int form) {
     constexpr int kMaxDev = 64;
-    static std::atomic<int> cap[kMaxDev][4];
+    static std::atomic<int> cap[kMaxDev][4][2];
     static std::once_flag init;
     std::call_once(init, [] {
         for (auto& d : cap)
-            for (auto& c : d) c.store(-1, std::memory_order_relaxed);
+            for (auto& c : d)
+                for (auto& f : c) f.store(-1, std::memory_order_relaxed);
     });
     const int k = T == 8 ? 0 : T == 16 ? 1 : T == 24 ? 2 : T == 32 ? 3 : -1;
     int dev = 0;
     if (k < 0 || hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return 0;
-    int c = cap[dev][k].load(std::memory_order_relaxed);
+    const int fi = form == kFormStaged ? 1 : 0;
+    int c = cap[dev][k][fi].load(std::memory_order_relaxed);
     if (c < 0) {
         int cus = 0, per = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 0;
-        const void* f = k == 0 ? reinterpret_cast<const void*>(&gae_fused_slots_kernel<8>)
-                        : k == 1 ? reinterpret_cast<const void*>(&gae_fused_slots_kernel<16>)
-                        : k == 2 ? reinterpret_cast<const void*>(&gae_fused_slots_kernel<24>)
-                                 : reinterpret_cast<const void*>(&gae_fused_slots_kernel<32>);
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, f, kBlock, 0) != hipSuccess) per = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fused_fn_t(T, form), kBlock, 0) != hipSuccess) per = 0;
         c = per * cus;
-        cap[dev][k].store(c, std::memory_order_relaxed);
+        cap[dev][k][fi].store(c, std::memory_order_relaxed);
     }
     return c;
+}
+
+bool coop_supported() {
+    constexpr int kMaxDev = 64;
+    static std::atomic<int> sup[kMaxDev];
+    static std::once_flag init;
+    std::call_once(init, [] {
+        for (auto& s : sup) s.store(-1, std::memory_order_relaxed);
+    });
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return false;
+    int s = sup[dev].load(std::memory_order_relaxed);
+    if (s < 0) {
+        int v = 0;
+        if (hipDeviceGetAttribute(&v, hipDeviceAttributeCooperativeLaunch, dev) != hipSuccess) v = 0;
+        s = v != 0;
+        sup[dev].store(s, std::memory_order_relaxed);
+    }
+    return s != 0;
+}
+
+bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+// The form rslrl_compute_returns_slots takes for these arguments (rslrl_compute_returns_slots_form reports it).
+int slots_form(int64_t T, int64_t N, const float* values, const float* rewards, const uint8_t* dones,
+               const float* log_prob, const float* returns, const float* advantages) {
+    static const bool fused_env = [] {
+        const char* e = std::getenv("RSLRL_GAE_FUSED");
+        return !(e && e[0] == '0');
+    }();
+    const int64_t cap_form = g_knob_form.load(std::memory_order_relaxed);
+    if (!fused_env || cap_form == 0) return kFormTwoLaunch;
+    if (!(T == 8 || T == 16 || T == 24 || T == 32) || N <= 0 || ceil_div(N, kBlock) > kMaxPartials)
+        return kFormTwoLaunch;
+    const int t = static_cast<int>(T);
+    if (cap_form != 1 && N % kStagedEnvs == 0 && aligned16(values) && aligned16(rewards) && aligned16(dones) &&
+        aligned16(log_prob) && aligned16(returns) && aligned16(advantages) &&
+        N / kStagedEnvs <= gae_fused_capacity(t, kFormStaged))
+        return kFormStaged;
+    if (ceil_div(N, kBlock) <= gae_fused_capacity(t, kFormOneLaunch)) return kFormOneLaunch;
+    return kFormTwoLaunch;
+}
+
+// launches the one-launch form; false when the runtime refused it (the caller runs the two-launch path)
+bool launch_fused(int form, int T, int64_t N, hipStream_t st, const float* values, const float* rewards,
+                  const uint8_t* dones, const float* last_values, float gamma, float lam, float* returns,
+                  float* advantages, const float* logp, float4* slots, double4* part, unsigned* bar) {
+    const unsigned nb = static_cast<unsigned>(form == kFormStaged ? N / kStagedEnvs : ceil_div(N, kBlock));
+    float eps = 1e-8f;
+    unsigned spin = static_cast<unsigned>(g_knob_spin.load(std::memory_order_relaxed));
+    unsigned sleep_units = static_cast<unsigned>(g_knob_sleep.load(std::memory_order_relaxed));
+    void* args[] = {&values, &rewards, &dones, &last_values, &gamma, &lam, &N, &eps, &returns,
+                    &advantages, &logp, &slots, &part, &bar, &spin, &sleep_units};
+    // cooperative launches are opt-in (RSLRL_GAE_COOP=1): on this runtime one costs ~6-17 us more per call than the
+    // whole kernel's barrier (profiles/r6_gae_probe*.json); the status word + NaN outputs are the default safety net
+    static const bool coop_env = [] {
+        const char* e = std::getenv("RSLRL_GAE_COOP");
+        return e && e[0] == '1';
+    }();
+    const int64_t coop_knob = g_knob_coop.load(std::memory_order_relaxed);
+    const bool coop = (coop_knob == 1 || (coop_knob < 0 && coop_env)) && coop_supported();
+    const void* f = fused_fn_t(T, form);
+    const hipError_t e = coop ? hipLaunchCooperativeKernel(f, dim3(nb), dim3(kBlock), args, 0, st)
+                              : hipLaunchKernel(f, dim3(nb), dim3(kBlock), args, 0, st);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();  // clear the refused launch; nothing ran
+        return false;
+    }
+    return true;
 }
 
 template <int TMAX>
@@ -472,7 +757,30 @@ using namespace rslrl;
 extern "C" size_t rslrl_compute_returns_workspace_bytes(int64_t T, int64_t N) {
     (void)T;
     (void)N;
-    return kBarOffset + 64;  // the partials, then the one-launch form's barrier words
+    // the partials, then the one-launch forms' barrier words (ticket, status, results; a generation word per group)
+    return kBarOffset + 4 * (kGenOffset + kGenStride * kMaxGenGroups);
+}
+
+extern "C" size_t rslrl_compute_returns_status_offset(void) { return kBarOffset + 4 * kStatusWord; }
+
+extern "C" int rslrl_compute_returns_slots_form(int64_t T, int64_t N, const float* values, const float* rewards,
+                                                const uint8_t* dones, const float* log_prob, const float* returns,
+                                                const float* advantages) {
+    if (T <= 0 || N <= 0) return kFormTwoLaunch;
+    return slots_form(T, N, values, rewards, dones, log_prob, returns, advantages);
+}
+
+extern "C" int rslrl_debug_knob(const char* name, int64_t value, int64_t* previous) {
+    if (!name) return RSLRL_E_INVALID_ARGUMENT;
+    const std::string k(name);
+    std::atomic<int64_t>* knob = k == "gae_form" ? &g_knob_form : k == "gae_coop" ? &g_knob_coop
+                               : k == "gae_spin_limit" ? &g_knob_spin : k == "gae_sleep" ? &g_knob_sleep : nullptr;
+    if (!knob) return RSLRL_E_INVALID_ARGUMENT;
+    if ((k == "gae_spin_limit" || k == "gae_sleep") && (value < 0 || value > 0xffffffffll))
+        return RSLRL_E_INVALID_ARGUMENT;
+    const int64_t prev = knob->exchange(value);
+    if (previous) *previous = prev;
+    return RSLRL_OK;
 }
 
 extern "C" size_t rslrl_normalize_workspace_bytes(int64_t n) {
@@ -506,23 +814,15 @@ int compute_returns_impl(const float* values, const float* rewards, const uint8_
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     const int nb = scan_blocks(N);
     const int t = static_cast<int>(T);
-    static const bool fused_on = [] {
-        const char* e = std::getenv("RSLRL_GAE_FUSED");
-        return !(e && e[0] == '0');
-    }();
-    if (slot && slot->record_floats == 0 && fused_on && nb == ceil_div(N, kBlock) && nb <= gae_fused_capacity(t)) {
-        // one launch: scan + grid barrier + normalisation + slots (bit-identical to the two-launch path below)
-        unsigned* bar = reinterpret_cast<unsigned*>(static_cast<char*>(workspace) + kBarOffset);
-        float4* sl = reinterpret_cast<float4*>(slot->records);
-#define RSLRL_GAE_FUSED_LAUNCH(TT)                                                                                    \
-    hipLaunchKernelGGL((gae_fused_slots_kernel<TT>), dim3(nb), dim3(kBlock), 0, st, values, rewards, dones,           \
-                       last_values, gamma, lam, N, 1e-8f, returns, advantages, slot->log_prob, sl, part, bar)
-        if (t == 8) RSLRL_GAE_FUSED_LAUNCH(8);
-        else if (t == 16) RSLRL_GAE_FUSED_LAUNCH(16);
-        else if (t == 24) RSLRL_GAE_FUSED_LAUNCH(24);
-        else RSLRL_GAE_FUSED_LAUNCH(32);
-#undef RSLRL_GAE_FUSED_LAUNCH
-        return launch_status();
+    if (slot && slot->record_floats == 0) {
+        const int form = slots_form(T, N, values, rewards, dones, slot->log_prob, returns, advantages);
+        // one launch: scan + grid barrier + normalisation + slots (bit-identical to the two-launch path below); a
+        // refused cooperative launch runs the two-launch path
+        if (form != kFormTwoLaunch &&
+            launch_fused(form, t, N, st, values, rewards, dones, last_values, gamma, lam, returns, advantages,
+                         slot->log_prob, reinterpret_cast<float4*>(slot->records), part,
+                         reinterpret_cast<unsigned*>(static_cast<char*>(workspace) + kBarOffset)))
+            return RSLRL_OK;
     }
     if (t <= 8)
         launch_scan<8>(nb, st, values, rewards, dones, last_values, gamma, lam, t, N, returns, advantages, part);

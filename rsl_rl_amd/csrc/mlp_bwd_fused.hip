@@ -327,7 +327,6 @@ __global__ __launch_bounds__(kHbThreads, 2) void hidden_bwd_kernel(HbArgs args) 
             if (has_next) hb_dma_h(hb_tile_rsrc(P.h, row0 + kHbT), stage);
         }
         float4 vn[8];
-        uint2 pl[8][3];  // the next tile's dZ units as bf16 planes
         HB_STAMP(3);
         // ---- weight gradient of the tile: dW[n][32 w + l32] += sum over rows of dZ[m][n] H[m][32 w + l32].  Block
         // k = 8 (2 i + st) + nb: row step (i, st), column block nb; the dZ^T fragments of block k + 1 are read while
@@ -369,14 +368,6 @@ __global__ __launch_bounds__(kHbThreads, 2) void hidden_bwd_kernel(HbArgs args) 
             if (LA && k + 1 < 32) read_t(k + 1, tf[(k + 1) & 1]);
             if (!LA) read_t(k, tf[k & 1]);
             dw[nb] = mfma_x6(tf[k & 1], hb, dw[nb]);
-            if (false) {
-                const int u = k - 16;
-                csum.x += vn[u].x;
-                csum.y += vn[u].y;
-                csum.z += vn[u].z;
-                csum.w += vn[u].w;
-                split4(vn[u], pl[u][0], pl[u][1], pl[u][2]);
-            }
             __builtin_amdgcn_sched_barrier(0);
         }
         HB_STAMP(4);

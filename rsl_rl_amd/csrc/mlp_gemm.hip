@@ -3114,9 +3114,10 @@ extern "C" int rslrl_value_head_fwd_bwd(const rslrl_linear_args_t* a, const rslr
     return launch_status();
 }
 
-extern "C" int64_t rslrl_value_head_partial_rows(int64_t M) {
+extern "C" int64_t rslrl_value_head_partial_rows(int64_t M, int32_t with_colsum) {
     if (M <= 0) return 0;
-    return value_head_stream_enabled() ? value_head_stream_rows(M) : ceil_div(M, kBM);
+    // the same dispatch as rslrl_value_head_fwd_bwd: the streaming form never takes colsum_partials
+    return value_head_stream_enabled() && !with_colsum ? value_head_stream_rows(M) : ceil_div(M, kBM);
 }
 
 // The actor's last hidden layer, output layer, the PPO loss and the output layer's backward in one launch

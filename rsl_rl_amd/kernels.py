@@ -7,7 +7,6 @@ torch stream and never synchronises.  CPU tensors are rejected: there is no CPU 
 from __future__ import annotations
 
 import contextlib
-import os
 import ctypes
 from collections import defaultdict
 
@@ -169,6 +168,41 @@ def normal_affine_(x: torch.Tensor, scale: torch.Tensor, loc: torch.Tensor) -> t
 # ------------------------------------------------------------------------------------------------
 # rollout_storage.py:127-149
 # ------------------------------------------------------------------------------------------------
+def _gae_workspace(dev: torch.device, T: int, N: int) -> torch.Tensor:
+    """compute_returns' workspace of the current stream: the one-launch forms keep a grid barrier's ticket in it, so two
+    streams must not share one (include/rslrl_amd.h, ABI 18)."""
+    return _ws.get(dev, ("gae", _stream(dev)), _lib.lib().rslrl_compute_returns_workspace_bytes(T, N))
+
+
+def gae_status_word(ws: torch.Tensor) -> torch.Tensor:
+    """The workspace's uint32 grid-barrier status word as a 1-element int32 device view (0 = ok)."""
+    off = _lib.lib().rslrl_compute_returns_status_offset()
+    return ws[off:off + 4].view(torch.int32)
+
+
+class GAEBarrierTimeout(RuntimeError):
+    """compute_returns' one-launch grid barrier timed out: its blocks were not co-resident (another kernel or process
+    held CUs), so that call's advantages are NaN."""
+
+
+def raise_on_gae_status(status: torch.Tensor, value: float | int | None = None) -> None:
+    """Raise GAEBarrierTimeout if the status word (or its already read-back `value`) is set; clears the word."""
+    v = int(status.item()) if value is None else int(value)
+    if v != 0:
+        with torch.inference_mode():  # the word may be a view made under the runner's inference mode
+            status.zero_()
+        raise GAEBarrierTimeout(
+            "rsl_rl_amd compute_returns: the one-launch GAE's grid barrier timed out (its blocks were not all resident "
+            "at once), so the advantages of that rollout are NaN; set RSLRL_GAE_FUSED=0 to use the two-launch form")
+
+
+def debug_knob(name: str, value: int) -> int:
+    """Set one of the library's test knobs (include/rslrl_amd.h rslrl_debug_knob); returns the previous value."""
+    prev = ctypes.c_int64(0)
+    _lib.check(_lib.lib().rslrl_debug_knob(name.encode(), int(value), ctypes.byref(prev)), "rslrl_debug_knob")
+    return prev.value
+
+
 def compute_returns(values, rewards, dones, last_values, gamma, lam, normalize_advantage, returns, advantages):
     """GAE + (optional) normalisation, written into `returns` / `advantages` ([T, N, 1] fp32, in place).
 
@@ -184,8 +218,7 @@ def compute_returns(values, rewards, dones, last_values, gamma, lam, normalize_a
         raise ValueError("compute_returns: inconsistent shapes")
     L = _lib.lib()
     dev = values.device
-    nbytes = L.rslrl_compute_returns_workspace_bytes(T, N)
-    ws = _ws.get(dev, "gae", nbytes)
+    ws = _gae_workspace(dev, T, N)
     # one span over the production entry point (scan + fused normalisation): algorithmic bytes of both passes
     moved = 17 * T * N + 4 * N + (8 * T * N if normalize_advantage else 0)
     with timer.span("compute_returns", dev, moved):
@@ -216,7 +249,7 @@ def compute_returns_records(values, rewards, dones, last_values, gamma, lam, ret
     R = records.shape[2]
     L = _lib.lib()
     dev = values.device
-    ws = _ws.get(dev, "gae", L.rslrl_compute_returns_workspace_bytes(T, N))
+    ws = _gae_workspace(dev, T, N)
     # scan (17 B + 4 B per env) + normalisation reading adv / value / log-prob / return and writing adv + the slot
     moved = 17 * T * N + 4 * N + (4 * 4 + 4 + 32) * T * N
     with timer.span("compute_returns", dev, moved):
@@ -231,7 +264,8 @@ def compute_returns_records(values, rewards, dones, last_values, gamma, lam, ret
 def compute_returns_slots(values, rewards, dones, last_values, gamma, lam, returns, advantages, log_prob, slots):
     """compute_returns with normalisation whose last pass also writes the scalar slot array
     slots[t, n] = {value, log-prob, return, advantage} (include/rslrl_amd.h rslrl_compute_returns_slots): slots
-    [T, N, 4] contiguous fp32, log_prob [T, N, 1] contiguous fp32."""
+    [T, N, 4] contiguous fp32, log_prob [T, N, 1] contiguous fp32.  Returns the workspace's barrier status word (a
+    1-element int32 device tensor, read it with raise_on_gae_status at the next synchronisation)."""
     _require_device(values, rewards, dones, last_values, returns, advantages, log_prob, slots)
     T, N = values.shape[0], values.shape[1]
     for t, dt in ((values, torch.float32), (rewards, torch.float32), (dones, torch.uint8), (last_values, torch.float32),
@@ -245,10 +279,12 @@ def compute_returns_slots(values, rewards, dones, last_values, gamma, lam, retur
         raise ValueError("compute_returns_slots: inconsistent shapes")
     L = _lib.lib()
     dev = values.device
-    ws = _ws.get(dev, "gae", L.rslrl_compute_returns_workspace_bytes(T, N))
-    if T in (8, 16, 24, 32) and N <= 131072 and os.environ.get("RSLRL_GAE_FUSED", "1") != "0":
-        # the one-launch form (ABI 16): read value, reward, done, log-prob (13 B) + last value per env, write return,
-        # advantage and the 16-byte slot (24 B)
+    ws = _gae_workspace(dev, T, N)
+    form = L.rslrl_compute_returns_slots_form(T, N, _ptr(values), _ptr(rewards), _ptr(dones), _ptr(log_prob),
+                                              _ptr(returns), _ptr(advantages))
+    if form != 0:
+        # the one-launch forms (ABI 16 / 18): read value, reward, done, log-prob (13 B) + last value per env, write
+        # return, advantage and the 16-byte slot (24 B)
         moved = 37 * T * N + 4 * N
     else:
         # scan (17 B + 4 B per env) + normalisation reading adv / value / log-prob / return, writing adv + the slot
@@ -260,6 +296,7 @@ def compute_returns_slots(values, rewards, dones, last_values, gamma, lam, retur
             ctypes.c_void_p(_stream(dev)),
         )
     _lib.check(rc, "rslrl_compute_returns_slots")
+    return gae_status_word(ws)
 
 
 def normalize_advantages_(adv: torch.Tensor, eps: float = 1e-8) -> torch.Tensor:

@@ -328,7 +328,7 @@ def value_head_fwd_bwd(x, b, N: int, img, b_out, out_img, w_out, head: ValueHead
     if rc == _lib.E_UNSUPPORTED:
         return None
     _lib.check(rc, "rslrl_value_head_fwd_bwd")
-    rows = L.rslrl_value_head_partial_rows(M)  # per tile, or per slice on the opt-in streaming form
+    rows = L.rslrl_value_head_partial_rows(M, 0)  # per slice on the streaming form, else per tile (no colsum passed)
     return dz, y, wpart[:rows]
 
 

@@ -15,6 +15,7 @@ returned by learn() through `self.last_iteration_stats` for benchmarking.
 from __future__ import annotations
 
 import os
+import sys
 import statistics
 import time
 import warnings
@@ -312,6 +313,14 @@ class OnPolicyRunner:
             "world_size": self.gpu_world_size,
         }
         one_device = os.getenv("RSLRL_TEST_ONE_DEVICE") == "1"
+        if one_device:
+            # never meant for a real job: say so on every rank, loudly
+            warnings.warn(
+                f"RSLRL_TEST_ONE_DEVICE=1: rank {self.gpu_global_rank} of {self.gpu_world_size} runs on cuda:0 over a "
+                "gloo group (a test-only override: every rank shares one GPU and RCCL is not used). Unset it for a "
+                "multi-GPU run.", RuntimeWarning, stacklevel=2)
+            print(f"[rsl_rl_amd] WARNING: RSLRL_TEST_ONE_DEVICE=1 -- rank {self.gpu_global_rank} on cuda:0 over gloo "
+                  "(test-only override)", file=sys.stderr, flush=True)
         if self.device != ("cuda:0" if one_device else f"cuda:{self.gpu_local_rank}"):
             raise ValueError(
                 f"Device '{self.device}' does not match expected device for local rank '{self.gpu_local_rank}'."

@@ -114,6 +114,7 @@ class RolloutStorage:
         self.step = 0
         self._fills = 0  # transitions added so far (any path): a slot written before the last one is stale
         self._slot_key = None  # what the slot array was filled from (compute_returns), or None
+        self.gae_status = None  # compute_returns' grid-barrier status word (kernels.compute_returns_slots), or None
 
         # mini-batch machinery (allocated on first use)
         self.perm_generator: torch.Generator | None = None
@@ -271,9 +272,10 @@ class RolloutStorage:
         if self.records is not None and normalize_advantage:
             # the normalisation pass also writes the slot array {value, log-prob, return, advantage} (coalesced
             # 16-byte units): the mini-batch generator gathers it beside the records (no slot copy per update)
-            kernels.compute_returns_slots(self.values, self.rewards, self.dones, last_values, float(gamma),
-                                          float(lam), self.returns, self.advantages, self.actions_log_prob,
-                                          self.slots)
+            # the one-launch form's grid-barrier status word: PPO.update reads it with its loss statistics
+            self.gae_status = kernels.compute_returns_slots(self.values, self.rewards, self.dones, last_values,
+                                                            float(gamma), float(lam), self.returns, self.advantages,
+                                                            self.actions_log_prob, self.slots)
             self._slot_key = self._slot_sources()
             return
         self._slot_key = None

@@ -21,6 +21,7 @@ SHORT = {
     "ppo_loss_quad_kernel": "ppo_loss",
     "gae_scan_kernel": "gae_scan",
     "gae_fused_slots_kernel": "compute_returns_one_launch",
+    "gae_staged_slots_kernel": "compute_returns_one_launch",
     "adv_normalize_kernel": "adv_normalize",
     "adv_normalize_slot_kernel": "adv_normalize_slot",
     "adv_normalize_slots_kernel": "adv_normalize_slots",
@@ -112,8 +113,12 @@ def main():
     ap.add_argument("--calib-fetch")
     ap.add_argument("--calib-write")
     ap.add_argument("-o", "--out", required=True)
+    ap.add_argument("--num-envs", type=int, default=None, help="envs per GPU of the profiled bench command")
+    ap.add_argument("--num-steps-per-env", type=int, default=24)
     args = ap.parse_args()
     res = {"units": "bytes per launch", "correction": "traffic = (2 * FETCH_SIZE + WRITE_SIZE) * 1024"}
+    if args.num_envs:  # bench.py reports this file's traffic only for the same workload
+        res["workload"] = {"num_envs_per_gpu": args.num_envs, "num_steps_per_env": args.num_steps_per_env}
     if args.calib_fetch and args.calib_write:
         cf = load(args.calib_fetch, "FETCH_SIZE")["copyBuffer"]
         cw = load(args.calib_write, "WRITE_SIZE")["copyBuffer"]

@@ -57,6 +57,36 @@ def test_argument_validation_without_gpu():
     assert L.rslrl_compute_returns_workspace_bytes(24, 65536) >= 16 * 256
 
 
+def test_gae_workspace_words_and_knobs_without_gpu():
+    """ABI 18: the status word sits after the partials and the barrier's ticket / generation, inside the workspace;
+    the test knobs validate their names and ranges and hand back the previous value (host code, no GPU)."""
+    L = _lib.lib()
+    ws = L.rslrl_compute_returns_workspace_bytes(24, 131072)
+    off = L.rslrl_compute_returns_status_offset()
+    assert off % 4 == 0 and off >= 8 + 2048 * 32 and off + 4 <= ws
+    prev = ctypes.c_int64(0)
+    assert L.rslrl_debug_knob(b"no_such_knob", 1, None) == -1
+    assert L.rslrl_debug_knob(None, 1, None) == -1
+    assert L.rslrl_debug_knob(b"gae_spin_limit", -1, None) == -1
+    assert L.rslrl_debug_knob(b"gae_spin_limit", 5, ctypes.byref(prev)) == 0
+    assert prev.value == 1 << 22
+    assert L.rslrl_debug_knob(b"gae_spin_limit", prev.value, ctypes.byref(prev)) == 0 and prev.value == 5
+    assert L.rslrl_debug_knob(b"gae_form", -1, ctypes.byref(prev)) == 0 and prev.value == -1
+    # forms need T in {8, 16, 24, 32} for a one-launch form; invalid sizes report the two-launch form
+    assert L.rslrl_compute_returns_slots_form(0, 4, None, None, None, None, None, None) == 0
+    assert L.rslrl_compute_returns_slots_form(5, 4096, None, None, None, None, None, None) == 0
+
+
+def test_value_head_partial_rows_follows_the_dispatch():
+    """ABI 18: a call with colsum_partials always takes the tiled head, so its partial-row count is M / 128
+    whatever the streaming default; without it the streaming form's per-slice count (<= 256 rows)."""
+    L = _lib.lib()
+    M = 393216
+    assert L.rslrl_value_head_partial_rows(M, 1) == M // 128
+    assert L.rslrl_value_head_partial_rows(M, 0) in (M // 128,) or L.rslrl_value_head_partial_rows(M, 0) <= 256
+    assert L.rslrl_value_head_partial_rows(0, 0) == 0
+
+
 def test_linear_abi_rejects_bad_shapes():
     L = _lib.lib()
     assert L.rslrl_linear_fwd(8, 10, 6, 8, 16, 8, 1, 8, None, None) == -1  # K % 4 != 0

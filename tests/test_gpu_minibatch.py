@@ -241,10 +241,12 @@ def test_compute_returns_slots_one_launch_rearms(cuda_device):
     for o in outs[1:]:
         assert all(torch.equal(a, b) for a, b in zip(outs[0], o))
     L = kernels._lib.lib()
-    ws = kernels._ws.get(values.device, "gae", L.rslrl_compute_returns_workspace_bytes(T, N))
-    words = ws[16384:16384 + 12].view(torch.int32).cpu().tolist()
+    ws = kernels._gae_workspace(values.device, T, N)
+    off = L.rslrl_compute_returns_status_offset() - 8  # [ticket][-][status]; group 0's generation 256 bytes on
+    words = ws[off:off + 12].view(torch.int32).cpu().tolist()
+    gen0 = ws[off + 256:off + 260].view(torch.int32).item()
     assert words[0] == 0 and words[2] == 0, words  # ticket re-armed, no barrier time-out
-    assert words[1] >= 3  # the generation advanced once per one-launch call
+    assert gen0 >= 3  # the generation advanced once per one-launch call
 
 
 @pytest.mark.parametrize("R,used", [(96, 84), (64, 56), (256, 252)])

@@ -18,8 +18,8 @@ from rsl_rl_amd.networks import fused_mlp
 pytestmark = pytest.mark.gpu
 
 
-def L_rows(M):
-    return _lib.lib().rslrl_value_head_partial_rows(M)
+def L_rows(M, with_colsum=False):
+    return _lib.lib().rslrl_value_head_partial_rows(M, int(with_colsum))
 
 
 def _stream_form():
