@@ -304,6 +304,23 @@ int elementwise_blocks(int64_t n) {
     return static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, 4 * kBlock), 2048)));
 }
 
+#ifdef RSLRL_GAE_STAMPS
+// diagnostic build only (never the shipped library; scripts/gae_stamps.py): per block, s_memrealtime (100 MHz, one clock
+// for the whole chip) at 6 points of the one-launch kernel -> g_gae_stamps[block * 8 + k]; [7] = 1 for the last arrival
+__device__ uint64_t* g_gae_stamps;
+#define GAE_STAMP(k)                                                                                              \
+    do {                                                                                                          \
+        if (g_gae_stamps && threadIdx.x == 0) {                                                                   \
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                                                      \
+            g_gae_stamps[static_cast<int64_t>(blockIdx.x) * 8 + (k)] = __builtin_amdgcn_s_memrealtime();            \
+        }                                                                                                         \
+    } while (0)
+#else
+#define GAE_STAMP(k) \
+    do {             \
+    } while (0)
+#endif
+
 // ---- compute_returns_slots in ONE launch: scan, grid barrier, normalisation --------------------------------------
 // Two kernels take this form; both keep the values and returns of their envs on chip through the whole launch, so the
 // normalisation reads neither the advantages nor the values back and the raw advantages are never written:
@@ -331,8 +348,9 @@ int elementwise_blocks(int64_t n) {
 // never as silently wrong numbers.  A late block still arrives, folds and re-arms, so the words are consistent for the
 // next call.  RSLRL_GAE_COOP=1 launches cooperatively instead (hipLaunchCooperativeKernel: the runtime refuses a grid
 // it cannot hold, and the call falls back to the two-launch path) -- opt-in, since it costs more than the barrier.
-// Workspace: [kMaxWaveParts double4 partials][ticket][-][status][-][mean][denom] then one generation word per group of
-// 64 blocks, 256 bytes apart; zero-filled before its first use, ticket left zero by every call.  One workspace per
+// Workspace: [kMaxWaveParts double4 partials][ticket][-][status] then, per group of 64 blocks, a 256-byte piece holding
+// the group's record {generation, mean, std + eps, check} and (128 bytes on) its arrival ticket; zero-filled before its
+// first use, tickets left zero by every call.  One workspace per
 // stream (two concurrent calls must not share a ticket).
 constexpr int kStagedEnvs = 64;                 // envs per block of the staged kernel (one wave of the scan's blocks)
 constexpr int kMaxWaveParts = 4 * kMaxPartials; // partials of the staged kernel: N / 64 <= 2048
@@ -362,39 +380,66 @@ constexpr int kGenStride = 64;  // words (256 bytes)
 constexpr int kGenOffset = 64;  // words after the barrier base
 constexpr int kMaxGenGroups = kMaxWaveParts / kGenGroup;
 
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ unsigned gen_check(unsigned g, unsigned m, unsigned d) {
+    return (g * 0x9e3779b1u) ^ (m + 0x7f4a7c15u) ^ ((d << 7) | (d >> 25)) ^ 0x5bd1e995u;
+}
+
 // Every block calls this after thread 0 stored its partial (partials[blockIdx.x]).  G partials make one scan-block
 // partial (chained in index order, as block_chan chains a scan block's waves); those are folded in fold_moments'
 // order.  Returns (mean, std + eps) in every thread; (NaN, NaN) after a barrier time-out.
-template <int G>
+template <int G, int NT>
 __device__ float2 grid_stats(const double4* partials, int64_t total, float eps, unsigned* bar, unsigned spin_limit,
                              unsigned sleep_units, double (*scratch)[3]) {
+    static_assert(NT == kBlock || NT == kWave, "256- or 64-thread blocks");
+    // the fold runs in fold_moments' 256-thread order whatever the block size: real thread r plays the virtual threads
+    // r + NT k (k < V), i.e. lane r of virtual wave k
+    constexpr int V = kBlock / NT;
+    constexpr int R = NT == kBlock ? kMaxPartials / kBlock : 1;  // rounds of 256 groups (the narrow form: N <= 65536)
     __shared__ float2 s_res;
     __shared__ int s_last;
     __shared__ unsigned s_gen;
     unsigned* ticket = bar;
-    unsigned* res = bar + 4;
     const unsigned nb = gridDim.x;
     unsigned* gen = bar + kGenOffset + kGenStride * (blockIdx.x / kGenGroup);
     __syncthreads();
     if (threadIdx.x == 0) {
+        // two-level arrival: a ticket per group of kGenGroup blocks (its own line), the group's last arrival takes a
+        // ticket of the grid -- at most 64 atomics queue on one address (1,024 on one word cost ~17 us at C3's
+        // staged grid, profiles/r6_gae_probe.json)
+        const unsigned grp = blockIdx.x / kGenGroup;
+        const unsigned gsize = min(static_cast<unsigned>(kGenGroup), nb - grp * kGenGroup);
+        unsigned* gticket = bar + kGenOffset + kGenStride * grp + kGenStride / 2;
         const unsigned g0 = __hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this block's partial (and the generation read) complete
-        const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_last = t == nb - 1;
+        int last = 0;
+        if (__hip_atomic_fetch_add(gticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gsize - 1) {
+            __hip_atomic_store(gticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // the group has arrived
+            const unsigned ngroups = (nb + kGenGroup - 1) / kGenGroup;
+            // one group (<= 64 blocks): its last arrival is the grid's, no second hop
+            last = ngroups == 1 ||
+                   __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ngroups - 1;
+        }
+        s_last = last;
         s_gen = g0;
     }
     __syncthreads();
     const unsigned g0 = s_gen;
+#ifdef RSLRL_GAE_STAMPS
+    if (g_gae_stamps && threadIdx.x == 0) g_gae_stamps[static_cast<int64_t>(blockIdx.x) * 8 + 7] = s_last;
+#endif
     if (s_last) {
         // every partial this thread folds is loaded before the first chan (one memory round trip; sc1: read at the
         // coherence point, where the other XCDs' atomic stores went)
-        constexpr int kPer = G * (kMaxPartials / kBlock);  // partials per thread at most (<= 512 groups of G)
+        constexpr int kPer = V * R * G;  // partials per thread
         const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
             const_cast<double4*>(partials), 0, static_cast<int>(sizeof(double4) * nb), 0x00020000);
         double3 q[kPer];
 #pragma unroll
-        for (int i = 0; i < kPer; ++i) {
-            const int idx = (threadIdx.x + kBlock * (i / G)) * G + (i % G);  // group gi = tid + 256 (i / G), member i % G
+        for (int i = 0; i < kPer; ++i) {  // i = ((k R) + j) G + member
+            const int k = i / (R * G), j = (i / G) % R;
+            const int idx = (threadIdx.x + NT * k + kBlock * j) * G + (i % G);
             const int off = idx < static_cast<int>(nb) ? idx * 32 : 0x7ffffff0;  // out of range reads 0
             const auto lo = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, 16 /* sc1 */);
             const auto hi = __builtin_amdgcn_raw_buffer_load_b64(rsrc, off + 16, 0, 16 /* sc1 */);
@@ -402,39 +447,67 @@ __device__ float2 grid_stats(const double4* partials, int64_t total, float eps, 
                                 __builtin_bit_cast(double, make_uint2(lo[2], lo[3])), __builtin_bit_cast(double, hi));
         }
         const int ngroups = static_cast<int>((nb + G - 1) / G);
-        Moments m{0.0, 0.0, 0.0};
+        Moments mv[V];
 #pragma unroll
-        for (int j = 0; j < kPer / G; ++j) {
-            const int gi = threadIdx.x + kBlock * j;
-            if (gi < ngroups) {
-                Moments p{q[j * G].x, q[j * G].y, q[j * G].z};
+        for (int k = 0; k < V; ++k) {
+            mv[k] = Moments{0.0, 0.0, 0.0};
 #pragma unroll
-                for (int k = 1; k < G; ++k)
-                    if (gi * G + k < static_cast<int>(nb)) p = chan(p, Moments{q[j * G + k].x, q[j * G + k].y, q[j * G + k].z});
-                m = chan(m, p);
+            for (int j = 0; j < R; ++j) {
+                const int gi = threadIdx.x + NT * k + kBlock * j;
+                const double3* qq = q + (k * R + j) * G;
+                if (gi < ngroups) {
+                    Moments p{qq[0].x, qq[0].y, qq[0].z};
+#pragma unroll
+                    for (int u = 1; u < G; ++u)
+                        if (gi * G + u < static_cast<int>(nb)) p = chan(p, Moments{qq[u].x, qq[u].y, qq[u].z});
+                    mv[k] = chan(mv[k], p);
+                }
             }
         }
-        m = block_chan(m, scratch);
+        Moments m;
+        if constexpr (V == 1) {
+            m = block_chan(mv[0], scratch);
+        } else {  // one real wave: each virtual wave's tree (block_chan's), then the virtual waves in order (lane 0)
+#pragma unroll
+            for (int k = 0; k < V; ++k) {
+#pragma unroll
+                for (int off = 32; off >= 1; off >>= 1) {
+                    const Moments o{__shfl_down(mv[k].n, off, kWave), __shfl_down(mv[k].mean, off, kWave),
+                                    __shfl_down(mv[k].m2, off, kWave)};
+                    if (static_cast<int>(threadIdx.x) < off) mv[k] = chan(mv[k], o);
+                }
+            }
+            m = mv[0];
+#pragma unroll
+            for (int k = 1; k < V; ++k) m = chan(m, mv[k]);
+        }
         if (threadIdx.x == 0) {
             const double var = total > 1 ? m.m2 / static_cast<double>(total - 1) : __builtin_nan("");
-            const float mean = static_cast<float>(m.mean);
-            const float denom = __fadd_rn(static_cast<float>(sqrt(var)), eps);  // rollout_storage.py:149
-            __hip_atomic_store(res, __float_as_uint(mean), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(res + 1, __float_as_uint(denom), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // results and re-armed ticket complete ...
-            s_res = make_float2(mean, denom);
+            s_res = make_float2(static_cast<float>(m.mean),
+                                __fadd_rn(static_cast<float>(sqrt(var)), eps));  // rollout_storage.py:149
+            __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed (lands by kernel end)
         }
         __syncthreads();
-        const unsigned ngen = (nb + kGenGroup - 1) / kGenGroup;
-        if (threadIdx.x < ngen) {  // ... before any group's generation moves
-            __hip_atomic_store(bar + kGenOffset + kGenStride * threadIdx.x, g0 + 1u, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
+        // publish {generation, mean, std + eps, check} as ONE 16-byte write-through store per group word: the waiters
+        // read the statistics with the generation (one poll load, no second round trip).  EVERY group's record moves
+        // (not only this grid's), so the generations stay equal whatever grid sizes share the workspace: a waiter
+        // compares against its own group's word, and lagging words could equal a waiter's snapshot.
+        if (threadIdx.x < kMaxGenGroups) {
+            const unsigned g1 = g0 + 1u;
+            const unsigned um = __float_as_uint(s_res.x), ud = __float_as_uint(s_res.y);
+            const u32x4 rec = {g1, um, ud, gen_check(g1, um, ud)};
+            unsigned* dst = bar + kGenOffset + kGenStride * threadIdx.x;
+            asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(dst), "v"(rec) : "memory");
         }
     } else if (threadIdx.x == 0) {
         unsigned polls = 0;
         bool ok = true;
-        while (__hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g0) {
+        u32x4 rec;
+        for (;;) {
+            // one 16-byte write-through load of the group's record; taken only with a new generation and a matching
+            // check word (a torn read of the two halves fails the check and polls again)
+            asm volatile("global_load_dwordx4 %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=&v"(rec) : "v"(gen) : "memory");
+            if (rec.x != g0 && rec.w == gen_check(rec.x, rec.y, rec.z)) break;
             if (polls++ >= spin_limit) {
                 ok = false;
                 break;
@@ -442,8 +515,7 @@ __device__ float2 grid_stats(const double4* partials, int64_t total, float eps, 
             for (unsigned z = 0; z < sleep_units; ++z) __builtin_amdgcn_s_sleep(2);
         }
         if (ok) {
-            s_res = make_float2(__uint_as_float(__hip_atomic_load(res, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)),
-                                __uint_as_float(__hip_atomic_load(res + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
+            s_res = make_float2(__uint_as_float(rec.y), __uint_as_float(rec.z));
         } else {
             __hip_atomic_store(bar + kStatusWord, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             s_res = make_float2(__builtin_nanf(""), __builtin_nanf(""));
@@ -453,18 +525,19 @@ __device__ float2 grid_stats(const double4* partials, int64_t total, float eps, 
     return s_res;
 }
 
-template <int T>
-__global__ __launch_bounds__(kBlock) void gae_fused_slots_kernel(
+template <int T, int NT>
+__global__ __launch_bounds__(NT) void gae_fused_slots_kernel(
     const float* __restrict__ values, const float* __restrict__ rewards, const uint8_t* __restrict__ dones,
     const float* __restrict__ last_values, float gamma, float lam, int64_t N, float eps, float* __restrict__ returns,
     float* __restrict__ advantages, const float* __restrict__ logp, float4* __restrict__ slots,
     double4* __restrict__ partials, unsigned* __restrict__ bar, unsigned spin_limit,
     unsigned sleep_units) {
-    __shared__ double scratch[kBlock / kWave][3];
-    const int64_t n = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    __shared__ double scratch[NT / kWave][3];
+    const int64_t n = static_cast<int64_t>(blockIdx.x) * NT + threadIdx.x;
     const bool ok = n < N;
     float v[T], ret[T];
     Moments m{0.0, 0.0, 0.0};
+    GAE_STAMP(0);
     if (ok) {
         float r[T];
         unsigned d[T];
@@ -495,14 +568,26 @@ __global__ __launch_bounds__(kBlock) void gae_fused_slots_kernel(
         }
         m = chan(m, Moments{static_cast<double>(T), mean, m2});
     }
-    m = block_chan(m, scratch);
+    if constexpr (NT == kBlock) {
+        m = block_chan(m, scratch);
+    } else {  // one wave per block: its partial is the wave tree of a 256-thread block's wave
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            const Moments o{__shfl_down(m.n, off, kWave), __shfl_down(m.mean, off, kWave), __shfl_down(m.m2, off, kWave)};
+            if (static_cast<int>(threadIdx.x) < off) m = chan(m, o);
+        }
+    }
+    GAE_STAMP(1);
     if (threadIdx.x == 0) store_partial(partials, blockIdx.x, m);
+    GAE_STAMP(2);
     float lp[T];  // the log-probs load while the grid gathers
     if (ok) {
 #pragma unroll
         for (int t = 0; t < T; ++t) lp[t] = logp[static_cast<int64_t>(t) * N + n];
     }
-    const float2 st = grid_stats<1>(partials, static_cast<int64_t>(T) * N, eps, bar, spin_limit, sleep_units, scratch);
+    GAE_STAMP(3);
+    const float2 st = grid_stats<kBlock / NT, NT>(partials, static_cast<int64_t>(T) * N, eps, bar, spin_limit, sleep_units, scratch);
+    GAE_STAMP(4);
     if (ok) {
 #pragma unroll
         for (int t = 0; t < T; ++t) {
@@ -512,6 +597,7 @@ __global__ __launch_bounds__(kBlock) void gae_fused_slots_kernel(
             slots[i] = make_float4(v[t], lp[t], ret[t], a);
         }
     }
+    GAE_STAMP(5);
 }
 
 template <int T>
@@ -601,7 +687,7 @@ __global__ __launch_bounds__(kBlock) void gae_staged_slots_kernel(
         if (tid == 0) store_partial(partials, blockIdx.x, m);
     }
     // ---- statistics over the grid (4 staged blocks = one scan block) ----
-    const float2 st = grid_stats<4>(partials, static_cast<int64_t>(T) * N, eps, bar, spin_limit, sleep_units, scratch);
+    const float2 st = grid_stats<4, kBlock>(partials, static_cast<int64_t>(T) * N, eps, bar, spin_limit, sleep_units, scratch);
     // ---- normalise and write: per thread its units of the tiles (the barrier's __syncthreads published s_r) ----
 #pragma unroll
     for (int j = 0; j < J; ++j) {
@@ -626,17 +712,25 @@ __global__ __launch_bounds__(kBlock) void gae_staged_slots_kernel(
 }
 
 // ---- host side: which form a call takes, device capacities, the debug knobs ----
-enum GaeForm { kFormTwoLaunch = 0, kFormOneLaunch = 1, kFormStaged = 2 };
+enum GaeForm { kFormTwoLaunch = 0, kFormOneLaunch = 1, kFormStaged = 2, kFormNarrow = 3 };
+constexpr int kNarrowMaxN = 65536;  // the narrow form's fold holds one round of 256 groups
 
-std::atomic<int64_t> g_knob_form{-1};       // -1 auto; 0 / 1 / 2 cap the form (tests: force a decline)
+std::atomic<int64_t> g_knob_form{-1};       // -1 auto; 0 / 1 / 2 / 3 force that form where it applies (else 0)
 std::atomic<int64_t> g_knob_coop{-1};       // -1 RSLRL_GAE_COOP (default 0), 0 plain launch, 1 cooperative
 std::atomic<int64_t> g_knob_spin{kDefaultSpinLimit};
 std::atomic<int64_t> g_knob_sleep{1};       // s_sleep 2 rounds between two polls of a waiting block
 
 template <int T>
 const void* fused_fn(int form) {
-    return form == kFormStaged ? reinterpret_cast<const void*>(&gae_staged_slots_kernel<T>)
-                               : reinterpret_cast<const void*>(&gae_fused_slots_kernel<T>);
+    return form == kFormStaged   ? reinterpret_cast<const void*>(&gae_staged_slots_kernel<T>)
+           : form == kFormNarrow ? reinterpret_cast<const void*>(&gae_fused_slots_kernel<T, kWave>)
+                                 : reinterpret_cast<const void*>(&gae_fused_slots_kernel<T, kBlock>);
+}
+
+int form_threads(int form) { return form == kFormNarrow ? kWave : kBlock; }
+
+int64_t form_blocks(int form, int64_t N) {
+    return form == kFormStaged ? N / kStagedEnvs : ceil_div(N, form_threads(form));
 }
 
 const void* fused_fn_t(int T, int form) {
@@ -647,7 +741,7 @@ const void* fused_fn_t(int T, int form) {
 // (device, T, form); concurrent first calls compute the same value
 int gae_fused_capacity(int T, int form) {
     constexpr int kMaxDev = 64;
-    static std::atomic<int> cap[kMaxDev][4][2];
+    static std::atomic<int> cap[kMaxDev][4][4];
     static std::once_flag init;
     std::call_once(init, [] {
         for (auto& d : cap)
@@ -657,12 +751,13 @@ int gae_fused_capacity(int T, int form) {
     const int k = T == 8 ? 0 : T == 16 ? 1 : T == 24 ? 2 : T == 32 ? 3 : -1;
     int dev = 0;
     if (k < 0 || hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return 0;
-    const int fi = form == kFormStaged ? 1 : 0;
+    const int fi = form;
     int c = cap[dev][k][fi].load(std::memory_order_relaxed);
     if (c < 0) {
         int cus = 0, per = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fused_fn_t(T, form), kBlock, 0) != hipSuccess) per = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fused_fn_t(T, form), form_threads(form), 0) != hipSuccess)
+            per = 0;
         c = per * cus;
         cap[dev][k][fi].store(c, std::memory_order_relaxed);
     }
@@ -697,16 +792,23 @@ int slots_form(int64_t T, int64_t N, const float* values, const float* rewards, 
         const char* e = std::getenv("RSLRL_GAE_FUSED");
         return !(e && e[0] == '0');
     }();
-    const int64_t cap_form = g_knob_form.load(std::memory_order_relaxed);
-    if (!fused_env || cap_form == 0) return kFormTwoLaunch;
+    const int64_t knob = g_knob_form.load(std::memory_order_relaxed);
+    if (!fused_env || knob == 0) return kFormTwoLaunch;
     if (!(T == 8 || T == 16 || T == 24 || T == 32) || N <= 0 || ceil_div(N, kBlock) > kMaxPartials)
         return kFormTwoLaunch;
     const int t = static_cast<int>(T);
-    if (cap_form != 1 && N % kStagedEnvs == 0 && aligned16(values) && aligned16(rewards) && aligned16(dones) &&
-        aligned16(log_prob) && aligned16(returns) && aligned16(advantages) &&
-        N / kStagedEnvs <= gae_fused_capacity(t, kFormStaged))
-        return kFormStaged;
-    if (ceil_div(N, kBlock) <= gae_fused_capacity(t, kFormOneLaunch)) return kFormOneLaunch;
+    const bool aligned = aligned16(values) && aligned16(rewards) && aligned16(dones) && aligned16(log_prob) &&
+                         aligned16(returns) && aligned16(advantages);
+    auto fits = [&](int form) {
+        if (form == kFormStaged && (N % kStagedEnvs != 0 || !aligned)) return false;
+        if (form == kFormNarrow && N > kNarrowMaxN) return false;
+        return form_blocks(form, N) <= gae_fused_capacity(t, form);
+    };
+    if (knob > 0) return knob <= kFormNarrow && fits(static_cast<int>(knob)) ? static_cast<int>(knob) : kFormTwoLaunch;
+    // auto, by measurement (profiles/r6_gae_probe.json, rocprof kernel durations at 16,384 / 32,768 / 65,536 envs, T 24):
+    // one env per lane in 256-thread blocks is the fastest form at every size (17.9 us at C3 vs 26.4 staged, 21.8
+    // narrow; 12.2 us at 16,384 envs vs 14.3 / 14.1); the staged and narrow forms stay selectable (gae_form 2 / 3)
+    if (fits(kFormOneLaunch)) return kFormOneLaunch;
     return kFormTwoLaunch;
 }
 
@@ -714,7 +816,7 @@ int slots_form(int64_t T, int64_t N, const float* values, const float* rewards, 
 bool launch_fused(int form, int T, int64_t N, hipStream_t st, const float* values, const float* rewards,
                   const uint8_t* dones, const float* last_values, float gamma, float lam, float* returns,
                   float* advantages, const float* logp, float4* slots, double4* part, unsigned* bar) {
-    const unsigned nb = static_cast<unsigned>(form == kFormStaged ? N / kStagedEnvs : ceil_div(N, kBlock));
+    const unsigned nb = static_cast<unsigned>(form_blocks(form, N));
     float eps = 1e-8f;
     unsigned spin = static_cast<unsigned>(g_knob_spin.load(std::memory_order_relaxed));
     unsigned sleep_units = static_cast<unsigned>(g_knob_sleep.load(std::memory_order_relaxed));
@@ -729,8 +831,9 @@ bool launch_fused(int form, int T, int64_t N, hipStream_t st, const float* value
     const int64_t coop_knob = g_knob_coop.load(std::memory_order_relaxed);
     const bool coop = (coop_knob == 1 || (coop_knob < 0 && coop_env)) && coop_supported();
     const void* f = fused_fn_t(T, form);
-    const hipError_t e = coop ? hipLaunchCooperativeKernel(f, dim3(nb), dim3(kBlock), args, 0, st)
-                              : hipLaunchKernel(f, dim3(nb), dim3(kBlock), args, 0, st);
+    const dim3 block(form_threads(form));
+    const hipError_t e = coop ? hipLaunchCooperativeKernel(f, dim3(nb), block, args, 0, st)
+                              : hipLaunchKernel(f, dim3(nb), block, args, 0, st);
     if (e != hipSuccess) {
         (void)hipGetLastError();  // clear the refused launch; nothing ran
         return false;
@@ -760,6 +863,13 @@ extern "C" size_t rslrl_compute_returns_workspace_bytes(int64_t T, int64_t N) {
     // the partials, then the one-launch forms' barrier words (ticket, status, results; a generation word per group)
     return kBarOffset + 4 * (kGenOffset + kGenStride * kMaxGenGroups);
 }
+
+#ifdef RSLRL_GAE_STAMPS
+extern "C" int rslrl_gae_debug_stamps(void* buf) {  // diagnostic build only
+    uint64_t* p = static_cast<uint64_t*>(buf);
+    return static_cast<int>(hipMemcpyToSymbol(HIP_SYMBOL(g_gae_stamps), &p, sizeof(p)));
+}
+#endif
 
 extern "C" size_t rslrl_compute_returns_status_offset(void) { return kBarOffset + 4 * kStatusWord; }
 

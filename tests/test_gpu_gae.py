@@ -125,25 +125,27 @@ def _slots_run(inp, form_cap=None, coop=None):
                                    (32, 8256, 1.0)])
 def test_slots_forms_bit_identical(T, N, p, cuda_device):
     """Every form of compute_returns_slots gives the same bits as the two-launch form (returns, normalised advantages,
-    the whole slot array); returns and raw advantages equal the oracle's.  N % 64 == 0 takes the staged form (unless the
-    device cannot hold N / 64 of its blocks), other N the one-env-per-lane launch."""
+    the whole slot array); returns and raw advantages equal the oracle's.  Forms: 1 one env per lane in 256-thread
+    blocks, 2 LDS-staged 64-env tiles (N % 64 == 0), 3 one env per lane in 64-thread blocks (N <= 65536), each forced
+    through the knob (a form that does not apply runs the two-launch form)."""
     inp = _slots_inputs(T, N, p, cuda_device, T * N + 3)
     base = _slots_run(inp, form_cap=0)
     assert base[0] == 0 and base[4] == 0
     forms = {0}
-    for cap in (1, 2):
+    for cap in (1, 2, 3):
         for coop in (0, 1):
             form, ret, adv, slots, status = _slots_run(inp, form_cap=cap, coop=coop)
-            assert form <= cap and status == 0
+            assert form in (cap, 0) and status == 0
             forms.add(form)
             assert torch.equal(ret, base[1]) and torch.equal(adv, base[2]), (cap, coop, form)
             assert torch.equal(slots, base[3]), (cap, coop, form)
     auto = _slots_run(inp)
     assert torch.equal(auto[3], base[3])
+    assert auto[0] != 0, "every shape here fits a one-launch form"
     if N % 64 == 0 and N <= 65536:
-        assert auto[0] == 2, "the staged form should take an aligned N % 64 == 0 rollout"
-    elif N % 64:
-        assert auto[0] == 1
+        assert 2 in forms and 3 in forms
+    if N <= 65536:
+        assert 3 in forms
     values, rewards, dones = (t.cpu().numpy().reshape(T, N) for t in inp[:3])
     oret, oadv = O.gae(values, rewards, dones, inp[3].cpu().numpy().reshape(N), 0.99, 0.95)
     assert np.array_equal(base[1].cpu().numpy().reshape(T, N), oret)
@@ -165,7 +167,7 @@ def test_slots_golden_all_forms(golden_meta, cuda_device):
         inp = (t(g("values"), T, N, 1), t(g("rewards"), T, N, 1), t(g("dones"), T, N, 1),
                t(g("last_values"), N, 1), logp)
         values, rewards, dones, last, _ = inp
-        for cap in (0, 1, 2):
+        for cap in (0, 1, 2, 3):
             old = kernels.debug_knob("gae_form", cap)
             try:
                 ret, adv = torch.empty_like(values), torch.empty_like(values)
@@ -184,16 +186,16 @@ def test_slots_barrier_timeout_is_loud_and_recovers(cuda_device):
     waiting at once) raises the workspace's status word and writes NaN advantages instead of normalising with partial
     statistics; raise_on_gae_status raises and clears the word, and the next call (normal limit) is bit-exact again --
     the late blocks re-armed the ticket.  Both one-launch forms, plain and cooperative launches."""
-    for N in (65536, 65536 + 100):  # the staged form, the one-env-per-lane form
+    for N, fm in ((65536, 2), (65536 + 100, 1), (16384, 3)):  # each one-launch form
         inp = _slots_inputs(24, N, 0.02, cuda_device, 11)
         base = _slots_run(inp, form_cap=0)
         for coop in (0, 1):
             old = kernels.debug_knob("gae_spin_limit", 0)
             try:
-                form, ret, adv, slots, status = _slots_run(inp, coop=coop)
+                form, ret, adv, slots, status = _slots_run(inp, form_cap=fm, coop=coop)
             finally:
                 kernels.debug_knob("gae_spin_limit", old)
-            assert form in (1, 2)
+            assert form == fm
             assert status != 0, "no block timed out with a zero spin limit"
             assert torch.isnan(adv).any() and torch.equal(ret, base[1])
             values, rewards, dones, last, logp = inp
@@ -202,7 +204,7 @@ def test_slots_barrier_timeout_is_loud_and_recovers(cuda_device):
             with pytest.raises(kernels.GAEBarrierTimeout):
                 kernels.raise_on_gae_status(word)
             assert int(word.item()) == 0
-            form, ret, adv, slots, status = _slots_run(inp, coop=coop)
+            form, ret, adv, slots, status = _slots_run(inp, form_cap=fm, coop=coop)
             assert status == 0 and torch.equal(adv, base[2]) and torch.equal(slots, base[3])
             bar = ws[kernels._lib.lib().rslrl_compute_returns_status_offset() - 8:].view(torch.int32)[:2].tolist()
             assert bar[0] == 0, bar  # ticket re-armed
@@ -232,3 +234,17 @@ def test_update_raises_on_gae_barrier_timeout(cuda_device):
     finally:
         kernels.debug_knob("gae_spin_limit", old)
     assert runner.alg.storage.step == 0 and runner.alg.storage.gae_status is None
+
+
+def test_slots_mixed_grid_sizes_share_a_workspace(cuda_device):
+    """Calls of different grid sizes (and forms) on one stream share the workspace's barrier words: each call moves
+    every group's generation word, so a call after a smaller grid still completes its barrier (no time-out, no NaN) and
+    matches the two-launch form bit for bit."""
+    cases = [(24, 65636), (24, 65536), (24, 4096), (24, 65636), (24, 131072), (8, 1000), (24, 65536), (32, 16384)]
+    inputs = {c: _slots_inputs(c[0], c[1], 0.02, cuda_device, c[1] + c[0]) for c in set(cases)}
+    base = {c: _slots_run(inputs[c], form_cap=0) for c in set(cases)}
+    for c in cases + cases[::-1]:
+        for fm in (None, 1, 2, 3):
+            form, ret, adv, slots, status = _slots_run(inputs[c], form_cap=fm)
+            assert status == 0, (c, form)
+            assert torch.equal(adv, base[c][2]) and torch.equal(slots, base[c][3]), (c, form)
