@@ -323,9 +323,12 @@ class PPO:
     def _early_params(self):
         """Parameters whose gradients the manual backward completes before its last layer: every Linear of the actor
         and the critic but the first (the paired backward runs the output layers, then the hidden layers from the top;
-        the first layers' weight gradients come last).  Their arena prefix is all-reduced while the first layers'
-        backward runs (RSLRL_OVERLAP_ALLREDUCE=0: one all-reduce after the backward, as before)."""
-        if os.environ.get("RSLRL_OVERLAP_ALLREDUCE", "1") == "0" or not isinstance(self.policy, ActorCritic):
+        the first layers' weight gradients come last).  With RSLRL_OVERLAP_ALLREDUCE=1 their arena prefix is
+        all-reduced while the first layers' backward runs.  Off by default since round 6: on RCCL at
+        world 1 the two collectives cost what the single one does (profiles/r6_overlap_ab.json), and at world > 1 the
+        fused backward holds every CU's registers and LDS (one 256-VGPR workgroup per CU), so the collective's kernel
+        cannot co-run with it anyway -- the split only doubles the latency-bound calls."""
+        if os.environ.get("RSLRL_OVERLAP_ALLREDUCE", "0") != "1" or not isinstance(self.policy, ActorCritic):
             return ()
         out = []
         for net in (self.policy.actor, self.policy.critic):

@@ -40,6 +40,7 @@ def _worker(rank, port, out_dir):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    os.environ["RSLRL_OVERLAP_ALLREDUCE"] = "1"  # the opt-in early-prefix layout (off by default since round 6)
     try:
         res = {}
         ppo = _make_ppo(rank)
@@ -186,3 +187,14 @@ def test_adapt_learning_rate_device_matches_host_rule():
             got = adapt_learning_rate_device(torch.tensor(lr, dtype=torch.float64), kl_t.reshape(1), desired)
             assert got.dtype == torch.float64
             assert got.item() == _reference_rule(lr, kl_t, desired), (lr, kl, got.item())
+
+
+def test_single_collective_is_the_default(monkeypatch):
+    """Round 6: without RSLRL_OVERLAP_ALLREDUCE=1 the arena has no early prefix, so update() issues ONE
+    all-reduce of the gradients + KL per mini-batch after the backward."""
+    monkeypatch.delenv("RSLRL_OVERLAP_ALLREDUCE", raising=False)
+    ppo = _make_ppo(0)
+    assert ppo._early_params() == ()
+    assert ppo.grad_arena().early_numel == 0
+    monkeypatch.setenv("RSLRL_OVERLAP_ALLREDUCE", "1")
+    assert len(ppo._early_params()) == 4
