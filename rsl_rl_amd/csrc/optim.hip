@@ -30,11 +30,42 @@ __device__ __forceinline__ Span block_span(int64_t total) {
     return {b < total ? b : total, b + per < total ? b + per : total};
 }
 
-// workspace: [0] arrival ticket (u32, zero before and after), then fp64 partials [kBlocks], then fp32 coef
+// workspace: [0, kTicketBytes) arrival tickets (u32, zero before and after: the grid's at 0, group g's at
+// 128 (g + 1) -- each on a line of its own), fp64 partials [kBlocks], fp32 coef, then per tensor {bc1, bc2 sqrt,
+// step size} (written by grad_sq_kernel's last block after it advanced the step counters, read by adam_kernel)
+constexpr int kTicketGroup = 64;  // blocks per arrival group: at most 64 atomics queue on one word (512 on one word
+                                  // was most of this launch's time, and of round 5's one-launch Adam)
+constexpr int kTicketBytes = 128 * (kBlocks / kTicketGroup + 1);
+constexpr size_t kPartOff = kTicketBytes;
+constexpr size_t kCoefOff = kPartOff + kBlocks * sizeof(double);
+constexpr size_t kConstOff = kCoefOff + 256;
+constexpr size_t kAdamWsBytes = kConstOff + 3 * sizeof(float) * RSLRL_ADAM_MAX_TENSORS;
+
 __global__ __launch_bounds__(kThreadsA) void grad_sq_kernel(rslrl_adam_args_t a, unsigned* ticket, double* part,
-                                                            float* coef) {
+                                                            float* coef, float* consts) {
     __shared__ double scratch[kThreadsA / kWave];
     __shared__ int last;
+    // torch: _foreach_add_(state_steps, 1) before the update -- block 0, one lane per tensor, all in flight at once,
+    // off the grid's critical path (the last block only folds the norm); on the same lane that tensor's bias
+    // corrections and step size for adam_kernel (fused_adam_utils.cuh's expressions, once per tensor instead of once
+    // per block and tensor).  adam_kernel reads neither the counters nor these before this launch has ended.
+    if (blockIdx.x == 0) {
+        float* sp = nullptr;
+#pragma unroll
+        for (int i = 0; i < RSLRL_ADAM_MAX_TENSORS; ++i)
+            if (static_cast<int>(threadIdx.x) == i) sp = a.t[i].step;
+        if (static_cast<int>(threadIdx.x) < a.n) {
+            const float st1 = *sp + 1.0f;
+            *sp = st1;
+            const double step = static_cast<double>(st1);
+            const double lr = a.lr_dev ? static_cast<double>(*a.lr_dev) : a.lr;
+            const float bc1 = static_cast<float>(1.0 - pow(static_cast<double>(a.beta1), step));
+            const float bc2s = static_cast<float>(sqrt(1.0 - pow(static_cast<double>(a.beta2), step)));
+            consts[3 * threadIdx.x] = bc1;
+            consts[3 * threadIdx.x + 1] = bc2s;
+            consts[3 * threadIdx.x + 2] = static_cast<float>(lr / static_cast<double>(bc1));
+        }
+    }
     const int64_t total = a.offsets[a.n];
     const Span sp = block_span(total);
     double s = 0.0;
@@ -60,8 +91,17 @@ __global__ __launch_bounds__(kThreadsA) void grad_sq_kernel(rslrl_adam_args_t a,
         __hip_atomic_store(reinterpret_cast<unsigned long long*>(part + blockIdx.x), __double_as_longlong(bsum),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        last = t == gridDim.x - 1;
+        // two-level arrival: the group's last block takes the grid's ticket
+        const unsigned grp = blockIdx.x / kTicketGroup;
+        const unsigned gsize = min(static_cast<unsigned>(kTicketGroup), gridDim.x - grp * kTicketGroup);
+        unsigned* gt = ticket + 32 * (grp + 1);
+        int l = 0;
+        if (__hip_atomic_fetch_add(gt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gsize - 1) {
+            __hip_atomic_store(gt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned ng = (gridDim.x + kTicketGroup - 1) / kTicketGroup;
+            l = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ng - 1;
+        }
+        last = l;
     }
     __syncthreads();
     if (!last) return;
@@ -82,15 +122,6 @@ __global__ __launch_bounds__(kThreadsA) void grad_sq_kernel(rslrl_adam_args_t a,
     __syncthreads();  // scratch is reused
     if ((threadIdx.x & (kWave - 1)) == 0) scratch[threadIdx.x / kWave] = pv;
     __syncthreads();
-    // torch: _foreach_add_(state_steps, 1) before the update -- one lane per tensor, all in flight at once (a
-    // loop on one lane waited out ~14 dependent load/store round trips)
-    {
-        float* sp = nullptr;
-#pragma unroll
-        for (int i = 0; i < RSLRL_ADAM_MAX_TENSORS; ++i)
-            if (static_cast<int>(threadIdx.x) == i) sp = a.t[i].step;
-        if (static_cast<int>(threadIdx.x) < a.n) *sp += 1.0f;
-    }
     if (threadIdx.x != 0) return;
     double tot = 0.0;
     for (int w = 0; w < kThreadsA / kWave; ++w) tot += scratch[w];
@@ -105,11 +136,11 @@ __global__ __launch_bounds__(kThreadsA) void grad_sq_kernel(rslrl_adam_args_t a,
     __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__global__ __launch_bounds__(kThreadsA) void adam_kernel(rslrl_adam_args_t a, const float* __restrict__ coef) {
+__global__ __launch_bounds__(kThreadsA) void adam_kernel(rslrl_adam_args_t a, const float* __restrict__ coef,
+                                                         const float* __restrict__ consts) {
     const int64_t total = a.offsets[a.n];
     const Span sp = block_span(total);
     const float c = *coef;
-    const double lr = a.lr_dev ? static_cast<double>(*a.lr_dev) : a.lr;
     const double b1 = a.beta1, b2 = a.beta2, eps = a.eps;
     // tensors in order, clipped to the block's span (wave-uniform tensor index: scalar pointer loads)
     for (int ti = 0; ti < a.n; ++ti) {
@@ -117,10 +148,8 @@ __global__ __launch_bounds__(kThreadsA) void adam_kernel(rslrl_adam_args_t a, co
         const int64_t lo = sp.begin > o0 ? sp.begin : o0, hi = sp.end < o1 ? sp.end : o1;
         if (lo >= hi) continue;
         const rslrl_adam_tensor_t t = a.t[ti];
-        const double step = static_cast<double>(*t.step);
-        const float bc1 = static_cast<float>(1.0 - pow(b1, step));
-        const float bc2s = static_cast<float>(sqrt(1.0 - pow(b2, step)));
-        const float step_size = static_cast<float>(lr / static_cast<double>(bc1));
+        const float bc2s = consts[3 * ti + 1];
+        const float step_size = consts[3 * ti + 2];
         for (int64_t e = lo + threadIdx.x; e < hi; e += kThreadsA) {
             const int64_t i = e - o0;
             const float g = t.grad[i] * c;  // the clipped gradient (fp32 multiply, as torch's foreach mul)
@@ -144,7 +173,7 @@ __global__ __launch_bounds__(kThreadsA) void adam_kernel(rslrl_adam_args_t a, co
 
 using namespace rslrl;
 
-extern "C" size_t rslrl_adam_workspace_bytes(void) { return 256 + kBlocks * sizeof(double) + 256; }
+extern "C" size_t rslrl_adam_workspace_bytes(void) { return kAdamWsBytes; }
 
 extern "C" int rslrl_clip_adam_step(const rslrl_adam_args_t* args, void* workspace, size_t workspace_bytes,
                                     rslrl_stream_t stream) {
@@ -161,12 +190,13 @@ extern "C" int rslrl_clip_adam_step(const rslrl_adam_args_t* args, void* workspa
     a.offsets[a.n] = off;  // all-empty tensors still advance the step counters (torch increments them too)
     char* ws = static_cast<char*>(workspace);
     unsigned* ticket = reinterpret_cast<unsigned*>(ws);
-    double* part = reinterpret_cast<double*>(ws + 256);
-    float* coef = reinterpret_cast<float*>(ws + 256 + kBlocks * sizeof(double));
+    double* part = reinterpret_cast<double*>(ws + kPartOff);
+    float* coef = reinterpret_cast<float*>(ws + kCoefOff);
+    float* consts = reinterpret_cast<float*>(ws + kConstOff);
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    hipLaunchKernelGGL(grad_sq_kernel, dim3(kBlocks), dim3(kThreadsA), 0, st, a, ticket, part, coef);
+    hipLaunchKernelGGL(grad_sq_kernel, dim3(kBlocks), dim3(kThreadsA), 0, st, a, ticket, part, coef, consts);
     int rc = launch_status();
     if (rc) return rc;
-    hipLaunchKernelGGL(adam_kernel, dim3(kBlocks), dim3(kThreadsA), 0, st, a, coef);
+    hipLaunchKernelGGL(adam_kernel, dim3(kBlocks), dim3(kThreadsA), 0, st, a, coef, consts);
     return launch_status();
 }
