@@ -80,6 +80,17 @@ def test_update_c3_matches_reference(golden_meta, cuda_device, monkeypatch):
     # bits), so the returns agree within fp32 rounding (GAE itself is bit-exact: tests/test_gpu_gae.py)
     assert torch.allclose(st.returns[:2, :256].cpu(), torch.from_numpy(z["returns_head"]), rtol=1e-5, atol=1e-6)
     assert torch.allclose(st.advantages[:2, :256].cpu(), torch.from_numpy(z["advantages_head"]), rtol=1e-5, atol=1e-6)
+    # the whole [T, N] GAE against the CPU oracle on the same inputs (our critic's bootstrap values): returns bit-exact,
+    # normalised advantages within 1e-5 (fp64 statistics in another order), the slot array {value, log-prob, return,
+    # advantage} exactly what the update gathers
+    from oracle import ppo_oracle as O
+    with torch.inference_mode():
+        lv = alg.policy.evaluate({"policy": torch.from_numpy(last_obs).to(dev)}).reshape(-1).cpu().numpy()
+    oret, oadv = O.gae(st.values.cpu().numpy().reshape(T, N), st.rewards.cpu().numpy().reshape(T, N),
+                       st.dones.cpu().numpy().reshape(T, N), lv, alg.gamma, alg.lam)
+    assert np.array_equal(st.returns.cpu().numpy().reshape(T, N), oret)
+    np.testing.assert_allclose(st.advantages.cpu().numpy().reshape(T, N), O.adv_normalize(oadv), rtol=1e-5, atol=1e-5)
+    assert torch.equal(st.slots, torch.cat([st.values, st.actions_log_prob, st.returns, st.advantages], dim=-1))
     torch.default_generator.set_state(torch.from_numpy(z["gen_state"].copy()))
 
     counts = {"actor_head": 0, "hidden_bwd": 0}
