@@ -110,13 +110,12 @@ __device__ __forceinline__ void fs_store_x1(const float4& v, int j, char* __rest
 }
 
 __device__ __forceinline__ float fs_elu_neg(float v) {  // mlp_gemm.hip elu_neg: the same expression
-    float t = __fmaf_rn(v, 2.7557319e-6f, 2.4801587e-5f);
-    t = __fmaf_rn(v, t, 1.9841270e-4f);
-    t = __fmaf_rn(v, t, 1.3888889e-3f);
-    t = __fmaf_rn(v, t, 8.3333333e-3f);
-    t = __fmaf_rn(v, t, 4.1666667e-2f);
-    t = __fmaf_rn(v, t, 1.6666667e-1f);
-    t = __fmaf_rn(v, t, 0.5f);
+    // minimax fit of expm1(v) / v on [-0.5, 0] (degree 5, Horner with explicit fma; round 6): 1.26 ulp at most against
+    // expm1 over every 7th fp32 in [-0.5, 0) (the degree-9 Taylor form it replaced: 1.14 ulp) in 3 fewer FMAs
+    float t = __fmaf_rn(v, 0.0011216326f, 0.008187376f);
+    t = __fmaf_rn(v, t, 0.04162908f);
+    t = __fmaf_rn(v, t, 0.16666223f);
+    t = __fmaf_rn(v, t, 0.49999982f);
     t = __fmaf_rn(v, t, 1.0f);
     const float poly = v * t;
     const float e = __expf(v) - 1.0f;

@@ -35,7 +35,8 @@ __device__ __forceinline__ float quad_sum(float v) {
 // 16 lanes per column, each adding rows l16, l16+16, l16+32, l16+48 in that order, then a 16-lane
 // butterfly.  Every load is issued before the first add, so the fold costs one memory round trip.
 // Loads use sc1 (bypass the non-coherent per-CU cache); the caller has acquired.
-template <int kMaxC>
+// kRows = 8 (rows l16 + 16 i, i < 8: n <= 128) for the groups of 128 blocks of a grid over 4096 blocks.
+template <int kMaxC, int kRows = 4>
 __device__ __forceinline__ void fold_columns(const double* __restrict__ src, int ld, int n, int ncols,
                                              double* __restrict__ out) {
     constexpr int kPasses = (kMaxC + 15) / 16;
@@ -43,12 +44,12 @@ __device__ __forceinline__ void fold_columns(const double* __restrict__ src, int
     const int cc = threadIdx.x >> 4;
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<double*>(src), 0, static_cast<int>(sizeof(double) * ncols * ld), 0x00020000);
-    double v[kPasses][4];
+    double v[kPasses][kRows];
 #pragma unroll
     for (int ps = 0; ps < kPasses; ++ps) {
         const int c = ps * 16 + cc;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < kRows; ++i) {
             const int r = l16 + 16 * i;
             // out-of-range offsets read 0 through the buffer resource
             const int off = (c < ncols && r < n) ? (c * ld + r) * 8 : 0x7ffffff0;
@@ -58,6 +59,8 @@ __device__ __forceinline__ void fold_columns(const double* __restrict__ src, int
 #pragma unroll
     for (int ps = 0; ps < kPasses; ++ps) {
         double t = ((v[ps][0] + v[ps][1]) + v[ps][2]) + v[ps][3];
+#pragma unroll
+        for (int i = 4; i < kRows; ++i) t += v[ps][i];
 #pragma unroll
         for (int off = 8; off >= 1; off >>= 1) t += __shfl_xor(t, off, kWave);
         const int c = ps * 16 + cc;
@@ -72,9 +75,12 @@ __device__ __forceinline__ void fold_columns(const double* __restrict__ src, int
 // ncols doubles).  Returns true only in that final block, with `folded` complete.  tickets: 1 + ng words, zero
 // before the launch and re-armed to zero by it (the global word by the caller of the final block: it returns with
 // tickets[0] still counting).  `flag`: an LDS int.  Called by every thread of the block.
-template <int kMaxC>
+// G: blocks per group -- kFoldGroup, or 2 kFoldGroup for grids over kFoldGroup^2 blocks (up to 8192; the groups then
+// fold 8 rows per lane, fold_columns<kMaxC, 8>)
+template <int kMaxC, int G = kFoldGroup>
 __device__ __forceinline__ bool fold_grid_partials(double* __restrict__ partials, unsigned* __restrict__ tickets,
                                                    int nb, int ncols, double v, double* folded, int* flag) {
+    constexpr int kFoldGroup = G;
     const int ng = (nb + kFoldGroup - 1) / kFoldGroup;
     if (static_cast<int>(threadIdx.x) < ncols)
         __hip_atomic_store(reinterpret_cast<unsigned long long*>(partials + static_cast<int64_t>(threadIdx.x) * nb +
@@ -97,7 +103,7 @@ __device__ __forceinline__ bool fold_grid_partials(double* __restrict__ partials
     __syncthreads();
     if (!*flag) return false;
     if (threadIdx.x == 0) __hip_atomic_store(tickets + 1 + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    fold_columns<kMaxC>(partials + g0, nb, gsz, ncols, folded);
+    fold_columns<kMaxC, (G > 64 ? 8 : 4)>(partials + g0, nb, gsz, ncols, folded);
     __syncthreads();
     if (ng == 1) return true;
     double* gpart = partials + static_cast<int64_t>(ncols) * nb;

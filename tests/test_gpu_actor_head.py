@@ -71,8 +71,9 @@ def _close(a, b, rtol):
 
 
 @pytest.mark.parametrize("M,clipped,kl", [(4096, True, True), (4096, False, False), (98304, True, True),
-                                          (393216, True, True)])
+                                          (393216, True, True), (786432, True, True)])
 def test_actor_head_matches_separate_launches(M, clipped, kl, cuda_device):
+    """786,432 rows (C4's 131,072 envs on one GPU: 6,144 tiles) fold the loss partials in groups of 128 tiles."""
     dev = cuda_device
     x, w, b, wo, bo, sigma, values, batch = _problem(M, dev, 21 + M)
     img, out_img, img_t = fused_mlp.bimages([(w, False), (wo, False, _lib.BIMAGE_LAYOUT_OUT), (wo, True)])
