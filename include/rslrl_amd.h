@@ -31,7 +31,7 @@ extern "C" {
 
 typedef struct ihipStream_t* rslrl_stream_t; /* == hipStream_t */
 
-#define RSLRL_ABI_VERSION 18
+#define RSLRL_ABI_VERSION 19
 
 enum {
     RSLRL_OK = 0,
@@ -82,9 +82,10 @@ int rslrl_compute_returns_records(const float* values, const float* rewards, con
  * the normalisation run as ONE launch (a grid barrier between the scan and the normalisation; same bits as the
  * two-launch form, RSLRL_GAE_FUSED=0 forces that).  The barrier words sit after the partials in the workspace:
  * a workspace must be zero-filled before its first use with this entry point (the library leaves it so).
- * ABI 18: for N a multiple of 64 (16-byte aligned pointers) the one launch is the LDS-staged form (64 envs per block,
- * N / 64 blocks; the same bits).  The one-launch forms run as a cooperative launch where the device supports it (a
- * refused launch runs the two-launch form).  A workspace serves one stream at a time (the barrier's ticket).  If the
+ * ABI 18: the one launch takes one env per lane in 256-thread blocks (the fastest of the three one-launch forms at
+ * every size measured; the LDS-staged and 64-thread forms stay selectable through rslrl_debug_knob("gae_form"), the
+ * same bits).  RSLRL_GAE_COOP=1 runs it as a cooperative launch (a refused launch runs the two-launch form; off by
+ * default: +6-17 us per call on this runtime).  A workspace serves one stream at a time (the barrier's ticket).  If the
  * grid barrier ever times out (blocks not co-resident) the call writes NaN advantages and sets the uint32 status word
  * at rslrl_compute_returns_status_offset() in the workspace to nonzero; the caller reads it at its next
  * synchronisation and clears it (PPO.update raises on it). */
@@ -102,8 +103,9 @@ size_t rslrl_compute_returns_status_offset(void);
 int rslrl_compute_returns_slots_form(int64_t T, int64_t N, const float* values, const float* rewards,
                                      const uint8_t* dones, const float* log_prob, const float* returns,
                                      const float* advantages);
-/* ABI 18: test / diagnostic knobs (not a reference interface).  "gae_form": -1 auto, else the highest
- * rslrl_compute_returns_slots form allowed (0 forces the two-launch path); "gae_coop": -1 auto, 0 plain launch, 1
+/* ABI 18: test / diagnostic knobs (not a reference interface).  "gae_form": -1 auto, else that
+ * rslrl_compute_returns_slots form where it fits, the two-launch path otherwise (0 forces it; 3 = one env per lane in
+ * 64-thread blocks); "gae_coop": -1 auto (RSLRL_GAE_COOP), 0 plain launch, 1
  * cooperative launch; "gae_spin_limit": polls before a grid-barrier wait gives up (default 2^22).  Writes the old
  * value into *previous (may be NULL). */
 int rslrl_debug_knob(const char* name, int64_t value, int64_t* previous);
@@ -564,6 +566,28 @@ int64_t rslrl_hidden_bwd_slices(int64_t M);
 size_t rslrl_hidden_bwd_partial_floats(void);
 int rslrl_hidden_bwd_pair(const rslrl_hidden_bwd_problem_t* p0, const rslrl_hidden_bwd_problem_t* p1, int64_t M,
                           int32_t width, rslrl_stream_t stream);
+
+/* ABI 19: the rollout's actor and critic forward in one launch -- policy.act + policy.evaluate of an env step
+ * (rsl_rl/algorithms/ppo.py:155-156, rsl_rl/networks/mlp.py:106-114): for each of the two problems, `hidden` Linear +
+ * ELU layers of width 256 (the first on the k0-wide input x) and the output Linear, y = MLP(x), on x6 arithmetic.  The
+ * hidden activations stay on chip.  y is bit-identical to the layer-by-layer path (rslrl_linear_gemm_pair per hidden
+ * layer, then RSLRL_LINEAR_FWD_OUT for the last hidden layer and the output layer).  bimage[l]: layer l's layout-0
+ * image (RSLRL_BIMAGE_LAYOUT_GEMM), out_image: the output layer's RSLRL_BIMAGE_LAYOUT_OUT image.  Both problems share
+ * M, k0 and hidden.  RSLRL_E_UNSUPPORTED (nothing launched) unless M is a multiple of 64, k0 in {16, 32, 48, 64},
+ * 2 <= hidden <= 4 and 1 <= nout <= 16. */
+typedef struct {
+    const float* x;         /* [M, k0], 16-byte aligned */
+    int32_t k0;
+    int32_t hidden;
+    const void* bimage[4];  /* layers 0 .. hidden - 1 */
+    const float* bias[4];   /* [256] each, 16-byte aligned */
+    const void* out_image;
+    const float* out_bias;  /* [nout] */
+    int32_t nout;
+    float* y;               /* [M, nout] */
+} rslrl_rollout_mlp_t;
+int rslrl_rollout_mlp_pair(const rslrl_rollout_mlp_t* a0, const rslrl_rollout_mlp_t* a1, int64_t M,
+                           rslrl_stream_t stream);
 
 /* ------------------------------------------------------------------------------------------------
  * Rollout-side record: for environment step t, in one launch,

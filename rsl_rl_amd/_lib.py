@@ -19,7 +19,7 @@ import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 # RSLRL_AMD_LIB: an alternative in-tree build of the same library (A/B kernel experiments)
 LIB_PATH = os.environ.get("RSLRL_AMD_LIB") or os.path.join(LIB_DIR, "librslrl_amd.so")
-ABI_VERSION = 18
+ABI_VERSION = 19
 
 # symbols declared in include/rslrl_amd.h (tests/test_capi.py checks the header against this list)
 EXPORTED_SYMBOLS = (
@@ -91,6 +91,7 @@ EXPORTED_SYMBOLS = (
     "rslrl_hidden_bwd_slices",
     "rslrl_hidden_bwd_partial_floats",
     "rslrl_hidden_bwd_pair",
+    "rslrl_rollout_mlp_pair",
 )
 
 MAX_GATHER_FIELDS = 16
@@ -367,6 +368,23 @@ class HiddenBwdProblem(ctypes.Structure):
     ]
 
 
+class RolloutMlp(ctypes.Structure):
+    """include/rslrl_amd.h rslrl_rollout_mlp_t"""
+    _fields_ = [
+        ("x", ctypes.c_void_p),
+        ("k0", ctypes.c_int32),
+        ("hidden", ctypes.c_int32),
+        ("bimage", ctypes.c_void_p * 4),
+        ("bias", ctypes.c_void_p * 4),
+        ("out_image", ctypes.c_void_p),
+        ("out_bias", ctypes.c_void_p),
+        ("nout", ctypes.c_int32),
+        ("y", ctypes.c_void_p),
+    ]
+
+
+ROLLOUT_MLP_MAX_HIDDEN, ROLLOUT_MLP_MAX_OUT, ROLLOUT_MLP_ROWS = 4, 16, 64
+
 RND_MAX_IN, RND_MAX_HIDDEN, RND_MAX_OUT = 64, 64, 8
 
 _lib = None
@@ -492,6 +510,8 @@ def _declare(L):
     L.rslrl_hidden_bwd_partial_floats.argtypes = []
     L.rslrl_hidden_bwd_pair.restype = ctypes.c_int
     L.rslrl_hidden_bwd_pair.argtypes = [ctypes.POINTER(HiddenBwdProblem), ctypes.POINTER(HiddenBwdProblem), I64, I32, P]
+    L.rslrl_rollout_mlp_pair.restype = ctypes.c_int
+    L.rslrl_rollout_mlp_pair.argtypes = [ctypes.POINTER(RolloutMlp), ctypes.POINTER(RolloutMlp), I64, P]
     L.rslrl_linear_wgrad_bias_pair.restype = ctypes.c_int
     L.rslrl_linear_wgrad_bias_pair.argtypes = [ctypes.POINTER(WgradProblem), ctypes.POINTER(WgradProblem), I64, I32,
                                                I32, I32, I32, I32, P]

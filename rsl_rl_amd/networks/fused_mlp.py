@@ -1208,6 +1208,50 @@ _side_streams: dict = {}
 _PAIR_TRAIN = os.environ.get("RSLRL_PAIR_TRAIN", "1") != "0"
 # RSLRL_OUT_PAIR=0 keeps the rollout's two fused output-layer launches separate (A/B)
 _OUT_PAIR = os.environ.get("RSLRL_OUT_PAIR", "1") != "0"
+# RSLRL_ROLLOUT_MLP=0 keeps the rollout's forward layer by layer (A/B; the same bits)
+_ROLLOUT_MLP = os.environ.get("RSLRL_ROLLOUT_MLP", "1") != "0"
+rollout_mlp_launches = 0
+
+
+def rollout_mlp_pair(xs, ws, bs, imgs, nh: int):
+    """The rollout's actor and critic forward, every layer in one launch (rslrl_rollout_mlp_pair): y = [y_a, y_b],
+    bit-identical to the layer-by-layer launches of fused_mlp_forward_pair; None when the shapes are not covered
+    (nothing launched).  xs: the two inputs [M, k0]; ws, bs, imgs: per network, as fused_mlp_forward_pair holds them
+    (x6 forward images, the output layer's image)."""
+    M, k0 = xs[0].shape
+    if (M % _lib.ROLLOUT_MLP_ROWS or k0 not in (16, 32, 48, 64) or not 2 <= nh <= _lib.ROLLOUT_MLP_MAX_HIDDEN
+            or xs[1].shape != xs[0].shape):
+        return None
+    for i in range(2):
+        w = ws[i]
+        if w[0].shape != (256, k0) or any(w[l].shape != (256, 256) for l in range(1, nh)) or w[nh].shape[1] != 256:
+            return None
+        if not 1 <= w[nh].shape[0] <= _lib.ROLLOUT_MLP_MAX_OUT or imgs[i][2] is None:
+            return None
+        if xs[i].data_ptr() % 16 or not xs[i].is_contiguous():
+            return None
+    ys = [torch.empty(M, ws[i][nh].shape[0], device=xs[0].device, dtype=torch.float32) for i in range(2)]
+    args = []
+    for i in range(2):
+        a = _lib.RolloutMlp()
+        a.x, a.k0, a.hidden = xs[i].data_ptr(), k0, nh
+        for l in range(nh):
+            a.bimage[l] = imgs[i][0][l].data_ptr()
+            a.bias[l] = bs[i][l].data_ptr()
+        a.out_image, a.out_bias = imgs[i][2].data_ptr(), bs[i][nh].data_ptr()
+        a.nout, a.y = ws[i][nh].shape[0], ys[i].data_ptr()
+        args.append(a)
+    nout = ys[0].shape[1] + ys[1].shape[1]
+    flops = 2 * M * 256 * (2 * k0 + 2 * 256 * (nh - 1) + nout)
+    with timer.span(f"rollout_mlp_pair[M={M},K={k0},hidden={nh},out={nout}]", xs[0].device, 4 * M * (2 * k0 + nout),
+                    flops):
+        rc = _lib.lib().rslrl_rollout_mlp_pair(ctypes.byref(args[0]), ctypes.byref(args[1]), M, _stream(xs[0]))
+    if rc == _lib.E_UNSUPPORTED:
+        return None
+    _lib.check(rc, "rslrl_rollout_mlp_pair")
+    global rollout_mlp_launches
+    rollout_mlp_launches += 1
+    return ys
 
 
 def side_stream(device):
@@ -1261,6 +1305,11 @@ def fused_mlp_forward_pair(mlp_a: nn.Sequential, x_a: torch.Tensor, mlp_b: nn.Se
             _pair_memo[memo_key] = (weakref.ref(mlp_a), weakref.ref(mlp_b), (ws, bs, h3, fuse, imgs, nh))
     arith = lambda l: _lib.ARITH_H3 if h3[l] else _lib.ARITH_X6  # noqa: E731
     h = [x_a if x_a.is_contiguous() else x_a.contiguous(), x_b if x_b.is_contiguous() else x_b.contiguous()]
+    y = None
+    if _ROLLOUT_MLP and not any(h3) and all(fuse):
+        y = rollout_mlp_pair(h, ws, bs, imgs, nh)
+    if y is not None:
+        return _unflatten(mlp_a, y[0]), _unflatten(mlp_b, y[1])
     amax = [None, None]
     y = [None, None]
     for l in range(nh):

@@ -1,7 +1,8 @@
-"""The ELU's negative branch on the GPU GEMM epilogues (mlp_gemm.hip elu_neg, mlp_fwd_stream.hip fs_elu_neg): a degree-5
+"""The ELU's negative branch on the GPU GEMM epilogues (mlp_gemm.hip elu_neg, mlp_fwd_stream.hip fs_elu_neg,
+rollout_mlp.hip rm_elu_neg): a degree-5
 polynomial for expm1 on [-0.5, 0], exp(v) - 1 below.  Host check of the polynomial part, evaluated as the kernels do
 (fp32 Horner with fused multiply-adds, then one fp32 multiply), against expm1 in fp64: within 1.3 ulp of fp32 on
-every 97th fp32 in [-0.5, 0); and both kernels carry the same coefficients (their outputs are compared bit for bit by
+every 97th fp32 in [-0.5, 0); and every kernel carries the same coefficients (their outputs are compared bit for bit by
 the GPU tests)."""
 
 import os
@@ -41,5 +42,7 @@ def test_elu_polynomial_is_fp32_faithful():
     assert ulp.max() <= 1.3, ulp.max()
 
 
-def test_both_epilogues_use_the_same_polynomial():
-    assert coefficients("mlp_gemm.hip", "elu_neg") == coefficients("mlp_fwd_stream.hip", "fs_elu_neg")
+def test_every_epilogue_uses_the_same_polynomial():
+    c = coefficients("mlp_gemm.hip", "elu_neg")
+    assert c == coefficients("mlp_fwd_stream.hip", "fs_elu_neg")
+    assert c == coefficients("rollout_mlp.hip", "rm_elu_neg")

@@ -81,7 +81,9 @@ def test_pair_rejects_mismatched_shapes(cuda_device):
 @pytest.mark.parametrize("critic_width,state_dependent_std", [(48, False), (48, True), (52, False)])
 def test_act_and_evaluate_matches_two_calls(critic_width, state_dependent_std, cuda_device, monkeypatch):
     """Same obs width: every hidden layer but the fused output layer goes through the pair launch; another
-    critic width: the pair does not qualify and the two forwards run."""
+    critic width: the pair does not qualify and the two forwards run.  (The layer-by-layer pair path: the one-launch
+    rollout forward, taken by default where it applies, is tests/test_gpu_rollout_mlp.py's.)"""
+    monkeypatch.setattr(fused_mlp, "_ROLLOUT_MLP", False)
     torch.manual_seed(0)
     obs = {"policy": torch.randn(4096, 48, device=cuda_device),
            "critic": torch.randn(4096, critic_width, device=cuda_device)}
