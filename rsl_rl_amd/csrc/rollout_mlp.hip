@@ -384,11 +384,12 @@ __global__ __launch_bounds__(kRmThreads, 2) void rollout_mlp_kernel(RmArgs a) {
 }
 
 template <int KC0>
-void rm_launch(const RmArgs& a, int nr0, int nr1, dim3 g, hipStream_t st) {
-    if (nr0 == 4 && nr1 == 1) hipLaunchKernelGGL((rollout_mlp_kernel<KC0, 4, 1>), g, dim3(kRmThreads), 0, st, a);
-    else if (nr0 == 4) hipLaunchKernelGGL((rollout_mlp_kernel<KC0, 4, 4>), g, dim3(kRmThreads), 0, st, a);
-    else if (nr1 == 1) hipLaunchKernelGGL((rollout_mlp_kernel<KC0, 1, 1>), g, dim3(kRmThreads), 0, st, a);
-    else hipLaunchKernelGGL((rollout_mlp_kernel<KC0, 1, 4>), g, dim3(kRmThreads), 0, st, a);
+void rm_launch(const RmArgs& a, int nr0, int nr1, int64_t M, hipStream_t st) {
+    const dim3 g(static_cast<unsigned>(M / kRmT), 2), b(kRmThreads);
+    if (nr0 == 4 && nr1 == 1) hipLaunchKernelGGL((rollout_mlp_kernel<KC0, 4, 1>), g, b, 0, st, a);
+    else if (nr0 == 4) hipLaunchKernelGGL((rollout_mlp_kernel<KC0, 4, 4>), g, b, 0, st, a);
+    else if (nr1 == 1) hipLaunchKernelGGL((rollout_mlp_kernel<KC0, 1, 1>), g, b, 0, st, a);
+    else hipLaunchKernelGGL((rollout_mlp_kernel<KC0, 1, 4>), g, b, 0, st, a);
 }
 
 bool rm_aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
@@ -429,13 +430,12 @@ extern "C" int rslrl_rollout_mlp_pair(const rslrl_rollout_mlp_t* a0, const rslrl
         p.nout = s.nout;
         nr[i] = s.nout <= 4 ? 1 : 4;  // the fused output kernel's choice (mlp_gemm.hip launch<kEpiBiasEluOut>)
     }
-    const dim3 g(static_cast<unsigned>(M / kRmT), 2);
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     switch (k0 / 16) {
-        case 1: rm_launch<1>(args, nr[0], nr[1], g, st); break;
-        case 2: rm_launch<2>(args, nr[0], nr[1], g, st); break;
-        case 3: rm_launch<3>(args, nr[0], nr[1], g, st); break;
-        default: rm_launch<4>(args, nr[0], nr[1], g, st); break;
+        case 1: rm_launch<1>(args, nr[0], nr[1], M, st); break;
+        case 2: rm_launch<2>(args, nr[0], nr[1], M, st); break;
+        case 3: rm_launch<3>(args, nr[0], nr[1], M, st); break;
+        default: rm_launch<4>(args, nr[0], nr[1], M, st); break;
     }
     return launch_status();
 }

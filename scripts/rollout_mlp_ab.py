@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--steps", type=int, default=240)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--graph", type=int, default=1)
+    ap.add_argument("--modes", nargs="+", default=["0", "1"], help="0: layer by layer; 1: rslrl_rollout_mlp_pair")
     ap.add_argument("--out", default="gpurun_out/rollout_mlp_ab.json")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
@@ -39,12 +40,10 @@ def main():
                           critic_hidden_dims=[256, 256, 256], actor_obs_normalization=True,
                           critic_obs_normalization=True).to(dev)
         pol.update_normalization(obs)
-        res, hres = {0: [], 1: []}, {0: [], 1: []}
+        res, hres = {m: [] for m in a.modes}, {m: [] for m in a.modes}
         for r in range(a.rounds):
-            for mode in ((0, 1) if r % 2 == 0 else (1, 0)):
-                if os.environ.get("RSLRL_ROLLOUT_MLP") is not None and a.rounds == 1:
-                    mode = int(os.environ["RSLRL_ROLLOUT_MLP"])
-                fused_mlp._ROLLOUT_MLP = bool(mode)
+            for mode in (a.modes if r % 2 == 0 else a.modes[::-1]):
+                fused_mlp._ROLLOUT_MLP = mode != "0"
                 g = RolloutActGraph(pol) if a.graph else None
                 with torch.inference_mode(), fused_mlp.frozen_weights():
                     for _ in range(4):  # eager, capture, replays
@@ -66,10 +65,10 @@ def main():
                 print(json.dumps({"num_envs": n, "round": r, "rollout_mlp": mode, "us_per_step": round(us, 2),
                                   "host_us_per_step": round(host, 2), "graph_used": bool(g is not None and g._graph is not None)}),
                       flush=True)
-        summ = {("one_launch" if m else "layer_by_layer"): {"us_per_step": [round(x, 2) for x in v],
+        summ = {("layer_by_layer" if m == "0" else "one_launch"): {"us_per_step": [round(x, 2) for x in v],
                                                           "median": round(statistics.median(v), 2),
                                                           "host_us_per_step_median": round(statistics.median(hres[m]), 2)}
-                for m, v in res.items()}
+                for m, v in res.items() if v}
         out["runs"].append({"num_envs": n, "steps": a.steps, "graph": bool(a.graph), **summ})
         print(json.dumps(out["runs"][-1]), flush=True)
     fused_mlp._ROLLOUT_MLP = True
