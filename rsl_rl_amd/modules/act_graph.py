@@ -50,6 +50,7 @@ class RolloutActGraph:
         self._dists = {}  # id(output tuple) -> the Normal over that graph's static mean / scale
         self._groups = None  # the observation groups the step reads
         self._mods = None  # the policy's modules (their parameters and buffers key the configuration)
+        self._parents = []  # [(module, its children)] of the modules that have children: a replaced module shows here
 
     @staticmethod
     def enabled() -> bool:
@@ -59,9 +60,12 @@ class RolloutActGraph:
         pol = self.policy
         if self._groups is None:
             self._groups = sorted(set(pol.obs_groups["policy"]) | set(pol.obs_groups["critic"]))
-            # the policy's modules, listed once: a step reads their parameter / buffer dicts directly (walking the module
-            # tree per step was ~20 us of host time at the 16,384-env share, where the rollout is host-bound)
+        # the policy's modules, listed once and re-listed when any module's children change: a step reads their
+        # parameter / buffer dicts directly (walking the module tree per step was ~20 us of host time at the 16,384-env
+        # share, where the rollout was host-bound)
+        if self._mods is None or any(tuple(m._modules.values()) != kids for m, kids in self._parents):
             self._mods = list(pol.modules())
+            self._parents = [(m, tuple(m._modules.values())) for m in self._mods if m._modules]
         shapes = []
         for g in self._groups:
             t = obs[g]
