@@ -29,6 +29,7 @@ SHORT = {
     "mlp_gemm_x6_actor_head_kernel": "x6_actor_head",
     "hidden_bwd_kernel": "x6_hidden_bwd_pair",
     "fwd_stream_kernel": "x6_fwd_stream_pair",
+    "rollout_mlp_kernel": "rollout_mlp_pair",
     "value_head_stream_kernel": "x6_value_head_stream",
     "out_bwd_valu_kernel": "out_bwd",
     "out_bwd_valu_pair_kernel": "out_bwd_pair",
