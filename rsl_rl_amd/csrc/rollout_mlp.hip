@@ -36,6 +36,12 @@ constexpr int kRmImgPlaneU = 256 * 32 / 16;  // 16-byte units of one plane of on
 constexpr int kRmImgChunkU = 3 * kRmImgPlaneU;
 constexpr int kRmOutPlaneUnits = 4 * 2 * 2 * 3 * 2 * 32;  // mlp_gemm.hip kOutImagePlaneUnits (BIMAGE_LAYOUT_OUT)
 constexpr uint32_t kRmRsrcFlags = 0x00020000;
+#ifndef RSLRL_RM_COOP
+#define RSLRL_RM_COOP 1  // cooperative per-chunk split into a plane stage (A/B knob: 0 = every wave splits on read)
+#endif
+constexpr int kRmStagePlane = kRmT * 32;          // one bf16 plane of one k-chunk: 2 KiB
+constexpr int kRmStageBuf = 3 * kRmStagePlane;    // 6 KiB
+constexpr int kRmLds = kRmT * 256 * 4 + (RSLRL_RM_COOP ? 2 * kRmStageBuf : 0);  // 76 KiB: two workgroups per CU
 
 struct RmProblem {
     const float* x;                 // [M, K0]
@@ -88,6 +94,17 @@ __device__ __forceinline__ f32x16 mfma_x6_ct(const bf16x8 (&x)[3], const bf16x8 
     acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[0], x[0], acc, 0, 0, 0);
     return acc;
 }
+
+using u32x2 = __attribute__((ext_vector_type(2))) unsigned int;
+
+__device__ __forceinline__ bf16x8 rm_lds_frag(int addr) {
+    typedef __attribute__((address_space(3))) bf16x8 lds_b8;
+    return *reinterpret_cast<const lds_b8*>(addr);
+}
+
+// workgroup barrier for LDS hand-offs only: the register prefetches in flight (weights, biases) stay in flight
+// (__syncthreads' fence would wait for them: vmcnt(0))
+__device__ __forceinline__ void rm_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 __device__ __forceinline__ float4 rm_lds_read(int addr) {
     typedef __attribute__((address_space(3))) f32x4 lds_f4;
@@ -169,7 +186,7 @@ __device__ __forceinline__ void rm_body(const RmProblem& P, int hidden, char* ld
                     vw[j][s2][0] = owf_at(j, s2, 0)[0];
                     vw[j][s2][1] = owf_at(j, s2, 0)[1];
                 }
-        } else {
+        } else if (!RSLRL_RM_COOP) {  // (the cooperative form reads them where they are used: registers)
 #pragma unroll
             for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -179,6 +196,79 @@ __device__ __forceinline__ void rm_body(const RmProblem& P, int hidden, char* ld
         }
     };
 
+#if RSLRL_RM_COOP
+    // Cooperative split (the default): per k-chunk each wave splits a quarter of the chunk -- rows 16 w + (lane & 15),
+    // column quad lane >> 4 -- into the three planes of a double-buffered 6 KiB stage past H, and after a workgroup
+    // barrier every wave reads its fragments from the stage: each value is split once instead of once per wave (the
+    // split was ~3 of the ~6 VALU per MFMA of an issue-bound loop).  Stage plane: [64 rows][32 bytes], 16-byte halves
+    // swapped when (row >> 3) & 1 (conflict-free ds_write_b64 quads and ds_read_b128 fragments).
+    char* const stage = lds + kRmT * 256 * 4;
+    const int srow = 16 * wave + (lane & 15), squad = lane >> 4;
+    const int s_rdb = static_cast<int>(reinterpret_cast<uintptr_t>(lds)) + srow * 1024;
+    int s_rq[4];  // fp32 H quad of chunk c: units 4 c + squad, swizzled by srow & 15 -> s_rdb + s_rq[c & 3] + 256 (c >> 2)
+#pragma unroll
+    for (int cc = 0; cc < 4; ++cc) s_rq[cc] = ((4 * cc + squad) ^ (srow & 15)) << 4;
+    const int s_wr = static_cast<int>(reinterpret_cast<uintptr_t>(stage)) + srow * 32 +
+                     16 * ((squad >> 1) ^ ((srow >> 3) & 1)) + 8 * (squad & 1);
+    int f_rd[2], fo[2];  // fragment (row 32 i + l32, half h) of a plane: offset fo, in the stage f_rd
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int r = 32 * i + l32;
+        fo[i] = r * 32 + 16 * (h ^ ((r >> 3) & 1));
+        f_rd[i] = static_cast<int>(reinterpret_cast<uintptr_t>(stage)) + fo[i];
+    }
+    // ---- first layer: the X tile split once, cooperatively, into planes in the H region (free until the first
+    // epilogue; plane q: [KC0 chunks][64 rows][32 bytes] as the stage), then fragments from LDS, C order
+    {
+        constexpr int K0 = 16 * KC0;
+        constexpr int kXPlane = KC0 * kRmStagePlane;
+        typedef __attribute__((address_space(3))) u32x2 lds_u2;
+        const int xbase = static_cast<int>(reinterpret_cast<uintptr_t>(lds));
+        const float4* xg = reinterpret_cast<const float4*>(P.x + row0 * K0);
+        float4 xq[KC0];
+#pragma unroll
+        for (int k = 0; k < KC0; ++k) xq[k] = xg[threadIdx.x + kRmThreads * k];  // unit u: row u / 4 KC0, quad u % 4 KC0
+        const __amdgpu_buffer_rsrc_t rw = img_rsrc(0, KC0);
+        bf16x8 wf[2][2][3];  // [slot][j][q]
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int q = 0; q < 3; ++q) wf[0][j][q] = wload(rw, 0, j, q);
+#pragma unroll
+        for (int k = 0; k < KC0; ++k) {
+            const int u = threadIdx.x + kRmThreads * k;
+            const int row = u / (4 * KC0), quad = u % (4 * KC0);
+            const int q4 = quad & 3;
+            uint2 w[3];
+            split4(xq[k], w[0], w[1], w[2]);
+            const int off = xbase + (quad >> 2) * kRmStagePlane + row * 32 + 16 * ((q4 >> 1) ^ ((row >> 3) & 1)) +
+                            8 * (q4 & 1);
+#pragma unroll
+            for (int q = 0; q < 3; ++q) *reinterpret_cast<lds_u2*>(off + q * kXPlane) = u32x2{w[q].x, w[q].y};
+        }
+        rm_barrier();
+#pragma unroll
+        for (int c = 0; c < KC0; ++c) {
+            const int sl = c & 1;
+            bf16x8 xf[2][3];
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int q = 0; q < 3; ++q) xf[i][q] = rm_lds_frag(xbase + fo[i] + c * kRmStagePlane + q * kXPlane);
+            if (c + 1 < KC0) {
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+#pragma unroll
+                    for (int q = 0; q < 3; ++q) wf[sl ^ 1][j][q] = wload(rw, c + 1, j, q);
+            }
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) acc[i][j] = mfma_x6_ct(xf[i], wf[sl][j], c == 0 ? f32x16{} : acc[i][j]);
+        }
+        rm_barrier();  // every wave has read the X planes: the epilogue may write H1 over them
+    }
+#else
     // ---- first layer: X from global memory (row 32 i + l32, columns 16 c + 8 h .. + 7), C order
     load_bias(0);
     {
@@ -225,9 +315,14 @@ __device__ __forceinline__ void rm_body(const RmProblem& P, int hidden, char* ld
         }
     }
 
+#endif
+
     // + b, ELU, fp32 into LDS (the caller has made sure no wave still reads the previous layer's H); then the next
     // epilogue's bias
     auto epilogue_to_lds = [&](int l) {
+#if RSLRL_RM_COOP
+        load_bias(l);  // in flight behind the other workgroup's MFMAs
+#endif
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -241,11 +336,60 @@ __device__ __forceinline__ void rm_body(const RmProblem& P, int hidden, char* ld
                     v.w = rm_elu(acc[i][j][4 * g + 3] + bn[j][g].w);
                     rm_lds_write(wr_addr(j, g) + 32768 * i, v);
                 }
+#if !RSLRL_RM_COOP
         load_bias(l + 1);
+#endif
     };
 
     // a square 256 x 256 layer over H in LDS: 16 chunks, weight fragments and H one chunk ahead (chunk 0's weights in
     // w0n).  CT: C order (hidden layers), else the fused output kernel's order (the last hidden layer)
+#if RSLRL_RM_COOP
+    auto stage_chunk = [&](int c, int buf) {
+        typedef __attribute__((address_space(3))) u32x2 lds_u2;
+        uint2 w[3];
+        split4(rm_lds_read(s_rdb + s_rq[c & 3] + 256 * (c >> 2)), w[0], w[1], w[2]);
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+            *reinterpret_cast<lds_u2*>(s_wr + buf * kRmStageBuf + q * kRmStagePlane) = u32x2{w[q].x, w[q].y};
+    };
+    auto square_layer = [&](int l, auto ct) {
+        constexpr bool CT = decltype(ct)::value;
+        const __amdgpu_buffer_rsrc_t rw = img_rsrc(l, 16);
+        bf16x8 wf[2][2][3];
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int q = 0; q < 3; ++q) wf[0][j][q] = wload(rw, 0, j, q);  // in flight over the stage's barrier
+        stage_chunk(0, 0);
+        rm_barrier();
+#pragma unroll
+        for (int c = 0; c < 16; ++c) {
+            const int sl = c & 1;
+            bf16x8 xf[2][3];
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int q = 0; q < 3; ++q) xf[i][q] = rm_lds_frag(f_rd[i] + sl * kRmStageBuf + q * kRmStagePlane);
+            if (c + 1 < 16) {
+                stage_chunk(c + 1, sl ^ 1);
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+#pragma unroll
+                    for (int q = 0; q < 3; ++q) wf[sl ^ 1][j][q] = wload(rw, c + 1, j, q);
+            }
+            // (the next layer's first weights, the output layer's weights and the biases are loaded after the loop:
+            // registers)
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    const f32x16 a0 = c == 0 ? f32x16{} : acc[i][j];
+                    acc[i][j] = CT ? mfma_x6_ct(xf[i], wf[sl][j], a0) : mfma_x6(wf[sl][j], xf[i], a0);
+                }
+            if (c + 1 < 16) rm_barrier();  // chunk c + 1 staged; stage buffer sl free again
+        }
+    };
+#else
     auto square_layer = [&](int l, auto ct) {
         constexpr bool CT = decltype(ct)::value;
         const __amdgpu_buffer_rsrc_t rw = img_rsrc(l, 16);
@@ -291,6 +435,8 @@ __device__ __forceinline__ void rm_body(const RmProblem& P, int hidden, char* ld
         }
     };
 
+#endif
+
     epilogue_to_lds(0);
     __syncthreads();
     for (int l = 1; l + 1 < hidden; ++l) {
@@ -306,6 +452,10 @@ __device__ __forceinline__ void rm_body(const RmProblem& P, int hidden, char* ld
     // red: [w][i][o][32 rows] partials of the 64-column group w
     float* red = reinterpret_cast<float*>(lds);
     const int nout = P.nout;
+#if RSLRL_RM_COOP
+    load_out_weights();  // in flight behind the other workgroup's MFMAs
+    load_bias(hidden - 1);
+#endif
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
         f32x16 oacc = f32x16{};
@@ -339,7 +489,9 @@ __device__ __forceinline__ void rm_body(const RmProblem& P, int hidden, char* ld
                     rm_split8(make_float4(v[8 * s2], v[8 * s2 + 1], v[8 * s2 + 2], v[8 * s2 + 3]),
                               make_float4(v[8 * s2 + 4], v[8 * s2 + 5], v[8 * s2 + 6], v[8 * s2 + 7]), vb);
 #pragma unroll
-                    for (int q = 0; q < 3; ++q) wa[q] = __builtin_bit_cast(bf16x8, ow[j][s2][q]);
+                    for (int q = 0; q < 3; ++q)
+                        wa[q] = __builtin_bit_cast(bf16x8, RSLRL_RM_COOP ? oimg[((j * 2 + s2) * 3 + q) * 64 + lane]
+                                                                          : ow[j][s2][q]);
                     oacc = mfma_x6(wa, vb, oacc);
                 }
             }
@@ -372,7 +524,7 @@ __device__ __forceinline__ void rm_body(const RmProblem& P, int hidden, char* ld
 
 template <int KC0, int NR0, int NR1>
 __global__ __launch_bounds__(kRmThreads, 2) void rollout_mlp_kernel(RmArgs a) {
-    __shared__ __attribute__((aligned(16))) char lds[kRmT * 256 * 4];
+    __shared__ __attribute__((aligned(16))) char lds[kRmLds];
     // (distinct opaque markers open the two branches: the bodies' common index arithmetic stays inside each)
     if (blockIdx.y == 0) {
         asm volatile("; rollout mlp: problem 0" ::: "memory");
