@@ -512,9 +512,11 @@ __device__ __forceinline__ void rm_body(const RmProblem& P, int hidden, char* ld
         }
     }
     __syncthreads();
+    // consecutive lanes take consecutive rows of one output: their partials sit in consecutive banks (output-major
+    // lanes hit 3 banks per 32 lanes)
     for (int idx = threadIdx.x; idx < kRmT * nout; idx += kRmThreads) {
-        const int rl = idx / nout;
-        const int o = idx - rl * nout;
+        const int rl = idx & (kRmT - 1);
+        const int o = idx / kRmT;
         const float* b = red + ((rl >> 5) * kRmOutMax + o) * 32 + (rl & 31);
         constexpr int kW = 2 * kRmOutMax * 32;  // stride of the column group w
         const float sum = ((b[0] + b[kW]) + b[2 * kW]) + b[3 * kW];
