@@ -31,7 +31,7 @@ extern "C" {
 
 typedef struct ihipStream_t* rslrl_stream_t; /* == hipStream_t */
 
-#define RSLRL_ABI_VERSION 19
+#define RSLRL_ABI_VERSION 20
 
 enum {
     RSLRL_OK = 0,
@@ -574,7 +574,12 @@ int rslrl_hidden_bwd_pair(const rslrl_hidden_bwd_problem_t* p0, const rslrl_hidd
  * layer, then RSLRL_LINEAR_FWD_OUT for the last hidden layer and the output layer).  bimage[l]: layer l's layout-0
  * image (RSLRL_BIMAGE_LAYOUT_GEMM), out_image: the output layer's RSLRL_BIMAGE_LAYOUT_OUT image.  Both problems share
  * M, k0 and hidden.  RSLRL_E_UNSUPPORTED (nothing launched) unless M is a multiple of 64, k0 in {16, 32, 48, 64},
- * 2 <= hidden <= 4 and 1 <= nout <= 16. */
+ * 2 <= hidden <= 4 and 1 <= nout <= 16.
+ * ABI 20: a1 may be NULL (one network: policy.evaluate of compute_returns' last values, ppo.py:175-176, or
+ * act_inference); and a problem may carry the Normal sample of ActorCritic.act (actor_critic.py:124-127,
+ * distribution.sample() = normal_(0, 1) * scale + loc): with `sample` non-NULL the kernel also rewrites
+ * sample[r][o] <- sample[r][o] * sample_scale[o] + y[r][o] with torch's two roundings (mul_, then add_) -- the
+ * standard normals in, the actions out, bit-identical to rslrl_normal_affine on y. */
 typedef struct {
     const float* x;         /* [M, k0], 16-byte aligned */
     int32_t k0;
@@ -585,6 +590,8 @@ typedef struct {
     const float* out_bias;  /* [nout] */
     int32_t nout;
     float* y;               /* [M, nout] */
+    float* sample;              /* [M, nout] standard normals in, actions out; NULL: no sample (ABI 20) */
+    const float* sample_scale;  /* [nout] the shared std (required with sample) */
 } rslrl_rollout_mlp_t;
 int rslrl_rollout_mlp_pair(const rslrl_rollout_mlp_t* a0, const rslrl_rollout_mlp_t* a1, int64_t M,
                            rslrl_stream_t stream);

@@ -19,7 +19,7 @@ import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 # RSLRL_AMD_LIB: an alternative in-tree build of the same library (A/B kernel experiments)
 LIB_PATH = os.environ.get("RSLRL_AMD_LIB") or os.path.join(LIB_DIR, "librslrl_amd.so")
-ABI_VERSION = 19
+ABI_VERSION = 20
 
 # symbols declared in include/rslrl_amd.h (tests/test_capi.py checks the header against this list)
 EXPORTED_SYMBOLS = (
@@ -128,6 +128,7 @@ BIMAGE_LAYOUT_H3 = 2
 
 ARITH_X6, ARITH_H3 = 1, 2
 LINEAR_FWD, LINEAR_FWD_ELU, LINEAR_DGRAD_ELU, LINEAR_DGRAD_ELU_WGRAD, LINEAR_FWD_OUT = 0, 1, 2, 3, 4
+E_INVALID_ARGUMENT = -1  # RSLRL_E_INVALID_ARGUMENT
 E_UNSUPPORTED = -3  # RSLRL_E_UNSUPPORTED
 
 
@@ -380,6 +381,8 @@ class RolloutMlp(ctypes.Structure):
         ("out_bias", ctypes.c_void_p),
         ("nout", ctypes.c_int32),
         ("y", ctypes.c_void_p),
+        ("sample", ctypes.c_void_p),
+        ("sample_scale", ctypes.c_void_p),
     ]
 
 

@@ -50,6 +50,8 @@ struct RmProblem {
     const uint4* oimg;              // output layer image (BIMAGE_LAYOUT_OUT)
     const float* obias;             // [nout]
     float* y;                       // [M, nout]
+    float* sample;                  // [M, nout] standard normals in, actions out (or null)
+    const float* sample_scale;      // [nout]
     int nout;
 };
 
@@ -511,16 +513,38 @@ __device__ __forceinline__ void rm_body(const RmProblem& P, int hidden, char* ld
             }
         }
     }
+    // this thread's output elements (consecutive lanes take consecutive rows of one output: their partials sit in
+    // consecutive banks; output-major lanes hit 3 banks per 32 lanes): their bias and the sample's normal and scale
+    // are loaded before the barrier, so the loads' latency overlaps its wait
+    constexpr int kPer = kRmT * kRmOutMax / kRmThreads;
+    float ob[kPer], se[kPer], ss[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        const int idx = threadIdx.x + k * kRmThreads;
+        if (idx < kRmT * nout) {
+            const int rl = idx & (kRmT - 1), o = idx / kRmT;
+            ob[k] = P.obias[o];
+            if (P.sample) {
+                se[k] = P.sample[(row0 + rl) * nout + o];
+                ss[k] = P.sample_scale[o];
+            }
+        }
+    }
     __syncthreads();
-    // consecutive lanes take consecutive rows of one output: their partials sit in consecutive banks (output-major
-    // lanes hit 3 banks per 32 lanes)
-    for (int idx = threadIdx.x; idx < kRmT * nout; idx += kRmThreads) {
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        const int idx = threadIdx.x + k * kRmThreads;
+        if (idx >= kRmT * nout) break;
         const int rl = idx & (kRmT - 1);
         const int o = idx / kRmT;
         const float* b = red + ((rl >> 5) * kRmOutMax + o) * 32 + (rl & 31);
         constexpr int kW = 2 * kRmOutMax * 32;  // stride of the column group w
         const float sum = ((b[0] + b[kW]) + b[2 * kW]) + b[3 * kW];
-        P.y[(row0 + rl) * nout + o] = sum + P.obias[o];
+        const float mu = sum + ob[k];
+        const int64_t e = (row0 + rl) * nout + o;
+        P.y[e] = mu;
+        if (P.sample)  // the Normal sample (rslrl_normal_affine's expression): eps * sigma, then + mu
+            P.sample[e] = __fadd_rn(__fmul_rn(se[k], ss[k]), mu);
     }
 }
 
@@ -538,8 +562,8 @@ __global__ __launch_bounds__(kRmThreads, 2) void rollout_mlp_kernel(RmArgs a) {
 }
 
 template <int KC0>
-void rm_launch(const RmArgs& a, int nr0, int nr1, int64_t M, hipStream_t st) {
-    const dim3 g(static_cast<unsigned>(M / kRmT), 2), b(kRmThreads);
+void rm_launch(const RmArgs& a, int nr0, int nr1, int64_t M, int problems, hipStream_t st) {
+    const dim3 g(static_cast<unsigned>(M / kRmT), static_cast<unsigned>(problems)), b(kRmThreads);
     if (nr0 == 4 && nr1 == 1) hipLaunchKernelGGL((rollout_mlp_kernel<KC0, 4, 1>), g, b, 0, st, a);
     else if (nr0 == 4) hipLaunchKernelGGL((rollout_mlp_kernel<KC0, 4, 4>), g, b, 0, st, a);
     else if (nr1 == 1) hipLaunchKernelGGL((rollout_mlp_kernel<KC0, 1, 1>), g, b, 0, st, a);
@@ -555,20 +579,23 @@ using namespace rslrl;
 
 extern "C" int rslrl_rollout_mlp_pair(const rslrl_rollout_mlp_t* a0, const rslrl_rollout_mlp_t* a1, int64_t M,
                                       rslrl_stream_t stream) {
-    if (!a0 || !a1 || M < 0) return RSLRL_E_INVALID_ARGUMENT;
+    if (!a0 || M < 0) return RSLRL_E_INVALID_ARGUMENT;
     if (M == 0) return RSLRL_OK;
+    const int problems = a1 ? 2 : 1;
     const rslrl_rollout_mlp_t* in[2] = {a0, a1};
     const int k0 = a0->k0, hidden = a0->hidden;
-    if (a1->k0 != k0 || a1->hidden != hidden) return RSLRL_E_UNSUPPORTED;
+    if (a1 && (a1->k0 != k0 || a1->hidden != hidden)) return RSLRL_E_UNSUPPORTED;
     if (M % kRmT || M / kRmT > INT32_MAX || k0 < 16 || k0 > 64 || k0 % 16 || hidden < 2 || hidden > kRmHidden)
         return RSLRL_E_UNSUPPORTED;
     RmArgs args{};
     args.hidden = hidden;
     int nr[2];
-    for (int i = 0; i < 2; ++i) {
+    nr[1] = 1;
+    for (int i = 0; i < problems; ++i) {
         const rslrl_rollout_mlp_t& s = *in[i];
         if (s.nout < 1 || s.nout > kRmOutMax) return RSLRL_E_UNSUPPORTED;
         if (!s.x || !s.out_image || !s.out_bias || !s.y) return RSLRL_E_INVALID_ARGUMENT;
+        if (s.sample && !s.sample_scale) return RSLRL_E_INVALID_ARGUMENT;
         if (!rm_aligned16(s.x) || !rm_aligned16(s.out_image)) return RSLRL_E_MISALIGNED;
         RmProblem& p = args.p[i];
         for (int l = 0; l < hidden; ++l) {
@@ -581,15 +608,17 @@ extern "C" int rslrl_rollout_mlp_pair(const rslrl_rollout_mlp_t* a0, const rslrl
         p.oimg = static_cast<const uint4*>(s.out_image);
         p.obias = s.out_bias;
         p.y = s.y;
+        p.sample = s.sample;
+        p.sample_scale = s.sample_scale;
         p.nout = s.nout;
         nr[i] = s.nout <= 4 ? 1 : 4;  // the fused output kernel's choice (mlp_gemm.hip launch<kEpiBiasEluOut>)
     }
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     switch (k0 / 16) {
-        case 1: rm_launch<1>(args, nr[0], nr[1], M, st); break;
-        case 2: rm_launch<2>(args, nr[0], nr[1], M, st); break;
-        case 3: rm_launch<3>(args, nr[0], nr[1], M, st); break;
-        default: rm_launch<4>(args, nr[0], nr[1], M, st); break;
+        case 1: rm_launch<1>(args, nr[0], nr[1], M, problems, st); break;
+        case 2: rm_launch<2>(args, nr[0], nr[1], M, problems, st); break;
+        case 3: rm_launch<3>(args, nr[0], nr[1], M, problems, st); break;
+        default: rm_launch<4>(args, nr[0], nr[1], M, problems, st); break;
     }
     return launch_status();
 }

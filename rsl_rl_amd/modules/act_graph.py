@@ -14,8 +14,15 @@ up, and at every step outside such a scope) and one without it, reading the imag
 Same values and the same random stream as the eager calls: the sample's standard normals are drawn eagerly into a
 static buffer right before each replay (the same normal_() on the same [N, A] shape from the default generator as
 the eager step draws -- outside the graph, so a replay does not need the two generator-state fill launches of a
-captured draw), and the graph scales and shifts them; tests/test_gpu_act_graph.py compares a graphed and an eager
-rollout bitwise.
+captured draw), and the graph scales and shifts them (inside the one-launch forward when it runs); tests/
+test_gpu_act_graph.py compares a graphed and an eager rollout bitwise.
+
+Observation buffers that recur (an env that writes its observations into a few persistent buffers -- the synthetic
+env's ring of three, a simulator's obs buffer) get graphs of their own that read the buffer in place: a pointer set
+seen twice is captured as a "direct" graph of the image-free step (reading the image graph's images), so such a step
+is one draw + one replay, without the copy into the static input.  A direct graph is replayed only while the
+observation tensors sit at exactly the pointers it was captured on (same shapes and strides: the configuration key),
+i.e. it reads the step's own observations; at most kMaxDirect pointer sets per configuration.
 The first call of a configuration runs eagerly, the second captures; any capture failure falls back to the eager
 path for that configuration.  RSLRL_ACT_GRAPH=0 disables it.
 """
@@ -34,6 +41,8 @@ from ..networks import fused_mlp
 
 
 class RolloutActGraph:
+    kMaxDirect = 4  # pointer sets with a direct graph, per configuration
+
     def __init__(self, policy):
         self.policy = policy
         self._key = None
@@ -51,6 +60,9 @@ class RolloutActGraph:
         self._groups = None  # the observation groups the step reads
         self._mods = None  # the policy's modules (their parameters and buffers key the configuration)
         self._parents = []  # [(module, its children)] of the modules that have children: a replaced module shows here
+        self._img_cache = None  # the image graph's fused_mlp image cache entries (the direct graphs read them)
+        self._direct = {}  # observation pointers -> (graph, outputs): the step reading those buffers in place
+        self._ptr_seen = {}  # observation pointers -> times seen (a pointer set seen twice gets a direct graph)
 
     @staticmethod
     def enabled() -> bool:
@@ -88,21 +100,30 @@ class RolloutActGraph:
         if key != self._key:
             self._key, self._seen, self._graph, self._static_in, self._out = key, 0, None, None, None
             self._graph_fwd, self._out_fwd, self._imgs, self._img_gen, self._eps = None, None, None, None, None
-            self._dists = {}
+            self._dists, self._img_cache, self._direct, self._ptr_seen = {}, None, {}, {}
         if self._graph is None:
             self._seen += 1
             if self._seen < 2:  # the first call of a configuration runs eagerly (lazy initialisations happen there)
                 return None
             if not self._capture(obs, key):
                 return None
-        for g, t in self._static_in.items():
-            t.copy_(obs[g])
-        self._eps.normal_()  # the draw the eager step makes (same generator, same shape, same order)
         frozen = fused_mlp._frozen_depth > 0
-        if frozen and self._graph_fwd is not None and self._img_gen == fused_mlp._frozen_gen:
+        current = frozen and self._graph_fwd is not None and self._img_gen == fused_mlp._frozen_gen
+        direct = self._direct_graph(obs) if current and fused_mlp._STEP_FUSION else None
+        if direct is not None:  # the observations are read in place: no copy
+            self._eps.normal_()  # the draw the eager step makes (same generator, same shape, same order)
+            direct[0].replay()
+            out = direct[1]
+        elif current:
+            for g, t in self._static_in.items():
+                t.copy_(obs[g])
+            self._eps.normal_()
             self._graph_fwd.replay()  # the images of this rollout's weights are current
             out = self._out_fwd
         else:
+            for g, t in self._static_in.items():
+                t.copy_(obs[g])
+            self._eps.normal_()
             self._graph.replay()
             self._img_gen = fused_mlp._frozen_gen if frozen else None
             out = self._out
@@ -120,6 +141,37 @@ class RolloutActGraph:
         self.policy.distribution = dist
         return actions.clone(), values
 
+    def _direct_graph(self, obs):
+        """The direct graph of the observations' pointer set (captured at its second sighting), or None."""
+        ptrs = tuple(obs[g].data_ptr() for g in self._groups)
+        hit = self._direct.get(ptrs)
+        if hit is not None or self._img_cache is None:
+            return hit
+        n = self._ptr_seen.get(ptrs, 0) + 1
+        if len(self._ptr_seen) >= 64 and ptrs not in self._ptr_seen:  # fresh pointers every step: stop counting
+            return None
+        self._ptr_seen[ptrs] = n
+        if n < 2 or len(self._direct) >= self.kMaxDirect:
+            return None
+        pol = self.policy
+        graph = torch.cuda.CUDAGraph()
+        pol._static_eps = self._eps
+        try:
+            with _capture_caches() as cache:
+                cache.update(self._img_cache)  # the image graph's images: no image build in this graph
+                with torch.cuda.graph(graph):
+                    actions, values = pol.act_and_evaluate({g: obs[g] for g in self._groups})
+                    dist = pol.distribution
+                    out = (actions, values, dist.loc, dist.scale)
+        except Exception as e:  # noqa: BLE001 -- stay on the copying graph for this pointer set
+            self._ptr_seen[ptrs] = -(1 << 30)
+            warnings.warn(f"rollout act() direct graph capture failed, copying the observations: {e}")
+            return None
+        finally:
+            pol._static_eps = None
+        self._direct[ptrs] = (graph, out)
+        return self._direct[ptrs]
+
     def _capture(self, obs, key) -> bool:
         pol = self.policy
         static_in = {g: obs[g].clone() for g in sorted(set(pol.obs_groups["policy"]) | set(pol.obs_groups["critic"]))}
@@ -134,6 +186,7 @@ class RolloutActGraph:
                     dist = pol.distribution
                     out = (actions, values, dist.loc, dist.scale)
                 imgs = [v[1] for v in cache.values()]
+                img_cache = dict(cache)
                 out_fwd = None
                 if imgs:  # the same step reading the cached images (no image launch in this graph)
                     with torch.cuda.graph(graph_fwd):
@@ -148,6 +201,7 @@ class RolloutActGraph:
             pol._static_eps = None
         self._graph, self._static_in, self._out, self._eps = graph, static_in, out, eps
         self._graph_fwd, self._out_fwd, self._imgs = (graph_fwd, out_fwd, imgs) if out_fwd is not None else (None,) * 3
+        self._img_cache = dict(img_cache) if out_fwd is not None else None
         self._img_gen = None  # the first replay runs the image build
         return True
 

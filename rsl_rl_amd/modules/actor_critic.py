@@ -284,7 +284,19 @@ class ActorCritic(nn.Module):
         pair does not qualify."""
         a_obs = self.actor_obs_normalizer(self.get_actor_obs(obs))
         c_obs = self.critic_obs_normalizer(self.get_critic_obs(obs))
-        pair = fused_mlp_forward_pair(self.actor, a_obs, self.critic, c_obs) if a_obs.is_cuda else None
+        if not a_obs.is_cuda:
+            pair = None
+        elif (getattr(self, "_static_eps", None) is not None and not self.state_dependent_std
+              and fused_mlp._STEP_FUSION):
+            # a captured rollout graph: its standard normals are drawn before the replay, so the forward's launch can
+            # also apply the sample (eps * std + mean, _sample's expression) -- one launch less per env step
+            std = self.std if self.noise_std_type == "scalar" else torch.exp(self.log_std)
+            pair = fused_mlp_forward_pair(self.actor, a_obs, self.critic, c_obs, sample=(self._static_eps, std))
+            if pair is not None and pair[2]:
+                self.distribution = Normal(pair[0], std.expand_as(pair[0]))
+                return self._static_eps, pair[1]
+        else:
+            pair = fused_mlp_forward_pair(self.actor, a_obs, self.critic, c_obs)
         if pair is None:
             self.update_distribution(a_obs)
             return self._sample(), self.critic(c_obs)

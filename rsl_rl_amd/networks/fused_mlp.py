@@ -1210,19 +1210,26 @@ _PAIR_TRAIN = os.environ.get("RSLRL_PAIR_TRAIN", "1") != "0"
 _OUT_PAIR = os.environ.get("RSLRL_OUT_PAIR", "1") != "0"
 # RSLRL_ROLLOUT_MLP=0 keeps the rollout's forward layer by layer (A/B; the same bits)
 _ROLLOUT_MLP = os.environ.get("RSLRL_ROLLOUT_MLP", "1") != "0"
+# RSLRL_ROLLOUT_STEP_FUSION=0 (A/B; the same bits): no Normal sample inside the one-launch forward, no single-network
+# one-launch forward (compute_returns' last values), no copy-free act graphs for recurring observation buffers
+_STEP_FUSION = os.environ.get("RSLRL_ROLLOUT_STEP_FUSION", "1") != "0"
 rollout_mlp_launches = 0
 
 
-def rollout_mlp_pair(xs, ws, bs, imgs, nh: int):
+def rollout_mlp_pair(xs, ws, bs, imgs, nh: int, sample=None):
     """The rollout's actor and critic forward, every layer in one launch (rslrl_rollout_mlp_pair): y = [y_a, y_b],
     bit-identical to the layer-by-layer launches of fused_mlp_forward_pair; None when the shapes are not covered
-    (nothing launched).  xs: the two inputs [M, k0]; ws, bs, imgs: per network, as fused_mlp_forward_pair holds them
-    (x6 forward images, the output layer's image)."""
+    (nothing launched).  xs: the two inputs [M, k0] (or one: a single network, fused_mlp_forward); ws, bs, imgs: per
+    network, as fused_mlp_forward_pair holds them (x6 forward images, the output layer's image).  sample: (eps, scale)
+    of the first network's Normal sample -- eps [M, nout] standard normals, rewritten in place to eps * scale + y
+    (ActorCritic._sample's expression, one launch less per env step); scale: the shared [nout] std.  A sample the
+    kernel does not take (other shapes, a per-row scale) returns None before anything launches."""
+    P = len(xs)
     M, k0 = xs[0].shape
     if (M % _lib.ROLLOUT_MLP_ROWS or k0 not in (16, 32, 48, 64) or not 2 <= nh <= _lib.ROLLOUT_MLP_MAX_HIDDEN
-            or xs[1].shape != xs[0].shape):
+            or any(x.shape != xs[0].shape for x in xs)):
         return None
-    for i in range(2):
+    for i in range(P):
         w = ws[i]
         if w[0].shape != (256, k0) or any(w[l].shape != (256, 256) for l in range(1, nh)) or w[nh].shape[1] != 256:
             return None
@@ -1230,9 +1237,16 @@ def rollout_mlp_pair(xs, ws, bs, imgs, nh: int):
             return None
         if xs[i].data_ptr() % 16 or not xs[i].is_contiguous():
             return None
-    ys = [torch.empty(M, ws[i][nh].shape[0], device=xs[0].device, dtype=torch.float32) for i in range(2)]
+    if sample is not None:
+        eps, scale = sample
+        A = ws[0][nh].shape[0]
+        if (eps.shape != (M, A) or not eps.is_contiguous() or eps.dtype != torch.float32 or eps.device != xs[0].device
+                or scale.shape != (A,) or not scale.is_contiguous() or scale.dtype != torch.float32
+                or scale.device != xs[0].device):
+            return None
+    ys = [torch.empty(M, ws[i][nh].shape[0], device=xs[0].device, dtype=torch.float32) for i in range(P)]
     args = []
-    for i in range(2):
+    for i in range(P):
         a = _lib.RolloutMlp()
         a.x, a.k0, a.hidden = xs[i].data_ptr(), k0, nh
         for l in range(nh):
@@ -1240,12 +1254,15 @@ def rollout_mlp_pair(xs, ws, bs, imgs, nh: int):
             a.bias[l] = bs[i][l].data_ptr()
         a.out_image, a.out_bias = imgs[i][2].data_ptr(), bs[i][nh].data_ptr()
         a.nout, a.y = ws[i][nh].shape[0], ys[i].data_ptr()
+        if i == 0 and sample is not None:
+            a.sample, a.sample_scale = sample[0].data_ptr(), sample[1].data_ptr()
         args.append(a)
-    nout = ys[0].shape[1] + ys[1].shape[1]
-    flops = 2 * M * 256 * (2 * k0 + 2 * 256 * (nh - 1) + nout)
-    with timer.span(f"rollout_mlp_pair[M={M},K={k0},hidden={nh},out={nout}]", xs[0].device, 4 * M * (2 * k0 + nout),
+    nout = sum(y.shape[1] for y in ys)
+    flops = 2 * M * 256 * (P * k0 + P * 256 * (nh - 1)) + 2 * M * 256 * nout
+    with timer.span(f"rollout_mlp_pair[M={M},K={k0},hidden={nh},out={nout}]", xs[0].device, 4 * M * (P * k0 + nout),
                     flops):
-        rc = _lib.lib().rslrl_rollout_mlp_pair(ctypes.byref(args[0]), ctypes.byref(args[1]), M, _stream(xs[0]))
+        rc = _lib.lib().rslrl_rollout_mlp_pair(ctypes.byref(args[0]), ctypes.byref(args[1]) if P == 2 else None, M,
+                                               _stream(xs[0]))
     if rc == _lib.E_UNSUPPORTED:
         return None
     _lib.check(rc, "rslrl_rollout_mlp_pair")
@@ -1267,11 +1284,14 @@ def side_stream(device):
     return s
 
 
-def fused_mlp_forward_pair(mlp_a: nn.Sequential, x_a: torch.Tensor, mlp_b: nn.Sequential, x_b: torch.Tensor):
+def fused_mlp_forward_pair(mlp_a: nn.Sequential, x_a: torch.Tensor, mlp_b: nn.Sequential, x_b: torch.Tensor,
+                           sample=None):
     """Inference forward of two MLPs (the actor and the critic of the rollout) with their same-shape hidden
     layers batched into one launch each (rslrl_linear_gemm_pair); identical results to two fused_mlp_forward
     calls.  Returns (y_a, y_b), or None when the pair does not qualify (gradients wanted, another GEMM mode,
-    different hidden shapes or batch sizes) -- the caller then runs the two forwards."""
+    different hidden shapes or batch sizes) -- the caller then runs the two forwards.
+    sample: (eps, scale) -- the Normal sample of the actor's output (rollout_mlp_pair): the result is then
+    (y_a, y_b, sampled), sampled telling whether eps now holds eps * scale + y_a (else the caller samples)."""
     # inside a frozen_weights() scope (the rollout) the weights, their images and the plan are fixed: the
     # structure checks, parameter lists, plans and image lookups run once per scope and pair (host time per
     # rollout step matters when a GPU holds few envs, DESIGN.md §7)
@@ -1306,10 +1326,16 @@ def fused_mlp_forward_pair(mlp_a: nn.Sequential, x_a: torch.Tensor, mlp_b: nn.Se
     arith = lambda l: _lib.ARITH_H3 if h3[l] else _lib.ARITH_X6  # noqa: E731
     h = [x_a if x_a.is_contiguous() else x_a.contiguous(), x_b if x_b.is_contiguous() else x_b.contiguous()]
     y = None
+    sampled = False
     if _ROLLOUT_MLP and not any(h3) and all(fuse):
-        y = rollout_mlp_pair(h, ws, bs, imgs, nh)
+        if sample is not None:
+            y = rollout_mlp_pair(h, ws, bs, imgs, nh, sample=sample)
+            sampled = y is not None
+        if y is None:
+            y = rollout_mlp_pair(h, ws, bs, imgs, nh)
     if y is not None:
-        return _unflatten(mlp_a, y[0]), _unflatten(mlp_b, y[1])
+        out = (_unflatten(mlp_a, y[0]), _unflatten(mlp_b, y[1]))
+        return out if sample is None else out + (sampled,)
     amax = [None, None]
     y = [None, None]
     for l in range(nh):
@@ -1351,7 +1377,7 @@ def fused_mlp_forward_pair(mlp_a: nn.Sequential, x_a: torch.Tensor, mlp_b: nn.Se
     for i, mlp in enumerate((mlp_a, mlp_b)):
         yi = y[i] if y[i] is not None else F.linear(h[i], ws[i][-1], bs[i][-1])
         out.append(_unflatten(mlp, yi))
-    return out[0], out[1]
+    return (out[0], out[1]) if sample is None else (out[0], out[1], False)
 
 
 def fused_mlp_forward(mlp: nn.Sequential, x: torch.Tensor) -> torch.Tensor:
@@ -1368,8 +1394,15 @@ def fused_mlp_forward(mlp: nn.Sequential, x: torch.Tensor) -> torch.Tensor:
         split, h3, fuse_out = _plan(ws)
         if split:  # the last activation never reaches HBM when the output layer is fused
             fwd_imgs, _, out_img = _forward_images(ws, h3, fuse_out, backward=False)
-            hs, _, y = _hidden_forward(x, ws, bs, h3, fuse_out, fwd_imgs, out_img, keep=False)
-            h = hs[-1]
+            y = None
+            if (_ROLLOUT_MLP and _STEP_FUSION and not any(h3) and fuse_out and x.is_cuda and x.dim() == 2
+                    and x.dtype == torch.float32):
+                # every layer in one launch (compute_returns' last values, act_inference): the same bits
+                r = rollout_mlp_pair([x], [ws], [bs], [(fwd_imgs, None, out_img)], len(ws) - 1)
+                y = r[0] if r is not None else None
+            if y is None:
+                hs, _, y = _hidden_forward(x, ws, bs, h3, fuse_out, fwd_imgs, out_img, keep=False)
+                h = hs[-1]
         else:
             h, y = x, None
             for m in linears[:-1]:

@@ -41,6 +41,7 @@ def test_graphed_rollout_matches_eager(hidden, n_envs, cuda_device, monkeypatch)
     eager, p_eager, _ = _run(False, monkeypatch, cuda_device, hidden, n_envs)
     graphed, p_graph, g = _run(True, monkeypatch, cuda_device, hidden, n_envs)
     assert g is not None and g._graph is not None, "the graph was not captured"
+    assert g._direct, "the env's observation ring should be read by direct graphs"
     for a, b in zip(eager, graphed):
         for k in a:
             assert torch.equal(a[k], b[k]), k
@@ -74,3 +75,38 @@ def test_act_graph_sees_a_replaced_submodule(cuda_device):
         torch.cuda.manual_seed(5)
         pol.act(obs)
         assert torch.equal(mean_g, pol.action_mean)
+
+
+def test_direct_graphs_read_recurring_observation_buffers(cuda_device):
+    """Observation buffers that recur get copy-free graphs (act_graph._direct_graph): a step that reads two alternating
+    buffers (rewritten between steps, as an env's ring is) and, in between, fresh tensors gives the eager
+    act_and_evaluate's actions, values and mean bit for bit, and the direct graphs are the ones replayed."""
+    from rsl_rl_amd.modules import ActorCritic
+    from rsl_rl_amd.modules.act_graph import RolloutActGraph
+    from rsl_rl_amd.networks import fused_mlp
+
+    torch.manual_seed(0)
+    dev = cuda_device
+    bufs = [torch.empty(4096, 48, device=dev) for _ in range(2)]
+    pol = ActorCritic({"policy": bufs[0]}, {"policy": ["policy"], "critic": ["policy"]}, 12,
+                      actor_hidden_dims=[256, 256, 256], critic_hidden_dims=[256, 256, 256]).to(dev)
+    g = RolloutActGraph(pol)
+    gen = torch.Generator(device=dev).manual_seed(1)
+    with torch.inference_mode(), fused_mlp.frozen_weights():
+        for step in range(12):
+            fresh = step in (7, 8)
+            x = torch.randn(4096, 48, device=dev, generator=gen)
+            if fresh:
+                obs = {"policy": x}
+            else:
+                bufs[step % 2].copy_(x)
+                obs = {"policy": bufs[step % 2]}
+            torch.cuda.manual_seed(100 + step)
+            res = g(obs)
+            if res is None:
+                res = pol.act_and_evaluate(obs)
+            a, v, mu = res[0].clone(), res[1].clone(), pol.action_mean.clone()
+            torch.cuda.manual_seed(100 + step)
+            a_ref, v_ref = pol.act_and_evaluate({"policy": x.clone()})
+            assert torch.equal(a, a_ref) and torch.equal(v, v_ref) and torch.equal(mu, pol.action_mean), step
+    assert all((b.data_ptr(),) in g._direct for b in bufs), "both recurring buffers should have a direct graph"

@@ -123,3 +123,68 @@ def test_act_and_evaluate_takes_one_launch(cuda_device):
         a, v = pol.act_and_evaluate(obs)
         assert fused_mlp.rollout_mlp_launches == n0 + 1
     assert torch.equal(a, a_ref) and torch.equal(v, v_ref) and torch.equal(pol.action_mean, mean_ref)
+
+
+@pytest.mark.parametrize("M,k0,hidden,nout", [
+    (16384, 48, 3, 1),     # compute_returns' last values at the 16,384-env share (C3's critic)
+    (4160, 48, 3, 12),     # 65 tiles, the actor (act_inference)
+    (2048, 32, 2, 7),
+])
+def test_rollout_mlp_single_network_matches_layer_by_layer(M, k0, hidden, nout, cuda_device, monkeypatch):
+    """One network through the one-launch kernel (a1 = NULL: fused_mlp_forward, i.e. policy.evaluate / act_inference)
+    against its layer-by-layer launches, bit for bit."""
+    dev = cuda_device
+    g = torch.Generator(device=dev).manual_seed(M + nout)
+    m = _mlp(k0, hidden, nout, dev, g)
+    x = torch.randn(M, k0, device=dev, generator=g)
+    with torch.inference_mode():
+        n0 = fused_mlp.rollout_mlp_launches
+        one = fused_mlp.fused_mlp_forward(m, x)
+        assert fused_mlp.rollout_mlp_launches == n0 + 1
+        monkeypatch.setattr(fused_mlp, "_ROLLOUT_MLP", False)
+        ref = fused_mlp.fused_mlp_forward(m, x)
+    assert torch.equal(one, ref), float((one - ref).abs().max())
+
+
+def test_rollout_mlp_sample_matches_normal_affine(cuda_device):
+    """The Normal sample applied in the one-launch forward (eps <- eps * std + mu) against rslrl_normal_affine on the
+    kernel's own mu, bit for bit; the outputs are those of the sample-free launch; a scale the kernel does not take
+    (per-row) declines before launching."""
+    from rsl_rl_amd import kernels
+
+    dev = cuda_device
+    g = torch.Generator(device=dev).manual_seed(11)
+    M = 16384
+    ma, mb = _mlp(48, 3, 12, dev, g), _mlp(48, 3, 1, dev, g)
+    xa, xb = torch.randn(M, 48, device=dev, generator=g), torch.randn(M, 48, device=dev, generator=g)
+    std = torch.rand(12, device=dev, generator=g) + 0.2
+    eps = torch.randn(M, 12, device=dev, generator=g)
+    eps0 = eps.clone()
+    with torch.inference_mode():
+        ya, yb, sampled = fused_mlp.fused_mlp_forward_pair(ma, xa, mb, xb, sample=(eps, std))
+        assert sampled
+        ra, rb = fused_mlp.fused_mlp_forward_pair(ma, xa, mb, xb)
+        ref = kernels.normal_affine_(eps0.clone(), std.expand(M, 12), ra)
+        assert torch.equal(ya, ra) and torch.equal(yb, rb)
+        assert torch.equal(eps, ref)
+        assert torch.equal(ref, eps0 * std + ra)  # torch's mul_ then add_
+        per_row = torch.rand(M, 12, device=dev, generator=g)
+        e2 = eps0.clone()
+        ya2, _, sampled2 = fused_mlp.fused_mlp_forward_pair(ma, xa, mb, xb, sample=(e2, per_row))
+        assert not sampled2 and torch.equal(e2, eps0) and torch.equal(ya2, ra)
+
+
+def test_rollout_mlp_c_abi_single_and_sample_arguments(cuda_device):
+    """a1 = NULL is one problem (M = 0 still a no-op); a sample without its scale is an invalid argument."""
+    L = _lib.lib()
+    x = torch.zeros(128, 48, device=cuda_device)
+    y = torch.full((128, 12), 7.0, device=cuda_device)
+    a = _lib.RolloutMlp()
+    a.x, a.k0, a.hidden, a.nout, a.y = x.data_ptr(), 48, 3, 12, y.data_ptr()
+    assert L.rslrl_rollout_mlp_pair(ctypes.byref(a), None, 0, None) == 0
+    assert L.rslrl_rollout_mlp_pair(None, ctypes.byref(a), 128, None) == _lib.E_INVALID_ARGUMENT
+    a.out_image, a.out_bias = x.data_ptr(), x.data_ptr()  # past the null checks: the sample check decides
+    a.sample = y.data_ptr()
+    assert L.rslrl_rollout_mlp_pair(ctypes.byref(a), None, 128, None) == _lib.E_INVALID_ARGUMENT
+    torch.cuda.synchronize()
+    assert bool((y == 7.0).all())
