@@ -18,11 +18,14 @@ captured draw), and the graph scales and shifts them (inside the one-launch forw
 test_gpu_act_graph.py compares a graphed and an eager rollout bitwise.
 
 Observation buffers that recur (an env that writes its observations into a few persistent buffers -- the synthetic
-env's ring of three, a simulator's obs buffer) get graphs of their own that read the buffer in place: a pointer set
-seen twice is captured as a "direct" graph of the image-free step (reading the image graph's images), so such a step
-is one draw + one replay, without the copy into the static input.  A direct graph is replayed only while the
-observation tensors sit at exactly the pointers it was captured on (same shapes and strides: the configuration key),
-i.e. it reads the step's own observations; at most kMaxDirect pointer sets per configuration.
+env's ring of three, a simulator's obs buffer) get graphs of their own that read the buffer in place: the step draws
+its normals into a fresh tensor (the caching allocator hands the same few blocks back once the caller drops earlier
+actions), and a (observation pointers, fresh-tensor pointer) set seen twice is captured as a "direct" graph of the
+image-free step (reading the image graph's images) that reads the observations and writes the actions in place into
+that fresh tensor -- one draw + one replay per step, without the copy into the static input or the actions' clone.
+A direct graph is replayed only while the observation tensors sit at exactly the pointers it was captured on (same
+shapes and strides: the configuration key), i.e. it reads the step's own observations, and writes only into the
+step's own freshly allocated actions; at most kMaxDirect pointer sets per configuration.
 The first call of a configuration runs eagerly, the second captures; any capture failure falls back to the eager
 path for that configuration.  RSLRL_ACT_GRAPH=0 disables it.
 """
@@ -41,7 +44,7 @@ from ..networks import fused_mlp
 
 
 class RolloutActGraph:
-    kMaxDirect = 4  # pointer sets with a direct graph, per configuration
+    kMaxDirect = 12  # pointer sets with a direct graph, per configuration
 
     def __init__(self, policy):
         self.policy = policy
@@ -109,12 +112,18 @@ class RolloutActGraph:
                 return None
         frozen = fused_mlp._frozen_depth > 0
         current = frozen and self._graph_fwd is not None and self._img_gen == fused_mlp._frozen_gen
-        direct = self._direct_graph(obs) if current and fused_mlp._STEP_FUSION else None
-        if direct is not None:  # the observations are read in place: no copy
-            self._eps.normal_()  # the draw the eager step makes (same generator, same shape, same order)
-            direct[0].replay()
-            out = direct[1]
-        elif current:
+        if current and fused_mlp._STEP_FUSION:
+            # the sample's normals go into a fresh tensor (the actions the caller receives: no clone); its block
+            # recurs once the caller has dropped an earlier step's actions
+            eps = torch.empty(self._eps.shape, dtype=self._eps.dtype, device=self._eps.device)
+            direct = self._direct_graph(obs, eps)
+            if direct is not None:  # the observations are read in place and the actions written in place: no copies
+                eps.normal_()  # the draw the eager step makes (same generator, same shape, same order)
+                direct[0].replay()
+                out = direct[1]
+                self.policy.distribution = self._dist(out)
+                return eps, out[1]
+        if current:
             for g, t in self._static_in.items():
                 t.copy_(obs[g])
             self._eps.normal_()
@@ -128,22 +137,26 @@ class RolloutActGraph:
             self._img_gen = fused_mlp._frozen_gen if frozen else None
             out = self._out
         actions, values = out[0], out[1]
-        # Aliasing contract: actions are cloned; the returned values and the distribution's mean / scale ARE the
-        # graph's static outputs, valid only until the next call (the next replay overwrites them; the eager path
-        # allocates new tensors).  PPO.act keeps them in its transition only until process_env_step copies them into
+        # Aliasing contract: actions are cloned (a direct graph's are the step's fresh tensor); the returned values
+        # and the distribution's mean / scale ARE the graph's static outputs, valid only until the next call (the next
+        # replay overwrites them; the eager path allocates new tensors).  PPO.act keeps them in its transition only until process_env_step copies them into
         # the storage in the same env step.  (A clone of values would add one launch per env step to the
         # host-bound rollout at the 16384-env share.)
         # one Normal per graph output set, built once: its loc / scale ARE the static outputs (a Normal per step cost
         # ~8 us of host time in torch.distributions' broadcast_all on the launch-bound rollout)
+        self.policy.distribution = self._dist(out)
+        return actions.clone(), values
+
+    def _dist(self, out):
         dist = self._dists.get(id(out))
         if dist is None or dist.loc is not out[2] or dist.scale is not out[3]:
             dist = self._dists[id(out)] = Normal(out[2], out[3])
-        self.policy.distribution = dist
-        return actions.clone(), values
+        return dist
 
-    def _direct_graph(self, obs):
-        """The direct graph of the observations' pointer set (captured at its second sighting), or None."""
-        ptrs = tuple(obs[g].data_ptr() for g in self._groups)
+    def _direct_graph(self, obs, eps):
+        """The direct graph of the observations' and the sample buffer's pointers (captured at their second
+        sighting), or None.  It reads the observations in place and writes the actions into `eps` in place."""
+        ptrs = tuple(obs[g].data_ptr() for g in self._groups) + (eps.data_ptr(),)
         hit = self._direct.get(ptrs)
         if hit is not None or self._img_cache is None:
             return hit
@@ -155,14 +168,15 @@ class RolloutActGraph:
             return None
         pol = self.policy
         graph = torch.cuda.CUDAGraph()
-        pol._static_eps = self._eps
+        pol._static_eps = eps
         try:
             with _capture_caches() as cache:
                 cache.update(self._img_cache)  # the image graph's images: no image build in this graph
                 with torch.cuda.graph(graph):
-                    actions, values = pol.act_and_evaluate({g: obs[g] for g in self._groups})
+                    _, values = pol.act_and_evaluate({g: obs[g] for g in self._groups})
                     dist = pol.distribution
-                    out = (actions, values, dist.loc, dist.scale)
+                    # no reference to the actions (this step's fresh tensor): its block must go back to the allocator
+                    out = (None, values, dist.loc, dist.scale)
         except Exception as e:  # noqa: BLE001 -- stay on the copying graph for this pointer set
             self._ptr_seen[ptrs] = -(1 << 30)
             warnings.warn(f"rollout act() direct graph capture failed, copying the observations: {e}")

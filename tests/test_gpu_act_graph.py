@@ -93,7 +93,7 @@ def test_direct_graphs_read_recurring_observation_buffers(cuda_device):
     g = RolloutActGraph(pol)
     gen = torch.Generator(device=dev).manual_seed(1)
     with torch.inference_mode(), fused_mlp.frozen_weights():
-        for step in range(12):
+        for step in range(30):
             fresh = step in (7, 8)
             x = torch.randn(4096, 48, device=dev, generator=gen)
             if fresh:
@@ -109,4 +109,34 @@ def test_direct_graphs_read_recurring_observation_buffers(cuda_device):
             torch.cuda.manual_seed(100 + step)
             a_ref, v_ref = pol.act_and_evaluate({"policy": x.clone()})
             assert torch.equal(a, a_ref) and torch.equal(v, v_ref) and torch.equal(mu, pol.action_mean), step
-    assert all((b.data_ptr(),) in g._direct for b in bufs), "both recurring buffers should have a direct graph"
+    assert {k[0] for k in g._direct} >= {b.data_ptr() for b in bufs}, "both recurring buffers should have a direct graph"
+
+
+def test_direct_graph_actions_are_fresh_tensors(cuda_device):
+    """A direct graph writes the actions into the step's freshly allocated tensor: actions a caller keeps are never
+    overwritten by later steps (their block is not handed out again while they live), and steps whose actions were
+    dropped reuse the blocks (the direct graphs replay)."""
+    from rsl_rl_amd.modules import ActorCritic
+    from rsl_rl_amd.modules.act_graph import RolloutActGraph
+    from rsl_rl_amd.networks import fused_mlp
+
+    torch.manual_seed(0)
+    dev = cuda_device
+    buf = torch.randn(4096, 48, device=dev)
+    pol = ActorCritic({"policy": buf}, {"policy": ["policy"], "critic": ["policy"]}, 12,
+                      actor_hidden_dims=[256, 256, 256], critic_hidden_dims=[256, 256, 256]).to(dev)
+    g = RolloutActGraph(pol)
+    kept = []
+    with torch.inference_mode(), fused_mlp.frozen_weights():
+        actions = None
+        for step in range(16):
+            buf.normal_()
+            res = g({"policy": buf})
+            actions = res[0] if res is not None else pol.act_and_evaluate({"policy": buf})[0]
+            if step in (9, 12):
+                kept.append((actions, actions.clone()))
+        torch.cuda.synchronize()
+    for a, snap in kept:
+        assert torch.equal(a, snap)
+    assert g._direct, "no direct graph was captured"
+    assert len({k[-1] for k in g._direct}) <= 4
