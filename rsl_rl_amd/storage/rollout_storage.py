@@ -389,7 +389,6 @@ class RolloutStorage:
         # permutation (:165) -- drawn lazily at the first next(), like the reference's generator body
         indices = self.draw_permutation(rows)
         self.last_indices = indices
-        self._start_prefetch(rows)  # the next update's permutation, drawn on a worker thread meanwhile
         p = self._packed_buffers(rows)
         if self.records is not None:
             R, offs = self.record_layout
@@ -413,8 +412,15 @@ class RolloutStorage:
                       (flat(self.sigma), p["sigma"])]
             kernels.gather_rows(pairs, indices)
 
+        prefetch = True
         for _epoch in range(num_epochs):
             for i in range(num_mini_batches):
+                if prefetch and (_epoch or i):
+                    # the next update's permutation, drawn on a worker thread meanwhile -- started once the first
+                    # mini-batch's launches are queued (starting the thread costs ~125 us of host time that the GPU
+                    # would otherwise wait out between the gather and the first mini-batch)
+                    self._start_prefetch(rows)
+                    prefetch = False
                 s = slice(i * mini_batch_size, (i + 1) * mini_batch_size)
                 obs_batch = TensorDict({k: v[s] for k, v in p["obs"].items()}, batch_size=[mini_batch_size],
                                        device=self.device)

@@ -85,10 +85,12 @@ def test_permutation_contents_and_tail_drop(cuda_device):
         assert torch.equal(batches[i][0]["policy"], batches[M + i][0]["policy"])
 
 
-def test_prefetched_permutation_matches_plain_draws(cuda_device):
+@pytest.mark.parametrize("M", [2, 1])
+def test_prefetched_permutation_matches_plain_draws(M, cuda_device):
     """The same sequence of updates with and without interference: every permutation equals torch.randperm on
-    the generator's state at that call, and the generator's state after each update matches."""
-    T, N, M = 4, 50, 2
+    the generator's state at that call, and the generator's state after each update matches.  The prefetch starts
+    at the second mini-batch: with one mini-batch per update every draw is synchronous."""
+    T, N = 4, 50
     n = (T * N // M) * M
     st = RolloutStorage("rl", N, T, {"policy": torch.zeros(N, 2)}, [3], cuda_device)
     st.perm_generator = torch.Generator().manual_seed(21)
