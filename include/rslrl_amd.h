@@ -31,7 +31,7 @@ extern "C" {
 
 typedef struct ihipStream_t* rslrl_stream_t; /* == hipStream_t */
 
-#define RSLRL_ABI_VERSION 20
+#define RSLRL_ABI_VERSION 21
 
 enum {
     RSLRL_OK = 0,
@@ -272,6 +272,23 @@ typedef struct {
 size_t rslrl_adam_workspace_bytes(void);
 int rslrl_clip_adam_step(const rslrl_adam_args_t* args /* host struct */, void* workspace, size_t workspace_bytes,
                          rslrl_stream_t stream);
+
+/* ABI 21: rslrl_ppo_update_tail and rslrl_clip_adam_step in the clip-and-Adam launches (one launch less per
+ * mini-batch): the tail's arguments as a struct (the meanings of rslrl_ppo_update_tail's); its lr rule and loss sums
+ * run in the norm launch before the step sizes are derived from the new lr (args->lr_dev is then normally tail->lr32).
+ * The same values as the two calls in sequence. */
+typedef struct {
+    const float* stats;
+    const float* kl;   /* with lr */
+    double* lr;        /* NULL: no lr rule (the loss sums only) */
+    float* lr32;       /* with lr */
+    int32_t round_fp32;
+    float kl_hi;
+    float kl_lo;
+    double* sums;      /* NULL: no loss sums */
+} rslrl_ppo_tail_t;
+int rslrl_clip_adam_step_tail(const rslrl_adam_args_t* args, const rslrl_ppo_tail_t* tail, void* workspace,
+                              size_t workspace_bytes, rslrl_stream_t stream);
 
 /* ------------------------------------------------------------------------------------------------
  * Actor/critic MLP layers on MFMA -- rsl_rl/networks/mlp.py:59-114

@@ -19,7 +19,7 @@ import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 # RSLRL_AMD_LIB: an alternative in-tree build of the same library (A/B kernel experiments)
 LIB_PATH = os.environ.get("RSLRL_AMD_LIB") or os.path.join(LIB_DIR, "librslrl_amd.so")
-ABI_VERSION = 20
+ABI_VERSION = 21
 
 # symbols declared in include/rslrl_amd.h (tests/test_capi.py checks the header against this list)
 EXPORTED_SYMBOLS = (
@@ -82,6 +82,7 @@ EXPORTED_SYMBOLS = (
     "rslrl_ppo_update_tail",
     "rslrl_adam_workspace_bytes",
     "rslrl_clip_adam_step",
+    "rslrl_clip_adam_step_tail",
     "rslrl_rnd_update_workspace_bytes",
     "rslrl_rnd_update",
     "rslrl_synthetic_env_step",
@@ -146,6 +147,13 @@ class AdamArgs(ctypes.Structure):
                 ("lr_dev", ctypes.c_void_p), ("beta1", ctypes.c_double), ("beta2", ctypes.c_double),
                 ("eps", ctypes.c_double), ("offsets", ctypes.c_int64 * (ADAM_MAX_TENSORS + 1)),
                 ("t", AdamTensor * ADAM_MAX_TENSORS)]
+
+
+class PpoTail(ctypes.Structure):
+    """rslrl_ppo_tail_t (include/rslrl_amd.h)."""
+    _fields_ = [("stats", ctypes.c_void_p), ("kl", ctypes.c_void_p), ("lr", ctypes.c_void_p), ("lr32", ctypes.c_void_p),
+                ("round_fp32", ctypes.c_int32), ("kl_hi", ctypes.c_float), ("kl_lo", ctypes.c_float),
+                ("sums", ctypes.c_void_p)]
 
 
 class LinearArgs(ctypes.Structure):
@@ -497,6 +505,8 @@ def _declare(L):
     L.rslrl_adam_workspace_bytes.argtypes = []
     L.rslrl_clip_adam_step.restype = ctypes.c_int
     L.rslrl_clip_adam_step.argtypes = [ctypes.POINTER(AdamArgs), P, SZ, P]
+    L.rslrl_clip_adam_step_tail.restype = ctypes.c_int
+    L.rslrl_clip_adam_step_tail.argtypes = [ctypes.POINTER(AdamArgs), ctypes.POINTER(PpoTail), P, SZ, P]
     L.rslrl_ppo_update_tail.restype = ctypes.c_int
     L.rslrl_ppo_update_tail.argtypes = [P, P, P, P, I32, F, F, P, P]
     L.rslrl_linear_wgrad_ex.restype = ctypes.c_int

@@ -41,6 +41,10 @@ from ..modules.rnd import RandomNetworkDistillation
 from ..storage import RolloutStorage
 from ..utils import string_to_callable
 
+# RSLRL_FUSED_TAIL=0 (A/B; the same values): the per-mini-batch lr rule / loss sums as their own launch instead of
+# inside the clip-and-Adam norm launch
+_FUSED_TAIL = os.environ.get("RSLRL_FUSED_TAIL", "1") != "0"
+
 
 def adapt_learning_rate(learning_rate: float, kl_mean: float, desired_kl: float) -> float:
     """The adaptive schedule of ppo.py:280-284."""
@@ -516,8 +520,8 @@ class PPO:
 
             # adaptive lr + loss statistics (ppo.py:259-294, :387-395)
             if adaptive and device_lr:
-                kernels.ppo_update_tail(stats, kl_src, lr_dev, lr32, self.desired_kl, sums,
-                                        round_fp32=self.is_multi_gpu)
+                tail = kernels.ppo_tail_args(stats, kl_src, lr_dev, lr32, self.desired_kl, sums,
+                                             round_fp32=self.is_multi_gpu)
             else:
                 if adaptive:  # host rule; the KL is already averaged over ranks
                     kl = kl_src.item()
@@ -526,15 +530,18 @@ class PPO:
                         self.learning_rate = torch.tensor(self.learning_rate, dtype=torch.float32).item()
                     for param_group in self.optimizer.param_groups:
                         param_group["lr"] = self.learning_rate
-                kernels.ppo_update_tail(stats, None, None, None, 0.0, sums)
+                tail = kernels.ppo_tail_args(stats, None, None, None, 0.0, sums)
+            fuse_tail = self._clip_adam is not None and _FUSED_TAIL
+            if not fuse_tail:
+                kernels.ppo_update_tail_args(tail, dev)
 
-            # clip + Adam (ppo.py:373-374)
+            # clip + Adam (ppo.py:373-374); the tail above runs inside the norm launch when fused
             if self._clip_adam is None:
                 nn.utils.clip_grad_norm_(self.policy.parameters(), self.max_grad_norm)
                 self.optimizer.step()
             else:
                 self._clip_adam.max_grad_norm = float(self.max_grad_norm)
-                self._clip_adam.step()
+                self._clip_adam.step(tail=tail if fuse_tail else None)
             if self.rnd_optimizer:
                 if rnd_fused and self._rnd_adam is not None:
                     self._rnd_adam.step()  # the reference's unclipped Adam on the predictor (ppo.py:383-384)

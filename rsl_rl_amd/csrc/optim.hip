@@ -41,15 +41,46 @@ constexpr size_t kCoefOff = kPartOff + kBlocks * sizeof(double);
 constexpr size_t kConstOff = kCoefOff + 256;
 constexpr size_t kAdamWsBytes = kConstOff + 3 * sizeof(float) * RSLRL_ADAM_MAX_TENSORS;
 
+// the per-mini-batch tail of PPO.update (ppo_loss.hip ppo_tail_kernel's expressions; ppo.py:259-294, :387-395), run
+// by one thread of the norm launch's block 0 when fused in (rslrl_clip_adam_step_tail)
+__device__ __forceinline__ void ppo_tail_device(const rslrl_ppo_tail_t& t, float* lr32_out) {
+    if (t.lr) {
+        const float kl = *t.kl;
+        double v = *t.lr;
+        if (kl > t.kl_hi) {
+            v = fmax(v / 1.5, 1e-5);
+        } else if (kl < t.kl_lo && kl > 0.0f) {
+            v = fmin(v * 1.5, 1e-2);
+        }
+        if (t.round_fp32) v = static_cast<double>(static_cast<float>(v));
+        *t.lr = v;
+        *t.lr32 = static_cast<float>(v);
+        *lr32_out = static_cast<float>(v);
+    }
+    if (t.sums) {
+        t.sums[0] += static_cast<double>(t.stats[2]);
+        t.sums[1] += static_cast<double>(t.stats[1]);
+        t.sums[2] += static_cast<double>(t.stats[3]);
+    }
+}
+
 __global__ __launch_bounds__(kThreadsA) void grad_sq_kernel(rslrl_adam_args_t a, unsigned* ticket, double* part,
-                                                            float* coef, float* consts) {
+                                                            float* coef, float* consts, rslrl_ppo_tail_t tail,
+                                                            int with_tail) {
     __shared__ double scratch[kThreadsA / kWave];
     __shared__ int last;
+    __shared__ float tail_lr32;
     // torch: _foreach_add_(state_steps, 1) before the update -- block 0, one lane per tensor, all in flight at once,
     // off the grid's critical path (the last block only folds the norm); on the same lane that tensor's bias
     // corrections and step size for adam_kernel (fused_adam_utils.cuh's expressions, once per tensor instead of once
     // per block and tensor).  adam_kernel reads neither the counters nor these before this launch has ended.
     if (blockIdx.x == 0) {
+        // the lr rule first: the step sizes below take the lr it wrote (handed over in LDS)
+        const bool tail_lr = with_tail && tail.lr && a.lr_dev == tail.lr32;
+        if (with_tail) {
+            if (threadIdx.x == 0) ppo_tail_device(tail, &tail_lr32);
+            __syncthreads();
+        }
         float* sp = nullptr;
 #pragma unroll
         for (int i = 0; i < RSLRL_ADAM_MAX_TENSORS; ++i)
@@ -58,7 +89,9 @@ __global__ __launch_bounds__(kThreadsA) void grad_sq_kernel(rslrl_adam_args_t a,
             const float st1 = *sp + 1.0f;
             *sp = st1;
             const double step = static_cast<double>(st1);
-            const double lr = a.lr_dev ? static_cast<double>(*a.lr_dev) : a.lr;
+            const double lr = tail_lr  ? static_cast<double>(tail_lr32)
+                              : a.lr_dev ? static_cast<double>(*a.lr_dev)
+                                         : a.lr;
             const float bc1 = static_cast<float>(1.0 - pow(static_cast<double>(a.beta1), step));
             const float bc2s = static_cast<float>(sqrt(1.0 - pow(static_cast<double>(a.beta2), step)));
             consts[3 * threadIdx.x] = bc1;
@@ -175,9 +208,12 @@ using namespace rslrl;
 
 extern "C" size_t rslrl_adam_workspace_bytes(void) { return kAdamWsBytes; }
 
-extern "C" int rslrl_clip_adam_step(const rslrl_adam_args_t* args, void* workspace, size_t workspace_bytes,
-                                    rslrl_stream_t stream) {
+namespace {
+int clip_adam(const rslrl_adam_args_t* args, const rslrl_ppo_tail_t* tail, void* workspace, size_t workspace_bytes,
+              rslrl_stream_t stream) {
     if (!args || !workspace || args->n < 1 || args->n > RSLRL_ADAM_MAX_TENSORS) return RSLRL_E_INVALID_ARGUMENT;
+    if (tail && (!tail->stats || (tail->lr && (!tail->lr32 || !tail->kl)))) return RSLRL_E_INVALID_ARGUMENT;
+    const rslrl_ppo_tail_t no_tail{};
     if (workspace_bytes < rslrl_adam_workspace_bytes()) return RSLRL_E_WORKSPACE_TOO_SMALL;
     rslrl_adam_args_t a = *args;
     int64_t off = 0;
@@ -194,9 +230,22 @@ extern "C" int rslrl_clip_adam_step(const rslrl_adam_args_t* args, void* workspa
     float* coef = reinterpret_cast<float*>(ws + kCoefOff);
     float* consts = reinterpret_cast<float*>(ws + kConstOff);
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    hipLaunchKernelGGL(grad_sq_kernel, dim3(kBlocks), dim3(kThreadsA), 0, st, a, ticket, part, coef, consts);
+    hipLaunchKernelGGL(grad_sq_kernel, dim3(kBlocks), dim3(kThreadsA), 0, st, a, ticket, part, coef, consts,
+                       tail ? *tail : no_tail, tail ? 1 : 0);
     int rc = launch_status();
     if (rc) return rc;
     hipLaunchKernelGGL(adam_kernel, dim3(kBlocks), dim3(kThreadsA), 0, st, a, coef, consts);
     return launch_status();
+}
+}  // namespace
+
+extern "C" int rslrl_clip_adam_step(const rslrl_adam_args_t* args, void* workspace, size_t workspace_bytes,
+                                    rslrl_stream_t stream) {
+    return clip_adam(args, nullptr, workspace, workspace_bytes, stream);
+}
+
+extern "C" int rslrl_clip_adam_step_tail(const rslrl_adam_args_t* args, const rslrl_ppo_tail_t* tail,
+                                         void* workspace, size_t workspace_bytes, rslrl_stream_t stream) {
+    if (!tail) return RSLRL_E_INVALID_ARGUMENT;
+    return clip_adam(args, tail, workspace, workspace_bytes, stream);
 }

@@ -168,7 +168,7 @@ __device__ __forceinline__ void rm_body(const RmProblem& P, int hidden, char* ld
 #pragma unroll
             for (int g = 0; g < 4; ++g) bn[j][g] = *reinterpret_cast<const float4*>(bias + 32 * j + 8 * g);
     };
-    auto load_w0 = [&](int l) {
+    [[maybe_unused]] auto load_w0 = [&](int l) {  // the split-on-read form (RSLRL_RM_COOP 0)
         const __amdgpu_buffer_rsrc_t rw = img_rsrc(l, 16);
 #pragma unroll
         for (int j = 0; j < 2; ++j)

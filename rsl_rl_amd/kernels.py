@@ -731,18 +731,29 @@ class RolloutRecordPlan:
         _lib.check(rc, "rslrl_rollout_record")
 
 
+def ppo_tail_args(stats, kl, lr, lr32, desired_kl, sums, round_fp32=False) -> _lib.PpoTail:
+    """rslrl_ppo_tail_t of the per-mini-batch tail (ppo_update_tail's arguments)."""
+    _require_device(stats, kl, lr, lr32, sums)
+    on = lr is not None
+    return _lib.PpoTail(stats.data_ptr(), kl.data_ptr() if on else None, lr.data_ptr() if on else None,
+                        lr32.data_ptr() if on else None, 1 if round_fp32 else 0,
+                        float(desired_kl) * 2.0 if on else 0.0, float(desired_kl) / 2.0 if on else 0.0,
+                        sums.data_ptr() if sums is not None else None)
+
+
+def ppo_update_tail_args(t: _lib.PpoTail, device) -> None:
+    """rslrl_ppo_update_tail of a ppo_tail_args struct (its own launch)."""
+    rc = _lib.lib().rslrl_ppo_update_tail(t.stats, t.kl, t.lr, t.lr32, t.round_fp32, t.kl_hi, t.kl_lo, t.sums,
+                                          _stream(device))
+    _lib.check(rc, "rslrl_ppo_update_tail")
+
+
 def ppo_update_tail(stats, kl, lr, lr32, desired_kl, sums, round_fp32=False):
     """One launch for the per-mini-batch tail of PPO.update (include/rslrl_amd.h rslrl_ppo_update_tail):
     the adaptive-KL lr rule on the fp64 device lr (when lr is not None; kl: fp32 device scalar) and the loss
-    statistics accumulation sums[0:3] += (value, surrogate, entropy) of stats."""
-    _require_device(stats, kl, lr, lr32, sums)
-    kl_hi = float(desired_kl) * 2.0 if lr is not None else 0.0
-    kl_lo = float(desired_kl) / 2.0 if lr is not None else 0.0
-    rc = _lib.lib().rslrl_ppo_update_tail(
-        stats.data_ptr(), kl.data_ptr() if lr is not None else None, lr.data_ptr() if lr is not None else None,
-        lr32.data_ptr() if lr is not None else None, 1 if round_fp32 else 0, kl_hi, kl_lo,
-        sums.data_ptr() if sums is not None else None, _stream(stats.device))
-    _lib.check(rc, "rslrl_ppo_update_tail")
+    statistics accumulation sums[0:3] += (value, surrogate, entropy) of stats.  FusedClipAdam.step(tail=...) runs
+    the same inside its norm launch."""
+    ppo_update_tail_args(ppo_tail_args(stats, kl, lr, lr32, desired_kl, sums, round_fp32), stats.device)
 
 
 class FusedClipAdam:
@@ -804,7 +815,9 @@ class FusedClipAdam:
                 if self.opt.state.get(p):
                     self._state(p)
 
-    def step(self, closure=None):
+    def step(self, closure=None, tail=None):
+        """tail: an rslrl_ppo_tail_t (ppo_tail_args) run inside the norm launch before the step sizes take the lr
+        (rslrl_clip_adam_step_tail: one launch less per mini-batch than ppo_update_tail + step)."""
         if closure is not None:
             raise RuntimeError("FusedClipAdam.step: closures are not supported")
         L = _lib.lib()
@@ -835,9 +848,16 @@ class FusedClipAdam:
                     t.param, t.grad = p.data_ptr(), grad.data_ptr()
                     t.exp_avg, t.exp_avg_sq = st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr()
                     t.step, t.numel = st["step"].data_ptr(), p.numel()
-                rc = L.rslrl_clip_adam_step(ctypes.byref(a), self.ws.data_ptr(), self.ws.numel() * 4,
-                                            _stream(self.ws.device))
+                if tail is not None:
+                    rc = L.rslrl_clip_adam_step_tail(ctypes.byref(a), ctypes.byref(tail), self.ws.data_ptr(),
+                                                     self.ws.numel() * 4, _stream(self.ws.device))
+                    tail = None
+                else:
+                    rc = L.rslrl_clip_adam_step(ctypes.byref(a), self.ws.data_ptr(), self.ws.numel() * 4,
+                                                _stream(self.ws.device))
                 _lib.check(rc, "rslrl_clip_adam_step")
+        if tail is not None:  # no group had gradients: the tail still runs
+            ppo_update_tail_args(tail, self.ws.device)
         for g, c in back:
             g.copy_(c)
         return None

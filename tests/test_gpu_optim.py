@@ -148,3 +148,42 @@ def test_resume_from_non_fused_adam_state(cuda_device):
         # plain (for-loop) Adam vs torch's fused arithmetic: fp32 rounding apart
         torch.testing.assert_close(po.data, pr.data, rtol=1e-5, atol=1e-6)
         torch.testing.assert_close(opt_o.state[po]["exp_avg_sq"], plain.state[pr]["exp_avg_sq"], rtol=1e-5, atol=1e-9)
+
+
+@pytest.mark.parametrize("round_fp32,with_lr", [(False, True), (True, True), (False, False)])
+def test_tail_inside_the_norm_launch_matches_separate_launches(round_fp32, with_lr, cuda_device):
+    """FusedClipAdam.step(tail=...) (rslrl_clip_adam_step_tail: the per-mini-batch lr rule and loss sums inside the
+    norm launch) against rslrl_ppo_update_tail then step(): the same lr trace, loss sums, parameters and moments, bit
+    for bit, over KLs that raise, lower and keep the lr."""
+    dev = cuda_device
+    runs = []
+    for fused in (False, True):
+        ps = _make(dev, 3)
+        lr32 = torch.full((), 1e-3, dtype=torch.float32, device=dev)
+        lr = torch.full((), 1e-3, dtype=torch.float64, device=dev)
+        opt = torch.optim.Adam(ps, lr=lr32 if with_lr else 1e-3, fused=True)
+        fca = kernels.FusedClipAdam(opt, 1.0)
+        sums = torch.zeros(4, dtype=torch.float64, device=dev)
+        g = torch.Generator(device=dev).manual_seed(2)
+        trace = []
+        for it, kl in enumerate((0.05, 0.001, 0.01, 0.03, 0.0001, 0.0)):
+            for p in ps:
+                p.grad = torch.randn(p.shape, device=dev, generator=g)
+            stats = torch.randn(8, device=dev, generator=g)
+            stats[kernels.STATS_KL] = kl
+            kl_src = stats[kernels.STATS_KL:kernels.STATS_KL + 1]
+            tail = kernels.ppo_tail_args(stats, kl_src if with_lr else None, lr if with_lr else None,
+                                         lr32 if with_lr else None, 0.01, sums, round_fp32=round_fp32)
+            if fused:
+                fca.step(tail=tail)
+            else:
+                kernels.ppo_update_tail_args(tail, dev)
+                fca.step()
+            trace.append((float(lr), float(lr32)))
+        torch.cuda.synchronize()
+        runs.append((trace, sums.clone(), [p.detach().clone() for p in ps],
+                     [opt.state[p]["exp_avg_sq"].clone() for p in ps]))
+    (t0, s0, p0, v0), (t1, s1, p1, v1) = runs
+    assert t0 == t1 and len(set(t0)) > 1 if with_lr else t0 == t1
+    assert torch.equal(s0, s1)
+    assert all(torch.equal(a, b) for a, b in zip(p0, p1)) and all(torch.equal(a, b) for a, b in zip(v0, v1))

@@ -65,7 +65,8 @@ def test_update_c1_matches_reference(golden_meta, cuda_device, one_rank_group):
     stepper = alg._clip_adam if alg._clip_adam is not None else alg.optimizer  # fused clip + Adam on a GPU
     assert alg._clip_adam is not None
     step = stepper.step
-    stepper.step = lambda *a, **k: (lr_trace.append(float(alg.optimizer.param_groups[0]["lr"])), step(*a, **k))[1]
+    # the lr the step uses, read after it: the per-mini-batch tail that sets it runs inside the step when fused
+    stepper.step = lambda *a, **k: (step(*a, **k), lr_trace.append(float(alg.optimizer.param_groups[0]["lr"])))[0]
     torch.default_generator.set_state(torch.from_numpy(z["gen_state"].copy()))
     loss = alg.update()
     assert lr_trace == m["lr_trace"]

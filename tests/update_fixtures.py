@@ -81,12 +81,14 @@ def run_recorded_update(alg, grads=None, rnd_grads=None):
     step = stepper.step
 
     def rec(*a, **k):
-        # the reference records its Python-float self.learning_rate; ours lives on the device in update()
+        if len(got) < want:  # pre-clip: the step writes the clipped gradients back
+            got.append(torch.cat([p.grad.reshape(-1) for p in alg.policy.parameters()]).cpu())
+        r = step(*a, **k)
+        # the reference records its Python-float self.learning_rate; ours lives on the device in update(), set by
+        # the per-mini-batch tail -- which runs inside the step's first launch when fused (FusedClipAdam tail=)
         lr = getattr(alg, "learning_rate_device", None)
         lr_trace.append(float(lr if lr is not None else alg.optimizer.param_groups[0]["lr"]))
-        if len(got) < want:
-            got.append(torch.cat([p.grad.reshape(-1) for p in alg.policy.parameters()]).cpu())
-        return step(*a, **k)
+        return r
 
     stepper.step = rec
     # the RND predictor's step: a fused clip-free Adam when the update runs it on the device, else the torch optimizer
