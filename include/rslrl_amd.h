@@ -592,9 +592,9 @@ int rslrl_hidden_bwd_pair(const rslrl_hidden_bwd_problem_t* p0, const rslrl_hidd
  * image (RSLRL_BIMAGE_LAYOUT_GEMM), out_image: the output layer's RSLRL_BIMAGE_LAYOUT_OUT image.  Both problems share
  * M, k0 and hidden.  RSLRL_E_UNSUPPORTED (nothing launched) unless M is a multiple of 64, k0 in {16, 32, 48, 64},
  * 2 <= hidden <= 4 and 1 <= nout <= 16.
- * ABI 20: a1 may be NULL (one network: policy.evaluate of compute_returns' last values, ppo.py:175-176, or
- * act_inference); and a problem may carry the Normal sample of ActorCritic.act (actor_critic.py:124-127,
- * distribution.sample() = normal_(0, 1) * scale + loc): with `sample` non-NULL the kernel also rewrites
+ * ABI 20: a1 may be NULL (one network: policy.evaluate of compute_returns' last values, ppo.py:171-173, or
+ * act_inference, actor_critic.py:148-151); and a problem may carry the Normal sample of ActorCritic.act
+ * (actor_critic.py:142-146, distribution.sample() = normal_(0, 1) * scale + loc): with `sample` non-NULL it also rewrites
  * sample[r][o] <- sample[r][o] * sample_scale[o] + y[r][o] with torch's two roundings (mul_, then add_) -- the
  * standard normals in, the actions out, bit-identical to rslrl_normal_affine on y. */
 typedef struct {
