@@ -124,7 +124,8 @@ class RolloutStorage:
         self._perm_bufs = [None, None]  # pinned staging buffers (ping-pong: one may still be uploading)
         self._perm_events = [None, None]
         self._perm_slot = 0
-        self._prefetch = None  # (n, state before, state after, slot, worker thread)
+        self._prefetch = None  # (n, state before, state after, slot, worker thread, done[, device copy, its event])
+        self._upload_stream = None  # side stream of stage_permutation's upload
 
     @staticmethod
     def _record_layout(training_type, obs, actions_shape, device):
@@ -266,6 +267,7 @@ class RolloutStorage:
 
     # ------------------------------------------------------------------ GAE (rollout_storage.py:127-149)
     def compute_returns(self, last_values, gamma, lam, normalize_advantage: bool = True):
+        self.stage_permutation()  # the next update's permutation, uploaded while the rollout's launches drain
         last_values = last_values.detach()
         if not last_values.is_contiguous():
             last_values = last_values.contiguous()
@@ -360,6 +362,28 @@ class RolloutStorage:
         worker.start()
         self._prefetch = (n, before, after, slot, worker, done)
 
+    def stage_permutation(self) -> None:
+        """Upload the next update's drawn-ahead permutation now, on a side stream (compute_returns calls this at the
+        end of the rollout, where the GPU still has the rollout's last launches queued): the update then finds it on
+        the device instead of paying the upload's host time where the GPU waits for its first launches.  Nothing is
+        decided here: draw_permutation still checks the generator state and falls back to a synchronous draw."""
+        pf = self._prefetch
+        if pf is None or len(pf) != 6 or torch.device(self.device).type != "cuda":
+            return
+        pn, _, _, slot, worker, done = pf
+        if worker.is_alive() or not done:
+            return
+        dev = torch.device(self.device)
+        if self._upload_stream is None:
+            self._upload_stream = torch.cuda.Stream(dev)
+        with torch.cuda.stream(self._upload_stream):
+            d = torch.empty(pn, dtype=torch.int32, device=dev)
+            d.copy_(self._perm_bufs[slot][:pn], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(self._upload_stream)
+        self._perm_events[slot] = ev  # the pinned buffer is rewritten only after this upload
+        self._prefetch = pf + (d, ev)
+
     def draw_permutation(self, n: int) -> torch.Tensor:
         """Device int32 permutation of range(n) with torch CPU randperm semantics on perm_generator.
 
@@ -368,13 +392,20 @@ class RolloutStorage:
         """
         pf, self._prefetch = self._prefetch, None
         if pf is not None:
-            pn, before, after, slot, worker, done = pf
+            pn, before, after, slot, worker, done = pf[:6]
             worker.join()
             gen = self._gen()
             # the drawn-ahead permutation is used only if its draw succeeded (the state advanced) and the generator
             # still holds the state it was drawn from; otherwise draw synchronously below
             if done and pn == n and not torch.equal(after, before) and torch.equal(gen.get_state(), before):
                 gen.set_state(after)
+                if len(pf) == 8:  # staged by stage_permutation: already (being) copied to the device
+                    d, ev = pf[6], pf[7]
+                    cur = torch.cuda.current_stream(d.device)
+                    cur.wait_event(ev)
+                    d.record_stream(cur)
+                    self._perm_slot = slot
+                    return d
                 return self._upload(self._perm_bufs[slot][:n], slot)
         slot = self._perm_slot ^ 1
         host = kernels.randperm_mt19937(n, self.perm_generator, out=self._staging(slot, n))

@@ -59,6 +59,14 @@ def main():
                 times[label].append((time.perf_counter() - t) * 1e6)
         setattr(obj, name, g)
 
+    from rsl_rl_amd.algorithms import ppo as ppo_mod
+    from rsl_rl_amd.modules import actor_critic as ac_mod
+
+    wrap(ac_mod.ActorCritic, "manual_update_ok", "manual_update_ok")
+    wrap(ppo_mod.PPO, "grad_arena", "grad_arena")
+    wrap(ac_mod.ActorCritic, "train_forward", "train_forward")
+    wrap(fused_mlp, "train_forward_pair", "train_forward_pair")
+    ac_mod.fused_mlp.train_forward_pair = fused_mlp.train_forward_pair
     wrap(rs.RolloutStorage, "draw_permutation", "draw_permutation")
     wrap(rs.RolloutStorage, "_start_prefetch", "start_prefetch")
     wrap(rs.RolloutStorage, "_packed_buffers", "packed_buffers")
@@ -69,8 +77,18 @@ def main():
     def bimages(specs):
         if "first_bimage" not in marks:
             marks["first_bimage"] = time.perf_counter()
-        return orig_bimages(specs)
+        t = time.perf_counter()
+        r = orig_bimages(specs)
+        times["bimages"].append((time.perf_counter() - t) * 1e6)
+        return r
     fused_mlp.bimages = bimages
+    orig_fwd_pair = fused_mlp.linear_fwd_pair
+
+    def linear_fwd_pair(*a, **k):
+        if "first_mlp" not in marks:
+            marks["first_mlp"] = time.perf_counter()
+        return orig_fwd_pair(*a, **k)
+    fused_mlp.linear_fwd_pair = linear_fwd_pair
 
     obs = env.get_observations()
     for it in range(a.iters):
@@ -86,6 +104,8 @@ def main():
         alg.update()
         if "first_bimage" in marks:
             times["update_entry_to_first_bimage"].append((marks["first_bimage"] - t0) * 1e6)
+        if "first_mlp" in marks:
+            times["update_entry_to_first_mlp_launch"].append((marks["first_mlp"] - t0) * 1e6)
     res = {k: {"median_us": round(statistics.median(v[1:] if len(v) > 2 else v), 1), "n": len(v)}
            for k, v in times.items()}
     res["num_envs"] = a.num_envs

@@ -85,25 +85,33 @@ def test_permutation_contents_and_tail_drop(cuda_device):
         assert torch.equal(batches[i][0]["policy"], batches[M + i][0]["policy"])
 
 
-@pytest.mark.parametrize("M", [2, 1])
-def test_prefetched_permutation_matches_plain_draws(M, cuda_device):
+@pytest.mark.parametrize("M,stage", [(2, False), (1, False), (2, True)])
+def test_prefetched_permutation_matches_plain_draws(M, stage, cuda_device):
     """The same sequence of updates with and without interference: every permutation equals torch.randperm on
     the generator's state at that call, and the generator's state after each update matches.  The prefetch starts
-    at the second mini-batch: with one mini-batch per update every draw is synchronous."""
+    at the second mini-batch: with one mini-batch per update every draw is synchronous.  stage: the drawn-ahead
+    permutation is uploaded early (stage_permutation, as compute_returns does), the reseed included."""
     T, N = 4, 50
     n = (T * N // M) * M
     st = RolloutStorage("rl", N, T, {"policy": torch.zeros(N, 2)}, [3], cuda_device)
     st.perm_generator = torch.Generator().manual_seed(21)
     ref = torch.Generator().manual_seed(21)
+    staged = 0
     for k in range(6):
         if k == 3:  # reseed both between two updates: the prepared permutation is stale and must be dropped
             st.perm_generator.manual_seed(5)
             ref.manual_seed(5)
+        if stage:
+            if st._prefetch is not None:
+                st._prefetch[4].join()  # the worker's draw is done (the rollout takes far longer in a run)
+            st.stage_permutation()
+            staged += st._prefetch is not None and len(st._prefetch) == 8
         for _ in st.mini_batch_generator(M, 1):
             pass
         expect = torch.randperm(n, generator=ref)
         assert torch.equal(st.last_indices.cpu().long(), expect), k
         assert torch.equal(st.perm_generator.get_state(), ref.get_state()), k
+    assert staged == (5 if stage else 0)  # every update but the first finds a drawn-ahead permutation
 
 
 @pytest.mark.parametrize("R,fields", [
