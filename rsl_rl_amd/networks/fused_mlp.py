@@ -123,6 +123,9 @@ def frozen_weights():
             _pair_memo.clear()
 
 
+_bimage_floats: dict = {}  # (depth, layout) -> image size in floats
+
+
 def bimages(specs):
     """Images for [(w, transposed[, layout]), ...]: transposed=False -> B = w ([N, K]), True -> B = w^T;
     layout _lib.BIMAGE_LAYOUT_OUT -> the output-layer image of linear_fwd_out.  One launch for every image not
@@ -143,29 +146,38 @@ def bimages(specs):
     if not todo:
         return out
     L = _lib.lib()
-
-    def nbytes(depth, layout):
-        if layout == _lib.BIMAGE_LAYOUT_OUT:
-            return L.rslrl_linear_out_image_bytes()
-        if layout == _lib.BIMAGE_LAYOUT_H3:
-            return L.rslrl_linear_bimage_h3_bytes(depth)
-        return L.rslrl_linear_bimage_bytes(depth)
-
-    sizes = [nbytes(depth, key[4]) // 4 for (_, _, _, _, depth, key) in todo]
+    # (the host side runs once per mini-batch in the update, the first time while the GPU waits: image sizes are
+    # looked up once per (depth, layout), the image views come from one split)
+    sizes = []
+    for (_, _, _, _, depth, key) in todo:
+        n = _bimage_floats.get((depth, key[4]))
+        if n is None:
+            layout = key[4]
+            if layout == _lib.BIMAGE_LAYOUT_OUT:
+                nb = L.rslrl_linear_out_image_bytes()
+            elif layout == _lib.BIMAGE_LAYOUT_H3:
+                nb = L.rslrl_linear_bimage_h3_bytes(depth)
+            else:
+                nb = L.rslrl_linear_bimage_bytes(depth)
+            n = _bimage_floats[(depth, key[4])] = nb // 4
+        sizes.append(n)
     buf = torch.empty(sum(sizes), dtype=torch.float32, device=todo[0][1].device)
+    views = buf.split(sizes)
+    base = buf.data_ptr()
     for start in range(0, len(todo), _lib.MAX_BIMAGES):
         part = todo[start:start + _lib.MAX_BIMAGES]
         descs = (_lib.BImageDesc * len(part))()
         off = sum(sizes[:start])
         keep = []
-        for d, (i, w, tr, rows, depth, key), n in zip(descs, part, sizes[start:start + len(part)]):
+        for j, (d, (i, w, tr, rows, depth, key)) in enumerate(zip(descs, part)):
             src = w.detach()
-            src = src if src.is_contiguous() else src.contiguous()
-            keep.append(src)
-            img = buf[off:off + n]
-            off += n
-            d.src, d.image, d.rows, d.depth, d.transposed = src.data_ptr(), img.data_ptr(), rows, depth, int(tr)
+            if not src.is_contiguous():
+                src = src.contiguous()
+                keep.append(src)
+            d.src, d.image, d.rows, d.depth, d.transposed = src.data_ptr(), base + 4 * off, rows, depth, int(tr)
             d.layout = key[4]
+            off += sizes[start + j]
+            img = views[start + j]
             out[i] = img
             if _frozen_depth:
                 _bimage_cache[key] = (weakref.ref(w), img)
