@@ -46,6 +46,13 @@ import threading
 import torch
 
 from .. import kernels
+
+# RSLRL_STAGE_PERM=1 (opt-in; the same permutations): the next update's permutation is uploaded at compute_returns on
+# a side stream (stage_permutation) instead of at the update's start.  Off by default: it saves 20-100 us of host time
+# where the GPU waits, but the same-box A/B at the 16,384-env share read 16.30 / 16.59 / 15.80 M with it against
+# 16.55 / 16.53 / 16.56 M without (profiles/r6_stage_perm_ab.json) -- a third stream in the rollout's queue set is
+# not worth that spread
+_STAGE_PERM = os.environ.get("RSLRL_STAGE_PERM", "0") == "1"
 from ..utils import TensorDict
 
 
@@ -368,7 +375,7 @@ class RolloutStorage:
         the device instead of paying the upload's host time where the GPU waits for its first launches.  Nothing is
         decided here: draw_permutation still checks the generator state and falls back to a synchronous draw."""
         pf = self._prefetch
-        if pf is None or len(pf) != 6 or torch.device(self.device).type != "cuda":
+        if pf is None or len(pf) != 6 or torch.device(self.device).type != "cuda" or not _STAGE_PERM:
             return
         pn, _, _, slot, worker, done = pf
         if worker.is_alive() or not done:

@@ -8,7 +8,7 @@ import torch
 from conftest import golden_path
 from oracle import ppo_oracle as O
 from rsl_rl_amd import kernels
-from rsl_rl_amd.storage import RolloutStorage
+from rsl_rl_amd.storage import RolloutStorage, rollout_storage
 
 pytestmark = pytest.mark.gpu
 
@@ -86,7 +86,7 @@ def test_permutation_contents_and_tail_drop(cuda_device):
 
 
 @pytest.mark.parametrize("M,stage", [(2, False), (1, False), (2, True)])
-def test_prefetched_permutation_matches_plain_draws(M, stage, cuda_device):
+def test_prefetched_permutation_matches_plain_draws(M, stage, cuda_device, monkeypatch):
     """The same sequence of updates with and without interference: every permutation equals torch.randperm on
     the generator's state at that call, and the generator's state after each update matches.  The prefetch starts
     at the second mini-batch: with one mini-batch per update every draw is synchronous.  stage: the drawn-ahead
@@ -102,6 +102,7 @@ def test_prefetched_permutation_matches_plain_draws(M, stage, cuda_device):
             st.perm_generator.manual_seed(5)
             ref.manual_seed(5)
         if stage:
+            monkeypatch.setattr(rollout_storage, "_STAGE_PERM", True)
             if st._prefetch is not None:
                 st._prefetch[4].join()  # the worker's draw is done (the rollout takes far longer in a run)
             st.stage_permutation()
