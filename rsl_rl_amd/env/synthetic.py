@@ -80,7 +80,6 @@ class SyntheticVecEnv(VecEnv):
         return self._obs, rewards, dones, {"time_outs": time_outs}
 
     def _step_fused(self):
-        from .. import _lib
         from ..kernels import _stream
 
         n, dev = self.num_envs, self.device
@@ -88,6 +87,10 @@ class SyntheticVecEnv(VecEnv):
         # consumes them within one; a ring instead of four allocations and a TensorDict per step: ~10 us of host time
         # on the launch-bound rollout of a small per-GPU share)
         if self._ring is None:
+            from .. import _lib
+
+            self._step_fn = _lib.lib().rslrl_synthetic_env_step
+            self._check = _lib.check
             self._ring = []
             for _ in range(self.kRing):
                 obs = torch.empty(n, self.num_obs, device=dev)
@@ -97,10 +100,10 @@ class SyntheticVecEnv(VecEnv):
                 self._ring.append((bufs, ptrs, {"time_outs": bufs[4]}))
         self._step_count += 1
         bufs, ptrs, extras = self._ring[self._step_count % self.kRing]
-        rc = _lib.lib().rslrl_synthetic_env_step(
+        rc = self._step_fn(
             ptrs[0], self.num_obs, ptrs[1], ptrs[2], ptrs[3], self.episode_length_buf.data_ptr(), n, self._seed,
             self._step_count & 0xFFFFFFFF, float(self.done_prob), float(self.timeout_prob), int(self.max_episode_length),
             _stream(dev))
-        _lib.check(rc, "rslrl_synthetic_env_step")
+        self._check(rc, "rslrl_synthetic_env_step")
         self._obs = bufs[0]
         return self._obs, bufs[2], bufs[3], dict(extras)

@@ -686,6 +686,7 @@ class RolloutRecordPlan:
         self.rows = [(k, outs[k].data_ptr(), outs[k].stride(0) * outs[k].element_size()) for k in self._OUTS]
         self.obs_rows = [(d.data_ptr(), d.stride(0) * d.element_size()) for d in obs_dsts]
         self.a, self.N, self.A, self.device, self.gamma = a, N, A, device, float(gamma)  # (a.gamma reads back as fp32)
+        self._fn = _lib.lib().rslrl_rollout_record  # bound once: the launch runs every env step
         self.dones_dtype, self.shared_sigma, self.obs_widths = dones_dtype, shared_sigma, tuple(obs_widths)
         self.key = (self.obs_widths, dones_dtype, time_outs_dtype, self.gamma, shared_sigma)
         obs_b = sum(8 * w for w in obs_widths)
@@ -727,7 +728,7 @@ class RolloutRecordPlan:
         for i, (src, (base, st)) in enumerate(zip(obs_srcs, self.obs_rows)):
             a.obs[i].src, a.obs[i].dst = src.data_ptr(), base + t * st
         with timer.span("rollout_record", self.device, self.bytes):
-            rc = _lib.lib().rslrl_rollout_record(ctypes.byref(a), _stream(self.device))  # the caller's current stream
+            rc = self._fn(ctypes.byref(a), _stream(self.device))  # the caller's current stream
         _lib.check(rc, "rslrl_rollout_record")
 
 
