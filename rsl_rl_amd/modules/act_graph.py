@@ -63,6 +63,7 @@ class RolloutActGraph:
         self._groups = None  # the observation groups the step reads
         self._mods = None  # the policy's modules (their parameters and buffers key the configuration)
         self._parents = []  # [(module, its children)] of the modules that have children: a replaced module shows here
+        self._tdicts = []  # the modules' parameter and buffer dicts (their entries key the configuration)
         self._img_cache = None  # the image graph's fused_mlp image cache entries (the direct graphs read them)
         self._direct = {}  # observation pointers -> (graph, outputs): the step reading those buffers in place
         self._ptr_seen = {}  # observation pointers -> times seen (a pointer set seen twice gets a direct graph)
@@ -81,14 +82,14 @@ class RolloutActGraph:
         if self._mods is None or any(tuple(m._modules.values()) != kids for m, kids in self._parents):
             self._mods = list(pol.modules())
             self._parents = [(m, tuple(m._modules.values())) for m in self._mods if m._modules]
+            self._tdicts = [d for m in self._mods for d in (m._parameters, m._buffers)]  # the dicts, read per step
         shapes = []
         for g in self._groups:
             t = obs[g]
             if not (isinstance(t, torch.Tensor) and t.is_cuda):
                 return None
             shapes.append((g, tuple(t.shape), t.dtype, t.device, t.stride()))
-        ptrs = tuple(t.data_ptr() for m in self._mods for d in (m._parameters, m._buffers) for t in d.values()
-                     if t is not None)
+        ptrs = tuple([t.data_ptr() for d in self._tdicts for t in d.values() if t is not None])
         return (tuple(shapes), ptrs, fused_mlp._mode, torch.is_inference_mode_enabled())
 
     def __call__(self, obs):
